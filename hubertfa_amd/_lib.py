@@ -1,0 +1,79 @@
+"""ctypes binding of libhfa.so, the C-ABI of hand-written gfx950 kernels (include/hfa.h).
+
+The product path has no fallback: if the library is missing or fails to load, every op raises
+``HFALibraryError``.  Signatures are declared once in ``_SIGS``; ``check(rc)`` turns a negative status into an
+exception carrying ``hfa_last_error()``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HFA_LIB", os.path.join(_HERE, "_build", "libhfa.so"))
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+LL = ctypes.c_longlong
+F = ctypes.c_float
+
+# name -> argtypes (restype int unless listed in _RESTYPE)
+_SIGS = {
+    "hfa_last_error": [],
+    "hfa_abi_version": [],
+    "hfa_build_arch": [],
+    # alignment decoder (viterbi.hip)
+    "hfa_viterbi_forward": [I, I, I, P, P, P, P, P, P, P, P, P, P, P],
+    "hfa_viterbi_backtrack": [I, I, I, P, P, P, P, P, P, P, P, P, P],
+    "hfa_lattice_prologue": [I, I, I, I, P, P, P, LL, LL, P, LL, LL, P, P, P, P, P, P, P, P, P],
+}
+_RESTYPE = {"hfa_last_error": ctypes.c_char_p, "hfa_build_arch": ctypes.c_char_p}
+
+
+class HFALibraryError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def register(name: str, argtypes: list, restype=ctypes.c_int):
+    """Kernel modules declare their entry points here before first use."""
+    _SIGS[name] = argtypes
+    if restype is not ctypes.c_int:
+        _RESTYPE[name] = restype
+    if _lib is not None:
+        _bind(_lib, name)
+
+
+def _bind(L, name):
+    fn = getattr(L, name)
+    fn.argtypes = _SIGS[name]
+    fn.restype = _RESTYPE.get(name, ctypes.c_int)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HFALibraryError(
+                f"libhfa.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; "
+                f"g.build()'` (make -C hubertfa_amd/csrc). There is no CPU fallback.")
+        try:
+            L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            raise HFALibraryError(f"failed to load {LIB_PATH}: {e}") from e
+        for name in _SIGS:
+            _bind(L, name)
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().hfa_last_error()
+        raise HFALibraryError(f"{what or 'libhfa'} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)

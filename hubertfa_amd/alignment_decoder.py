@@ -1,0 +1,226 @@
+"""Drop-in ``AlignmentDecoder`` (reference: tools/alignment_decoder.py) running its hot path on the GPU.
+
+Same constructor, same ``decode``/``_decode``/``forward_pass`` signatures and return values, same attributes
+(``ph_seq_id``, ``ph_idx_seq``, ``ph_frame_pred``, ``ph_time_int_pred``, ``edge_prob``, ``ph_pred_seq``,
+``ph_intervals_pred``, ``frame_confidence``, ``ctc_logits``).  The per-frame work (mask, log_softmax, edge
+sigmoid, lattice gather), the monotonic DP and the backtrack are HIP kernels (csrc/viterbi.hip); the host keeps
+only the O(#phones) interval/word assembly, in numpy, with the reference's dtypes.
+
+``decode_batch`` is the batched entry used by the pipeline: B utterances, one kernel launch per stage.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+def _device(t: torch.Tensor) -> torch.device:
+    if t.device.type == "cuda":
+        return t.device
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def assemble_intervals(ph_idx_seq, ph_time_int, edge_diff, T, frame_length, ph_seq, word_seq, ph_idx_to_word_idx):
+    """Fractional boundaries and word grouping (alignment_decoder.py:103-138), numpy f64 as the reference."""
+    ph_time_int = np.asarray(ph_time_int)
+    edge_diff = np.asarray(edge_diff, dtype=np.float64)
+    ph_time_fractional = (edge_diff[ph_time_int] / 2).clip(-0.5, 0.5)
+    ph_time_pred = frame_length * np.concatenate([ph_time_int.astype("float32") + ph_time_fractional, [T]])
+    ph_intervals = np.stack([ph_time_pred[:-1], ph_time_pred[1:]], axis=1)
+    ph_seq_pred, ph_intervals_pred, word_seq_pred, word_intervals_pred = [], [], [], []
+    word_idx_last = -1
+    for i, ph_idx in enumerate(ph_idx_seq):
+        if ph_seq[ph_idx] == "SP":
+            continue
+        ph_seq_pred.append(ph_seq[ph_idx])
+        ph_intervals_pred.append(ph_intervals[i, :])
+        word_idx = ph_idx_to_word_idx[ph_idx]
+        if word_idx == word_idx_last:
+            word_intervals_pred[-1][1] = ph_intervals[i, 1]
+        else:
+            word_seq_pred.append(word_seq[word_idx])
+            word_intervals_pred.append([ph_intervals[i, 0], ph_intervals[i, 1]])
+            word_idx_last = word_idx
+    return (np.array(ph_seq_pred), np.array(ph_intervals_pred).clip(min=0, max=None), np.array(word_seq_pred),
+            np.array(word_intervals_pred).clip(min=0, max=None))
+
+
+def total_confidence(frame_confidence: np.ndarray):
+    return np.exp(np.mean(np.log(frame_confidence + 1e-6)) / 3)  # (:97)
+
+
+class AlignmentDecoder:
+    """GPU alignment decoder with the reference's API (tools/alignment_decoder.py:8-24)."""
+
+    def __init__(self, vocab, melspec_config):
+        self.vocab = vocab
+        self.melspec_config = melspec_config
+        self.frame_length = self.melspec_config["hop_length"] / (self.melspec_config["sample_rate"])
+        self.ctc_logits = None
+        self.ph_seq_id = None
+        self.ph_idx_seq = None
+        self.ph_frame_pred = None
+        self.ph_time_int_pred = None
+        self.ph_intervals_pred = None
+        self.edge_prob = None
+        self.ph_pred_seq = None
+        self.frame_confidence = None
+
+    # -- frame trimming (alignment_decoder.py:45-50) ------------------------------------------------------
+    def num_frames(self, wav_length: float | None, n_logit_frames: int) -> int:
+        if wav_length is None:
+            return n_logit_frames
+        n = int((wav_length * self.melspec_config["sample_rate"] + 0.5) / self.melspec_config["hop_length"])
+        return min(n, n_logit_frames)
+
+    def ph_ids(self, ph_seq) -> np.ndarray:
+        return np.array([self.vocab["vocab"][ph] for ph in ph_seq])  # KeyError on OOV, as (:35)
+
+    # -- single utterance, reference signature (alignment_decoder.py:26-143) ------------------------------
+    def decode(self, ph_frame_logits, ph_edge_logits, ctc_logits, wav_length: float | None, ph_seq: list[str],
+               word_seq: list[str] = None, ph_idx_to_word_idx: list[int] = None):
+        ph_seq_id = self.ph_ids(ph_seq)
+        self.ph_seq_id = ph_seq_id
+        if word_seq is None:
+            word_seq = ph_seq
+            ph_idx_to_word_idx = np.arange(len(ph_seq))
+        res = self.decode_batch(ph_frame_logits, ph_edge_logits, [wav_length], [ph_seq], [word_seq],
+                                [ph_idx_to_word_idx], keep_frame_probs=True)[0]
+        T = res["T"]
+        self.ctc_logits = ctc_logits[:, :T, :].float().squeeze(0).cpu().numpy().astype("float32")
+        self.ph_frame_pred = res["ph_frame_pred"]
+        self.edge_prob = res["edge_prob"]
+        self.ph_idx_seq = res["ph_idx_seq"]
+        self.ph_time_int_pred = res["ph_time_int"]
+        self.frame_confidence = res["frame_confidence"]
+        self.ph_pred_seq = res["ph_seq"]
+        self.ph_intervals_pred = res["ph_intervals"]
+        return res["ph_seq"], res["ph_intervals"], res["word_seq"], res["word_intervals"], res["confidence"]
+
+    # -- batched path ---------------------------------------------------------------------------------------
+    def decode_batch(self, frame_logits, edge_logits, wav_lengths, ph_seqs, word_seqs=None, p2ws=None,
+                     keep_frame_probs: bool = False, host: bool = True):
+        """Decode B utterances: frame_logits [B,Tl,V], edge_logits [B,Tl] (GPU tensors, strided views OK).
+
+        Returns one dict per utterance with the reference decode() outputs (+ raw path arrays).
+        """
+        dev = _device(frame_logits)
+        frame_logits = frame_logits.to(dev).float()
+        edge_logits = edge_logits.to(dev).float()
+        if frame_logits.stride(2) != 1:
+            frame_logits = frame_logits.contiguous()
+        B, Tl, V = frame_logits.shape
+        Ts = [self.num_frames(w, Tl) for w in wav_lengths]
+        ids = [self.ph_ids(p) for p in ph_seqs]
+        Smax = max(len(i) for i in ids)
+        ids_pad = np.zeros((B, Smax), np.int32)
+        for b, i in enumerate(ids):
+            ids_pad[b, :len(i)] = i
+        T_t = torch.tensor(Ts, dtype=torch.int32, device=dev)
+        S_t = torch.tensor([len(i) for i in ids], dtype=torch.int32, device=dev)
+        ids_t = torch.from_numpy(ids_pad).to(dev)
+        lat = ops.lattice_prologue(frame_logits, edge_logits, ids_t, T_t, S_t, want_frame_probs=keep_frame_probs)
+        dp, bt, curr = self.init_dp(lat["prob_log"], ids_t, S_t)
+        ops.viterbi_forward(lat["prob_log"], lat["not_edge_log"], lat["edge_log"], curr, dp, bt, ids_t, T_t, S_t)
+        idx, tint, n, fc = ops.viterbi_backtrack(dp, bt, ids_t, T_t, S_t)
+        if not host:
+            return dict(ph_idx_seq=idx, ph_time_int=tint, n=n, frame_confidence=fc, edge_diff=lat["edge_diff"],
+                        T=T_t, lattice=lat)
+        # one device->host copy of the small per-utterance arrays
+        idx_h, tint_h, n_h, fc_h = idx.cpu().numpy(), tint.cpu().numpy(), n.cpu().numpy(), fc.cpu().numpy()
+        ed_h = lat["edge_diff"].cpu().numpy()
+        ep_h = lat["edge_prob"].cpu().numpy() if keep_frame_probs else None
+        fp_h = lat["ph_frame_pred"].cpu().numpy() if keep_frame_probs else None
+        out = []
+        for b in range(B):
+            T = Ts[b]
+            ph_seq = ph_seqs[b]
+            ws = word_seqs[b] if word_seqs is not None and word_seqs[b] is not None else ph_seq
+            pw = p2ws[b] if p2ws is not None and p2ws[b] is not None else np.arange(len(ph_seq))
+            k = int(n_h[b])
+            pis, pts = idx_h[b, :k].astype(np.int64), tint_h[b, :k].astype(np.int64)
+            fcb = fc_h[b, :T].copy()
+            edge_diff = np.concatenate([ed_h[b, :T - 1].astype(np.float64), [0.0]]) if T > 0 else np.zeros(0)
+            ph_p, ph_iv, w_p, w_iv = assemble_intervals(pis, pts, edge_diff, T, self.frame_length, ph_seq, ws, pw)
+            r = dict(T=T, ph_idx_seq=pis, ph_time_int=pts, frame_confidence=fcb, ph_seq=ph_p, ph_intervals=ph_iv,
+                     word_seq=w_p, word_intervals=w_iv, confidence=total_confidence(fcb))
+            if keep_frame_probs:
+                r["edge_prob"] = ep_h[b, :T].copy()
+                r["ph_frame_pred"] = fp_h[b, :T].copy()
+            out.append(r)
+        return out
+
+    @staticmethod
+    def init_dp(prob_log: torch.Tensor, ids_t: torch.Tensor, S_t: torch.Tensor):
+        """dp/bt/curr initialisation of _decode (alignment_decoder.py:244-254), on device."""
+        B, Tmax, Smax = prob_log.shape
+        dev = prob_log.device
+        dp = torch.full((B, Tmax, Smax), float("-inf"), dtype=torch.float32, device=dev)
+        bt = torch.full((B, Tmax, Smax), -1, dtype=torch.int8, device=dev)
+        curr = torch.full((B, Smax), float("-inf"), dtype=torch.float64, device=dev)
+        if Tmax == 0 or Smax == 0:
+            return dp, bt, curr
+        dp[:, 0, 0] = prob_log[:, 0, 0]
+        curr[:, 0] = prob_log[:, 0, 0].double()
+        if Smax > 1:
+            two = (ids_t[:, 0] == 0) & (S_t > 1)
+            dp[:, 0, 1] = torch.where(two, prob_log[:, 0, 1], dp[:, 0, 1])
+            curr[:, 1] = torch.where(two, prob_log[:, 0, 1].double(), curr[:, 1])
+        return dp, bt, curr
+
+    # -- reference static/numpy API on the GPU --------------------------------------------------------------
+    @staticmethod
+    def forward_pass(T, S, prob_log, not_edge_prob_log, edge_prob_log, curr_ph_max_prob_log, dp, backtrack_s,
+                     ph_seq_id, prob3_pad_len):
+        """numpy in/out with the reference's in-place semantics (alignment_decoder.py:170-230)."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        Smax = prob_log.shape[1]
+        pl = torch.from_numpy(np.ascontiguousarray(prob_log, np.float32))[None].to(dev)
+        nE = torch.from_numpy(np.ascontiguousarray(not_edge_prob_log, np.float32))[None].to(dev)
+        E = torch.from_numpy(np.ascontiguousarray(edge_prob_log, np.float32))[None].to(dev)
+        cu = torch.from_numpy(np.ascontiguousarray(curr_ph_max_prob_log, np.float64))[None].to(dev)
+        d = torch.from_numpy(np.ascontiguousarray(dp, np.float32))[None].to(dev)
+        bt = torch.from_numpy(np.ascontiguousarray(backtrack_s).astype(np.int8))[None].to(dev)
+        ids = torch.from_numpy(np.ascontiguousarray(ph_seq_id).astype(np.int32))[None].to(dev)
+        T_t = torch.tensor([T], dtype=torch.int32, device=dev)
+        S_t = torch.tensor([S], dtype=torch.int32, device=dev)
+        pad = torch.tensor([prob3_pad_len], dtype=torch.int32, device=dev)
+        assert Smax == S
+        ops.viterbi_forward(pl, nE, E, cu, d, bt, ids, T_t, S_t, pad)
+        dp[...] = d[0].cpu().numpy()
+        bt_h = bt[0].cpu().numpy().astype(np.int32)
+        bt_h[0] = backtrack_s[0]
+        backtrack_s[...] = bt_h
+        curr_ph_max_prob_log[...] = cu[0].cpu().numpy()
+        return dp, backtrack_s, curr_ph_max_prob_log
+
+    def _decode(self, ph_seq_id, ph_prob_log, edge_prob):
+        """(ph_idx_seq, ph_time_int, frame_confidence) from a host lattice (alignment_decoder.py:232-294)."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        ph_seq_id = np.asarray(ph_seq_id)
+        T = ph_prob_log.shape[0]
+        S = len(ph_seq_id)
+        prob_log = np.ascontiguousarray(ph_prob_log[:, ph_seq_id], np.float32)
+        E = np.log(edge_prob + 1e-6).astype("float32")  # numpy dtype rules of (:241-242)
+        nE = np.log(1 - edge_prob + 1e-6).astype("float32")
+        pl = torch.from_numpy(prob_log)[None].to(dev)
+        ids = torch.from_numpy(ph_seq_id.astype(np.int32))[None].to(dev)
+        T_t = torch.tensor([T], dtype=torch.int32, device=dev)
+        S_t = torch.tensor([S], dtype=torch.int32, device=dev)
+        dp, bt, curr = self.init_dp(pl, ids, S_t)
+        ops.viterbi_forward(pl, torch.from_numpy(nE)[None].to(dev), torch.from_numpy(E)[None].to(dev), curr, dp,
+                            bt, ids, T_t, S_t)
+        idx, tint, n, fc = ops.viterbi_backtrack(dp, bt, ids, T_t, S_t)
+        k = int(n[0])
+        return (idx[0, :k].cpu().numpy().astype(np.int64), tint[0, :k].cpu().numpy().astype(np.int64),
+                fc[0].cpu().numpy())
+
+    def ctc(self):
+        """Greedy CTC collapse (alignment_decoder.py:145-150); validation-only helper, host numpy."""
+        ctc = np.argmax(self.ctc_logits, axis=-1)
+        ctc_index = np.concatenate([[0], ctc])
+        ctc_index = (ctc_index[1:] != ctc_index[:-1]) * ctc != 0
+        ctc = ctc[ctc_index]
+        return np.array([ph_id for ph_id in ctc if ph_id != 0])

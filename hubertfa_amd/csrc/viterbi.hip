@@ -1,0 +1,390 @@
+// viterbi.hip — the alignment decoder's device path: lattice prologue, monotonic max-plus DP, backtrack.
+//
+// Replaces (reference, read-only at /root/reference):
+//   * AlignmentDecoder.decode, device part    tools/alignment_decoder.py:35-84   -> hfa_lattice_prologue
+//   * AlignmentDecoder._decode lattice prep   tools/alignment_decoder.py:239-242 -> hfa_lattice_prologue
+//   * AlignmentDecoder.forward_pass (numba)   tools/alignment_decoder.py:170-230 -> hfa_viterbi_forward
+//   * AlignmentDecoder._decode backtrack      tools/alignment_decoder.py:263-288 -> hfa_viterbi_backtrack
+//
+// Numerics: dp is f32, curr_ph_max_prob_log is f64.  prob1 = (dp+L)+nE in f32;
+// prob2/prob3 = f32( f64( (dp+L)+E in f32 ) + curr*(T/S) in f64 ).  Ties resolve by strict '>' in the order
+// stay(0) -> advance(1) -> skip(2).  This file is compiled with -ffp-contract=off and uses explicit
+// __dmul_rn/__dadd_rn so no FMA contraction changes a rounding.  Result: dp/bt bit-exact with the reference.
+//
+// Parallel structure (one wavefront per utterance): dp[t,.] depends only on dp[t-1, s], dp[t-1, s-1],
+// dp[t-1, s-2], so the front is the whole row t: each lane owns K contiguous states, T serial steps, the
+// batch spreads over CUs.  The only cross-lane traffic per step is the two "q" values of the left neighbour
+// lane (DPP/permute via __shfl_up).  Emission rows for t+1.. are prefetched a group ahead so the serial
+// chain never waits on HBM.
+#include "hfa_common.h"
+
+namespace {
+
+using hfa::neg_inf;
+
+constexpr int kGroup = 8;  // time steps per prefetch group
+
+template <int K>
+__global__ __launch_bounds__(64) void viterbi_forward_kernel(
+    int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
+    const int32_t* __restrict__ padv, const float* __restrict__ prob_log,
+    const float* __restrict__ not_edge_log, const float* __restrict__ edge_log, double* __restrict__ curr_io,
+    float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id) {
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int T = Tv[b];
+    const int S = Sv[b];
+    if (T <= 1 || S <= 0) return;
+    const int pad = padv ? padv[b] : (S >= 2 ? 2 : 1);
+    const size_t ts = (size_t)b * Tmax * Smax;
+    const float* pl = prob_log + ts;
+    float* d = dp + ts;
+    int8_t* bb = bt + ts;
+    const float* nEp = not_edge_log + (size_t)b * Tmax;
+    const float* Ep = edge_log + (size_t)b * Tmax;
+    const int32_t* ids = ph_seq_id + (size_t)b * Smax;
+    double* cu = curr_io + (size_t)b * Smax;
+    const double ratio = (double)T / (double)S;  // `T / S` (alignment_decoder.py:186), f64 true division
+
+    const int s0 = lane * K;
+    float dprev[K];
+    double curr[K];
+    bool valid[K], zero[K], allow3[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int s = s0 + k;
+        valid[k] = s < S;
+        dprev[k] = valid[k] ? d[s] : neg_inf();
+        curr[k] = valid[k] ? cu[s] : -__builtin_inf();
+        zero[k] = valid[k] && ids[s] == 0;
+        // prob3 (alignment_decoder.py:191-202): -inf for s < pad, and for s >= pad when
+        // (s - pad + 1 < S - 1 and ph_seq_id[s - pad + 1] != 0).
+        const int j = s - pad + 1;
+        allow3[k] = valid[k] && s >= pad && !((j < S - 1) && ids[j] != 0);
+    }
+
+    float Lc[kGroup][K], Ec[kGroup], nEc[kGroup];
+    float Ln[kGroup][K], En[kGroup], nEn[kGroup];
+    auto load_group = [&](int t0, float (&L)[kGroup][K], float (&E)[kGroup], float (&nE)[kGroup]) {
+#pragma unroll
+        for (int u = 0; u < kGroup; ++u) {
+            const int t = t0 + u;
+            const bool tv = t < T;
+            E[u] = tv ? Ep[t] : 0.0f;
+            nE[u] = tv ? nEp[t] : 0.0f;
+#pragma unroll
+            for (int k = 0; k < K; ++k) L[u][k] = (tv && valid[k]) ? pl[(size_t)t * Smax + s0 + k] : 0.0f;
+        }
+    };
+    load_group(1, Lc, Ec, nEc);
+
+    for (int t0 = 1; t0 < T; t0 += kGroup) {
+        if (t0 + kGroup < T) load_group(t0 + kGroup, Ln, En, nEn);
+#pragma unroll
+        for (int u = 0; u < kGroup; ++u) {
+            const int t = t0 + u;
+            if (t >= T) break;
+            const float E = Ec[u], nE = nEc[u];
+            float a[K], q[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                a[k] = __fadd_rn(dprev[k], Lc[u][k]);                                   // dp + L     (f32)
+                const float a2 = __fadd_rn(a[k], E);                                     //  + E       (f32)
+                q[k] = (float)__dadd_rn((double)a2, __dmul_rn(curr[k], ratio));          //  + C*T/S   (f64)
+            }
+            // left neighbour lane's last two q values (state s0-1, s0-2)
+            float qm1 = __shfl_up(q[K - 1], 1, 64);
+            float qm2 = (K >= 2) ? __shfl_up(q[K >= 2 ? K - 2 : 0], 1, 64) : __shfl_up(q[0], 2, 64);
+            if (lane < 1) qm1 = neg_inf();
+            if (K >= 2 ? lane < 1 : lane < 2) qm2 = neg_inf();
+            const size_t row = (size_t)t * Smax;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int s = s0 + k;
+                const float p1 = __fadd_rn(a[k], nE);
+                const float src1 = (k >= 1) ? q[k >= 1 ? k - 1 : 0] : qm1;
+                const float src2 = (k >= 2) ? q[k >= 2 ? k - 2 : 0] : (k == 1 ? qm1 : qm2);
+                const float p2 = (s == 0) ? neg_inf() : src1;
+                const float p3 = allow3[k] ? (pad == 1 ? src1 : src2) : neg_inf();
+                float best = p1;
+                int idx = 0;
+                if (p2 > best) { best = p2; idx = 1; }
+                if (p3 > best) { best = p3; idx = 2; }
+                if (valid[k]) {
+                    d[row + s] = best;
+                    bb[row + s] = (int8_t)idx;
+                }
+                const double Ld = (double)Lc[u][k];
+                if (idx == 0) curr[k] = (Ld > curr[k]) ? Ld : curr[k];  // max(curr, L) (:222)
+                else curr[k] = Ld;                                       // (:224)
+                if (zero[k]) curr[k] = 0.0;                              // (:226-228)
+                dprev[k] = best;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kGroup; ++u) {
+            Ec[u] = En[u];
+            nEc[u] = nEn[u];
+#pragma unroll
+            for (int k = 0; k < K; ++k) Lc[u][k] = Ln[u][k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (valid[k]) cu[s0 + k] = curr[k];
+}
+
+// Backtrack (alignment_decoder.py:263-288): one 256-thread workgroup per utterance.
+//   1. end state: S-2 if S>=2 and dp[T-1,S-2] > dp[T-1,S-1] and ph_seq_id[S-1]==0 else S-1 (:269-272)
+//   2. bt rows staged through LDS in chunks, one lane chases s(t) from T-1 down to 0 (serial by nature),
+//      recording path[t] = s | emit<<15 in LDS (emit: bt[t,s] != 0, always at t == 0 where bt is -1).
+//   3. all threads: frame_conf[t] = exp(dp[t,s_t] - dp[t-1,s_{t-1}]) (np.exp(np.diff(pad(fc,(1,0))))),
+//      and an ordered compaction of the emitted (s, t) pairs.
+constexpr int kBtThreads = 256;
+constexpr int kBtChunkBytes = 32768;
+
+__global__ __launch_bounds__(kBtThreads) void viterbi_backtrack_kernel(
+    int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
+    const float* __restrict__ dp, const int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id,
+    int32_t* __restrict__ ph_idx_seq, int32_t* __restrict__ ph_time_int, int32_t* __restrict__ n_out,
+    float* __restrict__ frame_conf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int8_t* chunk = reinterpret_cast<int8_t*>(smem);
+    uint16_t* path = reinterpret_cast<uint16_t*>(smem + kBtChunkBytes);
+    __shared__ int s_cur;
+    __shared__ int warp_cnt[kBtThreads / 64];
+
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int T = Tv[b];
+    const int S = Sv[b];
+    const size_t ts = (size_t)b * Tmax * Smax;
+    const float* d = dp + ts;
+    const int8_t* bb = bt + ts;
+    const int32_t* ids = ph_seq_id + (size_t)b * Smax;
+    if (T <= 0 || S <= 0) {
+        if (tid == 0) n_out[b] = 0;
+        return;
+    }
+    if (tid == 0) {
+        int s = S - 1;
+        if (S >= 2 && d[(size_t)(T - 1) * Smax + S - 2] > d[(size_t)(T - 1) * Smax + S - 1] && ids[S - 1] == 0)
+            s = S - 2;
+        s_cur = s;
+    }
+    const int rows_per_chunk = max(1, kBtChunkBytes / Smax);
+    for (int hi = T - 1; hi >= 0; hi -= rows_per_chunk) {
+        const int lo = max(0, hi - rows_per_chunk + 1);
+        const int nbytes = (hi - lo + 1) * Smax;
+        const int8_t* src = bb + (size_t)lo * Smax;
+        for (int i = tid; i < nbytes; i += kBtThreads) chunk[i] = src[i];
+        __syncthreads();
+        if (tid == 0) {
+            int s = s_cur;
+            for (int t = hi; t >= lo; --t) {
+                const int code = (t == 0) ? -1 : (int)chunk[(t - lo) * Smax + s];
+                const int emit = code != 0;
+                path[t] = (uint16_t)(s | (emit << 15));
+                if (emit) s -= code;
+            }
+            s_cur = s;
+        }
+        __syncthreads();
+    }
+    // confidence + ordered compaction of emitted (s, t)
+    int base = 0;
+    for (int t0 = 0; t0 < T; t0 += kBtThreads) {
+        const int t = t0 + tid;
+        int emit = 0, s = 0;
+        if (t < T) {
+            const uint16_t p = path[t];
+            s = p & 0x7fff;
+            emit = p >> 15;
+            const float v = d[(size_t)t * Smax + s];
+            float vp = 0.0f;
+            if (t > 0) vp = d[(size_t)(t - 1) * Smax + (path[t - 1] & 0x7fff)];
+            frame_conf[(size_t)b * Tmax + t] = expf(v - vp);
+        }
+        const unsigned long long m = __ballot(emit);
+        const int lane = tid & 63, w = tid >> 6;
+        const int before = __popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) warp_cnt[w] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int i = 0; i < w; ++i) off += warp_cnt[i];
+        int total = 0;
+        for (int i = 0; i < kBtThreads / 64; ++i) total += warp_cnt[i];
+        if (emit) {
+            ph_idx_seq[(size_t)b * Tmax + off + before] = s;
+            ph_time_int[(size_t)b * Tmax + off + before] = t;
+        }
+        base += total;
+        __syncthreads();
+    }
+    if (tid == 0) n_out[b] = base;
+}
+
+// Lattice prologue: one wavefront per DP frame row (alignment_decoder.py:35-84, 239-242).
+//   x = logits_f32 - 1e9*(v not in {0} U ph_seq_id)            (:37-40, :53)
+//   ph_prob_log = log_softmax(x), ph_frame_pred = softmax(x)     (:56-65)
+//   e = clamp((sigmoid(edge_logit) - 0.1) / 0.8, 0, 1)           (:68-71)
+//   edge_diff[t] = e[t+1]-e[t] (0 at T-1)   edge_prob = clip(e[t] + e[t-1], 0, 1) in f64   (:83-84)
+//   prob_log[t,s] = ph_prob_log[t, ph_seq_id[s]]; E = f32(log(edge_prob + 1e-6)); nE = f32(log(1-edge_prob+1e-6))
+constexpr int kProThreads = 256;
+constexpr int kMaxV = 1024;
+
+__global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
+    int Tmax, int V, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
+    const float* __restrict__ frame_logits, long long f_ld, long long f_bs, const float* __restrict__ edge_logits,
+    long long e_ld, long long e_bs, const int32_t* __restrict__ ph_seq_id, float* __restrict__ ph_prob_log,
+    float* __restrict__ ph_frame_pred, float* __restrict__ prob_log, float* __restrict__ edge_log,
+    float* __restrict__ not_edge_log, float* __restrict__ edge_diff, double* __restrict__ edge_prob_out) {
+    __shared__ unsigned char allowed[kMaxV];
+    __shared__ float lsm[kProThreads / 64][kMaxV];
+    const int b = blockIdx.y;
+    const int T = Tv[b];
+    const int S = Sv[b];
+    const int32_t* ids = ph_seq_id + (size_t)b * Smax;
+    for (int v = threadIdx.x; v < V; v += kProThreads) allowed[v] = (v == 0);
+    __syncthreads();
+    for (int s = threadIdx.x; s < S; s += kProThreads) {
+        const int v = ids[s];
+        if (v >= 0 && v < V) allowed[v] = 1;
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t = blockIdx.x * (kProThreads / 64) + w;
+    if (t >= T) return;
+    const float* xr = frame_logits + b * f_bs + t * f_ld;
+    float m = neg_inf();
+    for (int v = lane; v < V; v += 64) {
+        const float x = xr[v] - (allowed[v] ? 0.0f : 1e9f);
+        lsm[w][v] = x;
+        m = fmaxf(m, x);
+    }
+    m = hfa::wave_max(m);
+    float sum = 0.0f;
+    for (int v = lane; v < V; v += 64) sum += expf(lsm[w][v] - m);
+    sum = hfa::wave_sum(sum);
+    const float lse = logf(sum);
+    const float inv = 1.0f / sum;
+    for (int v = lane; v < V; v += 64) {
+        const float xm = lsm[w][v] - m;
+        const float lp = xm - lse;
+        if (ph_prob_log) ph_prob_log[((size_t)b * Tmax + t) * V + v] = lp;
+        if (ph_frame_pred) ph_frame_pred[((size_t)b * Tmax + t) * V + v] = expf(xm) * inv;
+        lsm[w][v] = lp;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int s = lane; s < S; s += 64) {
+        const int v = ids[s];
+        prob_log[((size_t)b * Tmax + t) * Smax + s] = lsm[w][v];
+    }
+    if (lane == 0) {
+        const float* er = edge_logits + b * e_bs;
+        auto edge_pred = [&](int tt) {
+            const float x = er[tt * e_ld];
+            const float sg = 1.0f / (1.0f + expf(-x));
+            return fminf(fmaxf((sg - 0.1f) / 0.8f, 0.0f), 1.0f);
+        };
+        const float e = edge_pred(t);
+        const float en = (t + 1 < T) ? edge_pred(t + 1) : 0.0f;
+        const float ep = (t > 0) ? edge_pred(t - 1) : 0.0f;
+        edge_diff[(size_t)b * Tmax + t] = (t + 1 < T) ? (en - e) : 0.0f;
+        double pr = (double)e + (double)ep;
+        pr = pr < 0.0 ? 0.0 : (pr > 1.0 ? 1.0 : pr);
+        if (edge_prob_out) edge_prob_out[(size_t)b * Tmax + t] = pr;
+        edge_log[(size_t)b * Tmax + t] = (float)log(pr + 1e-6);
+        not_edge_log[(size_t)b * Tmax + t] = (float)log(1.0 - pr + 1e-6);
+    }
+}
+
+template <int K>
+int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const int32_t* pad,
+                   const float* prob_log, const float* nE, const float* E, double* curr, float* dp, int8_t* bt,
+                   const int32_t* ids, hipStream_t st) {
+    hipLaunchKernelGGL(viterbi_forward_kernel<K>, dim3(B), dim3(64), 0, st, Tmax, Smax, T, S, pad, prob_log, nE,
+                       E, curr, dp, bt, ids);
+    return hfa::check_launch("hfa_viterbi_forward");
+}
+
+}  // namespace
+
+extern "C" {
+
+int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S,
+                        const int32_t* prob3_pad_len, const float* prob_log, const float* not_edge_log,
+                        const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,
+                        hipStream_t stream) {
+    if (B < 0 || Tmax < 0 || Smax < 0 || (B > 0 && (!T || !S || !prob_log || !not_edge_log || !edge_log ||
+                                                     !curr || !dp || !bt || !ph_seq_id))) {
+        hfa::set_error("hfa_viterbi_forward: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (B == 0 || Tmax == 0 || Smax == 0) return HFA_OK;
+    const int per_lane = (Smax + 63) / 64;
+    if (per_lane <= 1) return launch_forward<1>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
+                                                edge_log, curr, dp, bt, ph_seq_id, stream);
+    if (per_lane <= 2) return launch_forward<2>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
+                                                edge_log, curr, dp, bt, ph_seq_id, stream);
+    if (per_lane <= 4) return launch_forward<4>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
+                                                edge_log, curr, dp, bt, ph_seq_id, stream);
+    if (per_lane <= 8) return launch_forward<8>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
+                                                edge_log, curr, dp, bt, ph_seq_id, stream);
+    if (per_lane <= 16) return launch_forward<16>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
+                                                  edge_log, curr, dp, bt, ph_seq_id, stream);
+    if (per_lane <= 32) return launch_forward<32>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
+                                                  edge_log, curr, dp, bt, ph_seq_id, stream);
+    hfa::set_error("hfa_viterbi_forward: Smax=%d exceeds 2048 states per utterance", Smax);
+    return HFA_EINVAL;
+}
+
+int hfa_viterbi_backtrack(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const float* dp,
+                          const int8_t* bt, const int32_t* ph_seq_id, int32_t* ph_idx_seq, int32_t* ph_time_int,
+                          int32_t* n_out, float* frame_conf, hipStream_t stream) {
+    if (B < 0 || Tmax < 0 || Smax < 0 || Smax > 32767 || Tmax > 65536) {
+        hfa::set_error("hfa_viterbi_backtrack: bad sizes (Smax<=32767, Tmax<=65536)");
+        return HFA_EINVAL;
+    }
+    if (B == 0) return HFA_OK;
+    if (!T || !S || !dp || !bt || !ph_seq_id || !ph_idx_seq || !ph_time_int || !n_out || !frame_conf) {
+        hfa::set_error("hfa_viterbi_backtrack: null pointer");
+        return HFA_EINVAL;
+    }
+    const size_t lds = kBtChunkBytes + sizeof(uint16_t) * (size_t)(Tmax > 0 ? Tmax : 1);
+    if (lds > 65536) {
+        hipError_t e = hipFuncSetAttribute((const void*)viterbi_backtrack_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) {
+            hfa::set_error("hfa_viterbi_backtrack: cannot reserve %zu B of LDS: %s", lds, hipGetErrorString(e));
+            return -(int)e;
+        }
+    }
+    hipLaunchKernelGGL(viterbi_backtrack_kernel, dim3(B), dim3(kBtThreads), lds, stream, Tmax, Smax, T, S, dp, bt,
+                       ph_seq_id, ph_idx_seq, ph_time_int, n_out, frame_conf);
+    return hfa::check_launch("hfa_viterbi_backtrack");
+}
+
+int hfa_lattice_prologue(int B, int Tmax, int V, int Smax, const int32_t* T, const int32_t* S,
+                         const float* frame_logits, long long frame_ld, long long frame_bs,
+                         const float* edge_logits, long long edge_ld, long long edge_bs, const int32_t* ph_seq_id,
+                         float* ph_prob_log, float* ph_frame_pred, float* prob_log, float* edge_log,
+                         float* not_edge_log, float* edge_diff, double* edge_prob, hipStream_t stream) {
+    if (B < 0 || Tmax < 0 || V <= 0 || V > kMaxV || Smax < 0) {
+        hfa::set_error("hfa_lattice_prologue: bad sizes (0 < V <= %d)", kMaxV);
+        return HFA_EINVAL;
+    }
+    if (B == 0 || Tmax == 0) return HFA_OK;
+    if (!T || !S || !frame_logits || !edge_logits || !ph_seq_id || !prob_log || !edge_log || !not_edge_log ||
+        !edge_diff) {
+        hfa::set_error("hfa_lattice_prologue: null pointer");
+        return HFA_EINVAL;
+    }
+    dim3 grid((Tmax + kProThreads / 64 - 1) / (kProThreads / 64), B);
+    hipLaunchKernelGGL(lattice_prologue_kernel, grid, dim3(kProThreads), 0, stream, Tmax, V, Smax, T, S,
+                       frame_logits, frame_ld, frame_bs, edge_logits, edge_ld, edge_bs, ph_seq_id, ph_prob_log,
+                       ph_frame_pred, prob_log, edge_log, not_edge_log, edge_diff, edge_prob);
+    return hfa::check_launch("hfa_lattice_prologue");
+}
+
+}  // extern "C"

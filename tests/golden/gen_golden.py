@@ -1,0 +1,378 @@
+"""Generate the golden parity fixtures by importing the reference in THIS container (never on the GPU box).
+
+Run:  python tests/golden/gen_golden.py        (needs /root/reference; skips itself otherwise)
+
+The reference is pure Python.  ``numba`` is absent here, so ``numba.jit`` is stubbed as the
+identity: numba's scalar typing equals numpy's for this code (f32+f32->f32, f32+f64->f64) and numba performs no
+FMA contraction without fastmath, so the pure-Python execution is the reference's arithmetic.
+
+Everything written is DATA (inputs + expected outputs) under tests/golden/.  No reference source is copied.
+Weights come from ``hubertfa_amd.synth`` (numpy PCG64) so the GPU box can regenerate them bit-identically.
+
+Reference call sites exercised:
+  * tools/alignment_decoder.py:170-230  AlignmentDecoder.forward_pass   -> dp_cases.npz (dp, bt, curr)
+  * tools/alignment_decoder.py:232-294  AlignmentDecoder._decode        -> dp_cases.npz (path, confidence)
+  * tools/alignment_decoder.py:26-143   AlignmentDecoder.decode         -> decode_cases.npz
+  * networks/g2p/*.py                   G2P plugins                     -> g2p.json
+  * tools/post_processing.py:68-105     post_processing                 -> postproc.json
+  * tools/encoder.py:56-59              grid gather index (torch expr)  -> gather_index.npz
+  * networks/hubert/model.py            HubertSoft.units                -> hubert_soft.npz
+  * transformers HubertModel            cnhubert base / large(reduced)  -> hubert_hf_base.npz / hubert_hf_large.npz
+  * networks/layer/backbone/unet.py + head (forced_alignment.py:53-55,284-292) -> unet_head.npz
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+import warnings
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+from hubertfa_amd import synth  # noqa: E402
+
+
+def _import_reference():
+    stub = types.ModuleType("numba")
+    stub.jit = lambda f=None, **kw: f if f is not None else (lambda g: g)
+    sys.modules.setdefault("numba", stub)
+    sys.path.insert(0, REF)
+
+
+def _phone_seq_ids(r, n_inner: int, V: int, mode: str) -> np.ndarray:
+    """A G2P-shaped ph_seq_id: SP(0) framed, phones 1..V-1, SP between words (dictionary_g2p.py:37-39)."""
+    if mode == "g2p":
+        ids = [0]
+        while len(ids) < n_inner - 1:
+            for _ in range(int(r.integers(1, 3))):
+                ids.append(int(r.integers(1, V)))
+            ids.append(0)
+        ids = (ids + [0] * n_inner)[:n_inner]
+        if n_inner >= 2:
+            ids[-1] = 0
+        return np.array(ids, dtype=np.int64)
+    if mode == "no_sp_start":   # ph_seq_id[0] != 0
+        ids = r.integers(1, V, n_inner)
+        return ids.astype(np.int64)
+    if mode == "double_zero":   # AP/SP both map to id 0 -> consecutive id-0 states
+        ids = list(r.integers(0, V, n_inner))
+        for i in range(0, n_inner - 1, 5):
+            ids[i] = 0
+            ids[i + 1] = 0
+        return np.array(ids, dtype=np.int64)
+    if mode == "random":
+        return r.integers(0, V, n_inner).astype(np.int64)
+    raise ValueError(mode)
+
+
+def gen_dp_cases():
+    from tools.alignment_decoder import AlignmentDecoder
+    import torch
+
+    V = 63
+    dec = AlignmentDecoder({"vocab": {}, "vocab_size": V}, {"hop_length": 512, "sample_rate": 44100})
+    r = synth.rng(1234)
+    specs = []
+    for T in (1, 2, 5, 64, 430, 861):
+        for S in (1, 2, 3, 31, 91, 256):
+            if T * S > 861 * 91 * 1.2 and not (T == 861 and S == 256):
+                continue
+            specs.append((T, S, "g2p", "normal"))
+    specs += [(200, 31, "no_sp_start", "normal"), (300, 46, "double_zero", "normal"),
+              (300, 46, "random", "normal"), (120, 31, "g2p", "const"), (64, 31, "g2p", "const_edge"),
+              (20, 31, "g2p", "normal"), (30, 91, "g2p", "normal"),  # T < S: infeasible, -inf path
+              (861, 91, "g2p", "normal"), (861, 91, "double_zero", "normal"), (430, 46, "g2p", "normal")]
+    out = {"n": len(specs)}
+    for ci, (T, S, mode, lat) in enumerate(specs):
+        ids = _phone_seq_ids(r, S, V, mode)
+        if lat == "const":
+            logits = np.zeros((T, V), np.float32)
+        else:
+            logits = (3.0 * r.standard_normal((T, V))).astype(np.float32)
+        ph_prob_log = torch.log_softmax(torch.from_numpy(logits), -1).numpy().astype(np.float32)
+        if lat == "const_edge":
+            edge_prob = np.full(T, 0.5, np.float32)
+        else:
+            e = r.uniform(-0.2, 1.2, T).astype(np.float32)
+            edge_prob = np.clip(e, 0, 1).astype(np.float32)
+        # forward_pass inputs exactly as _decode builds them (alignment_decoder.py:239-257)
+        prob_log = ph_prob_log[:, ids]
+        E = np.log(edge_prob + 1e-6).astype("float32")
+        nE = np.log(1 - edge_prob + 1e-6).astype("float32")
+        curr = np.full(S, -np.inf)
+        dp = np.full((T, S), -np.inf, dtype="float32")
+        bt = np.full_like(dp, -1, dtype="int32")
+        dp[0, 0] = prob_log[0, 0]
+        curr[0] = prob_log[0, 0]
+        if ids[0] == 0 and prob_log.shape[-1] > 1:
+            dp[0, 1] = prob_log[0, 1]
+            curr[1] = prob_log[0, 1]
+        pad = 2 if S >= 2 else 1
+        dp, bt, curr = AlignmentDecoder.forward_pass(T, S, prob_log, nE, E, curr, dp, bt, ids, pad)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            idx, tint, fconf = dec._decode(ids, ph_prob_log, edge_prob)
+        p = f"c{ci}_"
+        out[p + "ids"] = ids.astype(np.int32)
+        out[p + "ph_prob_log"] = ph_prob_log
+        out[p + "edge_prob"] = edge_prob
+        out[p + "dp"] = dp
+        out[p + "bt"] = bt.astype(np.int8)
+        out[p + "curr"] = curr
+        out[p + "ph_idx_seq"] = idx.astype(np.int32)
+        out[p + "ph_time_int"] = tint.astype(np.int32)
+        out[p + "frame_confidence"] = fconf.astype(np.float32)
+        print(f"dp case {ci}: T={T} S={S} {mode}/{lat} n_ph={len(idx)}")
+    np.savez_compressed(os.path.join(HERE, "dp_cases.npz"), **out)
+
+
+def gen_decode_cases():
+    from tools.alignment_decoder import AlignmentDecoder
+    import torch
+
+    vocab = synth.synth_vocab()
+    dic = synth.synth_dictionary()
+    V = vocab["vocab_size"]
+    dec = AlignmentDecoder(vocab, {"hop_length": 512, "sample_rate": 44100})
+    r = synth.rng(99)
+    cases = []
+    arrays = {}
+    for ci, (n_words, secs, wl_mode) in enumerate(
+            [(15, 5.0, "exact"), (30, 10.0, "exact"), (4, 1.3, "exact"), (8, 2.0, "none"), (12, 3.1, "short")]):
+        lab = synth.synth_lab(n_words, dic, seed=100 + ci)
+        ph_seq, word_seq, p2w = ["SP"], [], [-1]
+        for w in lab.split(" "):
+            word_seq.append(w)
+            for ph in dic[w]:
+                ph_seq.append(ph)
+                p2w.append(len(word_seq) - 1)
+            ph_seq.append("SP")
+            p2w.append(-1)
+        if ci == 2:  # an AP (id 0) inside the sequence
+            ph_seq.insert(3, "AP")
+            p2w.insert(3, -1)
+        n44 = int(round(secs * 44100))
+        n_frames = n44 // 512 + 1
+        logits = (3.0 * r.standard_normal((1, n_frames, V + 2))).astype(np.float32)
+        lt = torch.from_numpy(logits)
+        frame, edge, ctc = lt[:, :, 2:], lt[:, :, 0], torch.cat([lt[:, :, [1]], lt[:, :, 3:]], dim=-1)
+        wav_length = n44 / 44100 if wl_mode == "exact" else (None if wl_mode == "none" else n44 / 44100 - 0.05)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            res = dec.decode(frame, edge, ctc, wav_length, ph_seq, word_seq, p2w)
+        ph_pred, ph_int, w_pred, w_int, conf = res
+        arrays[f"c{ci}_logits"] = logits
+        arrays[f"c{ci}_ph_intervals"] = np.asarray(ph_int, np.float64)
+        arrays[f"c{ci}_word_intervals"] = np.asarray(w_int, np.float64)
+        arrays[f"c{ci}_ph_idx_seq"] = dec.ph_idx_seq.astype(np.int32)
+        arrays[f"c{ci}_ph_time_int"] = dec.ph_time_int_pred.astype(np.int32)
+        arrays[f"c{ci}_frame_confidence"] = dec.frame_confidence.astype(np.float32)
+        arrays[f"c{ci}_edge_prob"] = dec.edge_prob.astype(np.float32)
+        cases.append({"ph_seq": ph_seq, "word_seq": word_seq, "ph_idx_to_word_idx": p2w,
+                      "wav_length": wav_length, "ph_seq_pred": [str(x) for x in ph_pred],
+                      "word_seq_pred": [str(x) for x in w_pred], "total_confidence": float(conf)})
+        print(f"decode case {ci}: S={len(ph_seq)} T={n_frames} conf={conf:.4f}")
+    np.savez_compressed(os.path.join(HERE, "decode_cases.npz"), **arrays)
+    with open(os.path.join(HERE, "decode_cases.json"), "w") as f:
+        json.dump({"vocab": vocab, "cases": cases}, f, indent=1)
+
+
+def gen_g2p():
+    from networks.g2p import DictionaryG2P, NoneG2P, PhonemeG2P
+
+    dic = synth.synth_dictionary(n_words=40)
+    dpath = os.path.join(HERE, "synth_dict.txt")
+    with open(dpath, "w") as f:
+        for w, phs in dic.items():
+            f.write(f"{w}\t{' '.join(phs)}\n")
+    g_dict = DictionaryG2P(dictionary=dpath)
+    g_none, g_ph = NoneG2P(), PhonemeG2P()
+    texts = ["w000 w001 w002", "w003  w004", "w005 oov_word w006", "w007", "w010 w011 w012 w013 w014 w015"]
+    ph_texts = ["a b c", "SP a SP SP b", "a b SP", "x"]
+    res = {"dictionary": "synth_dict.txt", "dict": [], "none": [], "phoneme": []}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for t in texts:
+            try:
+                ph, w, m = g_dict(t)
+                res["dict"].append({"text": t, "ph_seq": ph, "word_seq": w, "map": [int(x) for x in m]})
+            except Exception as e:  # noqa: BLE001
+                res["dict"].append({"text": t, "error": type(e).__name__})
+        for t in ph_texts:
+            for name, g in (("none", g_none), ("phoneme", g_ph)):
+                try:
+                    ph, w, m = g(t)
+                    res[name].append({"text": t, "ph_seq": list(ph), "word_seq": list(w),
+                                      "map": [int(x) for x in m]})
+                except Exception as e:  # noqa: BLE001
+                    res[name].append({"text": t, "error": type(e).__name__})
+    with open(os.path.join(HERE, "g2p.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print("g2p done")
+
+
+def gen_postproc():
+    from tools.post_processing import post_processing
+
+    r = synth.rng(5)
+    cases = []
+    # hand-made AP/SP gap cases + random jittered ones
+    base = [
+        (["a", "b", "c"], [[0.05, 0.5], [0.55, 1.0], [1.35, 2.0]], 2.05),
+        (["AP", "b", "AP", "AP"], [[0.2, 0.5], [0.6, 1.0], [1.1, 1.4], [1.5, 1.9]], 2.0),
+        (["a", "AP", "c"], [[0.0, 0.5], [0.58, 1.0], [1.2, 2.0]], 2.5),
+        (["a"], [[0.3, 0.9]], 1.0),
+        (["a", "b"], [[0.0, 0.5], [0.5, 1.0]], 1.0),
+    ]
+    for _ in range(6):
+        n = int(r.integers(2, 9))
+        edges = np.sort(r.uniform(0, 3.0, 2 * n))
+        seq = [("AP" if r.uniform() < 0.3 else f"x{i}") for i in range(n)]
+        base.append((seq, edges.reshape(n, 2).tolist(), float(edges[-1] + r.uniform(0, 0.3))))
+    preds = []
+    for i, (seq, iv, wl) in enumerate(base):
+        preds.append((f"utt{i}.wav", wl, 0.5, np.array(seq), np.array(iv, np.float64), np.array(seq),
+                      np.array(iv, np.float64)))
+    res, log = post_processing(preds)
+    for (seq, iv, wl), out in zip(base, res):
+        cases.append({"seq": seq, "intervals": iv, "wav_length": wl,
+                      "ph_seq": [str(x) for x in out[3]], "ph_intervals": np.asarray(out[4], float).tolist(),
+                      "word_seq": [str(x) for x in out[5]],
+                      "word_intervals": np.asarray(out[6], float).tolist()})
+    with open(os.path.join(HERE, "postproc.json"), "w") as f:
+        json.dump({"cases": cases, "n_errors": len(log)}, f, indent=1)
+    print("postproc done", len(log), "errors")
+
+
+def gen_gather_index():
+    import torch
+
+    out = {}
+    for secs in (1.0, 5.0, 10.0, 300.0, 0.01):
+        n44 = int(round(secs * 44100))
+        hop_size, sample_rate = 512, 44100
+        units = int(round(secs * 16000)) // 320 - 1  # Hubert frame count (any value: clamp bound)
+        units = max(units, 1)
+        # tools/encoder.py:56-58, executed verbatim as a torch expression
+        n_frames = n44 // hop_size + 1
+        ratio = (hop_size / sample_rate) / (320 / 16000)
+        index = torch.clamp(torch.round(ratio * torch.arange(n_frames)).long(), max=units - 1)
+        out[f"n{n44}_units{units}"] = index.numpy().astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "gather_index.npz"), **out)
+    print("gather done")
+
+
+def _to_torch_sd(sd):
+    import torch
+    return {k: torch.from_numpy(v.copy()) for k, v in sd.items()}
+
+
+def gen_hubert():
+    import torch
+    from transformers import HubertConfig, HubertModel
+    from networks.hubert.model import HubertSoft
+
+    torch.manual_seed(0)
+    wav = synth.synth_audio(16000, seed=3)
+    out = {"wav": wav}
+    # --- HF cnhubert base (12 layers), do_normalize applied on the host like Wav2Vec2FeatureExtractor ---
+    arch = synth.arch_cnhubert_base()
+    sd = synth.synth_hubert_state_dict(arch, seed=11)
+    cfg = HubertConfig()
+    cfg._attn_implementation = "eager"
+    m = HubertModel(cfg).eval()
+    tsd = _to_torch_sd(sd)
+    # HF holds the weight-norm as a parametrization: original0 = g, original1 = v
+    pre = "encoder.pos_conv_embed.conv."
+    tsd[pre + "parametrizations.weight.original0"] = tsd.pop(pre + "weight_g")
+    tsd[pre + "parametrizations.weight.original1"] = tsd.pop(pre + "weight_v")
+    missing, unexpected = m.load_state_dict(tsd, strict=False)
+    assert not unexpected and not [k for k in missing if "masked_spec" not in k], (missing, unexpected)
+    x = torch.from_numpy(wav)[None]
+    xn = (x - x.mean()) / torch.sqrt(x.var(unbiased=False) + 1e-7)
+    with torch.inference_mode():
+        feats = m.feature_extractor(xn)
+        proj = m.feature_projection(feats.transpose(1, 2))
+        hs = m(xn, output_hidden_states=True)
+    out["hf_base_input"] = xn.numpy()[0]
+    out["hf_base_feats"] = feats.numpy()[0]
+    out["hf_base_proj"] = proj.numpy()[0]
+    out["hf_base_layer1"] = hs.hidden_states[1].numpy()[0]
+    out["hf_base_out"] = hs.last_hidden_state.numpy()[0]
+    print("hf base out", hs.last_hidden_state.shape, float(hs.last_hidden_state.std()))
+    np.savez_compressed(os.path.join(HERE, "hubert_hf_base.npz"), **out)
+
+    # --- HF large-style (LN conv, stable LN), reduced to 2 layers to keep the fixture generator fast ---
+    arch = synth.arch_cnhubert_large(layers=2)
+    sd = synth.synth_hubert_state_dict(arch, seed=12)
+    cfg = HubertConfig(hidden_size=1024, num_hidden_layers=2, num_attention_heads=16, intermediate_size=4096,
+                       feat_extract_norm="layer", do_stable_layer_norm=True, conv_bias=True)
+    cfg._attn_implementation = "eager"
+    from transformers import HubertModel as HM
+    m = HM(cfg).eval()
+    tsd = _to_torch_sd(sd)
+    tsd[pre + "parametrizations.weight.original0"] = tsd.pop(pre + "weight_g")
+    tsd[pre + "parametrizations.weight.original1"] = tsd.pop(pre + "weight_v")
+    missing, unexpected = m.load_state_dict(tsd, strict=False)
+    assert not unexpected and not [k for k in missing if "masked_spec" not in k], (missing, unexpected)
+    with torch.inference_mode():
+        y = m(xn).last_hidden_state
+    np.savez_compressed(os.path.join(HERE, "hubert_hf_large.npz"), input=xn.numpy()[0], out=y.numpy()[0])
+    print("hf large out", y.shape, float(y.std()))
+
+    # --- bshall HubertSoft.units (pads 40/40, projects to 256) ---
+    arch = synth.arch_hubertsoft()
+    sd = synth.synth_hubert_state_dict(arch, seed=13)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        hsoft = HubertSoft().eval()
+    missing, unexpected = hsoft.load_state_dict(_to_torch_sd(sd), strict=True)
+    with torch.inference_mode():
+        u = hsoft.units(torch.from_numpy(wav)[None, None])
+    np.savez_compressed(os.path.join(HERE, "hubert_soft.npz"), wav=wav, out=u.numpy()[0])
+    print("hubertsoft out", u.shape, float(u.std()))
+
+
+def gen_unet():
+    import torch
+    from networks.layer.backbone.unet import UNetBackbone
+    from networks.layer.block.resnet_block import ResidualBasicBlock
+    from networks.layer.scaling.stride_conv import DownSampling, UpSampling
+
+    ua = synth.UNetArch()
+    sd = synth.synth_unet_state_dict(ua, seed=21)
+    bb = UNetBackbone(ua.input_dims, ua.output_dims, ua.hidden_dims, ResidualBasicBlock, DownSampling, UpSampling,
+                      ua.factor, ua.times, ua.scaleup).eval()
+    head = torch.nn.Linear(ua.output_dims, ua.vocab_size + 2).eval()
+    bb.load_state_dict({k[len("backbone."):]: torch.from_numpy(v) for k, v in sd.items() if k.startswith("backbone.")})
+    head.load_state_dict({k[len("head."):]: torch.from_numpy(v) for k, v in sd.items() if k.startswith("head.")})
+    out = {}
+    for T in (203, 862):
+        x = synth.rng(31 + T).standard_normal((1, T, ua.input_dims)).astype(np.float32)
+        with torch.inference_mode():
+            h = bb(torch.from_numpy(x))
+            logits = head(h)
+        out[f"T{T}_logits"] = logits.numpy()[0]
+        print("unet", T, logits.shape, float(logits.std()))
+    np.savez_compressed(os.path.join(HERE, "unet_head.npz"), **out)
+
+
+def main():
+    if not os.path.isdir(REF):
+        print("reference absent: fixtures are generated only in the survey/build container; skipping")
+        return
+    _import_reference()
+    which = sys.argv[1:] or ["dp", "decode", "g2p", "postproc", "gather", "hubert", "unet"]
+    for w in which:
+        {"dp": gen_dp_cases, "decode": gen_decode_cases, "g2p": gen_g2p, "postproc": gen_postproc,
+         "gather": gen_gather_index, "hubert": gen_hubert, "unet": gen_unet}[w]()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,137 @@
+"""GPU parity of the alignment decoder kernels against the reference goldens and the C oracle.
+
+Bit-exact bar: dp, backtrack codes, curr_ph_max_prob_log, ph_idx_seq, ph_time_int (integer/index work).
+Tolerances: frame_confidence rtol 2e-6 (expf vs numpy's float32 exp); per-frame log-probs atol 1e-5
+(north star allows 1e-4).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _cases():
+    z = np.load(os.path.join(GOLDEN, "dp_cases.npz"))
+    return z, int(z["n"])
+
+
+def _lattice(z, c):
+    from oracle import decode as od
+    p = f"c{c}_"
+    ids = z[p + "ids"].astype(np.int64)
+    return ids, od.lattice_inputs(ids, z[p + "ph_prob_log"], z[p + "edge_prob"])
+
+
+def test_forward_batched_bit_exact():
+    from hubertfa_amd import ops
+    z, n = _cases()
+    lats = [_lattice(z, c) for c in range(n)]
+    B = n
+    Tmax = max(l[1][4].shape[0] for l in lats)
+    Smax = max(l[1][4].shape[1] for l in lats)
+    pl = np.zeros((B, Tmax, Smax), np.float32)
+    E = np.zeros((B, Tmax), np.float32)
+    nE = np.zeros((B, Tmax), np.float32)
+    cu = np.full((B, Smax), -np.inf)
+    dp = np.full((B, Tmax, Smax), -np.inf, np.float32)
+    ids = np.zeros((B, Smax), np.int32)
+    Ts, Ss = [], []
+    for b, (i, (p, e, ne, c0, d0, _, _)) in enumerate(lats):
+        T, S = d0.shape
+        Ts.append(T); Ss.append(S)
+        pl[b, :T, :S] = p; E[b, :T] = e; nE[b, :T] = ne; cu[b, :S] = c0; dp[b, :T, :S] = d0; ids[b, :S] = i
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(a).to(dev)
+    dp_t, cu_t = t(dp), t(cu)
+    bt_t = torch.full((B, Tmax, Smax), -1, dtype=torch.int8, device=dev)
+    T_t = torch.tensor(Ts, dtype=torch.int32, device=dev)
+    S_t = torch.tensor(Ss, dtype=torch.int32, device=dev)
+    ids_t = t(ids)
+    ops.viterbi_forward(t(pl), t(nE), t(E), cu_t, dp_t, bt_t, ids_t, T_t, S_t)
+    dp_h, bt_h, cu_h = dp_t.cpu().numpy(), bt_t.cpu().numpy(), cu_t.cpu().numpy()
+    for b in range(B):
+        p = f"c{b}_"
+        T, S = Ts[b], Ss[b]
+        assert np.array_equal(dp_h[b, :T, :S].view(np.int32), z[p + "dp"].view(np.int32)), f"dp case {b}"
+        assert np.array_equal(bt_h[b, 1:T, :S], z[p + "bt"][1:]), f"bt case {b}"
+        assert np.array_equal(cu_h[b, :S].view(np.int64), z[p + "curr"].view(np.int64)), f"curr case {b}"
+    # backtrack on the same device buffers
+    idx, tint, nn, fc = ops.viterbi_backtrack(dp_t, bt_t, ids_t, T_t, S_t)
+    idx, tint, nn, fc = idx.cpu().numpy(), tint.cpu().numpy(), nn.cpu().numpy(), fc.cpu().numpy()
+    for b in range(B):
+        p = f"c{b}_"
+        k = nn[b]
+        assert np.array_equal(idx[b, :k], z[p + "ph_idx_seq"]), f"ph_idx_seq case {b}"
+        assert np.array_equal(tint[b, :k], z[p + "ph_time_int"]), f"ph_time_int case {b}"
+        np.testing.assert_allclose(fc[b, :Ts[b]], z[p + "frame_confidence"], rtol=2e-6, atol=0, equal_nan=True)
+
+
+def test_reference_api_forward_pass_and_decode():
+    from hubertfa_amd.alignment_decoder import AlignmentDecoder
+    z, n = _cases()
+    dec = AlignmentDecoder({"vocab": {}, "vocab_size": 63}, {"hop_length": 512, "sample_rate": 44100})
+    for c in (0, 7, 28, 33, 35, 36, 38, 40, 42):
+        ids, (p, e, ne, c0, d0, b0, pad) = _lattice(z, c)
+        T, S = d0.shape
+        d, b, cu = AlignmentDecoder.forward_pass(T, S, p, ne, e, c0, d0, b0, ids, pad)
+        pre = f"c{c}_"
+        assert np.array_equal(d.view(np.int32), z[pre + "dp"].view(np.int32))
+        assert np.array_equal(b, z[pre + "bt"].astype(np.int32))
+        idx, tint, fc = dec._decode(ids, z[pre + "ph_prob_log"], z[pre + "edge_prob"])
+        assert np.array_equal(idx, z[pre + "ph_idx_seq"]) and np.array_equal(tint, z[pre + "ph_time_int"])
+
+
+def test_prologue_logprobs_within_tolerance():
+    from hubertfa_amd import ops
+    meta = json.load(open(os.path.join(GOLDEN, "decode_cases.json")))
+    zz = np.load(os.path.join(GOLDEN, "decode_cases.npz"))
+    vocab = meta["vocab"]
+    for ci, case in enumerate(meta["cases"]):
+        logits = zz[f"c{ci}_logits"]
+        lt = torch.from_numpy(logits)
+        ids = np.array([vocab["vocab"][p] for p in case["ph_seq"]], np.int32)
+        mask = np.zeros(vocab["vocab_size"]); mask[ids] = 1; mask[0] = 1
+        x = lt[:, :, 2:].float() - (torch.from_numpy(mask)[None, None].logical_not() * 1e9).float()
+        ref_lp = torch.log_softmax(x, -1)[0].numpy()
+        ref_sm = torch.softmax(x, -1)[0].numpy()
+        dev = torch.device("cuda")
+        lg = lt.to(dev)
+        T = logits.shape[1]
+        out = ops.lattice_prologue(lg[:, :, 2:], lg[:, :, 0], torch.from_numpy(ids)[None].to(dev),
+                                   torch.tensor([T], dtype=torch.int32, device=dev),
+                                   torch.tensor([len(ids)], dtype=torch.int32, device=dev), want_frame_probs=True)
+        lp = out["ph_prob_log"][0].cpu().numpy()
+        allowed = np.zeros(vocab["vocab_size"], bool); allowed[ids] = True; allowed[0] = True
+        np.testing.assert_allclose(lp[:, allowed], ref_lp[:, allowed], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(out["ph_frame_pred"][0].cpu().numpy(), ref_sm, atol=1e-6, rtol=0)
+        np.testing.assert_allclose(out["prob_log"][0].cpu().numpy(), ref_lp[:, ids], atol=1e-5, rtol=0)
+        e = ((torch.sigmoid(lt[:, :, 0]) - 0.1) / 0.8).clamp(0, 1)[0].numpy()
+        ep = (e + np.concatenate(([0], e[:-1]))).clip(0, 1)
+        np.testing.assert_allclose(out["edge_prob"][0].cpu().numpy(), ep, atol=1e-6, rtol=0)
+        np.testing.assert_allclose(out["edge_log"][0].cpu().numpy(), np.log(ep + 1e-6).astype(np.float32),
+                                   atol=2e-4, rtol=1e-5)
+
+
+def test_decode_end_to_end_matches_reference():
+    from hubertfa_amd.alignment_decoder import AlignmentDecoder
+    meta = json.load(open(os.path.join(GOLDEN, "decode_cases.json")))
+    zz = np.load(os.path.join(GOLDEN, "decode_cases.npz"))
+    dec = AlignmentDecoder(meta["vocab"], {"hop_length": 512, "sample_rate": 44100})
+    for ci, case in enumerate(meta["cases"]):
+        lt = torch.from_numpy(zz[f"c{ci}_logits"]).cuda()
+        ph, ph_iv, w, w_iv, conf = dec.decode(lt[:, :, 2:], lt[:, :, 0], torch.cat([lt[:, :, [1]], lt[:, :, 3:]], -1),
+                                              case["wav_length"], case["ph_seq"], case["word_seq"],
+                                              case["ph_idx_to_word_idx"])
+        assert list(ph) == case["ph_seq_pred"], ci
+        assert list(w) == case["word_seq_pred"], ci
+        assert np.array_equal(dec.ph_idx_seq, zz[f"c{ci}_ph_idx_seq"]), ci
+        assert np.array_equal(dec.ph_time_int_pred, zz[f"c{ci}_ph_time_int"]), ci
+        np.testing.assert_allclose(ph_iv, zz[f"c{ci}_ph_intervals"], atol=1e-6)
+        np.testing.assert_allclose(w_iv, zz[f"c{ci}_word_intervals"], atol=1e-6)
+        np.testing.assert_allclose(conf, case["total_confidence"], rtol=1e-4)
