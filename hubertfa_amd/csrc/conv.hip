@@ -1,0 +1,172 @@
+// conv.hip — the first layer of the Hubert CNN feature extractor (C_in = 1, k = 10, stride 5, 512 channels).
+//
+// Replaces FeatureExtractor conv0 + GroupNorm(512, 512) + GELU (networks/hubert/model.py:98-99,108; HF
+// HubertGroupNormConvLayer) and, for the LN-conv (large) variant, the raw conv0 (+bias) that feeds a
+// LayerNorm+GELU (HF HubertLayerNormConvLayer).  conv1..6 are dense contractions and go through the MFMA
+// implicit GEMM (gemm.hip).
+//
+// conv0 does 10 MACs per output and writes 512 f32 channels per output frame (~65 MB per 10 s utterance):
+// it is HBM-store bound.  GroupNorm(512, 512) normalises each channel over ALL T, so the statistics need a
+// full pass before any output can be written.  Recomputing conv0 (10 FMAs) is far cheaper than writing and
+// re-reading 65 MB, so:
+//   pass 1 (stats):  conv0 on the fly, per-chunk per-channel f64 sum / sum-of-squares partials (no output);
+//   pass 2 (reduce): mean / rstd per (batch, channel);
+//   pass 3 (apply):  conv0 again (bit-identical explicit fmaf chain), normalise, GELU, one coalesced
+//                    channels-last store [B, T0, 512] that conv1's implicit GEMM reads directly.
+#include "hfa_common.h"
+
+namespace {
+
+constexpr int C0 = 512;        // channels
+constexpr int KW = 10;         // kernel width
+constexpr int ST = 5;          // stride
+constexpr int CH = 256;        // output frames per chunk
+constexpr int NT = 256;        // threads: 2 channels per thread
+
+__device__ __forceinline__ float conv10(const float* w, const float* xs) {
+    float v = 0.0f;
+#pragma unroll
+    for (int j = 0; j < KW; ++j) v = fmaf(w[j], xs[j], v);
+    return v;
+}
+
+__device__ __forceinline__ void stage_chunk(float* xs, const float* xb, int t0, int nt, int N) {
+    const int n = nt * ST + (KW - ST);
+    for (int i = threadIdx.x; i < n; i += NT) {
+        const int idx = t0 * ST + i;
+        xs[i] = idx < N ? xb[idx] : 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(NT) void conv0_stats_kernel(int N, int T0, const float* __restrict__ x, long long x_bs,
+                                                         const float* __restrict__ w0, double* __restrict__ part) {
+    __shared__ float xs[CH * ST + KW];
+    const int b = blockIdx.y, chunk = blockIdx.x;
+    const int t0 = chunk * CH;
+    const int nt = min(CH, T0 - t0);
+    stage_chunk(xs, x + b * x_bs, t0, nt, N);
+    const int c0 = threadIdx.x * 2;
+    float wa[KW], wb[KW];
+#pragma unroll
+    for (int j = 0; j < KW; ++j) {
+        wa[j] = w0[c0 * KW + j];
+        wb[j] = w0[(c0 + 1) * KW + j];
+    }
+    __syncthreads();
+    double sa = 0.0, qa = 0.0, sb = 0.0, qb = 0.0;
+    for (int t = 0; t < nt; ++t) {
+        const float va = conv10(wa, xs + t * ST);
+        const float vb = conv10(wb, xs + t * ST);
+        sa += va; qa += (double)va * va;
+        sb += vb; qb += (double)vb * vb;
+    }
+    double* pp = part + ((size_t)(b * gridDim.x + chunk) * C0 + c0) * 2;
+    pp[0] = sa; pp[1] = qa; pp[2] = sb; pp[3] = qb;
+}
+
+__global__ __launch_bounds__(NT) void conv0_reduce_kernel(int T0, int nchunk, const double* __restrict__ part,
+                                                          float eps, float* __restrict__ stats) {
+    const int b = blockIdx.x;
+    for (int c = threadIdx.x; c < C0; c += NT) {
+        double s = 0.0, q = 0.0;
+        for (int k = 0; k < nchunk; ++k) {
+            const double* pp = part + ((size_t)(b * nchunk + k) * C0 + c) * 2;
+            s += pp[0];
+            q += pp[1];
+        }
+        const double mean = s / T0;
+        double var = q / T0 - mean * mean;
+        if (var < 0) var = 0;
+        stats[(b * C0 + c) * 2] = (float)mean;
+        stats[(b * C0 + c) * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+    }
+}
+
+// mode 0: GroupNorm(stats) + affine + GELU; mode 1: + bias, no norm, no act (LN variant feeds a LayerNorm)
+template <int MODE>
+__global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const float* __restrict__ x, long long x_bs,
+                                                         const float* __restrict__ w0, const float* __restrict__ stats,
+                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                         const float* __restrict__ bias, float* __restrict__ y,
+                                                         long long y_bs) {
+    __shared__ float xs[CH * ST + KW];
+    const int b = blockIdx.y, chunk = blockIdx.x;
+    const int t0 = chunk * CH;
+    const int nt = min(CH, T0 - t0);
+    stage_chunk(xs, x + b * x_bs, t0, nt, N);
+    const int c0 = threadIdx.x * 2;
+    float wa[KW], wb[KW];
+#pragma unroll
+    for (int j = 0; j < KW; ++j) {
+        wa[j] = w0[c0 * KW + j];
+        wb[j] = w0[(c0 + 1) * KW + j];
+    }
+    float sa = 1.f, ha = 0.f, sb = 1.f, hb = 0.f;
+    float ma = 0.f, ra = 1.f, mb = 0.f, rb = 1.f;
+    if (MODE == 0) {
+        ma = stats[(b * C0 + c0) * 2]; ra = stats[(b * C0 + c0) * 2 + 1];
+        mb = stats[(b * C0 + c0 + 1) * 2]; rb = stats[(b * C0 + c0 + 1) * 2 + 1];
+        sa = gamma[c0]; ha = beta[c0]; sb = gamma[c0 + 1]; hb = beta[c0 + 1];
+    } else {
+        ha = bias ? bias[c0] : 0.f;
+        hb = bias ? bias[c0 + 1] : 0.f;
+    }
+    __syncthreads();
+    float* yb = y + b * y_bs + (long long)t0 * C0 + c0;
+    for (int t = 0; t < nt; ++t) {
+        float va = conv10(wa, xs + t * ST);
+        float vb = conv10(wb, xs + t * ST);
+        if (MODE == 0) {
+            va = hfa::gelu_erf((va - ma) * ra * sa + ha);
+            vb = hfa::gelu_erf((vb - mb) * rb * sb + hb);
+        } else {
+            va += ha;
+            vb += hb;
+        }
+        *reinterpret_cast<float2*>(yb + (long long)t * C0) = make_float2(va, vb);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+long long hfa_conv0_workspace_bytes(int B, int N) {
+    const int T0 = N >= KW ? (N - KW) / ST + 1 : 0;
+    const int nchunk = (T0 + CH - 1) / CH;
+    return (long long)B * nchunk * C0 * 2 * sizeof(double) + (long long)B * C0 * 2 * sizeof(float) + 64;
+}
+
+// x [B, N] (row stride x_bs) -> y [B, T0, 512] channels-last (row stride 512, batch stride y_bs).
+// norm = 1: GroupNorm(512,512)+GELU (gamma/beta required, workspace of hfa_conv0_workspace_bytes);
+// norm = 0: raw conv + bias (bias may be NULL).
+int hfa_conv0_f32(int B, int N, const float* x, long long x_bs, const float* w0, const float* bias, int norm,
+                  const float* gamma, const float* beta, float eps, void* workspace, float* y, long long y_bs,
+                  hipStream_t stream) {
+    if (B < 0 || N < KW) {
+        hfa::set_error("hfa_conv0_f32: need N >= %d samples (got %d)", KW, N);
+        return HFA_EINVAL;
+    }
+    if (B == 0) return HFA_OK;
+    if (!x || !w0 || !y || (norm && (!gamma || !beta || !workspace)) || ((uintptr_t)y & 7) || y_bs % 2) {
+        hfa::set_error("hfa_conv0_f32: bad pointer arguments");
+        return HFA_EINVAL;
+    }
+    const int T0 = (N - KW) / ST + 1;
+    const int nchunk = (T0 + CH - 1) / CH;
+    dim3 grid(nchunk, B);
+    if (norm) {
+        double* part = reinterpret_cast<double*>(workspace);
+        float* stats = reinterpret_cast<float*>(part + (size_t)B * nchunk * C0 * 2);
+        hipLaunchKernelGGL(conv0_stats_kernel, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, part);
+        hipLaunchKernelGGL(conv0_reduce_kernel, dim3(B), dim3(NT), 0, stream, T0, nchunk, part, eps, stats);
+        hipLaunchKernelGGL(conv0_apply_kernel<0>, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats, gamma, beta,
+                           bias, y, y_bs);
+    } else {
+        hipLaunchKernelGGL(conv0_apply_kernel<1>, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, nullptr, nullptr,
+                           nullptr, bias, y, y_bs);
+    }
+    return hfa::check_launch("hfa_conv0_f32");
+}
+
+}  // extern "C"

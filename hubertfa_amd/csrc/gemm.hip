@@ -1,0 +1,226 @@
+// gemm.hip — f32 MFMA implicit-GEMM (v_mfma_f32_32x32x2_f32) with fused epilogues, for every dense
+// contraction on the path:
+//   * nn.Linear / addmm: feature projection, QKV, out-proj, FFN (networks/hubert/model.py:27-33,122;
+//     transformers HubertAttention/HubertFeedForward), UNet shortcut + head (resnet_block.py:164-168,
+//     forced_alignment.py:53-55)
+//   * conv1d as implicit GEMM over a [T, C] (channels-last) activation: extractor conv1..6 (model.py:100-114),
+//     grouped positional conv k128/pad64/g16 (model.py:135-147), UNet k3 convs / k2 stride-2 down-sampling /
+//     k2 stride-2 transposed up-sampling (resnet_block.py:145-162, stride_conv.py:23-47)
+//   * the polyphase sinc resampler (torchaudio Resample: tools/load_wav.py:7, tools/encoder.py:46-48) as a
+//     GEMM over overlapping frames of the padded wave.
+//
+//   C[z](m, n) = epi( sum_k A[z](m, k) * W[z](n, k) + bias[n] ) + R[z](m, n)
+//   A[z](m, k): k = j*Cg + c,  t = m*stride + j - pad,  A(m,k) = (0 <= t < Tin) ? X[zb*sAb + zg*sAg + t*ldx + c] : 0
+//   z = zb*G + zg (batch x group), W[z] = W + zg*sWg (row n at n*ldw, K-contiguous = [Cout][k][Cin] im2col order)
+//
+// f32-in MFMA is bit-for-bit an fmaf chain (exact f32, no TF32 on gfx950), so this is the fp32 parity path.
+// Tile 128x128x16, 256 threads = 4 waves (2x2), each wave 64x64 = 2x2 MFMA 32x32 tiles, register-staged
+// double-buffered LDS with rows padded to 20 floats (ds_read_b128 conflict-free: row r -> bank 4*(5r mod 16)).
+// A lane's ds_read_b128 brings 4 consecutive k of its row; the 4 MFMAs of a k-octet consume one element each,
+// with the same permutation on the W side, so every k is summed exactly once.
+// Block ids are remapped so consecutive logical tiles (same A rows, adjacent W columns) share an XCD's L2.
+#include "hfa_common.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 128, BN = 128, BK = 16, LDL = BK + 4;
+constexpr int NT = 256;
+
+struct GemmP {
+    int M, N, K, G, m_tiles, n_tiles;
+    const float* A; long long sAb, sAg; int ldx, stride, pad, Cg, Tin;
+    const float* W; long long sWg; int ldw;
+    const float* bias; long long sBg;
+    const float* R; long long sRb, sRg; int ldr;
+    float* C; long long sCb, sCg; int ldc;
+};
+
+enum { EPI_NONE = 0, EPI_GELU = 1 };
+
+template <int EPI, bool VEC_A>
+__global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
+    __shared__ __attribute__((aligned(16))) float sA[2][BM * LDL];
+    __shared__ __attribute__((aligned(16))) float sB[2][BN * LDL];
+
+    // XCD-aware bijective remap of the tile id (cdna_hip_programming.md §5.5 T1)
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+    const int tm = wgid / p.n_tiles, tn = wgid - tm * p.n_tiles;
+    const int zb = blockIdx.z / p.G, zg = blockIdx.z - zb * p.G;
+
+    const float* Ab = p.A + zb * p.sAb + zg * p.sAg;
+    const float* Wb = p.W + zg * p.sWg;
+    const int tid = threadIdx.x;
+
+    // staging assignment: 2 float4 of A and 2 of W per thread per K-step
+    int a_row[2], a_c4[2], b_row[2];
+    bool b_ok[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int idx = tid + i * NT;
+        a_row[i] = tm * BM + (idx >> 2);
+        a_c4[i] = (idx & 3) * 4;
+        b_row[i] = tn * BN + (idx >> 2);
+        b_ok[i] = b_row[i] < p.N;
+    }
+    f32x4 ra[2], rb[2];
+    auto load_regs = [&](int k0) {
+        const int j = k0 / p.Cg;
+        const int c0 = k0 - j * p.Cg;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int m = a_row[i];
+            const int t = m * p.stride + j - p.pad;
+            const bool ok = (m < p.M) && (t >= 0) && (t < p.Tin);
+            if (VEC_A) {
+                ra[i] = ok ? *reinterpret_cast<const f32x4*>(Ab + (long long)t * p.ldx + c0 + a_c4[i])
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+            } else {
+                const float* src = Ab + (long long)t * p.ldx + c0 + a_c4[i];
+                ra[i] = ok ? f32x4{src[0], src[1], src[2], src[3]} : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            rb[i] = b_ok[i] ? *reinterpret_cast<const f32x4*>(Wb + (long long)b_row[i] * p.ldw + k0 + a_c4[i])
+                            : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto store_lds = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + i * NT;
+            const int row = idx >> 2;
+            *reinterpret_cast<f32x4*>(&sA[buf][row * LDL + a_c4[i]]) = ra[i];
+            *reinterpret_cast<f32x4*>(&sB[buf][row * LDL + a_c4[i]]) = rb[i];
+        }
+    };
+
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int r32 = lane & 31, h = lane >> 5;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+    const int nk = p.K / BK;
+    load_regs(0);
+    store_lds(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) load_regs((kt + 1) * BK);
+#pragma unroll
+        for (int kk = 0; kk < BK / 8; ++kk) {
+            f32x4 a[2], b[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                a[i] = *reinterpret_cast<const f32x4*>(&sA[cur][(wm * 64 + i * 32 + r32) * LDL + kk * 8 + h * 4]);
+                b[i] = *reinterpret_cast<const f32x4*>(&sB[cur][(wn * 64 + i * 32 + r32) * LDL + kk * 8 + h * 4]);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store_lds(cur ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    float* Cb = p.C + zb * p.sCb + zg * p.sCg;
+    const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
+    const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int col = tn * BN + wn * 64 + j * 32 + r32;
+        if (col >= p.N) continue;
+        const float bv = biasb ? biasb[col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = tm * BM + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (row >= p.M) continue;
+                float v = acc[i][j][e] + bv;
+                if (EPI == EPI_GELU) v = hfa::gelu_erf(v);
+                if (Rb) v += Rb[(long long)row * p.ldr + col];
+                Cb[(long long)row * p.ldc + col] = v;
+            }
+        }
+    }
+}
+
+template <int EPI>
+int launch(const GemmP& p, int Z, bool vec_a, hipStream_t st) {
+    dim3 grid(p.m_tiles * p.n_tiles, 1, Z);
+    if (vec_a) hipLaunchKernelGGL((gemm_f32_kernel<EPI, true>), grid, dim3(NT), 0, st, p);
+    else hipLaunchKernelGGL((gemm_f32_kernel<EPI, false>), grid, dim3(NT), 0, st, p);
+    return hfa::check_launch("hfa_conv_gemm_f32");
+}
+
+inline bool al16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg, int ldx,
+                      int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
+                      const float* bias, long long sBg, const float* R, long long sRb, long long sRg, int ldr,
+                      float* C, long long sCb, long long sCg, int ldc, int epilogue, hipStream_t stream) {
+    if (M < 0 || N < 0 || K < 0 || Zb < 0 || G < 1 || stride < 1 || Cg < 1) {
+        hfa::set_error("hfa_conv_gemm_f32: bad sizes M=%d N=%d K=%d Zb=%d G=%d", M, N, K, Zb, G);
+        return HFA_EINVAL;
+    }
+    if (M == 0 || N == 0 || Zb == 0) return HFA_OK;
+    if (!A || !W || !C || K == 0) {
+        hfa::set_error("hfa_conv_gemm_f32: null operand or K=0");
+        return HFA_EINVAL;
+    }
+    if (K % BK || Cg % BK || K % Cg) {
+        hfa::set_error("hfa_conv_gemm_f32: K=%d and Cg=%d must be multiples of %d with Cg | K", K, Cg, BK);
+        return HFA_EINVAL;
+    }
+    if (!al16(W) || ldw % 4 || sWg % 4) {
+        hfa::set_error("hfa_conv_gemm_f32: W must be 16-byte aligned with ldw, sWg multiples of 4");
+        return HFA_EINVAL;
+    }
+    if (epilogue != EPI_NONE && epilogue != EPI_GELU) {
+        hfa::set_error("hfa_conv_gemm_f32: unknown epilogue %d", epilogue);
+        return HFA_EINVAL;
+    }
+    const bool vec_a = al16(A) && ldx % 4 == 0 && sAb % 4 == 0 && sAg % 4 == 0;
+    GemmP p;
+    p.M = M; p.N = N; p.K = K; p.G = G;
+    p.m_tiles = (M + BM - 1) / BM;
+    p.n_tiles = (N + BN - 1) / BN;
+    p.A = A; p.sAb = sAb; p.sAg = sAg; p.ldx = ldx; p.stride = stride; p.pad = pad; p.Cg = Cg; p.Tin = Tin;
+    p.W = W; p.sWg = sWg; p.ldw = ldw;
+    p.bias = bias; p.sBg = sBg;
+    p.R = R; p.sRb = sRb; p.sRg = sRg; p.ldr = ldr;
+    p.C = C; p.sCb = sCb; p.sCg = sCg; p.ldc = ldc;
+    const long long tiles = (long long)p.m_tiles * p.n_tiles;
+    if (tiles > 0x7fffffffLL || (long long)Zb * G > 65535) {
+        hfa::set_error("hfa_conv_gemm_f32: grid too large");
+        return HFA_EINVAL;
+    }
+    const int Z = Zb * G;
+    return epilogue == EPI_GELU ? launch<EPI_GELU>(p, Z, vec_a, stream) : launch<EPI_NONE>(p, Z, vec_a, stream);
+}
+
+int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, int ldw, const float* bias,
+                 const float* R, int ldr, float* C, int ldc, int epilogue, hipStream_t stream) {
+    return hfa_conv_gemm_f32(M, N, K, 1, 1, A, 0, 0, lda, 1, 0, K, M, W, 0, ldw, bias, 0, R, 0, 0, ldr, C, 0, 0,
+                             ldc, epilogue, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,168 @@
+// misc.hip — bandwidth kernels around the encoder: frame-grid gather, wave normalisation, padding,
+// element-wise add, and the sinc resampler entry point (a pad + the MFMA implicit GEMM of gemm.hip).
+#include "hfa_common.h"
+
+extern "C" int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg,
+                                 int ldx, int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
+                                 const float* bias, long long sBg, const float* R, long long sRb, long long sRg,
+                                 int ldr, float* C, long long sCb, long long sCg, int ldc, int epilogue,
+                                 hipStream_t stream);
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// UnitsEncoder.encode nearest-frame gather (tools/encoder.py:56-59):
+//   index[k] = clamp(round(f32(ratio) * f32(k)), max=U-1) (torch f32 promotion, round half to even);
+//   out[b, k, :] = units[b, index[k], :] for k < n_frames; rows n_frames..T_pad-1 are zero (UNet pad,
+//   networks/layer/backbone/unet.py:103-106).  One wavefront per output row, float4 copies.
+__global__ __launch_bounds__(256) void units_gather_kernel(int U, int C, const float* __restrict__ units,
+                                                           long long u_bs, int u_ld, int n_frames, int T_pad,
+                                                           float ratio, float* __restrict__ out, long long o_bs,
+                                                           int o_ld) {
+    const int b = blockIdx.y;
+    const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (k >= T_pad) return;
+    float* orow = out + b * o_bs + (long long)k * o_ld;
+    if (k >= n_frames) {
+        for (int c = lane * 4; c < C; c += 256) *reinterpret_cast<f32x4*>(orow + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+        return;
+    }
+    int idx = (int)rintf(__fmul_rn(ratio, (float)k));
+    idx = idx < U - 1 ? idx : U - 1;
+    const float* irow = units + b * u_bs + (long long)idx * u_ld;
+    for (int c = lane * 4; c < C; c += 256) *reinterpret_cast<f32x4*>(orow + c) = *reinterpret_cast<const f32x4*>(irow + c);
+}
+
+// Wav2Vec2FeatureExtractor zero_mean_unit_var_norm (transformers feature_extraction_wav2vec2.py): per row
+// (x - mean) / sqrt(var + 1e-7), biased variance.  One workgroup per row, f64 statistics.
+__global__ __launch_bounds__(256) void wav_normalize_kernel(int N, const float* __restrict__ x, long long x_bs,
+                                                            float eps, float* __restrict__ y, long long y_bs) {
+    const int b = blockIdx.x;
+    const float* xr = x + b * x_bs;
+    double s = 0.0, ss = 0.0;
+    for (int i = threadIdx.x; i < N; i += 256) {
+        const double v = xr[i];
+        s += v;
+        ss += v * v;
+    }
+    __shared__ double red[2][4];
+    s = hfa::wave_sum_d(s);
+    ss = hfa::wave_sum_d(ss);
+    if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = s; red[1][threadIdx.x >> 6] = ss; }
+    __syncthreads();
+    const double S = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const double SS = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    const double mean = S / N;
+    double var = SS / N - mean * mean;
+    if (var < 0) var = 0;
+    const float meanf = (float)mean;
+    const float den = (float)sqrt((double)(float)var + (double)eps);
+    float* yr = y + b * y_bs;
+    for (int i = threadIdx.x; i < N; i += 256) yr[i] = (xr[i] - meanf) / den;
+}
+
+// y[b, i] = x[b, i - left] inside [0, N), else 0, for i < N_out.
+__global__ __launch_bounds__(256) void pad_rows_kernel(int N, const float* __restrict__ x, long long x_bs, int left,
+                                                       int N_out, float* __restrict__ y, long long y_bs) {
+    const int b = blockIdx.y;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < N_out; i += gridDim.x * 256) {
+        const int s = i - left;
+        y[b * y_bs + i] = (s >= 0 && s < N) ? x[b * x_bs + s] : 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(256) void add_kernel(long long n4, const f32x4* __restrict__ a,
+                                                  const f32x4* __restrict__ b, f32x4* __restrict__ o) {
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) o[i] = a[i] + b[i];
+}
+
+inline int grid1d(long long n, int per = 256, int cap = 8192) {
+    long long g = (n + per - 1) / per;
+    return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+}  // namespace
+
+extern "C" {
+
+int hfa_units_gather_f32(int B, int U, int C, const float* units, long long u_bs, int u_ld, int n_frames, int T_pad,
+                         float ratio, float* out, long long o_bs, int o_ld, hipStream_t stream) {
+    if (B < 0 || U < 1 || C <= 0 || C % 4 || n_frames < 0 || T_pad < n_frames || u_ld % 4 || o_ld % 4 ||
+        u_bs % 4 || o_bs % 4 || (((uintptr_t)units | (uintptr_t)out) & 15)) {
+        hfa::set_error("hfa_units_gather_f32: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (B == 0 || T_pad == 0) return HFA_OK;
+    hipLaunchKernelGGL(units_gather_kernel, dim3((T_pad + 3) / 4, B), dim3(256), 0, stream, U, C, units, u_bs, u_ld,
+                       n_frames, T_pad, ratio, out, o_bs, o_ld);
+    return hfa::check_launch("hfa_units_gather_f32");
+}
+
+int hfa_wav_normalize_f32(int B, int N, const float* x, long long x_bs, float eps, float* y, long long y_bs,
+                          hipStream_t stream) {
+    if (B < 0 || N <= 0 || !x || !y) {
+        hfa::set_error("hfa_wav_normalize_f32: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (B == 0) return HFA_OK;
+    hipLaunchKernelGGL(wav_normalize_kernel, dim3(B), dim3(256), 0, stream, N, x, x_bs, eps, y, y_bs);
+    return hfa::check_launch("hfa_wav_normalize_f32");
+}
+
+int hfa_pad_rows_f32(int B, int N, const float* x, long long x_bs, int left, int N_out, float* y, long long y_bs,
+                     hipStream_t stream) {
+    if (B < 0 || N < 0 || N_out < 0 || !x || !y) {
+        hfa::set_error("hfa_pad_rows_f32: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (B == 0 || N_out == 0) return HFA_OK;
+    hipLaunchKernelGGL(pad_rows_kernel, dim3(grid1d(N_out, 256, 1024), B), dim3(256), 0, stream, N, x, x_bs, left,
+                       N_out, y, y_bs);
+    return hfa::check_launch("hfa_pad_rows_f32");
+}
+
+int hfa_add_f32(long long n, const float* a, const float* b, float* out, hipStream_t stream) {
+    if (n < 0 || n % 4 || (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15)) {
+        hfa::set_error("hfa_add_f32: n must be a multiple of 4 and operands 16-byte aligned");
+        return HFA_EINVAL;
+    }
+    if (n == 0) return HFA_OK;
+    hipLaunchKernelGGL(add_kernel, dim3(grid1d(n / 4)), dim3(256), 0, stream, n / 4,
+                       reinterpret_cast<const f32x4*>(a), reinterpret_cast<const f32x4*>(b),
+                       reinterpret_cast<f32x4*>(out));
+    return hfa::check_launch("hfa_add_f32");
+}
+
+// torchaudio Resample (sinc_interp_hann) as pad + implicit GEMM (tools/load_wav.py:7, tools/encoder.py:46-48):
+//   xpad = pad(x, (width, width + orig)); out[f*new + p] = sum_k xpad[f*orig + k] * kernel[p][k]
+// orig/new are the gcd-reduced rates, kernel [new][Kpad] (taps 2*width+orig zero-padded to Kpad % 16 == 0).
+// y must hold F*new floats per row (F = N/orig + 1, y_bs >= F*new); the valid length is ceil(new*N/orig).
+long long hfa_resample_workspace_bytes(int B, int N, int orig, int Kpad) {
+    const long long F = N / orig + 1;
+    return (long long)B * (F * orig + Kpad + 4) * sizeof(float) + 64;
+}
+
+int hfa_resample_f32(int B, int N, const float* x, long long x_bs, int orig, int newr, const float* kernel, int Kpad,
+                     int width, void* workspace, float* y, long long y_bs, hipStream_t stream) {
+    if (B < 0 || N <= 0 || orig <= 0 || newr <= 0 || Kpad % 16 || Kpad < 2 * width + orig || !x || !kernel ||
+        !workspace || !y) {
+        hfa::set_error("hfa_resample_f32: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (B == 0) return HFA_OK;
+    const long long F = N / orig + 1;
+    if (y_bs < F * newr) {
+        hfa::set_error("hfa_resample_f32: y_bs=%lld < F*new=%lld", y_bs, F * newr);
+        return HFA_EINVAL;
+    }
+    const long long plen = F * orig + Kpad + 4;
+    float* xpad = reinterpret_cast<float*>(workspace);
+    int rc = hfa_pad_rows_f32(B, N, x, x_bs, width, (int)plen, xpad, plen, stream);
+    if (rc) return rc;
+    return hfa_conv_gemm_f32((int)F, newr, Kpad, B, 1, xpad, plen, 0, orig, 1, 0, Kpad, (int)F, kernel, 0, Kpad,
+                             nullptr, 0, nullptr, 0, 0, 0, y, y_bs, 0, newr, 0, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,172 @@
+// norm.hip — LayerNorm / GroupNorm (+ fused activation) for channels-last [rows, C] activations.
+//
+// Replaces ATen layer_norm / group_norm (+ gelu / hardswish) on the path:
+//   * Hubert: feature_projection LN (model.py:121; HF HubertFeatureProjection), encoder LN after pos-conv
+//     (model.py:25,52; HF HubertEncoder.layer_norm), per-layer norm1/norm2 (post-LN) or pre-LN + final LN
+//     (HF HubertEncoderLayerStableLayerNorm), LN-conv feature extractor of the large variant
+//     (HF HubertLayerNormConvLayer: conv -> LN over channels -> GELU).
+//   * UNet ResidualBasicBlock: GroupNorm(16) + Hardswish and LN + Hardswish (resnet_block.py:145-173).
+// HBM-bound: one wavefront per row, the row held in registers (C <= 4096), float4 loads, two-pass
+// mean/variance in f32 like ATen's reference path, then y = (x - mean) * rstd * gamma + beta.
+#include "hfa_common.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+enum { ACT_NONE = 0, ACT_GELU = 1, ACT_HARDSWISH = 2 };
+
+__device__ __forceinline__ float act_apply(float v, int act) {
+    if (act == ACT_GELU) return hfa::gelu_erf(v);
+    if (act == ACT_HARDSWISH) return hfa::hardswish(v);
+    return v;
+}
+
+// Row-per-wave LayerNorm; C % 4 == 0, C <= 64*4*VPL
+template <int VPL>
+__global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const float* __restrict__ x, long long ldx,
+                                                        const float* __restrict__ res, long long ldr,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps, int act,
+                                                        float* __restrict__ y, long long ldy) {
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wave >= rows) return;
+    const float* xr = x + wave * ldx;
+    const float* rr = res ? res + wave * ldr : nullptr;
+    f32x4 v[VPL];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+        const int c = (lane + i * 64) * 4;
+        if (c < C) {
+            v[i] = *reinterpret_cast<const f32x4*>(xr + c);
+            if (rr) v[i] += *reinterpret_cast<const f32x4*>(rr + c);
+        } else {
+            v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+    }
+    const float mean = hfa::wave_sum(s) / (float)C;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+        const int c = (lane + i * 64) * 4;
+        if (c < C) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float d = v[i][e] - mean;
+                ss += d * d;
+            }
+        }
+    }
+    const float var = hfa::wave_sum(ss) / (float)C;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    float* yr = y + wave * ldy;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+        const int c = (lane + i * 64) * 4;
+        if (c < C) {
+            const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c);
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(beta + c);
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = act_apply((v[i][e] - mean) * rstd * g[e] + bb[e], act);
+            *reinterpret_cast<f32x4*>(yr + c) = o;
+        }
+    }
+}
+
+// GroupNorm over a channels-last [T, C] slab per batch item: group g = channels [g*Cg, (g+1)*Cg) over all T.
+// One workgroup per (batch, group); f64 accumulation of the statistics, then a second sweep applies the
+// affine + activation.  (torch.nn.GroupNorm on [B, C, T]: biased variance, eps inside the sqrt.)
+__global__ __launch_bounds__(256) void groupnorm_kernel(int T, int C, int G, const float* __restrict__ x,
+                                                        long long x_bs, int ldx, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps, int act,
+                                                        float* __restrict__ y, long long y_bs, int ldy) {
+    const int b = blockIdx.y, g = blockIdx.x;
+    const int Cg = C / G;
+    const float* xb = x + b * x_bs + g * Cg;
+    float* yb = y + b * y_bs + g * Cg;
+    const int n = T * Cg;
+    double s = 0.0, ss = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int t = i / Cg, c = i - t * Cg;
+        const double v = xb[(long long)t * ldx + c];
+        s += v;
+        ss += v * v;
+    }
+    __shared__ double red[2][4];
+    s = hfa::wave_sum_d(s);
+    ss = hfa::wave_sum_d(ss);
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = s;
+        red[1][threadIdx.x >> 6] = ss;
+    }
+    __syncthreads();
+    double S = 0.0, SS = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        S += red[0][w];
+        SS += red[1][w];
+    }
+    const double mean_d = S / n;
+    double var_d = SS / n - mean_d * mean_d;
+    if (var_d < 0) var_d = 0;
+    const float mean = (float)mean_d;
+    const float rstd = (float)(1.0 / sqrt(var_d + (double)eps));
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int t = i / Cg, c = i - t * Cg;
+        const float v = xb[(long long)t * ldx + c];
+        yb[(long long)t * ldy + c] = act_apply((v - mean) * rstd * gamma[g * Cg + c] + beta[g * Cg + c], act);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const float* res, long long ldr,
+                      const float* gamma, const float* beta, float eps, int act, float* y, long long ldy,
+                      hipStream_t stream) {
+    if (rows < 0 || C <= 0 || C % 4 || C > 4096 || act < 0 || act > 2) {
+        hfa::set_error("hfa_layernorm_f32: bad sizes rows=%d C=%d (C%%4==0, C<=4096)", rows, C);
+        return HFA_EINVAL;
+    }
+    if (rows == 0) return HFA_OK;
+    if (!x || !gamma || !beta || !y || (((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) & 15) ||
+        ldx % 4 || ldy % 4 || (res && (((uintptr_t)res & 15) || ldr % 4))) {
+        hfa::set_error("hfa_layernorm_f32: operands must be non-null, 16-byte aligned, strides multiple of 4");
+        return HFA_EINVAL;
+    }
+    const int blocks = (rows + 3) / 4;
+    const int vpl = (C + 255) / 256;
+#define HFA_LN(V)                                                                                               \
+    hipLaunchKernelGGL(layernorm_kernel<V>, dim3(blocks), dim3(256), 0, stream, rows, C, x, ldx, res, ldr, gamma, \
+                       beta, eps, act, y, ldy)
+    if (vpl <= 1) HFA_LN(1);
+    else if (vpl <= 2) HFA_LN(2);
+    else if (vpl <= 3) HFA_LN(3);
+    else if (vpl <= 4) HFA_LN(4);
+    else if (vpl <= 8) HFA_LN(8);
+    else HFA_LN(16);
+#undef HFA_LN
+    return hfa::check_launch("hfa_layernorm_f32");
+}
+
+int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,
+                      const float* beta, float eps, int act, float* y, long long y_bs, int ldy, hipStream_t stream) {
+    if (B < 0 || T < 0 || C <= 0 || G <= 0 || C % G || act < 0 || act > 2) {
+        hfa::set_error("hfa_groupnorm_f32: bad sizes");
+        return HFA_EINVAL;
+    }
+    if (B == 0 || T == 0) return HFA_OK;
+    if (!x || !gamma || !beta || !y) {
+        hfa::set_error("hfa_groupnorm_f32: null pointer");
+        return HFA_EINVAL;
+    }
+    hipLaunchKernelGGL(groupnorm_kernel, dim3(G, B), dim3(256), 0, stream, T, C, G, x, x_bs, ldx, gamma, beta, eps,
+                       act, y, y_bs, ldy);
+    return hfa::check_launch("hfa_groupnorm_f32");
+}
+
+}  // extern "C"

@@ -111,3 +111,147 @@ def lattice_prologue(frame_logits, edge_logits, ph_seq_id, T, S, want_frame_prob
               _ptr(out["prob_log"]), _ptr(out["edge_log"]), _ptr(out["not_edge_log"]), _ptr(out["edge_diff"]),
               _ptr(out["edge_prob"]), _stream(dev))
     return out
+
+
+# ------------------------------------------------------------------------------------------------------------
+# Encoder kernels (gemm.hip, attention.hip, norm.hip, conv.hip, misc.hip)
+# ------------------------------------------------------------------------------------------------------------
+EPI_NONE, EPI_GELU = 0, 1
+ACT_NONE, ACT_GELU, ACT_HARDSWISH = 0, 1, 2
+
+_P_, _I_, _LL_, _F_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
+_lib.register("hfa_conv_gemm_f32", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_, _LL_, _I_,
+                                    _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _I_, _P_])
+_lib.register("hfa_gemm_f32", [_I_, _I_, _I_, _P_, _I_, _P_, _I_, _P_, _P_, _I_, _P_, _I_, _I_, _P_])
+_lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_,
+                                    _LL_, _I_, _P_])
+_lib.register("hfa_layernorm_f32", [_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _P_])
+_lib.register("hfa_groupnorm_f32", [_I_, _I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_])
+_lib.register("hfa_conv0_workspace_bytes", [_I_, _I_], ctypes.c_longlong)
+_lib.register("hfa_conv0_f32", [_I_, _I_, _P_, _LL_, _P_, _P_, _I_, _P_, _P_, _F_, _P_, _P_, _LL_, _P_])
+_lib.register("hfa_units_gather_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_])
+_lib.register("hfa_wav_normalize_f32", [_I_, _I_, _P_, _LL_, _F_, _P_, _LL_, _P_])
+_lib.register("hfa_pad_rows_f32", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _LL_, _P_])
+_lib.register("hfa_add_f32", [_LL_, _P_, _P_, _P_, _P_])
+_lib.register("hfa_resample_workspace_bytes", [_I_, _I_, _I_, _I_], ctypes.c_longlong)
+_lib.register("hfa_resample_f32", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _I_, _I_, _P_, _P_, _LL_, _P_])
+
+
+def conv_gemm(A, W, C, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None, Tin=None, sWg=0,
+              ldw=None, bias=None, sBg=0, R=None, sRb=0, sRg=0, ldr=0, sCb=0, sCg=0, ldc, epilogue=EPI_NONE):
+    """Implicit-GEMM conv / Linear on MFMA (see gemm.hip for the exact A/W/C addressing)."""
+    for t, n in ((A, "A"), (W, "W"), (C, "C")):
+        _need(t, torch.float32, n, contiguous=False)
+    _lib.call("hfa_conv_gemm_f32", M, N, K, Zb, G, _ptr(A), sAb, sAg, ldx, stride, pad, Cg or K,
+              Tin if Tin is not None else M, _ptr(W), sWg, ldw if ldw is not None else K, _ptr(bias), sBg, _ptr(R),
+              sRb, sRg, ldr, _ptr(C), sCb, sCg, ldc, epilogue, _stream(C.device))
+
+
+def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
+    """y = epi(x @ W^T + bias) (+ residual); x [..., K] rows contiguous, W [N, K] contiguous."""
+    K = x.shape[-1]
+    N = W.shape[0]
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    if out is None:
+        out = torch.empty((*x.shape[:-1], N), dtype=torch.float32, device=x.device)
+    o2 = out.view(-1, N)
+    r2 = residual.reshape(-1, N) if residual is not None else None
+    _need(W, torch.float32, "W")
+    _lib.call("hfa_gemm_f32", M, N, K, _ptr(x2), x2.stride(0), _ptr(W), W.stride(0), _ptr(bias), _ptr(r2),
+              r2.stride(0) if r2 is not None else 0, _ptr(o2), o2.stride(0), epilogue, _stream(x.device))
+    return out
+
+
+def attention(q, k, v, out, *, B, H, L, head_dim, scale, q_bs, q_ld, k_bs, k_ld, v_bs, v_ld, o_bs, o_ld):
+    _lib.call("hfa_attention_f32", B, H, L, head_dim, float(scale), _ptr(q), q_bs, q_ld, _ptr(k), k_bs, k_ld,
+              _ptr(v), v_bs, v_ld, _ptr(out), o_bs, o_ld, _stream(out.device))
+    return out
+
+
+def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None):
+    C = x.shape[-1]
+    x2 = x.reshape(-1, C)
+    if out is None:
+        out = torch.empty_like(x)
+    o2 = out.view(-1, C)
+    r2 = residual.reshape(-1, C) if residual is not None else None
+    _lib.call("hfa_layernorm_f32", x2.shape[0], C, _ptr(x2), x2.stride(0), _ptr(r2),
+              r2.stride(0) if r2 is not None else 0, _ptr(gamma), _ptr(beta), float(eps), act, _ptr(o2),
+              o2.stride(0), _stream(x.device))
+    return out
+
+
+def groupnorm(x, G, gamma, beta, eps=1e-5, act=ACT_NONE, out=None):
+    """GroupNorm over channels-last x [B, T, C] (stats over T x C/G per group)."""
+    B, T, C = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    _lib.call("hfa_groupnorm_f32", B, T, C, G, _ptr(x), x.stride(0), x.stride(1), _ptr(gamma), _ptr(beta),
+              float(eps), act, _ptr(out), out.stride(0), out.stride(1), _stream(x.device))
+    return out
+
+
+def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, workspace=None):
+    """First extractor conv (1->512, k10, s5) -> [B, T0, 512]; GroupNorm+GELU when gamma/beta are given."""
+    B, N = x.shape
+    T0 = (N - 10) // 5 + 1
+    if out is None:
+        out = torch.empty((B, T0, 512), dtype=torch.float32, device=x.device)
+    norm = gamma is not None
+    if norm and workspace is None:
+        nbytes = _lib.lib().hfa_conv0_workspace_bytes(B, N)
+        workspace = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+    _lib.call("hfa_conv0_f32", B, N, _ptr(x), x.stride(0), _ptr(w0), _ptr(bias), 1 if norm else 0, _ptr(gamma),
+              _ptr(beta), float(eps), _ptr(workspace), _ptr(out), out.stride(0), _stream(x.device))
+    return out
+
+
+def units_gather(units, n_frames, T_pad, ratio, out=None):
+    B, U, C = units.shape
+    if out is None:
+        out = torch.empty((B, T_pad, C), dtype=torch.float32, device=units.device)
+    _lib.call("hfa_units_gather_f32", B, U, C, _ptr(units), units.stride(0), units.stride(1), n_frames, T_pad,
+              float(ratio), _ptr(out), out.stride(0), out.stride(1), _stream(units.device))
+    return out
+
+
+def wav_normalize(x, eps=1e-7, out=None):
+    B, N = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    _lib.call("hfa_wav_normalize_f32", B, N, _ptr(x), x.stride(0), float(eps), _ptr(out), out.stride(0),
+              _stream(x.device))
+    return out
+
+
+def pad_rows(x, left, n_out, out=None):
+    B, N = x.shape
+    if out is None:
+        out = torch.empty((B, n_out), dtype=torch.float32, device=x.device)
+    _lib.call("hfa_pad_rows_f32", B, N, _ptr(x), x.stride(0), left, n_out, _ptr(out), out.stride(0),
+              _stream(x.device))
+    return out
+
+
+def add(a, b, out=None):
+    if out is None:
+        out = torch.empty_like(a)
+    _lib.call("hfa_add_f32", a.numel(), _ptr(a), _ptr(b), _ptr(out), _stream(a.device))
+    return out
+
+
+def resample(x, orig, new, kernel, width, out=None, workspace=None):
+    """Sinc resample rows of x [B, N] (gcd-reduced orig/new rates); returns [B, ceil(new*N/orig)] view."""
+    import math
+    B, N = x.shape
+    Kpad = kernel.shape[1]
+    F = N // orig + 1
+    if out is None:
+        out = torch.empty((B, F * new), dtype=torch.float32, device=x.device)
+    if workspace is None:
+        nbytes = _lib.lib().hfa_resample_workspace_bytes(B, N, orig, Kpad)
+        workspace = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+    _lib.call("hfa_resample_f32", B, N, _ptr(x), x.stride(0), orig, new, _ptr(kernel), Kpad, width,
+              _ptr(workspace), _ptr(out), out.stride(0), _stream(x.device))
+    return out[:, : int(math.ceil(new * N / orig))]

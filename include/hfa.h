@@ -61,6 +61,74 @@ int hfa_lattice_prologue(int B, int Tmax, int V, int Smax, const int32_t* T, con
                          float* ph_prob_log, float* ph_frame_pred, float* prob_log, float* edge_log,
                          float* not_edge_log, float* edge_diff, double* edge_prob, hipStream_t stream);
 
+/* ---- dense contractions (hubertfa_amd/csrc/gemm.hip): f32 MFMA implicit GEMM ---------------------------------
+ * C[z](m,n) = epi(sum_k A[z](m,k) W[z](n,k) + bias[zg*sBg + n]) + R[z](m,n),  z = zb*G + zg,
+ * A[z](m,k): k = j*Cg + c, t = m*stride + j - pad, value X[zb*sAb + zg*sAg + t*ldx + c] if 0 <= t < Tin else 0.
+ * W[z] row n at W + zg*sWg + n*ldw (K contiguous, conv weights in [Cout][k][Cin] im2col order).
+ * epilogue: 0 none, 1 erf-GELU (applied before the residual add).  K % 16 == 0, Cg % 16 == 0, Cg | K.
+ * Replaces ATen addmm (nn.Linear) and conv1d on the path:
+ *   networks/hubert/model.py:100-114 (conv1-6), :122 (projection), :135-147 (grouped positional conv),
+ *   :27-33 (nn.TransformerEncoderLayer in/out proj, linear1/2), transformers HubertAttention/HubertFeedForward,
+ *   networks/layer/block/resnet_block.py:145-168 (k3 convs, shortcut), networks/layer/scaling/stride_conv.py:23-47
+ *   (k2 s2 conv, ConvTranspose), networks/task/forced_alignment.py:53-55 (head). */
+int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg, int ldx,
+                      int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
+                      const float* bias, long long sBg, const float* R, long long sRb, long long sRg, int ldr,
+                      float* C, long long sCb, long long sCg, int ldc, int epilogue, hipStream_t stream);
+/* Plain Linear: C[M,N] = epi(A[M,K] W[N,K]^T + bias) + R. */
+int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, int ldw, const float* bias,
+                 const float* R, int ldr, float* C, int ldc, int epilogue, hipStream_t stream);
+
+/* ---- attention (hubertfa_amd/csrc/attention.hip) -----------------------------------------------------------
+ * O = softmax(scale * Q K^T) V per (batch, head), head_dim 64, fp32 MFMA flash attention.
+ * Q(b,h,i,d) at q + b*q_bs + i*q_ld + h*64 + d (same for k, v, o).
+ * Replaces nn.MultiheadAttention/SDPA in networks/hubert/model.py:27-32 and transformers
+ * modeling_hubert.py HubertAttention (eager_attention_forward). */
+int hfa_attention_f32(int B, int H, int L, int head_dim, float scale, const float* q, long long q_bs, int q_ld,
+                      const float* k, long long k_bs, int k_ld, const float* v, long long v_bs, int v_ld, float* o,
+                      long long o_bs, int o_ld, hipStream_t stream);
+
+/* ---- normalisation (hubertfa_amd/csrc/norm.hip); act: 0 none, 1 erf-GELU, 2 Hardswish -----------------------
+ * y = act(LayerNorm(x (+ res)) * gamma + beta) over rows of C <= 4096 (C % 4 == 0).
+ * Replaces LayerNorm in networks/hubert/model.py:25,121 and nn.TransformerEncoderLayer norm1/2,
+ * transformers HubertFeatureProjection/HubertEncoder(*StableLayerNorm)/HubertLayerNormConvLayer,
+ * networks/layer/block/resnet_block.py:170-173 (LN + Hardswish). */
+int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const float* res, long long ldr,
+                      const float* gamma, const float* beta, float eps, int act, float* y, long long ldy,
+                      hipStream_t stream);
+/* GroupNorm(G, C) over a channels-last [B, T, C] tensor (+act).  Replaces resnet_block.py:153-154
+ * (nn.GroupNorm(16, C) + nn.Hardswish). */
+int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,
+                      const float* beta, float eps, int act, float* y, long long y_bs, int ldy, hipStream_t stream);
+
+/* ---- extractor conv0 (hubertfa_amd/csrc/conv.hip) ------------------------------------------------------------
+ * x [B, N] -> y [B, T0, 512] channels-last, T0 = (N-10)/5+1.  norm=1: GroupNorm(512,512) + GELU
+ * (networks/hubert/model.py:98-99,108; transformers HubertGroupNormConvLayer), needs a workspace of
+ * hfa_conv0_workspace_bytes(B, N).  norm=0: conv + bias only (HubertLayerNormConvLayer's conv). */
+long long hfa_conv0_workspace_bytes(int B, int N);
+int hfa_conv0_f32(int B, int N, const float* x, long long x_bs, const float* w0, const float* bias, int norm,
+                  const float* gamma, const float* beta, float eps, void* workspace, float* y, long long y_bs,
+                  hipStream_t stream);
+
+/* ---- glue (hubertfa_amd/csrc/misc.hip) -----------------------------------------------------------------------
+ * Nearest-frame gather onto the DP grid, tools/encoder.py:56-59: idx[k] = min(rint(f32(ratio)*k), U-1),
+ * out[b,k,:] = units[b,idx[k],:] for k < n_frames, zero rows up to T_pad (unet.py:103-106 padding). */
+int hfa_units_gather_f32(int B, int U, int C, const float* units, long long u_bs, int u_ld, int n_frames, int T_pad,
+                         float ratio, float* out, long long o_bs, int o_ld, hipStream_t stream);
+/* Wav2Vec2FeatureExtractor zero-mean/unit-variance normalisation (tools/encoder.py:94-95). */
+int hfa_wav_normalize_f32(int B, int N, const float* x, long long x_bs, float eps, float* y, long long y_bs,
+                          hipStream_t stream);
+/* Zero padding of rows (networks/hubert/model.py:77 F.pad 40/40; resampler edge padding). */
+int hfa_pad_rows_f32(int B, int N, const float* x, long long x_bs, int left, int N_out, float* y, long long y_bs,
+                     hipStream_t stream);
+/* out = a + b (UNet skip connection, networks/layer/backbone/unet.py:114). */
+int hfa_add_f32(long long n, const float* a, const float* b, float* out, hipStream_t stream);
+/* torchaudio.transforms.Resample (sinc_interp_hann) as pad + MFMA GEMM (tools/load_wav.py:7,
+ * tools/encoder.py:46-48).  orig/newr gcd-reduced; kernel [newr][Kpad]; y_bs >= (N/orig+1)*newr. */
+long long hfa_resample_workspace_bytes(int B, int N, int orig, int Kpad);
+int hfa_resample_f32(int B, int N, const float* x, long long x_bs, int orig, int newr, const float* kernel, int Kpad,
+                     int width, void* workspace, float* y, long long y_bs, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

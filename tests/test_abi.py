@@ -19,7 +19,7 @@ def test_header_declares_entry_points():
 
 
 def test_library_exports_every_declared_symbol():
-    from hubertfa_amd import _lib
+    from hubertfa_amd import _lib, ops  # noqa: F401  (ops registers the encoder signatures)
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("libhfa.so not built (run __graft_entry__.build())")
     L = _lib.lib()

@@ -1,0 +1,164 @@
+"""Layer-level numerics of every encoder HIP kernel against a plain PyTorch fp32/fp64 CPU reference.
+
+Tolerances are written per test; the f32 MFMA path is an exact fmaf chain, so differences are summation-order
+only (~1e-6 relative at K <= 6144).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+F = torch.nn.functional
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _r(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+def _close(got, ref, rtol, atol):
+    got = got.detach().cpu().double()
+    ref = ref.detach().cpu().double()
+    err = (got - ref).abs()
+    bound = atol + rtol * ref.abs()
+    assert bool((err <= bound).all()), f"max err {float(err.max()):.3e}, max rel {float((err / (ref.abs() + 1e-30)).max()):.3e}"
+
+
+@pytest.mark.parametrize("M,N,K,epi,res", [(300, 200, 128, 0, False), (1000, 768, 768, 1, False),
+                                           (257, 65, 192, 0, True), (4096, 3072, 768, 1, False),
+                                           (130, 2304, 768, 0, False), (64, 768, 3072, 0, True)])
+def test_gemm_linear(M, N, K, epi, res):
+    from hubertfa_amd import ops
+    x, w, b = _r(M, K, seed=1), _r(N, K, seed=2, scale=K ** -0.5), _r(N, seed=3)
+    r = _r(M, N, seed=4) if res else None
+    ref = x.double() @ w.double().T + b.double()
+    if epi:
+        ref = F.gelu(ref)
+    if res:
+        ref = ref + r.double()
+    d = torch.device("cuda")
+    got = ops.linear(x.to(d), w.to(d), b.to(d), residual=r.to(d) if res else None, epilogue=epi)
+    _close(got, ref, 2e-5, 2e-5)
+
+
+@pytest.mark.parametrize("Cin,Cout,k,s,pad,T,G", [(512, 512, 3, 2, 0, 301, 1), (512, 512, 2, 2, 0, 100, 1),
+                                                  (192, 192, 3, 1, 1, 64, 1), (768, 768, 128, 1, 64, 49, 16),
+                                                  (192, 384, 2, 2, 0, 40, 1)])
+def test_conv_gemm_vs_conv1d(Cin, Cout, k, s, pad, T, G):
+    """Implicit-GEMM conv on channels-last activations == torch conv1d (channels-first)."""
+    from hubertfa_amd import ops
+    B = 2
+    x = _r(B, T, Cin, seed=5)
+    w = _r(Cout, Cin // G, k, seed=6, scale=(Cin // G * k) ** -0.5)
+    b = _r(Cout, seed=7)
+    ref = F.conv1d(x.double().transpose(1, 2), w.double(), b.double(), stride=s, padding=pad, groups=G)
+    ref = ref.transpose(1, 2)
+    Tout = ref.shape[1]
+    d = torch.device("cuda")
+    Cg, Ng = Cin // G, Cout // G
+    # im2col weight order [Cout][k][Cin/G]
+    wk = w.permute(0, 2, 1).contiguous().to(d)
+    out = torch.empty(B, Tout, Cout, device=d)
+    xd = x.to(d)
+    ops.conv_gemm(xd, wk, out, M=Tout, N=Ng, K=k * Cg, Zb=B, G=G, sAb=T * Cin, sAg=Cg, ldx=Cin, stride=s, pad=pad,
+                  Cg=Cg, Tin=T, sWg=Ng * k * Cg, bias=b.to(d), sBg=Ng, sCb=Tout * Cout, sCg=Ng, ldc=Cout)
+    _close(out, ref, 5e-5, 5e-5)
+
+
+@pytest.mark.parametrize("B,H,L", [(2, 12, 499), (1, 16, 49), (3, 12, 64), (1, 12, 1)])
+def test_attention(B, H, L):
+    from hubertfa_amd import ops
+    D = 64
+    qkv = _r(B, L, 3 * H * D, seed=8, scale=1.5)
+    q, k, v = qkv.double().split(H * D, dim=-1)
+    q = q.view(B, L, H, D).transpose(1, 2)
+    k = k.view(B, L, H, D).transpose(1, 2)
+    v = v.view(B, L, H, D).transpose(1, 2)
+    att = torch.softmax((q @ k.transpose(-1, -2)) * D ** -0.5, -1) @ v
+    ref = att.transpose(1, 2).reshape(B, L, H * D)
+    d = torch.device("cuda")
+    qd = qkv.to(d)
+    out = torch.empty(B, L, H * D, device=d)
+    ops.attention(qd, qd[..., H * D:], qd[..., 2 * H * D:], out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5,
+                  q_bs=L * 3 * H * D, q_ld=3 * H * D, k_bs=L * 3 * H * D, k_ld=3 * H * D, v_bs=L * 3 * H * D,
+                  v_ld=3 * H * D, o_bs=L * H * D, o_ld=H * D)
+    _close(out, ref, 1e-4, 2e-5)
+
+
+@pytest.mark.parametrize("C,act", [(768, 0), (512, 1), (192, 2), (1024, 0), (384, 2)])
+def test_layernorm(C, act):
+    from hubertfa_amd import ops
+    x = _r(333, C, seed=9, scale=3.0) + 0.5
+    g, b = _r(C, seed=10) * 0.1 + 1, _r(C, seed=11) * 0.1
+    ref = F.layer_norm(x.double(), (C,), g.double(), b.double(), 1e-5)
+    ref = [lambda t: t, F.gelu, F.hardswish][act](ref)
+    d = torch.device("cuda")
+    got = ops.layernorm(x.to(d), g.to(d), b.to(d), 1e-5, act=act)
+    _close(got, ref, 1e-5, 2e-5)
+
+
+def test_groupnorm_hardswish():
+    from hubertfa_amd import ops
+    B, T, C = 3, 864, 192
+    x = _r(B, T, C, seed=12, scale=2.0) + 0.3
+    g, b = _r(C, seed=13) * 0.1 + 1, _r(C, seed=14) * 0.1
+    ref = F.hardswish(F.group_norm(x.double().transpose(1, 2), 16, g.double(), b.double(), 1e-5)).transpose(1, 2)
+    d = torch.device("cuda")
+    got = ops.groupnorm(x.to(d), 16, g.to(d), b.to(d), 1e-5, act=ops.ACT_HARDSWISH)
+    _close(got, ref, 1e-5, 2e-5)
+
+
+def test_conv0_groupnorm_gelu():
+    from hubertfa_amd import ops
+    B, N = 2, 16000
+    x = _r(B, N, seed=15, scale=0.3)
+    w = _r(512, 1, 10, seed=16, scale=0.3)
+    g, b = _r(512, seed=17) * 0.1 + 1, _r(512, seed=18) * 0.1
+    c = F.conv1d(x.double()[:, None], w.double(), stride=5)
+    ref = F.gelu(F.group_norm(c, 512, g.double(), b.double(), 1e-5)).transpose(1, 2)
+    d = torch.device("cuda")
+    got = ops.conv0(x.to(d), w.view(512, 10).contiguous().to(d), gamma=g.to(d), beta=b.to(d))
+    _close(got, ref, 1e-4, 1e-5)
+    raw = ops.conv0(x.to(d), w.view(512, 10).contiguous().to(d), bias=b.to(d))
+    _close(raw, (c + b.double()[None, :, None]).transpose(1, 2), 1e-5, 1e-6)
+
+
+def test_units_gather_matches_reference_index():
+    from hubertfa_amd import ops
+    z = np.load(os.path.join(GOLDEN, "gather_index.npz"))
+    d = torch.device("cuda")
+    for key in z.files:
+        n44 = int(key.split("_")[0][1:])
+        U = int(key.split("units")[1])
+        idx = z[key]
+        n_frames = n44 // 512 + 1
+        C = 8
+        units = torch.arange(U, dtype=torch.float32).repeat_interleave(C).view(1, U, C).to(d)
+        ratio = (512 / 44100) / (320 / 16000)
+        out = ops.units_gather(units, n_frames, n_frames + 3, ratio).cpu().numpy()
+        assert np.array_equal(out[0, :n_frames, 0].astype(np.int32), idx), key
+        assert np.all(out[0, n_frames:] == 0)
+
+
+def test_resample_vs_restated_torchaudio():
+    from hubertfa_amd.resample import Resampler
+    from oracle.resample import resample as ref_resample
+    x = _r(2, 16000, seed=19, scale=0.2)
+    for o, n, w in ((16000, 44100, 6), (44100, 16000, 128)):
+        xx = x if o == 16000 else ref_resample(x, 16000, 44100, 6)
+        ref = ref_resample(xx.double(), o, n, w) if False else ref_resample(xx, o, n, w)
+        got = Resampler(o, n, w)(xx.cuda())
+        assert got.shape == ref.shape
+        _close(got, ref, 1e-4, 2e-6)
+
+
+def test_wav_normalize():
+    from hubertfa_amd import ops
+    x = _r(3, 16000, seed=20, scale=0.3) + 0.01
+    ref = (x.double() - x.double().mean(-1, keepdim=True)) / torch.sqrt(x.double().var(-1, unbiased=False, keepdim=True) + 1e-7)
+    got = ops.wav_normalize(x.cuda())
+    _close(got, ref, 1e-5, 1e-5)
