@@ -1,0 +1,237 @@
+"""Hubert encoders (HF ``HubertModel`` = cnhubert, bshall ``HubertSoft``) executed on libhfa's gfx950 kernels.
+
+Reference arithmetic:
+  * HF HubertModel.forward (transformers modeling_hubert.py): HubertFeatureEncoder -> HubertFeatureProjection ->
+    HubertEncoder (pos-conv, +x, LN, post-LN layers) or HubertEncoderStableLayerNorm (pre-LN layers, final LN).
+  * bshall Hubert.encode / HubertSoft.units (networks/hubert/model.py:45-54, 75-79, 95-172).
+  * cnhubert input normalisation (tools/encoder.py:94-95 -> Wav2Vec2FeatureExtractor.zero_mean_unit_var_norm).
+
+Layout: activations are channels-last [B, T, C] f32 in HBM from conv0 onward, so every conv is an implicit GEMM
+with overlapping rows (no im2col buffer) and every Linear reads rows directly.  Weights are converted once at
+load: conv weights to [Cout][k][Cin] im2col order, Q/K/V fused into one [3H, H] projection, the positional
+conv's weight-norm folded (torch._weight_norm, dim=2).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import ops
+from .synth import HubertArch
+
+
+def _t(x) -> torch.Tensor:
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(np.ascontiguousarray(x))
+    return x.detach().cpu()
+
+
+def _strip(sd: dict) -> dict:
+    out = {}
+    for k, v in sd.items():
+        for pre in ("module.", "hubert."):
+            if k.startswith(pre):
+                k = k[len(pre):]
+        out[k] = v
+    return out
+
+
+def _conv_im2col(w: torch.Tensor) -> torch.Tensor:
+    """torch conv weight [Cout, Cin, k] -> [Cout, k*Cin] with k-major (matches the GEMM's A addressing)."""
+    return w.permute(0, 2, 1).reshape(w.shape[0], -1).contiguous()
+
+
+def _weight_norm(sd: dict, prefix: str) -> torch.Tensor:
+    if prefix + "weight" in sd:
+        return _t(sd[prefix + "weight"]).float()
+    if prefix + "weight_g" in sd:
+        g, v = _t(sd[prefix + "weight_g"]).float(), _t(sd[prefix + "weight_v"]).float()
+    else:
+        g = _t(sd[prefix + "parametrizations.weight.original0"]).float()
+        v = _t(sd[prefix + "parametrizations.weight.original1"]).float()
+    return torch._weight_norm(v, g, 2)
+
+
+class _Layer:
+    __slots__ = ("wqkv", "bqkv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w", "ln2_b")
+
+
+class HubertEncoder:
+    """Hubert forward on HIP kernels.  ``forward(wav[B, N]) -> units[B, L, C_out]`` (f32, channels-last)."""
+
+    def __init__(self, arch: HubertArch, state_dict: dict, device: str | torch.device = "cuda"):
+        self.arch = arch
+        self.device = torch.device(device)
+        sd = _strip(state_dict)
+        dev = self.device
+
+        def P(name):
+            return _t(sd[name]).float().contiguous().to(dev)
+
+        hf = arch.layout == "hf"
+        n_conv = len(arch.conv_dim)
+        self.conv_w, self.conv_b, self.conv_ln = [], [], []
+        for i in range(n_conv):
+            pre = f"feature_extractor.conv_layers.{i}." if hf else f"feature_extractor.conv{i}."
+            w = _t(sd[pre + "conv.weight" if hf else pre + "weight"]).float()
+            self.conv_w.append((w.reshape(w.shape[0], -1) if i == 0 else _conv_im2col(w)).contiguous().to(dev))
+            bkey = pre + ("conv.bias" if hf else "bias")
+            self.conv_b.append(P(bkey) if bkey in sd else None)
+            if hf and (arch.feat_extract_norm == "layer" or i == 0):
+                self.conv_ln.append((P(pre + "layer_norm.weight"), P(pre + "layer_norm.bias")))
+            elif not hf and i == 0:
+                self.conv_ln.append((P("feature_extractor.norm0.weight"), P("feature_extractor.norm0.bias")))
+            else:
+                self.conv_ln.append(None)
+        fp = "feature_projection."
+        self.fp_ln = (P(fp + ("layer_norm" if hf else "norm") + ".weight"), P(fp + ("layer_norm" if hf else "norm") + ".bias"))
+        self.fp_w, self.fp_b = P(fp + "projection.weight"), P(fp + "projection.bias")
+        pc = "encoder.pos_conv_embed.conv." if hf else "positional_embedding.conv."
+        self.pos_w = _conv_im2col(_weight_norm(sd, pc)).to(dev)          # [H, k*H/G] grouped im2col
+        self.pos_b = P(pc + "bias")
+        self.enc_ln = (P("encoder.layer_norm.weight"), P("encoder.layer_norm.bias")) if hf else \
+            (P("norm.weight"), P("norm.bias"))
+        self.layers = []
+        for l in range(arch.layers):
+            L = _Layer()
+            p = f"encoder.layers.{l}."
+            if hf:
+                a = p + "attention."
+                L.wqkv = torch.cat([_t(sd[a + f"{n}_proj.weight"]).float() for n in "qkv"], 0).contiguous().to(dev)
+                L.bqkv = torch.cat([_t(sd[a + f"{n}_proj.bias"]).float() for n in "qkv"], 0).contiguous().to(dev)
+                L.wo, L.bo = P(a + "out_proj.weight"), P(a + "out_proj.bias")
+                L.ln1_w, L.ln1_b = P(p + "layer_norm.weight"), P(p + "layer_norm.bias")
+                L.w1, L.b1 = P(p + "feed_forward.intermediate_dense.weight"), P(p + "feed_forward.intermediate_dense.bias")
+                L.w2, L.b2 = P(p + "feed_forward.output_dense.weight"), P(p + "feed_forward.output_dense.bias")
+                L.ln2_w, L.ln2_b = P(p + "final_layer_norm.weight"), P(p + "final_layer_norm.bias")
+            else:
+                L.wqkv, L.bqkv = P(p + "self_attn.in_proj_weight"), P(p + "self_attn.in_proj_bias")
+                L.wo, L.bo = P(p + "self_attn.out_proj.weight"), P(p + "self_attn.out_proj.bias")
+                L.ln1_w, L.ln1_b = P(p + "norm1.weight"), P(p + "norm1.bias")
+                L.w1, L.b1 = P(p + "linear1.weight"), P(p + "linear1.bias")
+                L.w2, L.b2 = P(p + "linear2.weight"), P(p + "linear2.bias")
+                L.ln2_w, L.ln2_b = P(p + "norm2.weight"), P(p + "norm2.bias")
+            self.layers.append(L)
+        self.proj = (P("proj.weight"), P("proj.bias")) if (not hf and arch.proj_dim) else None
+        self._ws = {}
+
+    # ----------------------------------------------------------------------------------------------------------
+    def _workspace(self, name, nbytes):
+        buf = self._ws.get(name)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+            self._ws[name] = buf
+        return buf
+
+    def feature_extractor(self, x: torch.Tensor) -> torch.Tensor:
+        """[B, N] -> [B, L, 512] (channels-last); GELU applied after every conv."""
+        a = self.arch
+        B, N = x.shape
+        ln0 = self.conv_ln[0]
+        if a.feat_extract_norm == "group":
+            ws = self._workspace("conv0", ops._lib.lib().hfa_conv0_workspace_bytes(B, N))
+            h = ops.conv0(x, self.conv_w[0], gamma=ln0[0], beta=ln0[1], eps=1e-5, workspace=ws)
+        else:
+            h = ops.conv0(x, self.conv_w[0], bias=self.conv_b[0])
+            h = ops.layernorm(h, ln0[0], ln0[1], a.layer_norm_eps, act=ops.ACT_GELU, out=h)
+        for i in range(1, len(a.conv_dim)):
+            k, s = a.conv_kernel[i], a.conv_stride[i]
+            Tin, Cin = h.shape[1], h.shape[2]
+            Tout = (Tin - k) // s + 1
+            Cout = a.conv_dim[i]
+            out = torch.empty((B, Tout, Cout), dtype=torch.float32, device=x.device)
+            layer_norm = self.conv_ln[i] is not None
+            ops.conv_gemm(h, self.conv_w[i], out, M=Tout, N=Cout, K=k * Cin, Zb=B, sAb=Tin * Cin, ldx=Cin,
+                          stride=s, Cg=Cin, Tin=Tin, bias=self.conv_b[i], sCb=Tout * Cout, ldc=Cout,
+                          epilogue=ops.EPI_NONE if layer_norm else ops.EPI_GELU)
+            if layer_norm:
+                out = ops.layernorm(out, self.conv_ln[i][0], self.conv_ln[i][1], a.layer_norm_eps,
+                                    act=ops.ACT_GELU, out=out)
+            h = out
+        return h
+
+    def positional(self, h: torch.Tensor) -> torch.Tensor:
+        """h + GELU(grouped conv k128 pad64 (+bias), last frame dropped) — one GEMM launch over (batch, group)."""
+        a = self.arch
+        B, L, H = h.shape
+        G, k = a.pos_groups, a.pos_kernel
+        Cg = H // G
+        out = torch.empty_like(h)
+        ops.conv_gemm(h, self.pos_w, out, M=L, N=Cg, K=k * Cg, Zb=B, G=G, sAb=L * H, sAg=Cg, ldx=H, stride=1,
+                      pad=k // 2, Cg=Cg, Tin=L, sWg=Cg * k * Cg, bias=self.pos_b, sBg=Cg, R=h, sRb=L * H, sRg=Cg,
+                      ldr=H, sCb=L * H, sCg=Cg, ldc=H, epilogue=ops.EPI_GELU)
+        return out
+
+    def attention_block(self, h_in: torch.Tensor, L_: _Layer) -> torch.Tensor:
+        a = self.arch
+        B, L, H = h_in.shape
+        nh = a.heads
+        dh = H // nh
+        qkv = ops.linear(h_in, L_.wqkv, L_.bqkv)
+        o = torch.empty((B, L, H), dtype=torch.float32, device=h_in.device)
+        ops.attention(qkv, qkv[..., H:], qkv[..., 2 * H:], o, B=B, H=nh, L=L, head_dim=dh, scale=dh ** -0.5,
+                      q_bs=L * 3 * H, q_ld=3 * H, k_bs=L * 3 * H, k_ld=3 * H, v_bs=L * 3 * H, v_ld=3 * H,
+                      o_bs=L * H, o_ld=H)
+        return o
+
+    def layer(self, h: torch.Tensor, L_: _Layer) -> torch.Tensor:
+        eps = self.arch.layer_norm_eps
+        if not self.arch.stable_layer_norm:   # post-LN (HubertEncoderLayer / nn.TransformerEncoderLayer)
+            o = self.attention_block(h, L_)
+            h1 = ops.linear(o, L_.wo, L_.bo, residual=h)
+            h1 = ops.layernorm(h1, L_.ln1_w, L_.ln1_b, eps, out=h1)
+            f = ops.linear(h1, L_.w1, L_.b1, epilogue=ops.EPI_GELU)
+            h2 = ops.linear(f, L_.w2, L_.b2, residual=h1)
+            return ops.layernorm(h2, L_.ln2_w, L_.ln2_b, eps, out=h2)
+        # pre-LN (HubertEncoderLayerStableLayerNorm)
+        a_ = ops.layernorm(h, L_.ln1_w, L_.ln1_b, eps)
+        o = self.attention_block(a_, L_)
+        h = ops.linear(o, L_.wo, L_.bo, residual=h)
+        a_ = ops.layernorm(h, L_.ln2_w, L_.ln2_b, eps)
+        f = ops.linear(a_, L_.w1, L_.b1, epilogue=ops.EPI_GELU)
+        return ops.linear(f, L_.w2, L_.b2, residual=h)
+
+    @torch.no_grad()
+    def forward(self, wav: torch.Tensor, n_layers: int | None = None) -> torch.Tensor:
+        a = self.arch
+        x = wav.float().contiguous()
+        if x.dim() == 1:
+            x = x[None]
+        if a.do_normalize:
+            x = ops.wav_normalize(x, 1e-7)
+        if a.wav_pad:
+            x = ops.pad_rows(x, a.wav_pad, x.shape[1] + 2 * a.wav_pad)
+        feats = self.feature_extractor(x)
+        fln = ops.layernorm(feats, self.fp_ln[0], self.fp_ln[1], a.layer_norm_eps)
+        h = ops.linear(fln, self.fp_w, self.fp_b)
+        h = self.positional(h)
+        if not a.stable_layer_norm:
+            h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
+        for L_ in self.layers[:n_layers]:
+            h = self.layer(h, L_)
+        if a.stable_layer_norm:
+            h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
+        if self.proj is not None:
+            h = ops.linear(h, self.proj[0], self.proj[1])
+        return h
+
+    __call__ = forward
+
+    def flops(self, n_samples: int) -> float:
+        """Algorithmic FLOPs of one forward over ``n_samples`` (MAC = 2 FLOP), excluding norms/activations."""
+        a = self.arch
+        n = n_samples + 2 * a.wav_pad
+        f = 0.0
+        T = n
+        for i, (cd, k, s) in enumerate(zip(a.conv_dim, a.conv_kernel, a.conv_stride)):
+            cin = 1 if i == 0 else a.conv_dim[i - 1]
+            T = (T - k) // s + 1
+            f += 2.0 * T * cd * cin * k
+        L, H = T, a.hidden
+        f += 2.0 * L * a.conv_dim[-1] * H                                        # projection
+        f += 2.0 * L * H * (H // a.pos_groups) * a.pos_kernel                   # positional conv
+        per_layer = 2.0 * L * H * 3 * H + 2.0 * L * H * H + 2.0 * 2 * L * H * a.ffn + 4.0 * L * L * H
+        f += a.layers * per_layer
+        if a.proj_dim:
+            f += 2.0 * L * H * a.proj_dim
+        return f

@@ -1,0 +1,155 @@
+"""Lattice producer: ``UNetBackbone`` + ``head`` of LitForcedAlignmentTask on libhfa kernels.
+
+Reference: networks/layer/backbone/unet.py:9-119 (UNetBackbone), networks/layer/block/resnet_block.py:4-50
+(ResidualBasicBlock), networks/layer/scaling/stride_conv.py:6-47 (DownSampling / UpSampling),
+networks/task/forced_alignment.py:53-55, 284-292 (head + logit split).
+
+All tensors stay channels-last [B, T, C]: the k3 convs are implicit GEMMs with pad 1 (zero rows outside [0, T)),
+the stride-2 down-sampling conv is an implicit GEMM with overlapping-free rows, the transposed up-sampling conv is
+ONE GEMM whose [T, 2*Cout] output is bit-for-bit the [2T, Cout] layout, GroupNorm/LayerNorm fuse their
+Hardswish, and the residual shortcut is the second conv's epilogue.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import ops
+from .synth import UNetArch
+
+
+def _t(x):
+    return torch.from_numpy(np.ascontiguousarray(x)) if isinstance(x, np.ndarray) else x.detach().cpu()
+
+
+class _Block:
+    def __init__(self, sd, pre, dev):
+        P = lambda n: _t(sd[pre + n]).float().contiguous().to(dev)  # noqa: E731
+        w1 = _t(sd[pre + "block.0.weight"]).float()
+        w2 = _t(sd[pre + "block.3.weight"]).float()
+        self.cin, self.hid, self.cout = w1.shape[1], w1.shape[0], w2.shape[0]
+        self.w1 = w1.permute(0, 2, 1).reshape(self.hid, -1).contiguous().to(dev)
+        self.w2 = w2.permute(0, 2, 1).reshape(self.cout, -1).contiguous().to(dev)
+        self.gn = (P("block.1.weight"), P("block.1.bias"))
+        self.n_groups = 16
+        self.sc = P("shortcut.0.weight") if pre + "shortcut.0.weight" in sd else None
+        self.ln = (P("out.0.weight"), P("out.0.bias"))
+
+    def __call__(self, x):
+        B, T, _ = x.shape
+        h = torch.empty((B, T, self.hid), dtype=torch.float32, device=x.device)
+        ops.conv_gemm(x, self.w1, h, M=T, N=self.hid, K=3 * self.cin, Zb=B, sAb=T * self.cin, ldx=self.cin, stride=1,
+                      pad=1, Cg=self.cin, Tin=T, sCb=T * self.hid, ldc=self.hid)
+        h = ops.groupnorm(h, self.n_groups, self.gn[0], self.gn[1], 1e-5, act=ops.ACT_HARDSWISH, out=h)
+        sc = x if self.sc is None else ops.linear(x, self.sc)
+        y = torch.empty((B, T, self.cout), dtype=torch.float32, device=x.device)
+        ops.conv_gemm(h, self.w2, y, M=T, N=self.cout, K=3 * self.hid, Zb=B, sAb=T * self.hid, ldx=self.hid, stride=1,
+                      pad=1, Cg=self.hid, Tin=T, R=sc, sRb=T * self.cout, ldr=self.cout, sCb=T * self.cout,
+                      ldc=self.cout)
+        return ops.layernorm(y, self.ln[0], self.ln[1], 1e-5, act=ops.ACT_HARDSWISH, out=y)
+
+
+class _Down:
+    def __init__(self, sd, pre, dev):
+        w = _t(sd[pre + "conv.weight"]).float()       # [Cout, Cin, f]
+        self.cout, self.cin, self.f = w.shape
+        self.w = w.permute(0, 2, 1).reshape(self.cout, -1).contiguous().to(dev)
+        self.b = _t(sd[pre + "conv.bias"]).float().contiguous().to(dev)
+
+    def __call__(self, x):
+        B, T, _ = x.shape
+        assert T % self.f == 0, "T is pre-padded to a multiple of factor**times (unet.py:103-106)"
+        To = T // self.f
+        y = torch.empty((B, To, self.cout), dtype=torch.float32, device=x.device)
+        ops.conv_gemm(x, self.w, y, M=To, N=self.cout, K=self.f * self.cin, Zb=B, sAb=T * self.cin, ldx=self.cin,
+                      stride=self.f, Cg=self.cin, Tin=T, bias=self.b, sCb=To * self.cout, ldc=self.cout)
+        return y
+
+
+class _Up:
+    def __init__(self, sd, pre, dev):
+        w = _t(sd[pre + "conv.weight"]).float()       # ConvTranspose1d: [Cin, Cout, f]
+        self.cin, self.cout, self.f = w.shape
+        # out[f*t + j, o] = sum_c x[t, c] w[c, o, j] + b[o]  ->  W'[(j, o), c]
+        self.w = w.permute(2, 1, 0).reshape(self.f * self.cout, self.cin).contiguous().to(dev)
+        b = _t(sd[pre + "conv.bias"]).float()
+        self.b = b.repeat(self.f).contiguous().to(dev)
+
+    def __call__(self, x):
+        B, T, _ = x.shape
+        y = ops.linear(x, self.w, self.b)
+        return y.view(B, T * self.f, self.cout)
+
+
+class LatticeHead:
+    """UNet backbone + linear head: features [B, T_pad, C_in] -> logits [B, T_pad, V+2]."""
+
+    def __init__(self, arch: UNetArch, state_dict: dict, device="cuda"):
+        dev = torch.device(device)
+        self.arch = arch
+        sd = {k[len("backbone."):] if k.startswith("backbone.") else k: v for k, v in state_dict.items()}
+        self.divisible = arch.factor ** arch.times
+        self.encoders = [[_Block(sd, "encoders.0.", dev)]]
+        for i in range(1, arch.times):
+            self.encoders.append([_Down(sd, f"encoders.{i}.0.", dev), _Block(sd, f"encoders.{i}.1.", dev)])
+        self.bottleneck = [_Down(sd, "bottle_neck.0.", dev), _Block(sd, "bottle_neck.1.", dev),
+                           _Up(sd, "bottle_neck.2.", dev)]
+        self.decoders = []
+        for i in range(arch.times - 1):
+            self.decoders.append([_Block(sd, f"decoders.{i}.0.", dev), _Up(sd, f"decoders.{i}.1.", dev)])
+        self.decoders.append([_Block(sd, f"decoders.{arch.times - 1}.", dev)])
+        self.head_w = _t(sd["head.weight"]).float().contiguous().to(dev)
+        self.head_b = _t(sd["head.bias"]).float().contiguous().to(dev)
+        self.vocab_size = self.head_w.shape[0] - 2
+
+    def padded_len(self, T: int) -> int:
+        r = T % self.divisible
+        return T if r == 0 else T + self.divisible - r
+
+    @staticmethod
+    def _seq(mods, x):
+        for m in mods:
+            x = m(x)
+        return x
+
+    @torch.no_grad()
+    def backbone(self, x: torch.Tensor) -> torch.Tensor:
+        """x [B, T_pad, C_in] with T_pad % factor**times == 0 (zero rows beyond the real T)."""
+        h = [x]
+        for enc in self.encoders:
+            h.append(self._seq(enc, h[-1]))
+        y = self._seq(self.bottleneck, h[-1])
+        for i, dec in enumerate(self.decoders):
+            y = self._seq(dec, ops.add(y, h[-1 - i]))
+        return y
+
+    @torch.no_grad()
+    def logits(self, x: torch.Tensor) -> torch.Tensor:
+        return ops.linear(self.backbone(x), self.head_w, self.head_b)
+
+    @staticmethod
+    def split(logits: torch.Tensor):
+        """(ph_frame_logits, ph_edge_logits, ctc_logits) views, forced_alignment.py:287-292."""
+        return logits[:, :, 2:], logits[:, :, 0], torch.cat([logits[:, :, [1]], logits[:, :, 3:]], dim=-1)
+
+    def flops(self, T_pad: int) -> float:
+        a = self.arch
+        f = 0.0
+
+        def blk(T, ci, co):
+            hid = max(16 * (co // 16), 16)
+            return 2.0 * T * (3 * ci * hid + 3 * hid * co + (ci * co if ci != co else 0))
+        T = T_pad
+        f += blk(T, a.input_dims, a.hidden_dims)
+        for i in range(1, a.times):
+            T //= a.factor
+            f += 2.0 * T * a.ch(i - 1) * a.ch(i) * a.factor + blk(T, a.ch(i), a.ch(i))
+        Tb = T // a.factor
+        f += 2.0 * Tb * a.ch(a.times - 1) * a.ch(a.times) * a.factor + blk(Tb, a.ch(a.times), a.ch(a.times))
+        f += 2.0 * Tb * a.ch(a.times) * a.ch(a.times - 1) * a.factor
+        for i in range(1, a.times):
+            f += blk(T, a.ch(a.times - i), a.ch(a.times - i)) + 2.0 * T * a.ch(a.times - i) * a.ch(a.times - i - 1) * a.factor
+            T *= a.factor
+        f += blk(T, a.hidden_dims, a.output_dims)
+        f += 2.0 * T * a.output_dims * (a.vocab_size + 2)
+        return f
