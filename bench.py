@@ -1,0 +1,208 @@
+#!/usr/bin/env python
+"""bench.py — BASELINE.json config 2: B=32 x 10 s 16 kHz utterances, Hubert-base (cnhubert), 1 MI355X.
+
+One step = the whole infer path for one batch, wave in HBM -> phoneme boundaries on the host:
+  16k->44.1k sinc resample (load_wav) -> 44.1k->16k sinc resample (UnitsEncoder) -> Hubert-base (7 convs,
+  projection, positional conv, 12 post-LN layers) -> nearest-frame gather -> UNet + head -> lattice prologue
+  -> Viterbi DP -> backtrack -> device->host copy -> interval/word assembly (+ RCCL gather of boundary arrays
+  when N > 1).  All arithmetic is f32 (the parity configuration).  Weights are seeded synthetic (no checkpoint
+  offline), inputs are synthetic harmonic audio + 30 two-phone words (S = 91).
+
+Multi-GPU: one process per GPU (torch.distributed.run); each rank aligns its own B utterances (weak scaling);
+the only collective is the boundary-array all_gather.  Timing: barrier + synchronize on both sides of exactly
+K steps, max over ranks.
+
+Also reported (rank 0):
+  * roofline of the dominant kernel (gemm_f32_kernel<1, true>: the GELU-epilogue implicit GEMM = conv1..6 + FFN
+    up-projections, ~2/3 of all FLOPs): algorithmic FLOPs per launch / average launch time (HIP events on the
+    launching stream over the timed steps) against the 157.3 TFLOP/s f32 MFMA peak;
+  * cpu_baseline (N = 1 only): the CPU oracle (torch-CPU fp32 modules on the host threads + the C Viterbi) on a
+    bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "aligned audio sec/sec (RTF^-1) + frames/sec, Hubert-base, 1/2/4/8 MI355X"
+F32_MFMA_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="utterances per GPU per step")
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--words", type=int, default=30)
+    ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="CPU baseline time budget (seconds)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe", default="gemm_f32_kernel<1, true>")
+    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
+                    help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def make_inputs(B, seconds, words, seed0):
+    import numpy as np
+    from hubertfa_amd import synth
+    n16 = int(round(seconds * 16000))
+    wav = np.stack([synth.synth_audio(n16, 16000, seed=seed0 + i) for i in range(B)])
+    d = synth.synth_dictionary(n_words=400)
+    two = sorted(w for w, p in d.items() if len(p) == 2)
+    r = synth.rng(seed0 + 12345)
+    ph_seqs, word_seqs, p2ws = [], [], []
+    for i in range(B):
+        ws = [two[int(j)] for j in r.integers(0, len(two), words)]
+        ph, p2w = ["SP"], [-1]
+        for wi, w in enumerate(ws):
+            for p in d[w]:
+                ph.append(p)
+                p2w.append(wi)
+            ph.append("SP")
+            p2w.append(-1)
+        ph_seqs.append(ph)
+        word_seqs.append(ws)
+        p2ws.append(p2w)
+    return wav, ph_seqs, word_seqs, p2ws
+
+
+def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s):
+    """CPU oracle on a bounded sample (whole utterances until the budget is spent)."""
+    import numpy as np
+    import torch
+    from hubertfa_amd import synth
+    from oracle import decode as odec, hubert_cpu, resample as ores
+    hp = ckpt["hyper_parameters"]
+    import yaml
+    vocab = yaml.safe_load(hp["vocab_text"])
+    arch = synth.arch_cnhubert_base()
+    sd = synth.synth_hubert_state_dict(arch, seed=0)
+    ua = synth.UNetArch(vocab_size=vocab["vocab_size"])
+    usd = {k: v.numpy() for k, v in ckpt["state_dict"].items()}
+    threads = torch.get_num_threads()
+    done, t0 = 0, time.perf_counter()
+    while done < len(wav):
+        x16 = torch.from_numpy(wav[done:done + 1])
+        x44 = ores.resample(x16, 16000, 44100, 6)
+        xr = ores.resample(x44, 44100, 16000, 128)
+        units = hubert_cpu.hubert_forward(arch, sd, xr)
+        n44 = x44.shape[-1]
+        n_frames = n44 // 512 + 1
+        ratio = (512 / 44100) / (320 / 16000)
+        idx = torch.clamp(torch.round(ratio * torch.arange(n_frames)).long(), max=units.shape[1] - 1)
+        feats = units[:, idx]
+        logits = hubert_cpu.unet_head_forward(ua, usd, feats)
+        odec.decode(vocab, logits[:, :, 2:], logits[:, :, 0], n44 / 44100, ph_seqs[done], word_seqs[done],
+                    p2ws[done])
+        done += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    el = time.perf_counter() - t0
+    secs = done * wav.shape[1] / 16000
+    return {"value": secs / el, "unit": "audio_s/s", "cores": threads, "kind": "port",
+            "sample": f"{done} x {wav.shape[1] / 16000:.0f} s utterances of the same workload, sequential B=1 "
+                      f"(oracle: torch-CPU fp32 resample+Hubert-base+UNet, C Viterbi), {el:.1f} s wall"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from hubertfa_amd import ops
+    from hubertfa_amd.distributed import env_rank_world, gather_boundaries
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+
+    rank, world, local = env_rank_world()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
+    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
+    task.on_predict_start()
+    B = args.batch
+    wav_np, ph_seqs, word_seqs, p2ws = make_inputs(B, args.seconds, args.words, seed0=1000 * (rank + 1))
+    wav = torch.from_numpy(wav_np).to(dev)
+
+    def step():
+        dev_out = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False)
+        if world > 1:
+            gather_boundaries(dev_out)
+        return task.decoder.assemble(dev_out, ph_seqs, word_seqs, p2ws)
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+    probe = ops.KernelProbe(args.probe)
+    ops.PROBE = probe
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ops.PROBE = None
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    n_frames = res[0]["T"]
+    audio_s = world * B * args.seconds * args.steps
+    value = audio_s / el
+    frames_ps = world * B * n_frames * args.steps / el
+    ps = probe.summary()
+    achieved = ps["avg_flops"] / (ps["avg_ms"] * 1e-3) / 1e12 if ps["launches"] else None
+    hub_flops = task.unitsEncoder.model.flops(int(round(args.seconds * 16000)))
+    head_flops = task.head.flops(task.head.padded_len(n_frames))
+
+    traffic = None
+    if os.path.exists(args.traffic_file):
+        try:
+            with open(args.traffic_file) as f:
+                tj = json.load(f)
+            if tj.get("kernel") == args.probe:
+                traffic = tj.get("bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"config 2: B={B} x {args.seconds:g} s 16 kHz utterances per GPU, Hubert-base "
+                               f"(cnhubert arch) + UNet head + Viterbi; full infer path wave(HBM)->boundaries(host)",
+                   "global_batch": world * B, "seconds_per_utterance": args.seconds, "dp_frames": n_frames,
+                   "states": len(ph_seqs[0]), "parallelism": f"utterance-dp{world}"},
+        "frames_per_s": frames_ps,
+        "realtime_factor": value,
+        "encoder_tflops": world * B * (hub_flops + head_flops) * args.steps / el / 1e12,
+        "roofline": {"bound": "mfma", "kernel": args.probe, "achieved": achieved, "peak": F32_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / F32_MFMA_PEAK_TFLOPS if achieved else None,
+                     "traffic": traffic, "launches": ps["launches"], "avg_launch_ms": ps["avg_ms"],
+                     "flops_per_launch": ps["avg_flops"]},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(wav_np, ph_seqs, word_seqs, p2ws, ckpt, args.cpu_sample_s)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -125,16 +125,25 @@ class AlignmentDecoder:
         dp, bt, curr = self.init_dp(lat["prob_log"], ids_t, S_t)
         ops.viterbi_forward(lat["prob_log"], lat["not_edge_log"], lat["edge_log"], curr, dp, bt, ids_t, T_t, S_t)
         idx, tint, n, fc = ops.viterbi_backtrack(dp, bt, ids_t, T_t, S_t)
+        dev_out = dict(ph_idx_seq=idx, ph_time_int=tint, n=n, frame_confidence=fc, edge_diff=lat["edge_diff"],
+                       T=Ts, lattice=lat)
         if not host:
-            return dict(ph_idx_seq=idx, ph_time_int=tint, n=n, frame_confidence=fc, edge_diff=lat["edge_diff"],
-                        T=T_t, lattice=lat)
-        # one device->host copy of the small per-utterance arrays
-        idx_h, tint_h, n_h, fc_h = idx.cpu().numpy(), tint.cpu().numpy(), n.cpu().numpy(), fc.cpu().numpy()
-        ed_h = lat["edge_diff"].cpu().numpy()
+            return dev_out
+        return self.assemble(dev_out, ph_seqs, word_seqs, p2ws, keep_frame_probs)
+
+    def assemble(self, dev_out, ph_seqs, word_seqs=None, p2ws=None, keep_frame_probs: bool = False):
+        """Host half of decode for a batch: one D2H copy, then per-utterance interval/word assembly."""
+        Ts = dev_out["T"]
+        lat = dev_out["lattice"]
+        idx_h = dev_out["ph_idx_seq"].cpu().numpy()
+        tint_h = dev_out["ph_time_int"].cpu().numpy()
+        n_h = dev_out["n"].cpu().numpy()
+        fc_h = dev_out["frame_confidence"].cpu().numpy()
+        ed_h = dev_out["edge_diff"].cpu().numpy()
         ep_h = lat["edge_prob"].cpu().numpy() if keep_frame_probs else None
         fp_h = lat["ph_frame_pred"].cpu().numpy() if keep_frame_probs else None
         out = []
-        for b in range(B):
+        for b in range(len(ph_seqs)):
             T = Ts[b]
             ph_seq = ph_seqs[b]
             ws = word_seqs[b] if word_seqs is not None and word_seqs[b] is not None else ph_seq

@@ -1,0 +1,121 @@
+"""Drop-in ``UnitsEncoder`` (reference: tools/encoder.py:10-60) on the HIP Hubert encoders.
+
+``UnitsEncoder(encoder, encoder_ckpt, encoder_sample_rate=16000, encoder_hop_size=320, device=None)`` and
+``.encode(audio[B, N], sample_rate, hop_size) -> [B, C, T]`` keep the reference signature and semantics:
+  1. resample ``sample_rate -> encoder_sample_rate`` with a 128-wide sinc (encoder.py:41-48),
+  2. the <400-sample pad applied to the ORIGINAL audio, exactly as the reference does (encoder.py:51-52),
+  3. the model ('cnhubert' = HF HubertModel folder, 'hubertsoft' = bshall .pt; encoder.py:17-22),
+  4. nearest-index gather onto the hop grid (encoder.py:55-59).
+``encode_frames`` returns the channels-last, zero-padded [B, T_pad, C] tensor the lattice head consumes, which
+saves the reference's transpose round trip.
+
+Model locations: a HF folder (config.json, model.safetensors | pytorch_model.bin, preprocessor_config.json),
+a bshall checkpoint (``torch.load(path)["hubert"]``), or ``synth:<seed>`` for seeded synthetic weights.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import torch
+
+from . import ops, synth
+from .hubert import HubertEncoder
+from .resample import Resampler
+
+
+def _load_tensors(path: str) -> dict:
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        return load_file(path)
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def arch_from_hf_config(cfg: dict, do_normalize: bool) -> synth.HubertArch:
+    if cfg.get("hidden_act", "gelu") != "gelu" or cfg.get("feat_extract_activation", "gelu") != "gelu":
+        raise ValueError("only erf-GELU Hubert configs are supported")
+    if cfg.get("conv_pos_batch_norm", False):
+        raise ValueError("conv_pos_batch_norm Hubert variants are not supported")
+    return synth.HubertArch(
+        layout="hf", hidden=cfg.get("hidden_size", 768), layers=cfg.get("num_hidden_layers", 12),
+        heads=cfg.get("num_attention_heads", 12), ffn=cfg.get("intermediate_size", 3072),
+        conv_dim=tuple(cfg.get("conv_dim", (512,) * 7)), conv_kernel=tuple(cfg.get("conv_kernel", (10, 3, 3, 3, 3, 2, 2))),
+        conv_stride=tuple(cfg.get("conv_stride", (5, 2, 2, 2, 2, 2, 2))),
+        feat_extract_norm=cfg.get("feat_extract_norm", "group"), conv_bias=cfg.get("conv_bias", False),
+        stable_layer_norm=cfg.get("do_stable_layer_norm", False),
+        pos_kernel=cfg.get("num_conv_pos_embeddings", 128), pos_groups=cfg.get("num_conv_pos_embedding_groups", 16),
+        layer_norm_eps=cfg.get("layer_norm_eps", 1e-5), do_normalize=do_normalize)
+
+
+def load_hubert(encoder: str, encoder_ckpt: str, device) -> HubertEncoder:
+    """Build a HIP Hubert from the reference's encoder name + checkpoint location (encoder.py:17-30)."""
+    if encoder_ckpt.startswith("synth:"):
+        seed = int(encoder_ckpt.split(":", 1)[1] or 0)
+        arch = {"cnhubert": synth.arch_cnhubert_base, "cnhubert-large": synth.arch_cnhubert_large,
+                "hubertsoft": synth.arch_hubertsoft}[encoder]()
+        return HubertEncoder(arch, synth.synth_hubert_state_dict(arch, seed=seed), device)
+    if encoder in ("cnhubert", "cnhubert-large"):
+        with open(os.path.join(encoder_ckpt, "config.json")) as f:
+            cfg = json.load(f)
+        do_norm = True   # Wav2Vec2FeatureExtractor default
+        pp = os.path.join(encoder_ckpt, "preprocessor_config.json")
+        if os.path.exists(pp):
+            with open(pp) as f:
+                do_norm = bool(json.load(f).get("do_normalize", True))
+        for name in ("model.safetensors", "pytorch_model.bin"):
+            p = os.path.join(encoder_ckpt, name)
+            if os.path.exists(p):
+                return HubertEncoder(arch_from_hf_config(cfg, do_norm), _load_tensors(p), device)
+        raise FileNotFoundError(f"no model.safetensors / pytorch_model.bin in {encoder_ckpt}")
+    if encoder == "hubertsoft":
+        ckpt = _load_tensors(encoder_ckpt)
+        return HubertEncoder(synth.arch_hubertsoft(), ckpt["hubert"] if "hubert" in ckpt else ckpt, device)
+    raise ValueError(f" [x] Unknown units encoder: {encoder}")
+
+
+class UnitsEncoder:
+    def __init__(self, encoder, encoder_ckpt, encoder_sample_rate=16000, encoder_hop_size=320, device=None):
+        if device is None:
+            device = "cuda"
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("hubertfa_amd runs on the GPU only (no CPU fallback)")
+        self.model = load_hubert(encoder, encoder_ckpt, self.device)
+        self.resample_kernel = {}
+        self.encoder_sample_rate = encoder_sample_rate
+        self.encoder_hop_size = encoder_hop_size
+
+    def _resample(self, audio, sample_rate):
+        if sample_rate == self.encoder_sample_rate:
+            return audio
+        key = str(sample_rate)
+        if key not in self.resample_kernel:
+            self.resample_kernel[key] = Resampler(sample_rate, self.encoder_sample_rate, 128, self.device)
+        return self.resample_kernel[key](audio)
+
+    def grid(self, n_samples: int, sample_rate: int, hop_size: int):
+        n_frames = n_samples // hop_size + 1
+        ratio = (hop_size / sample_rate) / (self.encoder_hop_size / self.encoder_sample_rate)
+        return n_frames, ratio
+
+    @torch.no_grad()
+    def units(self, audio: torch.Tensor, sample_rate: int) -> torch.Tensor:
+        audio = audio.to(self.device).float()
+        if audio.dim() == 1:
+            audio = audio[None]
+        audio_res = self._resample(audio, sample_rate)
+        if audio_res.size(-1) < 400:   # reference pads the ORIGINAL audio here (encoder.py:51-52)
+            audio_res = torch.nn.functional.pad(audio, (0, 400 - audio_res.size(-1)))
+        return self.model(audio_res.contiguous())
+
+    @torch.no_grad()
+    def encode_frames(self, audio: torch.Tensor, sample_rate: int, hop_size: int, pad_to: int = 1):
+        """[B, N] -> (features [B, T_pad, C] channels-last, n_frames); rows >= n_frames are zero."""
+        units = self.units(audio, sample_rate)
+        n_frames, ratio = self.grid(audio.shape[-1], sample_rate, hop_size)
+        T_pad = (n_frames + pad_to - 1) // pad_to * pad_to
+        return ops.units_gather(units.contiguous(), n_frames, T_pad, ratio), n_frames
+
+    def encode(self, audio, sample_rate, hop_size):
+        feats, n = self.encode_frames(audio, sample_rate, hop_size)
+        return feats[:, :n].transpose(1, 2)   # [B, C, T] like the reference

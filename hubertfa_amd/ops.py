@@ -137,14 +137,55 @@ _lib.register("hfa_resample_workspace_bytes", [_I_, _I_, _I_, _I_], ctypes.c_lon
 _lib.register("hfa_resample_f32", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _I_, _I_, _P_, _P_, _LL_, _P_])
 
 
+class KernelProbe:
+    """Times every launch of one kernel instantiation with HIP events on the launching stream (bench.py).
+
+    ``name`` is the rocprof kernel symbol stem, e.g. ``gemm_f32_kernel<1, true>``; per launch the algorithmic
+    FLOPs are recorded next to the event pair, so achieved = sum(flops) / sum(durations)."""
+
+    def __init__(self, name: str):
+        self.name = name
+        self.records = []
+
+    def __call__(self, name: str, flops: float, launch):
+        if name != self.name:
+            return launch()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        launch()
+        e.record()
+        self.records.append((s, e, flops))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        n = len(self.records)
+        ms = sum(s.elapsed_time(e) for s, e, _ in self.records)
+        fl = sum(f for _, _, f in self.records)
+        return {"launches": n, "total_ms": ms, "avg_ms": ms / max(n, 1), "flops": fl,
+                "avg_flops": fl / max(n, 1)}
+
+
+PROBE = None
+
+
+def _gemm_name(epilogue: int, A, ldx: int, sAb: int, sAg: int) -> str:
+    vec = A.data_ptr() % 16 == 0 and ldx % 4 == 0 and sAb % 4 == 0 and sAg % 4 == 0
+    return f"gemm_f32_kernel<{epilogue}, {'true' if vec else 'false'}>"
+
+
 def conv_gemm(A, W, C, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None, Tin=None, sWg=0,
               ldw=None, bias=None, sBg=0, R=None, sRb=0, sRg=0, ldr=0, sCb=0, sCg=0, ldc, epilogue=EPI_NONE):
     """Implicit-GEMM conv / Linear on MFMA (see gemm.hip for the exact A/W/C addressing)."""
     for t, n in ((A, "A"), (W, "W"), (C, "C")):
         _need(t, torch.float32, n, contiguous=False)
-    _lib.call("hfa_conv_gemm_f32", M, N, K, Zb, G, _ptr(A), sAb, sAg, ldx, stride, pad, Cg or K,
-              Tin if Tin is not None else M, _ptr(W), sWg, ldw if ldw is not None else K, _ptr(bias), sBg, _ptr(R),
-              sRb, sRg, ldr, _ptr(C), sCb, sCg, ldc, epilogue, _stream(C.device))
+
+    def launch():
+        _lib.call("hfa_conv_gemm_f32", M, N, K, Zb, G, _ptr(A), sAb, sAg, ldx, stride, pad, Cg or K,
+                  Tin if Tin is not None else M, _ptr(W), sWg, ldw if ldw is not None else K, _ptr(bias), sBg,
+                  _ptr(R), sRb, sRg, ldr, _ptr(C), sCb, sCg, ldc, epilogue, _stream(C.device))
+    if PROBE is None:
+        return launch()
+    PROBE(_gemm_name(epilogue, A, ldx, sAb, sAg), 2.0 * M * N * K * Zb * G, launch)
 
 
 def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
@@ -158,8 +199,14 @@ def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
     o2 = out.view(-1, N)
     r2 = residual.reshape(-1, N) if residual is not None else None
     _need(W, torch.float32, "W")
-    _lib.call("hfa_gemm_f32", M, N, K, _ptr(x2), x2.stride(0), _ptr(W), W.stride(0), _ptr(bias), _ptr(r2),
-              r2.stride(0) if r2 is not None else 0, _ptr(o2), o2.stride(0), epilogue, _stream(x.device))
+
+    def launch():
+        _lib.call("hfa_gemm_f32", M, N, K, _ptr(x2), x2.stride(0), _ptr(W), W.stride(0), _ptr(bias), _ptr(r2),
+                  r2.stride(0) if r2 is not None else 0, _ptr(o2), o2.stride(0), epilogue, _stream(x.device))
+    if PROBE is None:
+        launch()
+    else:
+        PROBE(_gemm_name(epilogue, x2, x2.stride(0), 0, 0), 2.0 * M * N * K, launch)
     return out
 
 

@@ -1,0 +1,137 @@
+"""Inference surface of ``LitForcedAlignmentTask`` without Lightning (networks/task/forced_alignment.py).
+
+Kept: ``load_from_checkpoint(path)`` (reads ``state_dict`` + ``hyper_parameters`` of a Lightning .ckpt),
+``forward(x[B,T,C]) -> (ph_frame_logits, ph_edge_logits, ctc_logits)`` (:284-292), ``on_predict_start`` (:143-152),
+``predict_step(batch, batch_idx)`` (:154-186) with the same 7-tuple result.  Training/validation/losses are out
+of scope; loss-module buffers in the checkpoint are ignored.
+
+Added: ``align_batch`` — B equal-length utterances through one pass of GPU kernels (resample, Hubert, gather,
+UNet+head, lattice prologue, DP, backtrack), the path the benchmark and the batched CLI use.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import yaml
+
+from . import synth
+from .alignment_decoder import AlignmentDecoder
+from .encoder import UnitsEncoder
+from .resample import Resampler
+from .unet import LatticeHead
+from .wav_io import load_wav
+
+
+class ForcedAlignmentTask:
+    def __init__(self, vocab_text, vowel_text, model_config, hubert_config, melspec_config, optimizer_config=None,
+                 loss_config=None, *, state_dict=None, device="cuda"):
+        self.hparams = dict(vocab_text=vocab_text, vowel_text=vowel_text, model_config=model_config,
+                            hubert_config=hubert_config, melspec_config=melspec_config,
+                            optimizer_config=optimizer_config, loss_config=loss_config)
+        self.device = torch.device(device)
+        self.vocab = yaml.safe_load(vocab_text)
+        self.vowel = yaml.safe_load(vowel_text) if vowel_text else None
+        self.ignored_phones = self.vocab.get("ignored_phonemes", [])
+        self.melspec_config = melspec_config
+        self.hubert_config = hubert_config
+        arch = synth.UNetArch(input_dims=hubert_config["channel"], hidden_dims=model_config["hidden_dims"],
+                              output_dims=model_config["hidden_dims"],
+                              factor=model_config["down_sampling_factor"], times=model_config["down_sampling_times"],
+                              scaleup=model_config["channels_scaleup_factor"], vocab_size=self.vocab["vocab_size"])
+        if state_dict is None:
+            raise ValueError("state_dict (backbone.*, head.*) is required")
+        sd = {k: v for k, v in state_dict.items() if k.startswith("backbone.") or k.startswith("head.")}
+        self.head = LatticeHead(arch, sd, self.device)
+        self.decoder = AlignmentDecoder(self.vocab, self.melspec_config)
+        self.unitsEncoder = None
+        self._upsamplers = {}
+
+    # -- checkpoint ---------------------------------------------------------------------------------------------
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, device="cuda", hubert_model_path=None):
+        ckpt = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+        hp = dict(ckpt["hyper_parameters"])
+        if hubert_model_path is not None:
+            hp["hubert_config"] = dict(hp["hubert_config"], model_path=hubert_model_path)
+        return cls(hp["vocab_text"], hp.get("vowel_text"), hp["model_config"], hp["hubert_config"],
+                   hp["melspec_config"], hp.get("optimizer_config"), hp.get("loss_config"),
+                   state_dict=ckpt["state_dict"], device=device)
+
+    # -- reference surface --------------------------------------------------------------------------------------
+    def on_predict_start(self):
+        if self.unitsEncoder is None:
+            hc = self.hubert_config
+            self.unitsEncoder = UnitsEncoder(hc["encoder"], hc["model_path"], hc["sample_rate"], hc["hop_size"],
+                                             self.device)
+
+    @torch.no_grad()
+    def forward(self, x):
+        """x [B, T, C] -> (ph_frame_logits [B,T,V], ph_edge_logits [B,T], ctc_logits [B,T,V])."""
+        x = x.to(self.device).float()
+        T = x.shape[1]
+        Tp = self.head.padded_len(T)
+        if Tp != T:
+            x = torch.nn.functional.pad(x, (0, 0, 0, Tp - T))
+        logits = self.head.logits(x.contiguous())[:, :T]
+        return LatticeHead.split(logits)
+
+    __call__ = forward
+
+    def predict_step(self, batch, batch_idx=0):
+        wav_path, ph_seq, word_seq, ph_idx_to_word_idx = batch
+        sr = self.melspec_config["sample_rate"]
+        waveform = load_wav(wav_path, self.device, sr)
+        wav_length = waveform.shape[0] / sr
+        res = self.align_batch(waveform[None], [ph_seq], [word_seq], [ph_idx_to_word_idx])[0]
+        return (wav_path, wav_length, res["confidence"], res["ph_seq"], res["ph_intervals"], res["word_seq"],
+                res["word_intervals"])
+
+    # -- batched GPU path ---------------------------------------------------------------------------------------
+    def upsampler(self, sr: int):
+        target = self.melspec_config["sample_rate"]
+        if sr not in self._upsamplers:
+            self._upsamplers[sr] = Resampler(sr, target, 6, self.device)
+        return self._upsamplers[sr]
+
+    @torch.no_grad()
+    def align_batch(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
+                    host: bool = True):
+        """B equal-length waveforms [B, N] (at melspec sample_rate, or ``wav_sr`` to resample first, like
+        load_wav) -> list of decode results (dicts with ph_seq / ph_intervals / word_seq / word_intervals /
+        confidence / raw path)."""
+        self.on_predict_start()
+        sr = self.melspec_config["sample_rate"]
+        hop = self.melspec_config["hop_length"]
+        waves = waves.to(self.device).float()
+        if wav_sr is not None and wav_sr != sr:
+            waves = self.upsampler(wav_sr)(waves)
+        n = waves.shape[-1]
+        feats, n_frames = self.unitsEncoder.encode_frames(waves, sr, hop, pad_to=self.head.divisible)
+        logits = self.head.logits(feats)
+        frame, edge, _ = LatticeHead.split(logits[:, :n_frames])
+        wl = [n / sr] * waves.shape[0]
+        return self.decoder.decode_batch(frame, edge, wl, ph_seqs, word_seqs, p2ws, host=host)
+
+
+def synth_checkpoint(path: str | None = None, *, encoder="cnhubert", model_path="synth:0", seed=1,
+                     n_phones: int = 62) -> dict:
+    """A Lightning-layout checkpoint dict with seeded weights (optionally saved to ``path``)."""
+    vocab = synth.synth_vocab(n_phones)
+    channel = 256 if encoder == "hubertsoft" else (1024 if encoder == "cnhubert-large" else 768)
+    ua = synth.UNetArch(input_dims=channel, vocab_size=vocab["vocab_size"])
+    sd = {k: torch.from_numpy(v) for k, v in synth.synth_unet_state_dict(ua, seed=seed).items()}
+    hp = {
+        "vocab_text": yaml.safe_dump(vocab),
+        "vowel_text": yaml.safe_dump({"vowel": []}),
+        "model_config": {"hidden_dims": ua.hidden_dims, "down_sampling_factor": ua.factor,
+                         "down_sampling_times": ua.times, "channels_scaleup_factor": ua.scaleup},
+        "hubert_config": {"encoder": encoder, "model_path": model_path, "sample_rate": 16000, "hop_size": 320,
+                          "channel": channel},
+        "melspec_config": {"n_mels": 128, "sample_rate": 44100, "win_length": 1024, "hop_length": 512,
+                           "n_fft": 2048, "fmin": 40, "fmax": 16000, "clamp": 0.00001},
+        "optimizer_config": {}, "loss_config": {},
+    }
+    ckpt = {"state_dict": sd, "hyper_parameters": hp}
+    if path is not None:
+        torch.save(ckpt, path)
+    return ckpt

@@ -1,0 +1,66 @@
+"""End-to-end parity of the GPU infer path (wave -> boundaries) against the CPU oracle at config-2 geometry.
+
+Bars (north star): per-frame log-probs within 1e-4 (fp32); phoneme boundary indices bit-exact with the CPU
+reference path.  Boundary exactness is asserted per utterance; the lattice difference that could break it is
+bounded by the log-prob check.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _inputs(B, seconds, words, seed0):
+    import bench
+    return bench.make_inputs(B, seconds, words, seed0)
+
+
+def test_full_path_logprobs_and_boundaries_vs_oracle():
+    import yaml
+    from hubertfa_amd import synth
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+    from oracle import decode as odec, hubert_cpu, resample as ores
+    dev = torch.device("cuda")
+    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
+    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
+    vocab = yaml.safe_load(ckpt["hyper_parameters"]["vocab_text"])
+    B = 3
+    wav, ph_seqs, word_seqs, p2ws = _inputs(B, 10.0, 30, 777)
+    task.on_predict_start()
+    dev_out = task.align_batch(torch.from_numpy(wav).to(dev), ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False)
+    res = task.decoder.assemble(dev_out, ph_seqs, word_seqs, p2ws)
+    gpu_pl = dev_out["lattice"]["prob_log"].cpu().numpy()
+    arch = synth.arch_cnhubert_base()
+    sd = synth.synth_hubert_state_dict(arch, seed=0)
+    ua = synth.UNetArch(vocab_size=vocab["vocab_size"])
+    usd = {k: v.numpy() for k, v in ckpt["state_dict"].items()}
+    worst = 0.0
+    for b in range(B):
+        x44 = ores.resample(torch.from_numpy(wav[b:b + 1]), 16000, 44100, 6)
+        units = hubert_cpu.hubert_forward(arch, sd, ores.resample(x44, 44100, 16000, 128))
+        n44 = x44.shape[-1]
+        nf = n44 // 512 + 1
+        idx = torch.clamp(torch.round(((512 / 44100) / (320 / 16000)) * torch.arange(nf)).long(),
+                          max=units.shape[1] - 1)
+        logits = hubert_cpu.unet_head_forward(ua, usd, units[:, idx])
+        ph, ph_iv, w, w_iv, conf, ex = odec.decode(vocab, logits[:, :, 2:], logits[:, :, 0], n44 / 44100,
+                                                   ph_seqs[b], word_seqs[b], p2ws[b])
+        T = res[b]["T"]
+        assert T == 861
+        ids = np.array([vocab["vocab"][p] for p in ph_seqs[b]])
+        err = np.abs(gpu_pl[b, :T, :len(ids)] - ex["ph_prob_log"][:, ids]).max()
+        worst = max(worst, float(err))
+        assert err < 1e-4, f"utt {b}: per-frame log-prob error {err:.2e} > 1e-4"
+        assert np.array_equal(res[b]["ph_idx_seq"], ex["idx"]), f"utt {b}: phone path differs"
+        assert np.array_equal(res[b]["ph_time_int"], ex["tint"]), f"utt {b}: boundary frames differ"
+        assert list(res[b]["ph_seq"]) == list(ph) and list(res[b]["word_seq"]) == list(w)
+        np.testing.assert_allclose(res[b]["ph_intervals"], ph_iv, atol=1e-5)
+        np.testing.assert_allclose(res[b]["confidence"], conf, rtol=1e-4)
+    print(f"max per-frame log-prob error over {B} x 10 s: {worst:.2e}")
+
+
+def test_smoke_entry():
+    from hubertfa_amd.smoke import run_smoke
+    r = run_smoke()
+    assert r["boundary_exact"] >= 1
