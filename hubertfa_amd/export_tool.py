@@ -1,0 +1,156 @@
+"""Output writers (reference: tools/export_tool.py:7-92).
+
+* ``<wav_dir>/TextGrid/<stem>.TextGrid`` (or ``<out_path>/TextGrid/``) with IntervalTiers ``words`` and ``phones``
+  in Praat long-text format, laid out like the ``textgrid`` PyPI package's ``TextGrid.write`` (gaps filled with
+  empty intervals, xmax = last interval end).  The ``textgrid`` package is absent here, so byte-level parity with
+  it is UNPINNED; the format is Praat's ooTextFile and is read back by tests/test_host.py.
+* ``<wav_dir>/confidence/confidence.csv`` with columns ``name,confidence`` (pandas ``to_csv``, as the reference).
+"""
+from __future__ import annotations
+
+import pathlib
+
+
+class _Interval:
+    __slots__ = ("minTime", "maxTime", "mark")
+
+    def __init__(self, minTime, maxTime, mark):
+        if minTime >= maxTime:   # Praat has no zero/negative-length intervals
+            raise ValueError(minTime, maxTime)
+        self.minTime, self.maxTime, self.mark = minTime, maxTime, mark
+
+
+class IntervalTier:
+    def __init__(self, name=None, minTime=0.0, maxTime=None):
+        self.name, self.minTime, self.maxTime = name, minTime, maxTime
+        self.intervals: list[_Interval] = []
+
+    def add(self, minTime, maxTime, mark):
+        iv = _Interval(minTime, maxTime, mark)
+        if iv.minTime < self.minTime:
+            raise ValueError(self.minTime)
+        if self.maxTime and iv.maxTime > self.maxTime:
+            raise ValueError(self.maxTime)
+        pos = 0
+        while pos < len(self.intervals) and self.intervals[pos].minTime < iv.minTime:
+            pos += 1
+        for nb in self.intervals[max(pos - 1, 0):pos + 1]:
+            if nb.minTime < iv.maxTime and iv.minTime < nb.maxTime:
+                raise ValueError("overlapping intervals", nb.minTime, nb.maxTime, minTime, maxTime)
+        self.intervals.insert(pos, iv)
+
+    def filled(self, null=""):
+        out, prev = [], self.minTime
+        for iv in self.intervals:
+            if prev < iv.minTime:
+                out.append(_Interval(prev, iv.minTime, null))
+            out.append(iv)
+            prev = iv.maxTime
+        if self.maxTime is not None and prev < self.maxTime:
+            out.append(_Interval(prev, self.maxTime, null))
+        return out
+
+
+class TextGrid:
+    def __init__(self, name=None, minTime=0.0, maxTime=None):
+        self.name, self.minTime, self.maxTime = name, minTime, maxTime
+        self.tiers: list[IntervalTier] = []
+
+    def append(self, tier):
+        if self.maxTime is not None and tier.maxTime is not None and tier.maxTime > self.maxTime:
+            raise ValueError(self.maxTime)
+        self.tiers.append(tier)
+
+    def lines(self, null=""):
+        maxT = self.maxTime or max((t.maxTime if t.maxTime else t.intervals[-1].maxTime) for t in self.tiers)
+        yield 'File type = "ooTextFile"'
+        yield 'Object class = "TextGrid"'
+        yield ""
+        yield f"xmin = {self.minTime}"
+        yield f"xmax = {maxT}"
+        yield "tiers? <exists>"
+        yield f"size = {len(self.tiers)}"
+        yield "item []:"
+        for i, tier in enumerate(self.tiers, 1):
+            ivs = tier.filled(null)
+            yield f"\titem [{i}]:"
+            yield '\t\tclass = "IntervalTier"'
+            yield f'\t\tname = "{tier.name}"'
+            yield f"\t\txmin = {tier.minTime}"
+            yield f"\t\txmax = {maxT}"
+            yield f"\t\tintervals: size = {len(ivs)}"
+            for j, iv in enumerate(ivs, 1):
+                yield f"\t\t\tintervals [{j}]:"
+                yield f"\t\t\t\txmin = {iv.minTime}"
+                yield f"\t\t\t\txmax = {iv.maxTime}"
+                yield '\t\t\t\ttext = "{}"'.format(str(iv.mark).replace('"', '""'))
+
+    def write(self, path, null=""):
+        with open(path, "w", encoding="utf-8") as f:
+            for line in self.lines(null):
+                f.write(line + "\n")
+
+
+def read_textgrid(path):
+    """Minimal reader of the long text format written above -> {tier: [(xmin, xmax, text), ...]}."""
+    tiers, cur, iv = {}, None, {}
+    for raw in open(path, encoding="utf-8"):
+        s = raw.strip()
+        if s.startswith("name = "):
+            cur = s[len('name = "'):-1]
+            tiers[cur] = []
+        elif cur is not None and s.startswith("xmin = ") and raw.startswith("\t\t\t\t"):
+            iv = {"xmin": float(s[7:])}
+        elif cur is not None and s.startswith("xmax = ") and raw.startswith("\t\t\t\t"):
+            iv["xmax"] = float(s[7:])
+        elif cur is not None and s.startswith("text = "):
+            tiers[cur].append((iv["xmin"], iv["xmax"], s[len('text = "'):-1].replace('""', '"')))
+    return tiers
+
+
+class Exporter:
+    def __init__(self, predictions, log, out_path=None):
+        self.predictions = predictions
+        self.log = log
+        self.out_path = pathlib.Path(out_path) if out_path else None
+
+    def save_textgrids(self):
+        print("Saving TextGrids...")
+        for wav_path, wav_length, confidence, ph_seq, ph_intervals, word_seq, word_intervals in self.predictions:
+            wav_path = pathlib.Path(wav_path)
+            tg = TextGrid()
+            word_tier = IntervalTier(name="words")
+            ph_tier = IntervalTier(name="phones")
+            for word, (start, end) in zip(word_seq, word_intervals):
+                word_tier.add(start, end, word)
+            for ph, (start, end) in zip(ph_seq, ph_intervals):
+                ph_tier.add(minTime=float(start), maxTime=end, mark=ph)
+            tg.append(word_tier)
+            tg.append(ph_tier)
+            base = self.out_path if self.out_path is not None else wav_path.parent
+            tg_path = base / "TextGrid" / wav_path.with_suffix(".TextGrid").name
+            tg_path.parent.mkdir(parents=True, exist_ok=True)
+            tg.write(tg_path)
+
+    def save_confidence_fn(self):
+        import pandas as pd
+        print("saving confidence...")
+        per_folder = {}
+        for wav_path, _, confidence, *_ in self.predictions:
+            wav_path = pathlib.Path(wav_path)
+            d = per_folder.setdefault(wav_path.parent, {"name": [], "confidence": []})
+            d["name"].append(wav_path.with_suffix("").name)
+            d["confidence"].append(confidence)
+        for folder, data in per_folder.items():
+            path = folder / "confidence"
+            path.mkdir(parents=True, exist_ok=True)
+            pd.DataFrame(data).to_csv(path / "confidence.csv", index=False)
+
+    def export(self, out_formats):
+        self.save_textgrids()
+        if "confidence" in out_formats:
+            self.save_confidence_fn()
+        if self.log:
+            print("error:")
+            for line in self.log:
+                print(line)

@@ -1,0 +1,147 @@
+"""Host-side drop-ins (CPU): G2P plugins and post-processing against the reference goldens, TextGrid/CSV writers,
+WAV I/O, checkpoint round trip, and the multi-rank boundary gather over gloo (world size 2)."""
+import json
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_g2p_plugins_match_reference():
+    from hubertfa_amd.g2p import DictionaryG2P, NoneG2P, PhonemeG2P
+    gold = json.load(open(os.path.join(GOLDEN, "g2p.json")))
+    g = DictionaryG2P(dictionary=os.path.join(GOLDEN, gold["dictionary"]))
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for case in gold["dict"]:
+            if "error" in case:
+                with pytest.raises(Exception):
+                    g(case["text"])
+                continue
+            ph, w, m = g(case["text"])
+            assert (ph, w, [int(x) for x in m]) == (case["ph_seq"], case["word_seq"], case["map"]), case["text"]
+        for name, cls in (("none", NoneG2P), ("phoneme", PhonemeG2P)):
+            for case in gold[name]:
+                if "error" in case:
+                    with pytest.raises(Exception):
+                        cls()(case["text"])
+                    continue
+                ph, w, m = cls()(case["text"])
+                assert list(ph) == case["ph_seq"] and list(w) == case["word_seq"], (name, case["text"])
+                assert [int(x) for x in m] == case["map"]
+
+
+def test_post_processing_matches_reference():
+    from hubertfa_amd.post_processing import post_processing
+    gold = json.load(open(os.path.join(GOLDEN, "postproc.json")))
+    preds = []
+    for i, c in enumerate(gold["cases"]):
+        iv = np.array(c["intervals"], np.float64)
+        preds.append((f"utt{i}.wav", c["wav_length"], 0.5, np.array(c["seq"]), iv.copy(), np.array(c["seq"]),
+                      iv.copy()))
+    res, log = post_processing(preds)
+    assert len(log) == gold["n_errors"]
+    for c, r in zip(gold["cases"], res):
+        assert [str(x) for x in r[3]] == c["ph_seq"] and [str(x) for x in r[5]] == c["word_seq"]
+        np.testing.assert_array_equal(np.asarray(r[4], float), np.asarray(c["ph_intervals"], float))
+        np.testing.assert_array_equal(np.asarray(r[6], float), np.asarray(c["word_intervals"], float))
+
+
+def test_post_processing_collects_errors():
+    from hubertfa_amd.post_processing import post_processing
+    res, log = post_processing([("bad.wav", 1.0, 0.1, np.array([]), np.zeros((0, 2)), np.array([]),
+                                 np.zeros((0, 2)))])
+    assert res == [] and len(log) == 1
+
+
+def test_textgrid_and_confidence_export(tmp_path):
+    import pandas as pd
+    from hubertfa_amd.export_tool import Exporter, read_textgrid
+    from hubertfa_amd.post_processing import post_processing
+    wav = tmp_path / "a" / "utt.wav"
+    wav.parent.mkdir()
+    wav.write_bytes(b"")
+    ph_iv = np.array([[0.05, 0.4], [0.4, 0.9], [1.3, 1.5]])
+    w_iv = np.array([[0.05, 0.9], [1.3, 1.5]])
+    preds, log = post_processing([(wav, 2.0, np.float32(0.25), np.array(["a", "b", 'q"x']), ph_iv,
+                                   np.array(["w1", "w2"]), w_iv)])
+    Exporter(preds, log).export(["textgrid", "confidence"])
+    tg = read_textgrid(tmp_path / "a" / "TextGrid" / "utt.TextGrid")
+    assert [t[2] for t in tg["words"]] == ["w1", "SP", "w2", "SP"]
+    assert [t[2] for t in tg["phones"]] == ["a", "b", "SP", 'q"x', "SP"]
+    assert tg["phones"][0][0] == 0.0 and tg["phones"][-1][1] == 2.0
+    for tier in tg.values():   # contiguous, non-overlapping
+        assert all(abs(a[1] - b[0]) < 1e-12 for a, b in zip(tier[:-1], tier[1:]))
+    df = pd.read_csv(tmp_path / "a" / "confidence" / "confidence.csv")
+    assert list(df.columns) == ["name", "confidence"] and df["name"][0] == "utt"
+
+
+def test_wav_roundtrip(tmp_path):
+    from hubertfa_amd import synth
+    from hubertfa_amd.wav_io import read_wav, write_wav
+    x = synth.synth_audio(4000, seed=2)
+    p = tmp_path / "x.wav"
+    write_wav(p, x, 16000)
+    y, sr = read_wav(p)
+    assert sr == 16000 and y.shape == (1, 4000)
+    np.testing.assert_array_equal(y[0], x)   # synth audio is already s16-quantised
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    import torch
+    from hubertfa_amd.task import synth_checkpoint
+    p = tmp_path / "m.ckpt"
+    ck = synth_checkpoint(str(p))
+    loaded = torch.load(p, map_location="cpu", weights_only=True)
+    assert set(loaded["state_dict"]) == set(ck["state_dict"])
+    assert loaded["hyper_parameters"]["hubert_config"]["encoder"] == "cnhubert"
+
+
+def test_lpt_sharding_balances():
+    from hubertfa_amd.distributed import shard_lpt
+    costs = [10, 9, 8, 7, 6, 5, 4, 3, 2, 1]
+    shards = shard_lpt(costs, 3)
+    assert sorted(i for s in shards for i in s) == list(range(10))
+    loads = [sum(costs[i] for i in s) for s in shards]
+    assert max(loads) - min(loads) <= 2
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from hubertfa_amd.distributed import gather_boundaries
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, T = 3, 7
+    dev_out = {"ph_idx_seq": torch.full((B, T), rank, dtype=torch.int32),
+               "ph_time_int": torch.arange(B * T, dtype=torch.int32).view(B, T) + 100 * rank,
+               "n": torch.full((B,), rank + 1, dtype=torch.int32),
+               "frame_confidence": torch.full((B, T), float(rank))}
+    g = gather_boundaries(dev_out)
+    if rank == 0:
+        q.put({k: v.numpy().tolist() for k, v in g.items()})
+    dist.destroy_process_group()
+
+
+def test_boundary_gather_world2_gloo():
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array(res["ph_idx_seq"]).shape == (6, 7)
+    assert np.array(res["n"]).tolist() == [1, 1, 1, 2, 2, 2]
+    assert np.array(res["ph_time_int"])[3, 0] == 100
