@@ -9,6 +9,7 @@ rank 0 gathers the per-utterance results and writes the TextGrids / confidence.c
 """
 from __future__ import annotations
 
+import math
 import pathlib
 
 import click
@@ -34,7 +35,8 @@ def _predict(task, dataset, batch_size: int):
             wav = torch.from_numpy(__import__("numpy").stack([c[1] for c in chunk])).to(task.device)
             res = task.align_batch(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
                                    wav_sr=file_sr)
-            n44 = task.upsampler(file_sr)(wav[:1]).shape[-1] if file_sr != sr else wav.shape[-1]
+            g = math.gcd(sr, file_sr)
+            n44 = math.ceil((sr // g) * wav.shape[-1] / (file_sr // g)) if file_sr != sr else wav.shape[-1]
             for c, r in zip(chunk, res):
                 out[str(c[0])] = (c[0], n44 / sr, r["confidence"], r["ph_seq"], r["ph_intervals"], r["word_seq"],
                                   r["word_intervals"])
