@@ -14,8 +14,9 @@
 //   z = zb*G + zg (batch x group), W[z] = W + zg*sWg (row n at n*ldw, K-contiguous = [Cout][k][Cin] im2col order)
 //
 // f32-in MFMA is bit-for-bit an fmaf chain (exact f32, no TF32 on gfx950), so this is the fp32 parity path.
-// Tile 128x128x16, 256 threads = 4 waves (2x2), each wave 64x64 = 2x2 MFMA 32x32 tiles, register-staged
-// double-buffered LDS with rows padded to 20 floats (ds_read_b128 conflict-free: row r -> bank 4*(5r mod 16)).
+// Tile 128 x BN x BK (BN 128, or 64 for N <= 64; BK 32 when K and Cg allow, else 16), 256 threads = 4 waves
+// (2x2), each wave 64 x BN/2 of MFMA 32x32 tiles, register-staged double-buffered LDS with rows padded to
+// BK+4 floats (ds_read_b128 conflict-free).
 // A lane's ds_read_b128 brings 4 consecutive k of its row; the 4 MFMAs of a k-octet consume one element each,
 // with the same permutation on the W side, so every k is summed exactly once.
 // Block ids are remapped so consecutive logical tiles (same A rows, adjacent W columns) share an XCD's L2.
@@ -26,7 +27,7 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128, BN = 128, BK = 16, LDL = BK + 4;
+constexpr int BM = 128;
 constexpr int NT = 256;
 
 struct GemmP {
@@ -40,8 +41,15 @@ struct GemmP {
 
 enum { EPI_NONE = 0, EPI_GELU = 1 };
 
-template <int EPI, bool VEC_A>
+// Tile BM x BN x BK, 4 waves as 2 x 2, each wave (BM/2) x (BN/2) = TI x TJ MFMA 32x32 tiles.
+// LDS rows padded to BK+4 floats: row r starts at bank 4*((BK/4+1)*r mod 16) -> ds_read_b128 conflict-free.
+template <int EPI, bool VEC_A, int BK, int BN>
 __global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
+    constexpr int LDL = BK + 4;
+    constexpr int TI = BM / 2 / 32, TJ = BN / 2 / 32;
+    constexpr int CPR = BK / 4;                 // float4 chunks per row per K-step
+    constexpr int LA = BM * CPR / NT;           // A float4 loads per thread
+    constexpr int LB = BN * CPR / NT;           // W float4 loads per thread
     __shared__ __attribute__((aligned(16))) float sA[2][BM * LDL];
     __shared__ __attribute__((aligned(16))) float sB[2][BN * LDL];
 
@@ -56,55 +64,54 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
     const float* Wb = p.W + zg * p.sWg;
     const int tid = threadIdx.x;
 
-    // staging assignment: 2 float4 of A and 2 of W per thread per K-step
-    int a_row[2], a_c4[2], b_row[2];
-    bool b_ok[2];
+    int a_row[LA], a_c4[LA], b_row[LB], b_c4[LB];
+    bool b_ok[LB];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < LA; ++i) {
         const int idx = tid + i * NT;
-        a_row[i] = tm * BM + (idx >> 2);
-        a_c4[i] = (idx & 3) * 4;
-        b_row[i] = tn * BN + (idx >> 2);
-        b_ok[i] = b_row[i] < p.N;
+        a_row[i] = idx / CPR;
+        a_c4[i] = (idx % CPR) * 4;
     }
-    f32x4 ra[2], rb[2];
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+        const int idx = tid + i * NT;
+        b_row[i] = idx / CPR;
+        b_c4[i] = (idx % CPR) * 4;
+        b_ok[i] = tn * BN + b_row[i] < p.N;
+    }
+    f32x4 ra[LA], rb[LB];
     auto load_regs = [&](int k0) {
         const int j = k0 / p.Cg;
         const int c0 = k0 - j * p.Cg;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int m = a_row[i];
+        for (int i = 0; i < LA; ++i) {
+            const int m = tm * BM + a_row[i];
             const int t = m * p.stride + j - p.pad;
             const bool ok = (m < p.M) && (t >= 0) && (t < p.Tin);
-            if (VEC_A) {
-                ra[i] = ok ? *reinterpret_cast<const f32x4*>(Ab + (long long)t * p.ldx + c0 + a_c4[i])
-                           : f32x4{0.f, 0.f, 0.f, 0.f};
-            } else {
-                const float* src = Ab + (long long)t * p.ldx + c0 + a_c4[i];
-                ra[i] = ok ? f32x4{src[0], src[1], src[2], src[3]} : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-            rb[i] = b_ok[i] ? *reinterpret_cast<const f32x4*>(Wb + (long long)b_row[i] * p.ldw + k0 + a_c4[i])
-                            : f32x4{0.f, 0.f, 0.f, 0.f};
+            const float* src = Ab + (long long)t * p.ldx + c0 + a_c4[i];
+            if (VEC_A) ra[i] = ok ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
+            else ra[i] = ok ? f32x4{src[0], src[1], src[2], src[3]} : f32x4{0.f, 0.f, 0.f, 0.f};
         }
+#pragma unroll
+        for (int i = 0; i < LB; ++i)
+            rb[i] = b_ok[i] ? *reinterpret_cast<const f32x4*>(Wb + (long long)(tn * BN + b_row[i]) * p.ldw + k0 + b_c4[i])
+                            : f32x4{0.f, 0.f, 0.f, 0.f};
     };
     auto store_lds = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int idx = tid + i * NT;
-            const int row = idx >> 2;
-            *reinterpret_cast<f32x4*>(&sA[buf][row * LDL + a_c4[i]]) = ra[i];
-            *reinterpret_cast<f32x4*>(&sB[buf][row * LDL + a_c4[i]]) = rb[i];
-        }
+        for (int i = 0; i < LA; ++i) *reinterpret_cast<f32x4*>(&sA[buf][a_row[i] * LDL + a_c4[i]]) = ra[i];
+#pragma unroll
+        for (int i = 0; i < LB; ++i) *reinterpret_cast<f32x4*>(&sB[buf][b_row[i] * LDL + b_c4[i]]) = rb[i];
     };
 
     const int wave = tid >> 6, lane = tid & 63;
     const int wm = wave >> 1, wn = wave & 1;
     const int r32 = lane & 31, h = lane >> 5;
-    f32x16 acc[2][2];
+    f32x16 acc[TI][TJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TJ; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
@@ -117,18 +124,19 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
         if (kt + 1 < nk) load_regs((kt + 1) * BK);
 #pragma unroll
         for (int kk = 0; kk < BK / 8; ++kk) {
-            f32x4 a[2], b[2];
+            f32x4 a[TI], b[TJ];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                a[i] = *reinterpret_cast<const f32x4*>(&sA[cur][(wm * 64 + i * 32 + r32) * LDL + kk * 8 + h * 4]);
-                b[i] = *reinterpret_cast<const f32x4*>(&sB[cur][(wn * 64 + i * 32 + r32) * LDL + kk * 8 + h * 4]);
-            }
+            for (int i = 0; i < TI; ++i)
+                a[i] = *reinterpret_cast<const f32x4*>(&sA[cur][(wm * (BM / 2) + i * 32 + r32) * LDL + kk * 8 + h * 4]);
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+                b[j] = *reinterpret_cast<const f32x4*>(&sB[cur][(wn * (BN / 2) + j * 32 + r32) * LDL + kk * 8 + h * 4]);
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < TI; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
+                    for (int j = 0; j < TJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
         }
         if (kt + 1 < nk) store_lds(cur ^ 1);
@@ -140,15 +148,15 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
     const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
     const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int col = tn * BN + wn * 64 + j * 32 + r32;
+    for (int j = 0; j < TJ; ++j) {
+        const int col = tn * BN + wn * (BN / 2) + j * 32 + r32;
         if (col >= p.N) continue;
         const float bv = biasb ? biasb[col] : 0.0f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < TI; ++i) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const int row = tm * BM + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                const int row = tm * BM + wm * (BM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
                 if (row >= p.M) continue;
                 float v = acc[i][j][e] + bv;
                 if (EPI == EPI_GELU) v = hfa::gelu_erf(v);
@@ -159,12 +167,28 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
     }
 }
 
+int g_force_bk = 0, g_force_bn = 0;   // tuning overrides (hfa_gemm_tuning), 0 = automatic
+
+template <int EPI, int BK, int BN>
+int launch_cfg(GemmP p, int Z, bool vec_a, hipStream_t st) {
+    p.n_tiles = (p.N + BN - 1) / BN;
+    dim3 grid(p.m_tiles * p.n_tiles, 1, Z);
+    if (vec_a) hipLaunchKernelGGL((gemm_f32_kernel<EPI, true, BK, BN>), grid, dim3(NT), 0, st, p);
+    else hipLaunchKernelGGL((gemm_f32_kernel<EPI, false, BK, BN>), grid, dim3(NT), 0, st, p);
+    return hfa::check_launch("hfa_conv_gemm_f32");
+}
+
 template <int EPI>
 int launch(const GemmP& p, int Z, bool vec_a, hipStream_t st) {
-    dim3 grid(p.m_tiles * p.n_tiles, 1, Z);
-    if (vec_a) hipLaunchKernelGGL((gemm_f32_kernel<EPI, true>), grid, dim3(NT), 0, st, p);
-    else hipLaunchKernelGGL((gemm_f32_kernel<EPI, false>), grid, dim3(NT), 0, st, p);
-    return hfa::check_launch("hfa_conv_gemm_f32");
+    // measured (scripts/gemm_bench.py): BK=16 keeps 3 blocks/CU and wins on every workload shape; BN=64 wins
+    // for N <= 64 (grouped positional conv) and for grids too small to fill 256 CUs twice (UNet).
+    int bk = 16;
+    const long long blocks128 = (long long)p.m_tiles * ((p.N + 127) / 128) * Z;
+    int bn = (p.N <= 64 || blocks128 < 512) ? 64 : 128;
+    if (g_force_bk == 16 || (g_force_bk == 32 && p.K % 32 == 0 && p.Cg % 32 == 0)) bk = g_force_bk;
+    if (g_force_bn == 64 || g_force_bn == 128) bn = g_force_bn;
+    if (bk == 32) return bn == 64 ? launch_cfg<EPI, 32, 64>(p, Z, vec_a, st) : launch_cfg<EPI, 32, 128>(p, Z, vec_a, st);
+    return bn == 64 ? launch_cfg<EPI, 16, 64>(p, Z, vec_a, st) : launch_cfg<EPI, 16, 128>(p, Z, vec_a, st);
 }
 
 inline bool al16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
@@ -186,8 +210,8 @@ int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long l
         hfa::set_error("hfa_conv_gemm_f32: null operand or K=0");
         return HFA_EINVAL;
     }
-    if (K % BK || Cg % BK || K % Cg) {
-        hfa::set_error("hfa_conv_gemm_f32: K=%d and Cg=%d must be multiples of %d with Cg | K", K, Cg, BK);
+    if (K % 16 || Cg % 16 || K % Cg) {
+        hfa::set_error("hfa_conv_gemm_f32: K=%d and Cg=%d must be multiples of 16 with Cg | K", K, Cg);
         return HFA_EINVAL;
     }
     if (!al16(W) || ldw % 4 || sWg % 4) {
@@ -202,7 +226,7 @@ int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long l
     GemmP p;
     p.M = M; p.N = N; p.K = K; p.G = G;
     p.m_tiles = (M + BM - 1) / BM;
-    p.n_tiles = (N + BN - 1) / BN;
+    p.n_tiles = (N + 63) / 64;   // upper bound for the size check; launch() sets the real value
     p.A = A; p.sAb = sAb; p.sAg = sAg; p.ldx = ldx; p.stride = stride; p.pad = pad; p.Cg = Cg; p.Tin = Tin;
     p.W = W; p.sWg = sWg; p.ldw = ldw;
     p.bias = bias; p.sBg = sBg;
@@ -215,6 +239,12 @@ int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long l
     }
     const int Z = Zb * G;
     return epilogue == EPI_GELU ? launch<EPI_GELU>(p, Z, vec_a, stream) : launch<EPI_NONE>(p, Z, vec_a, stream);
+}
+
+int hfa_gemm_tuning(int force_bk, int force_bn) {
+    g_force_bk = force_bk;
+    g_force_bn = force_bn;
+    return HFA_OK;
 }
 
 int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, int ldw, const float* bias,

@@ -122,6 +122,7 @@ ACT_NONE, ACT_GELU, ACT_HARDSWISH = 0, 1, 2
 _P_, _I_, _LL_, _F_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
 _lib.register("hfa_conv_gemm_f32", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_, _LL_, _I_,
                                     _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _I_, _P_])
+_lib.register("hfa_gemm_tuning", [_I_, _I_])
 _lib.register("hfa_gemm_f32", [_I_, _I_, _I_, _P_, _I_, _P_, _I_, _P_, _P_, _I_, _P_, _I_, _I_, _P_])
 _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_,
                                     _LL_, _I_, _P_])
@@ -168,9 +169,13 @@ class KernelProbe:
 PROBE = None
 
 
-def _gemm_name(epilogue: int, A, ldx: int, sAb: int, sAg: int) -> str:
+def _gemm_name(epilogue: int, A, ldx: int, sAb: int, sAg: int, M: int, N: int, Z: int) -> str:
+    """rocprof symbol of the instantiation hfa_conv_gemm_f32 dispatches to (mirrors gemm.hip launch())."""
     vec = A.data_ptr() % 16 == 0 and ldx % 4 == 0 and sAb % 4 == 0 and sAg % 4 == 0
-    return f"gemm_f32_kernel<{epilogue}, {'true' if vec else 'false'}>"
+    bk = 16
+    blocks128 = -(-M // 128) * -(-N // 128) * Z
+    bn = 64 if (N <= 64 or blocks128 < 512) else 128
+    return f"gemm_f32_kernel<{epilogue}, {'true' if vec else 'false'}, {bk}, {bn}>"
 
 
 def conv_gemm(A, W, C, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None, Tin=None, sWg=0,
@@ -185,7 +190,7 @@ def conv_gemm(A, W, C, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0
                   _ptr(R), sRb, sRg, ldr, _ptr(C), sCb, sCg, ldc, epilogue, _stream(C.device))
     if PROBE is None:
         return launch()
-    PROBE(_gemm_name(epilogue, A, ldx, sAb, sAg), 2.0 * M * N * K * Zb * G, launch)
+    PROBE(_gemm_name(epilogue, A, ldx, sAb, sAg, M, N, Zb * G), 2.0 * M * N * K * Zb * G, launch)
 
 
 def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
@@ -206,7 +211,7 @@ def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
     if PROBE is None:
         launch()
     else:
-        PROBE(_gemm_name(epilogue, x2, x2.stride(0), 0, 0), 2.0 * M * N * K, launch)
+        PROBE(_gemm_name(epilogue, x2, x2.stride(0), 0, 0, M, N, 1), 2.0 * M * N * K, launch)
     return out
 
 

@@ -75,6 +75,8 @@ int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long l
                       int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
                       const float* bias, long long sBg, const float* R, long long sRb, long long sRg, int ldr,
                       float* C, long long sCb, long long sCg, int ldc, int epilogue, hipStream_t stream);
+/* Tuning hook for benchmarks: force the K-step (16/32) and N tile (64/128) of hfa_conv_gemm_f32; 0 = automatic. */
+int hfa_gemm_tuning(int force_bk, int force_bn);
 /* Plain Linear: C[M,N] = epi(A[M,K] W[N,K]^T + bias) + R. */
 int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, int ldw, const float* bias,
                  const float* R, int ldr, float* C, int ldc, int epilogue, hipStream_t stream);

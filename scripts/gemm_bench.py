@@ -1,0 +1,77 @@
+"""GEMM microbenchmark over the workload's shapes and tile variants (run on the GPU box).
+
+python scripts/gemm_bench.py [--reps 20]  -> one line per (shape, variant): ms, TFLOP/s
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from hubertfa_amd import ops, _lib  # noqa: E402
+
+B = 32
+SHAPES = [
+    # name, Tin, Cin, Cout, k, stride, pad, G, epi, M(out rows)
+    ("conv1", 31999, 512, 512, 3, 2, 0, 1, 1),
+    ("conv3", 7999, 512, 512, 3, 2, 0, 1, 1),
+    ("conv5", 1999, 512, 512, 2, 2, 0, 1, 1),
+    ("qkv", 499, 768, 2304, 1, 1, 0, 1, 0),
+    ("outproj", 499, 768, 768, 1, 1, 0, 1, 0),
+    ("ffn1", 499, 768, 3072, 1, 1, 0, 1, 1),
+    ("ffn2", 499, 3072, 768, 1, 1, 0, 1, 0),
+    ("posconv", 499, 768, 768, 128, 1, 64, 16, 1),
+    ("unet_k3", 864, 192, 192, 3, 1, 1, 1, 0),
+]
+
+
+def run(shape, bk, bn, reps):
+    name, Tin, Cin, Cout, k, s, pad, G, epi = shape
+    dev = torch.device("cuda")
+    Tout = (Tin + 2 * pad - k) // s + 1
+    if name == "posconv":
+        Tout = Tin
+    Cg, Ng = Cin // G, Cout // G
+    x = torch.randn(B, Tin, Cin, device=dev)
+    w = torch.randn(Cout, k * Cg, device=dev) * (k * Cg) ** -0.5
+    b = torch.randn(Cout, device=dev)
+    y = torch.empty(B, Tout, Cout, device=dev)
+    _lib.lib().hfa_gemm_tuning(bk, bn)
+
+    def go():
+        ops.conv_gemm(x, w, y, M=Tout, N=Ng, K=k * Cg, Zb=B, G=G, sAb=Tin * Cin, sAg=Cg, ldx=Cin, stride=s, pad=pad,
+                      Cg=Cg, Tin=Tin, sWg=Ng * k * Cg, bias=b, sBg=Ng, sCb=Tout * Cout, sCg=Ng, ldc=Cout,
+                      epilogue=epi)
+    for _ in range(3):
+        go()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        go()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flops = 2.0 * B * Tout * Cout * k * Cg
+    return ms, flops / ms / 1e9
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--variants", default="16x128,32x128,16x64,32x64")
+    args = ap.parse_args()
+    variants = [tuple(int(v) for v in s.split("x")) for s in args.variants.split(",")]
+    for shape in SHAPES:
+        for bk, bn in variants:
+            if bk == 32 and (shape[2] // shape[7]) % 32:
+                continue
+            ms, tf = run(shape, bk, bn, args.reps)
+            print(f"{shape[0]:10s} bk={bk:2d} bn={bn:3d}  {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+    _lib.lib().hfa_gemm_tuning(0, 0)
+
+
+if __name__ == "__main__":
+    main()

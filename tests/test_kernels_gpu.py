@@ -69,6 +69,27 @@ def test_conv_gemm_vs_conv1d(Cin, Cout, k, s, pad, T, G):
     _close(out, ref, 5e-5, 5e-5)
 
 
+@pytest.mark.parametrize("bk,bn", [(16, 128), (32, 128), (16, 64), (32, 64)])
+def test_gemm_tile_variants(bk, bn):
+    """Every tile instantiation is exact on a conv and a Linear shape with tails in M and N."""
+    from hubertfa_amd import ops, _lib
+    _lib.lib().hfa_gemm_tuning(bk, bn)
+    try:
+        d = torch.device("cuda")
+        x, w, b = _r(2, 301, 512, seed=21), _r(200, 512, 3, seed=22, scale=(3 * 512) ** -0.5), _r(200, seed=23)
+        ref = F.gelu(F.conv1d(x.double().transpose(1, 2), w.double(), b.double(), stride=2)).transpose(1, 2)
+        Tout = ref.shape[1]
+        out = torch.empty(2, Tout, 200, device=d)
+        ops.conv_gemm(x.to(d), w.permute(0, 2, 1).contiguous().view(200, -1).to(d), out, M=Tout, N=200, K=1536,
+                      Zb=2, sAb=301 * 512, ldx=512, stride=2, Cg=512, Tin=301, bias=b.to(d), sCb=Tout * 200, ldc=200,
+                      epilogue=ops.EPI_GELU)
+        _close(out, ref, 5e-5, 5e-5)
+        x2, w2 = _r(77, 96, seed=24), _r(50, 96, seed=25)
+        _close(ops.linear(x2.to(d), w2.to(d)), x2.double() @ w2.double().T, 2e-5, 2e-5)
+    finally:
+        _lib.lib().hfa_gemm_tuning(0, 0)
+
+
 @pytest.mark.parametrize("B,H,L", [(2, 12, 499), (1, 16, 49), (3, 12, 64), (1, 12, 1)])
 def test_attention(B, H, L):
     from hubertfa_amd import ops
