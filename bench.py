@@ -13,9 +13,10 @@ the only collective is the boundary-array all_gather.  Timing: barrier + synchro
 K steps, max over ranks.
 
 Also reported (rank 0):
-  * roofline of the dominant kernel (gemm_f32_kernel<1, true, 16, 128>: the GELU-epilogue implicit GEMM =
-    conv1..6 + the 12 FFN up-projections, ~2/3 of all FLOPs): algorithmic FLOPs per launch / average launch time (HIP events on the
-    launching stream over the timed steps) against the 157.3 TFLOP/s f32 MFMA peak;
+  * roofline of the dominant kernel (gemm_f32_kernel<1, true, 16, 128, 256, 2, 4>: the GELU-epilogue implicit
+    GEMM of the CNN extractor conv1..6, ~1/3 of all FLOPs and the largest launches): algorithmic FLOPs per
+    launch / average launch time (HIP events on the launching stream over the timed steps) against the
+    157.3 TFLOP/s f32 MFMA peak;
   * cpu_baseline (N = 1 only): the CPU oracle (torch-CPU fp32 modules on the host threads + the C Viterbi) on a
     bounded sample of the same workload.
 """
@@ -44,7 +45,7 @@ def parse():
     ap.add_argument("--words", type=int, default=30)
     ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="CPU baseline time budget (seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--probe", default="gemm_f32_kernel<1, true, 16, 128>")
+    ap.add_argument("--probe", default="gemm_f32_kernel<1, true, 16, 128, 256, 2, 4>")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()

@@ -14,11 +14,10 @@
 //   z = zb*G + zg (batch x group), W[z] = W + zg*sWg (row n at n*ldw, K-contiguous = [Cout][k][Cin] im2col order)
 //
 // f32-in MFMA is bit-for-bit an fmaf chain (exact f32, no TF32 on gfx950), so this is the fp32 parity path.
-// Tile 128 x BN x BK (BN 128, or 64 for N <= 64; BK 32 when K and Cg allow, else 16), 256 threads = 4 waves
-// (2x2), each wave 64 x BN/2 of MFMA 32x32 tiles, register-staged double-buffered LDS with rows padded to
-// BK+4 floats (ds_read_b128 conflict-free).
-// A lane's ds_read_b128 brings 4 consecutive k of its row; the 4 MFMAs of a k-octet consume one element each,
-// with the same permutation on the W side, so every k is summed exactly once.
+// Tile BM x BN x BK with WM x WN waves, each wave (BM/WM) x (BN/WN) = TI x TJ MFMA 32x32 tiles; A and W tiles
+// are register-staged into double-buffered LDS whose rows are padded to BK+4 floats (ds_read_b128
+// conflict-free).  A lane's ds_read_b128 brings 4 consecutive k of its row; the 4 MFMAs of a k-octet consume
+// one element each, with the same permutation on the W side, so every k is summed exactly once.
 // Block ids are remapped so consecutive logical tiles (same A rows, adjacent W columns) share an XCD's L2.
 #include "hfa_common.h"
 
@@ -26,9 +25,6 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-constexpr int BM = 128;
-constexpr int NT = 256;
 
 struct GemmP {
     int M, N, K, G, m_tiles, n_tiles;
@@ -41,15 +37,15 @@ struct GemmP {
 
 enum { EPI_NONE = 0, EPI_GELU = 1 };
 
-// Tile BM x BN x BK, 4 waves as 2 x 2, each wave (BM/2) x (BN/2) = TI x TJ MFMA 32x32 tiles.
-// LDS rows padded to BK+4 floats: row r starts at bank 4*((BK/4+1)*r mod 16) -> ds_read_b128 conflict-free.
-template <int EPI, bool VEC_A, int BK, int BN>
-__global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
+template <int EPI, bool VEC_A, int BK, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(const GemmP p) {
+    constexpr int NT = 64 * WM * WN;
     constexpr int LDL = BK + 4;
-    constexpr int TI = BM / 2 / 32, TJ = BN / 2 / 32;
+    constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
     constexpr int CPR = BK / 4;                 // float4 chunks per row per K-step
     constexpr int LA = BM * CPR / NT;           // A float4 loads per thread
     constexpr int LB = BN * CPR / NT;           // W float4 loads per thread
+    static_assert(LA * NT == BM * CPR && LB * NT == BN * CPR, "tile/thread mismatch");
     __shared__ __attribute__((aligned(16))) float sA[2][BM * LDL];
     __shared__ __attribute__((aligned(16))) float sB[2][BN * LDL];
 
@@ -105,7 +101,7 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
     };
 
     const int wave = tid >> 6, lane = tid & 63;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WN, wn = wave % WN;
     const int r32 = lane & 31, h = lane >> 5;
     f32x16 acc[TI][TJ];
 #pragma unroll
@@ -127,10 +123,10 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
             f32x4 a[TI], b[TJ];
 #pragma unroll
             for (int i = 0; i < TI; ++i)
-                a[i] = *reinterpret_cast<const f32x4*>(&sA[cur][(wm * (BM / 2) + i * 32 + r32) * LDL + kk * 8 + h * 4]);
+                a[i] = *reinterpret_cast<const f32x4*>(&sA[cur][(wm * (BM / WM) + i * 32 + r32) * LDL + kk * 8 + h * 4]);
 #pragma unroll
             for (int j = 0; j < TJ; ++j)
-                b[j] = *reinterpret_cast<const f32x4*>(&sB[cur][(wn * (BN / 2) + j * 32 + r32) * LDL + kk * 8 + h * 4]);
+                b[j] = *reinterpret_cast<const f32x4*>(&sB[cur][(wn * (BN / WN) + j * 32 + r32) * LDL + kk * 8 + h * 4]);
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -149,14 +145,14 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
     const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
-        const int col = tn * BN + wn * (BN / 2) + j * 32 + r32;
+        const int col = tn * BN + wn * (BN / WN) + j * 32 + r32;
         if (col >= p.N) continue;
         const float bv = biasb ? biasb[col] : 0.0f;
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const int row = tm * BM + wm * (BM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                const int row = tm * BM + wm * (BM / WM) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
                 if (row >= p.M) continue;
                 float v = acc[i][j][e] + bv;
                 if (EPI == EPI_GELU) v = hfa::gelu_erf(v);
@@ -167,28 +163,52 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(const GemmP p) {
     }
 }
 
-int g_force_bk = 0, g_force_bn = 0;   // tuning overrides (hfa_gemm_tuning), 0 = automatic
+// Tile configurations (BM x BN, WM x WN waves); scripts/gemm_bench.py measures each on the workload's shapes.
+enum { CFG_AUTO = 0, CFG_128x128 = 1, CFG_128x64 = 2, CFG_256x128 = 3, CFG_128x256 = 4, CFG_256x128_W4 = 5,
+       CFG_128x256_W4 = 6, CFG_COUNT = 7 };
+int g_force_bk = 0, g_force_cfg = 0;   // tuning overrides (hfa_gemm_tuning), 0 = automatic
 
-template <int EPI, int BK, int BN>
+template <int EPI, int BK, int BM, int BN, int WM, int WN>
 int launch_cfg(GemmP p, int Z, bool vec_a, hipStream_t st) {
+    p.m_tiles = (p.M + BM - 1) / BM;
     p.n_tiles = (p.N + BN - 1) / BN;
-    dim3 grid(p.m_tiles * p.n_tiles, 1, Z);
-    if (vec_a) hipLaunchKernelGGL((gemm_f32_kernel<EPI, true, BK, BN>), grid, dim3(NT), 0, st, p);
-    else hipLaunchKernelGGL((gemm_f32_kernel<EPI, false, BK, BN>), grid, dim3(NT), 0, st, p);
+    const long long tiles = (long long)p.m_tiles * p.n_tiles;
+    if (tiles > 0x7fffffffLL) {
+        hfa::set_error("hfa_conv_gemm_f32: grid too large");
+        return HFA_EINVAL;
+    }
+    dim3 grid((unsigned)tiles, 1, Z);
+    if (vec_a) hipLaunchKernelGGL((gemm_f32_kernel<EPI, true, BK, BM, BN, WM, WN>), grid, dim3(64 * WM * WN), 0, st, p);
+    else hipLaunchKernelGGL((gemm_f32_kernel<EPI, false, BK, BM, BN, WM, WN>), grid, dim3(64 * WM * WN), 0, st, p);
     return hfa::check_launch("hfa_conv_gemm_f32");
+}
+
+template <int EPI, int BK>
+int launch_bk(int cfg, const GemmP& p, int Z, bool vec_a, hipStream_t st) {
+    switch (cfg) {
+        case CFG_128x64: return launch_cfg<EPI, BK, 128, 64, 2, 2>(p, Z, vec_a, st);
+        case CFG_256x128: return launch_cfg<EPI, BK, 256, 128, 4, 2>(p, Z, vec_a, st);
+        case CFG_128x256: return launch_cfg<EPI, BK, 128, 256, 2, 4>(p, Z, vec_a, st);
+        case CFG_256x128_W4: return launch_cfg<EPI, BK, 256, 128, 2, 2>(p, Z, vec_a, st);
+        case CFG_128x256_W4: return launch_cfg<EPI, BK, 128, 256, 2, 2>(p, Z, vec_a, st);
+        default: return launch_cfg<EPI, BK, 128, 128, 2, 2>(p, Z, vec_a, st);
+    }
 }
 
 template <int EPI>
 int launch(const GemmP& p, int Z, bool vec_a, hipStream_t st) {
-    // measured (scripts/gemm_bench.py): BK=16 keeps 3 blocks/CU and wins on every workload shape; BN=64 wins
-    // for N <= 64 (grouped positional conv) and for grids too small to fill 256 CUs twice (UNet).
-    int bk = 16;
-    const long long blocks128 = (long long)p.m_tiles * ((p.N + 127) / 128) * Z;
-    int bn = (p.N <= 64 || blocks128 < 512) ? 64 : 128;
-    if (g_force_bk == 16 || (g_force_bk == 32 && p.K % 32 == 0 && p.Cg % 32 == 0)) bk = g_force_bk;
-    if (g_force_bn == 64 || g_force_bn == 128) bn = g_force_bn;
-    if (bk == 32) return bn == 64 ? launch_cfg<EPI, 32, 64>(p, Z, vec_a, st) : launch_cfg<EPI, 32, 128>(p, Z, vec_a, st);
-    return bn == 64 ? launch_cfg<EPI, 16, 64>(p, Z, vec_a, st) : launch_cfg<EPI, 16, 128>(p, Z, vec_a, st);
+    // measured (scripts/gemm_bench.py): BK=16 keeps 3 blocks/CU and wins on every workload shape; the 64-wide
+    // N tile wins for N <= 64 (grouped positional conv) and for grids too small to fill 256 CUs twice (UNet).
+    // The 8-wave 128x256 tile wins on the extractor convs (long K over overlapping rows, M*Z >= 30k rows:
+    // +3..29 %) and loses on the transformer's Linear shapes (-5..-20 %).
+    const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
+    int cfg = (p.N <= 64 || blocks128 < 512) ? CFG_128x64 : CFG_128x128;
+    if (cfg == CFG_128x128 && p.N >= 512 && p.K >= 1024 && (long long)p.M * Z >= 30000 && p.stride > 1)
+        cfg = CFG_128x256;
+    if (g_force_cfg > 0 && g_force_cfg < CFG_COUNT) cfg = g_force_cfg;
+    const bool bk32_ok = p.K % 32 == 0 && p.Cg % 32 == 0;
+    if (g_force_bk == 32 && bk32_ok) return launch_bk<EPI, 32>(cfg, p, Z, vec_a, st);
+    return launch_bk<EPI, 16>(cfg, p, Z, vec_a, st);
 }
 
 inline bool al16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
@@ -222,28 +242,26 @@ int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long l
         hfa::set_error("hfa_conv_gemm_f32: unknown epilogue %d", epilogue);
         return HFA_EINVAL;
     }
+    if ((long long)Zb * G > 65535) {
+        hfa::set_error("hfa_conv_gemm_f32: Zb*G=%lld exceeds the grid z limit", (long long)Zb * G);
+        return HFA_EINVAL;
+    }
     const bool vec_a = al16(A) && ldx % 4 == 0 && sAb % 4 == 0 && sAg % 4 == 0;
     GemmP p;
     p.M = M; p.N = N; p.K = K; p.G = G;
-    p.m_tiles = (M + BM - 1) / BM;
-    p.n_tiles = (N + 63) / 64;   // upper bound for the size check; launch() sets the real value
+    p.m_tiles = p.n_tiles = 0;   // set per tile configuration in launch_cfg
     p.A = A; p.sAb = sAb; p.sAg = sAg; p.ldx = ldx; p.stride = stride; p.pad = pad; p.Cg = Cg; p.Tin = Tin;
     p.W = W; p.sWg = sWg; p.ldw = ldw;
     p.bias = bias; p.sBg = sBg;
     p.R = R; p.sRb = sRb; p.sRg = sRg; p.ldr = ldr;
     p.C = C; p.sCb = sCb; p.sCg = sCg; p.ldc = ldc;
-    const long long tiles = (long long)p.m_tiles * p.n_tiles;
-    if (tiles > 0x7fffffffLL || (long long)Zb * G > 65535) {
-        hfa::set_error("hfa_conv_gemm_f32: grid too large");
-        return HFA_EINVAL;
-    }
     const int Z = Zb * G;
     return epilogue == EPI_GELU ? launch<EPI_GELU>(p, Z, vec_a, stream) : launch<EPI_NONE>(p, Z, vec_a, stream);
 }
 
-int hfa_gemm_tuning(int force_bk, int force_bn) {
+int hfa_gemm_tuning(int force_bk, int force_cfg) {
     g_force_bk = force_bk;
-    g_force_bn = force_bn;
+    g_force_cfg = force_cfg;
     return HFA_OK;
 }
 

@@ -22,16 +22,20 @@ namespace {
 
 using hfa::neg_inf;
 
-constexpr int kGroup = 8;  // time steps per prefetch group
-
-template <int K>
-__global__ __launch_bounds__(64) void viterbi_forward_kernel(
+// One workgroup per utterance: NW waves x 64 lanes, each lane owning K contiguous states; G time steps of
+// emissions are prefetched one group ahead.  With NW > 1 the two boundary q values of each wave's last lane
+// cross to the next wave through a double-buffered LDS slot (one barrier per time step).
+template <int K, int NW, int G>
+__global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
     const int32_t* __restrict__ padv, const float* __restrict__ prob_log,
     const float* __restrict__ not_edge_log, const float* __restrict__ edge_log, double* __restrict__ curr_io,
     float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id) {
+    static_assert(NW == 1 || K >= 2, "multi-wave DP needs >= 2 states per lane");
+    __shared__ float xq[2][NW][2];
     const int b = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int g = threadIdx.x;
+    const int lane = g & 63, wave = g >> 6;
     const int T = Tv[b];
     const int S = Sv[b];
     if (T <= 1 || S <= 0) return;
@@ -46,7 +50,7 @@ __global__ __launch_bounds__(64) void viterbi_forward_kernel(
     double* cu = curr_io + (size_t)b * Smax;
     const double ratio = (double)T / (double)S;  // `T / S` (alignment_decoder.py:186), f64 true division
 
-    const int s0 = lane * K;
+    const int s0 = g * K;
     float dprev[K];
     double curr[K];
     bool valid[K], zero[K], allow3[K];
@@ -63,11 +67,11 @@ __global__ __launch_bounds__(64) void viterbi_forward_kernel(
         allow3[k] = valid[k] && s >= pad && !((j < S - 1) && ids[j] != 0);
     }
 
-    float Lc[kGroup][K], Ec[kGroup], nEc[kGroup];
-    float Ln[kGroup][K], En[kGroup], nEn[kGroup];
-    auto load_group = [&](int t0, float (&L)[kGroup][K], float (&E)[kGroup], float (&nE)[kGroup]) {
+    float Lc[G][K], Ec[G], nEc[G];
+    float Ln[G][K], En[G], nEn[G];
+    auto load_group = [&](int t0, float (&L)[G][K], float (&E)[G], float (&nE)[G]) {
 #pragma unroll
-        for (int u = 0; u < kGroup; ++u) {
+        for (int u = 0; u < G; ++u) {
             const int t = t0 + u;
             const bool tv = t < T;
             E[u] = tv ? Ep[t] : 0.0f;
@@ -78,12 +82,12 @@ __global__ __launch_bounds__(64) void viterbi_forward_kernel(
     };
     load_group(1, Lc, Ec, nEc);
 
-    for (int t0 = 1; t0 < T; t0 += kGroup) {
-        if (t0 + kGroup < T) load_group(t0 + kGroup, Ln, En, nEn);
+    for (int t0 = 1; t0 < T; t0 += G) {
+        if (t0 + G < T) load_group(t0 + G, Ln, En, nEn);
 #pragma unroll
-        for (int u = 0; u < kGroup; ++u) {
+        for (int u = 0; u < G; ++u) {
             const int t = t0 + u;
-            if (t >= T) break;
+            if (t >= T) break;   // uniform over the workgroup
             const float E = Ec[u], nE = nEc[u];
             float a[K], q[K];
 #pragma unroll
@@ -92,11 +96,22 @@ __global__ __launch_bounds__(64) void viterbi_forward_kernel(
                 const float a2 = __fadd_rn(a[k], E);                                     //  + E       (f32)
                 q[k] = (float)__dadd_rn((double)a2, __dmul_rn(curr[k], ratio));          //  + C*T/S   (f64)
             }
-            // left neighbour lane's last two q values (state s0-1, s0-2)
+            // left neighbour lane's last two q values (states s0-1, s0-2)
             float qm1 = __shfl_up(q[K - 1], 1, 64);
             float qm2 = (K >= 2) ? __shfl_up(q[K >= 2 ? K - 2 : 0], 1, 64) : __shfl_up(q[0], 2, 64);
             if (lane < 1) qm1 = neg_inf();
             if (K >= 2 ? lane < 1 : lane < 2) qm2 = neg_inf();
+            if (NW > 1) {
+                if (lane == 63) {
+                    xq[t & 1][wave][0] = q[K - 1];
+                    xq[t & 1][wave][1] = q[K >= 2 ? K - 2 : 0];
+                }
+                __syncthreads();
+                if (lane == 0 && wave > 0) {
+                    qm1 = xq[t & 1][wave - 1][0];
+                    qm2 = xq[t & 1][wave - 1][1];
+                }
+            }
             const size_t row = (size_t)t * Smax;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -122,7 +137,7 @@ __global__ __launch_bounds__(64) void viterbi_forward_kernel(
             }
         }
 #pragma unroll
-        for (int u = 0; u < kGroup; ++u) {
+        for (int u = 0; u < G; ++u) {
             Ec[u] = En[u];
             nEc[u] = nEn[u];
 #pragma unroll
@@ -299,12 +314,12 @@ __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
     }
 }
 
-template <int K>
+template <int K, int NW, int G>
 int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const int32_t* pad,
                    const float* prob_log, const float* nE, const float* E, double* curr, float* dp, int8_t* bt,
                    const int32_t* ids, hipStream_t st) {
-    hipLaunchKernelGGL(viterbi_forward_kernel<K>, dim3(B), dim3(64), 0, st, Tmax, Smax, T, S, pad, prob_log, nE,
-                       E, curr, dp, bt, ids);
+    hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T, S, pad,
+                       prob_log, nE, E, curr, dp, bt, ids);
     return hfa::check_launch("hfa_viterbi_forward");
 }
 
@@ -322,20 +337,22 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
         return HFA_EINVAL;
     }
     if (B == 0 || Tmax == 0 || Smax == 0) return HFA_OK;
+    // one wave while a lane holds <= 8 states; beyond that 8 states per lane over up to 16 waves
+#define HFA_FWD(K, NW, G)                                                                                       \
+    return launch_forward<K, NW, G>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log, edge_log, curr, \
+                                    dp, bt, ph_seq_id, stream)
     const int per_lane = (Smax + 63) / 64;
-    if (per_lane <= 1) return launch_forward<1>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
-                                                edge_log, curr, dp, bt, ph_seq_id, stream);
-    if (per_lane <= 2) return launch_forward<2>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
-                                                edge_log, curr, dp, bt, ph_seq_id, stream);
-    if (per_lane <= 4) return launch_forward<4>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
-                                                edge_log, curr, dp, bt, ph_seq_id, stream);
-    if (per_lane <= 8) return launch_forward<8>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
-                                                edge_log, curr, dp, bt, ph_seq_id, stream);
-    if (per_lane <= 16) return launch_forward<16>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
-                                                  edge_log, curr, dp, bt, ph_seq_id, stream);
-    if (per_lane <= 32) return launch_forward<32>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log,
-                                                  edge_log, curr, dp, bt, ph_seq_id, stream);
-    hfa::set_error("hfa_viterbi_forward: Smax=%d exceeds 2048 states per utterance", Smax);
+    if (per_lane <= 1) HFA_FWD(1, 1, 8);
+    if (per_lane <= 2) HFA_FWD(2, 1, 8);
+    if (per_lane <= 4) HFA_FWD(4, 1, 8);
+    if (per_lane <= 8) HFA_FWD(8, 1, 4);
+    const int waves = (Smax + 511) / 512;
+    if (waves <= 2) HFA_FWD(8, 2, 4);
+    if (waves <= 4) HFA_FWD(8, 4, 4);
+    if (waves <= 8) HFA_FWD(8, 8, 4);
+    if (waves <= 16) HFA_FWD(8, 16, 2);   // 1024 threads cap VGPRs at 128: shorter prefetch ring
+#undef HFA_FWD
+    hfa::set_error("hfa_viterbi_forward: Smax=%d exceeds 8192 states per utterance", Smax);
     return HFA_EINVAL;
 }
 

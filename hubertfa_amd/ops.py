@@ -169,13 +169,15 @@ class KernelProbe:
 PROBE = None
 
 
-def _gemm_name(epilogue: int, A, ldx: int, sAb: int, sAg: int, M: int, N: int, Z: int) -> str:
+def _gemm_name(epilogue: int, A, ldx: int, sAb: int, sAg: int, M: int, N: int, K: int, Z: int,
+               stride: int) -> str:
     """rocprof symbol of the instantiation hfa_conv_gemm_f32 dispatches to (mirrors gemm.hip launch())."""
     vec = A.data_ptr() % 16 == 0 and ldx % 4 == 0 and sAb % 4 == 0 and sAg % 4 == 0
-    bk = 16
     blocks128 = -(-M // 128) * -(-N // 128) * Z
-    bn = 64 if (N <= 64 or blocks128 < 512) else 128
-    return f"gemm_f32_kernel<{epilogue}, {'true' if vec else 'false'}, {bk}, {bn}>"
+    tile = "128, 64, 2, 2" if (N <= 64 or blocks128 < 512) else "128, 128, 2, 2"
+    if tile == "128, 128, 2, 2" and N >= 512 and K >= 1024 and M * Z >= 30000 and stride > 1:
+        tile = "128, 256, 2, 4"
+    return f"gemm_f32_kernel<{epilogue}, {'true' if vec else 'false'}, 16, {tile}>"
 
 
 def conv_gemm(A, W, C, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None, Tin=None, sWg=0,
@@ -190,7 +192,7 @@ def conv_gemm(A, W, C, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0
                   _ptr(R), sRb, sRg, ldr, _ptr(C), sCb, sCg, ldc, epilogue, _stream(C.device))
     if PROBE is None:
         return launch()
-    PROBE(_gemm_name(epilogue, A, ldx, sAb, sAg, M, N, Zb * G), 2.0 * M * N * K * Zb * G, launch)
+    PROBE(_gemm_name(epilogue, A, ldx, sAb, sAg, M, N, K, Zb * G, stride), 2.0 * M * N * K * Zb * G, launch)
 
 
 def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
@@ -211,7 +213,7 @@ def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
     if PROBE is None:
         launch()
     else:
-        PROBE(_gemm_name(epilogue, x2, x2.stride(0), 0, 0, M, N, 1), 2.0 * M * N * K, launch)
+        PROBE(_gemm_name(epilogue, x2, x2.stride(0), 0, 0, M, N, K, 1, 1), 2.0 * M * N * K, launch)
     return out
 
 

@@ -35,7 +35,7 @@ const char* hfa_build_arch(void);
  *   curr [B,Smax] f64 (in/out, = curr_ph_max_prob_log), dp [B,Tmax,Smax] f32 (row 0 in, rows 1.. out),
  *   bt [B,Tmax,Smax] i8 (rows 1.. out; = backtrack_s), prob3_pad_len [B] i32 or NULL (=2 if S>=2 else 1).
  * Bit-exact with the reference (f32 sums, f64 curr*(T/S) term, strict '>' ties stay->advance->skip).
- * Smax <= 2048. */
+ * Smax <= 8192 (one wave up to 512 states, then 8 states per lane over up to 16 waves). */
 int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S,
                         const int32_t* prob3_pad_len, const float* prob_log, const float* not_edge_log,
                         const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,

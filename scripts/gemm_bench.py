@@ -27,7 +27,7 @@ SHAPES = [
 ]
 
 
-def run(shape, bk, bn, reps):
+def run(shape, bk, cfg, reps):
     name, Tin, Cin, Cout, k, s, pad, G, epi = shape
     dev = torch.device("cuda")
     Tout = (Tin + 2 * pad - k) // s + 1
@@ -38,7 +38,7 @@ def run(shape, bk, bn, reps):
     w = torch.randn(Cout, k * Cg, device=dev) * (k * Cg) ** -0.5
     b = torch.randn(Cout, device=dev)
     y = torch.empty(B, Tout, Cout, device=dev)
-    _lib.lib().hfa_gemm_tuning(bk, bn)
+    _lib.lib().hfa_gemm_tuning(bk, cfg)
 
     def go():
         ops.conv_gemm(x, w, y, M=Tout, N=Ng, K=k * Cg, Zb=B, G=G, sAb=Tin * Cin, sAg=Cg, ldx=Cin, stride=s, pad=pad,
@@ -61,15 +61,17 @@ def run(shape, bk, bn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--variants", default="16x128,32x128,16x64,32x64")
+    ap.add_argument("--variants", default="16:1,16:2,16:3,16:4,16:5,16:6")
     args = ap.parse_args()
-    variants = [tuple(int(v) for v in s.split("x")) for s in args.variants.split(",")]
+    names = {1: "128x128/2x2", 2: "128x64/2x2", 3: "256x128/4x2", 4: "128x256/2x4", 5: "256x128/2x2",
+             6: "128x256/2x2"}
+    variants = [tuple(int(v) for v in s.split(":")) for s in args.variants.split(",")]
     for shape in SHAPES:
-        for bk, bn in variants:
+        for bk, cfg in variants:
             if bk == 32 and (shape[2] // shape[7]) % 32:
                 continue
-            ms, tf = run(shape, bk, bn, args.reps)
-            print(f"{shape[0]:10s} bk={bk:2d} bn={bn:3d}  {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+            ms, tf = run(shape, bk, cfg, args.reps)
+            print(f"{shape[0]:10s} bk={bk:2d} {names[cfg]:12s} {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
     _lib.lib().hfa_gemm_tuning(0, 0)
 
 

@@ -69,7 +69,7 @@ def test_conv_gemm_vs_conv1d(Cin, Cout, k, s, pad, T, G):
     _close(out, ref, 5e-5, 5e-5)
 
 
-@pytest.mark.parametrize("bk,bn", [(16, 128), (32, 128), (16, 64), (32, 64)])
+@pytest.mark.parametrize("bk,bn", [(16, c) for c in range(1, 7)] + [(32, 1), (32, 3)])
 def test_gemm_tile_variants(bk, bn):
     """Every tile instantiation is exact on a conv and a Linear shape with tails in M and N."""
     from hubertfa_amd import ops, _lib

@@ -72,6 +72,39 @@ def test_forward_batched_bit_exact():
         np.testing.assert_allclose(fc[b, :Ts[b]], z[p + "frame_confidence"], rtol=2e-6, atol=0, equal_nan=True)
 
 
+@pytest.mark.parametrize("T,S", [(700, 300), (1200, 513), (3000, 1801), (2500, 4100), (4200, 8000)])
+def test_forward_many_states_vs_oracle(T, S):
+    """Single- and multi-wave DP variants (S up to 8192) bit-exact with the pinned C oracle."""
+    from hubertfa_amd import ops
+    from oracle import decode as od
+    r = np.random.default_rng(T * 7 + S)
+    V = 63
+    ids = r.integers(1, V, S).astype(np.int64)
+    ids[::3] = 0
+    ids[0] = ids[-1] = 0
+    logits = (3 * r.standard_normal((T, V))).astype(np.float32)
+    ph_prob_log = torch.log_softmax(torch.from_numpy(logits), -1).numpy()
+    edge = np.clip(r.uniform(-0.2, 1.2, T), 0, 1)
+    pl, E, nE, cu, dp, bt, pad = od.lattice_inputs(ids, ph_prob_log, edge)
+    d_ref, b_ref, c_ref = od.forward_pass(T, S, pl, nE, E, cu.copy(), dp.copy(), bt.copy(), ids, pad)
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))[None].to(dev)
+    dp_t, cu_t = t(dp), t(cu)
+    bt_t = torch.full((1, T, S), -1, dtype=torch.int8, device=dev)
+    ids_t = t(ids.astype(np.int32))
+    Tt = torch.tensor([T], dtype=torch.int32, device=dev)
+    St = torch.tensor([S], dtype=torch.int32, device=dev)
+    ops.viterbi_forward(t(pl), t(nE), t(E), cu_t, dp_t, bt_t, ids_t, Tt, St)
+    assert np.array_equal(dp_t[0].cpu().numpy().view(np.int32), d_ref.view(np.int32))
+    assert np.array_equal(bt_t[0, 1:].cpu().numpy().astype(np.int32), b_ref[1:])
+    assert np.array_equal(cu_t[0].cpu().numpy().view(np.int64), c_ref.view(np.int64))
+    idx, tint, n, fc = ops.viterbi_backtrack(dp_t, bt_t, ids_t, Tt, St)
+    i_ref, t_ref, f_ref = od.backtrack(d_ref, b_ref, ids)
+    k = int(n[0])
+    assert np.array_equal(idx[0, :k].cpu().numpy(), i_ref) and np.array_equal(tint[0, :k].cpu().numpy(), t_ref)
+    np.testing.assert_allclose(fc[0].cpu().numpy(), f_ref, rtol=2e-6, atol=0, equal_nan=True)
+
+
 def test_reference_api_forward_pass_and_decode():
     from hubertfa_amd.alignment_decoder import AlignmentDecoder
     z, n = _cases()
