@@ -45,7 +45,12 @@ def parse():
     ap.add_argument("--words", type=int, default=30)
     ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="CPU baseline time budget (seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--probe", default="gemm_f32_kernel<1, true, 16, 128, 256, 2, 4>")
+    ap.add_argument("--encoder", default="base", choices=["base", "large", "soft"],
+                    help="base = cnhubert (config 2/3), large = cnhubert-large 24L/1024 (config 4), soft = hubertsoft")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo only for rehearsals")
+    ap.add_argument("--device", type=int, default=None, help="force every rank onto this device (rehearsal)")
+    ap.add_argument("--probe", default="auto",
+                    help="kernel instantiation to time; auto = the one carrying the most FLOPs in a warmup census")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -75,7 +80,7 @@ def make_inputs(B, seconds, words, seed0):
     return wav, ph_seqs, word_seqs, p2ws
 
 
-def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s):
+def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s, encoder="cnhubert"):
     """CPU oracle on a bounded sample (whole utterances until the budget is spent)."""
     import numpy as np
     import torch
@@ -84,14 +89,16 @@ def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s):
     hp = ckpt["hyper_parameters"]
     import yaml
     vocab = yaml.safe_load(hp["vocab_text"])
-    arch = synth.arch_cnhubert_base()
+    arch = {"cnhubert": synth.arch_cnhubert_base, "cnhubert-large": synth.arch_cnhubert_large,
+            "hubertsoft": synth.arch_hubertsoft}[encoder]()
     sd = synth.synth_hubert_state_dict(arch, seed=0)
-    ua = synth.UNetArch(vocab_size=vocab["vocab_size"])
+    ua = synth.UNetArch(input_dims=arch.out_channels, vocab_size=vocab["vocab_size"])
     usd = {k: v.numpy() for k, v in ckpt["state_dict"].items()}
     threads = torch.get_num_threads()
     done, t0 = 0, time.perf_counter()
-    while done < len(wav):
-        x16 = torch.from_numpy(wav[done:done + 1])
+    while time.perf_counter() - t0 < budget_s:   # cycle over the batch until the budget is spent
+        i = done % len(wav)
+        x16 = torch.from_numpy(wav[i:i + 1])
         x44 = ores.resample(x16, 16000, 44100, 6)
         xr = ores.resample(x44, 44100, 16000, 128)
         units = hubert_cpu.hubert_forward(arch, sd, xr)
@@ -101,16 +108,13 @@ def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s):
         idx = torch.clamp(torch.round(ratio * torch.arange(n_frames)).long(), max=units.shape[1] - 1)
         feats = units[:, idx]
         logits = hubert_cpu.unet_head_forward(ua, usd, feats)
-        odec.decode(vocab, logits[:, :, 2:], logits[:, :, 0], n44 / 44100, ph_seqs[done], word_seqs[done],
-                    p2ws[done])
+        odec.decode(vocab, logits[:, :, 2:], logits[:, :, 0], n44 / 44100, ph_seqs[i], word_seqs[i], p2ws[i])
         done += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
     el = time.perf_counter() - t0
     secs = done * wav.shape[1] / 16000
     return {"value": secs / el, "unit": "audio_s/s", "cores": threads, "kind": "port",
             "sample": f"{done} x {wav.shape[1] / 16000:.0f} s utterances of the same workload, sequential B=1 "
-                      f"(oracle: torch-CPU fp32 resample+Hubert-base+UNet, C Viterbi), {el:.1f} s wall"}
+                      f"(oracle: torch-CPU fp32 resample + {encoder} + UNet, C Viterbi), {el:.1f} s wall"}
 
 
 def main():
@@ -123,35 +127,57 @@ def main():
     from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
 
     rank, world, local = env_rank_world()
+    if args.device is not None:          # rehearsal of the N>1 path on a 1-GPU box (all ranks on one device)
+        local = args.device
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
-    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
+    encoder = {"base": "cnhubert", "large": "cnhubert-large", "soft": "hubertsoft"}[args.encoder]
+    ckpt = synth_checkpoint(encoder=encoder, model_path="synth:0", seed=1)
     task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
     task.on_predict_start()
     B = args.batch
     wav_np, ph_seqs, word_seqs, p2ws = make_inputs(B, args.seconds, args.words, seed0=1000 * (rank + 1))
     wav = torch.from_numpy(wav_np).to(dev)
 
-    def step():
+    def launch():
+        """GPU half of one step (+ the boundary gather) and the async D2H of its results."""
         dev_out = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False)
         if world > 1:
             gather_boundaries(dev_out)
-        return task.decoder.assemble(dev_out, ph_seqs, word_seqs, p2ws)
+        return task.decoder.fetch(dev_out)
 
-    for _ in range(args.warmup):
-        res = step()
+    def finish(handle):
+        return task.decoder.assemble(handle, ph_seqs, word_seqs, p2ws)
+
+    def run(k):
+        """k steps, software-pipelined: the host assembles batch i while the GPU runs batch i+1."""
+        pending, res = None, None
+        for _ in range(k):
+            h = launch()
+            if pending is not None:
+                res = finish(pending)
+            pending = h
+        return finish(pending) if pending is not None else res
+
+    census = ops.KernelProbe(None)
+    ops.PROBE = census
+    res = run(max(args.warmup, 1))
+    ops.PROBE = None
     torch.cuda.synchronize()
-    probe = ops.KernelProbe(args.probe)
+    probe_name = census.dominant() if args.probe == "auto" else args.probe
+    probe = ops.KernelProbe(probe_name)
     ops.PROBE = probe
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
+    res = run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -176,7 +202,7 @@ def main():
         try:
             with open(args.traffic_file) as f:
                 tj = json.load(f)
-            if tj.get("kernel") == args.probe:
+            if tj.get("kernel") == probe_name:
                 traffic = tj.get("bytes_per_launch")
         except Exception:  # noqa: BLE001
             traffic = None
@@ -185,20 +211,24 @@ def main():
         "metric": METRIC, "value": value, "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"config 2: B={B} x {args.seconds:g} s 16 kHz utterances per GPU, Hubert-base "
-                               f"(cnhubert arch) + UNet head + Viterbi; full infer path wave(HBM)->boundaries(host)",
+        "config": {"workload": f"config {'4' if args.encoder == 'large' else ('3' if world > 1 else '2')}: "
+                               f"B={B} x {args.seconds:g} s 16 kHz utterances per GPU, "
+                               f"{ {'base': 'Hubert-base (cnhubert arch)', 'large': 'Hubert-large (cnhubert-large arch)', 'soft': 'HubertSoft'}[args.encoder]}"
+                               f" + UNet head + Viterbi; full infer path wave(HBM)->boundaries(host), host assembly "
+                               f"pipelined one batch behind the GPU",
+                   "encoder": encoder,
                    "global_batch": world * B, "seconds_per_utterance": args.seconds, "dp_frames": n_frames,
                    "states": len(ph_seqs[0]), "parallelism": f"utterance-dp{world}"},
         "frames_per_s": frames_ps,
         "realtime_factor": value,
         "encoder_tflops": world * B * (hub_flops + head_flops) * args.steps / el / 1e12,
-        "roofline": {"bound": "mfma", "kernel": args.probe, "achieved": achieved, "peak": F32_MFMA_PEAK_TFLOPS,
+        "roofline": {"bound": "mfma", "kernel": probe_name, "achieved": achieved, "peak": F32_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / F32_MFMA_PEAK_TFLOPS if achieved else None,
                      "traffic": traffic, "launches": ps["launches"], "avg_launch_ms": ps["avg_ms"],
                      "flops_per_launch": ps["avg_flops"]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(wav_np, ph_seqs, word_seqs, p2ws, ckpt, args.cpu_sample_s)
+        out["cpu_baseline"] = cpu_baseline(wav_np, ph_seqs, word_seqs, p2ws, ckpt, args.cpu_sample_s, encoder)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

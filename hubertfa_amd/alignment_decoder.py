@@ -118,9 +118,15 @@ class AlignmentDecoder:
         ids_pad = np.zeros((B, Smax), np.int32)
         for b, i in enumerate(ids):
             ids_pad[b, :len(i)] = i
-        T_t = torch.tensor(Ts, dtype=torch.int32, device=dev)
-        S_t = torch.tensor([len(i) for i in ids], dtype=torch.int32, device=dev)
-        ids_t = torch.from_numpy(ids_pad).to(dev)
+        # one pinned staging buffer -> one async H2D copy (keeps the stream free-running)
+        meta = np.zeros((B, Smax + 2), np.int32)
+        meta[:, 0] = Ts
+        meta[:, 1] = [len(i) for i in ids]
+        meta[:, 2:] = ids_pad
+        meta_t = torch.from_numpy(meta).pin_memory().to(dev, non_blocking=True)
+        T_t = meta_t[:, 0].contiguous()
+        S_t = meta_t[:, 1].contiguous()
+        ids_t = meta_t[:, 2:].contiguous()
         lat = ops.lattice_prologue(frame_logits, edge_logits, ids_t, T_t, S_t, want_frame_probs=keep_frame_probs)
         dp, bt, curr = self.init_dp(lat["prob_log"], ids_t, S_t)
         ops.viterbi_forward(lat["prob_log"], lat["not_edge_log"], lat["edge_log"], curr, dp, bt, ids_t, T_t, S_t)
@@ -131,17 +137,36 @@ class AlignmentDecoder:
             return dev_out
         return self.assemble(dev_out, ph_seqs, word_seqs, p2ws, keep_frame_probs)
 
+    _FETCH_KEYS = ("ph_idx_seq", "ph_time_int", "n", "frame_confidence", "edge_diff")
+
+    def fetch(self, dev_out, keep_frame_probs: bool = False):
+        """Enqueue the D2H copies of a batch's boundary arrays into pinned memory; returns a handle that
+        ``assemble`` completes.  Lets the host assemble batch i while the GPU runs batch i+1."""
+        keys = list(self._FETCH_KEYS)
+        src = {k: dev_out[k] for k in keys}
+        if keep_frame_probs:
+            src["edge_prob"] = dev_out["lattice"]["edge_prob"]
+            src["ph_frame_pred"] = dev_out["lattice"]["ph_frame_pred"]
+        host = {}
+        for k, t in src.items():
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            host[k] = h
+        ev = torch.cuda.Event()
+        ev.record()
+        return {"T": dev_out["T"], "host": host, "event": ev}
+
     def assemble(self, dev_out, ph_seqs, word_seqs=None, p2ws=None, keep_frame_probs: bool = False):
-        """Host half of decode for a batch: one D2H copy, then per-utterance interval/word assembly."""
+        """Host half of decode for a batch (from ``decode_batch(host=False)`` or ``fetch``): per-utterance
+        interval/word assembly."""
+        if "host" not in dev_out:
+            dev_out = self.fetch(dev_out, keep_frame_probs)
+        dev_out["event"].synchronize()
+        hd = {k: v.numpy() for k, v in dev_out["host"].items()}
         Ts = dev_out["T"]
-        lat = dev_out["lattice"]
-        idx_h = dev_out["ph_idx_seq"].cpu().numpy()
-        tint_h = dev_out["ph_time_int"].cpu().numpy()
-        n_h = dev_out["n"].cpu().numpy()
-        fc_h = dev_out["frame_confidence"].cpu().numpy()
-        ed_h = dev_out["edge_diff"].cpu().numpy()
-        ep_h = lat["edge_prob"].cpu().numpy() if keep_frame_probs else None
-        fp_h = lat["ph_frame_pred"].cpu().numpy() if keep_frame_probs else None
+        idx_h, tint_h, n_h, fc_h, ed_h = (hd[k] for k in self._FETCH_KEYS)
+        ep_h = hd.get("edge_prob") if keep_frame_probs else None
+        fp_h = hd.get("ph_frame_pred") if keep_frame_probs else None
         out = []
         for b in range(len(ph_seqs)):
             T = Ts[b]
@@ -166,9 +191,14 @@ class AlignmentDecoder:
         """dp/bt/curr initialisation of _decode (alignment_decoder.py:244-254), on device."""
         B, Tmax, Smax = prob_log.shape
         dev = prob_log.device
-        dp = torch.full((B, Tmax, Smax), float("-inf"), dtype=torch.float32, device=dev)
-        bt = torch.full((B, Tmax, Smax), -1, dtype=torch.int8, device=dev)
+        # rows 1.. of dp/bt are fully written by the forward kernel for every valid (t, s); row 0 of bt is
+        # never read (the backtrack always emits at t == 0), so only dp row 0 and curr need initialising.
+        dp = torch.empty((B, Tmax, Smax), dtype=torch.float32, device=dev)
+        bt = torch.empty((B, Tmax, Smax), dtype=torch.int8, device=dev)
         curr = torch.full((B, Smax), float("-inf"), dtype=torch.float64, device=dev)
+        if Tmax == 0 or Smax == 0:
+            return dp, bt, curr
+        dp[:, 0, :] = float("-inf")
         if Tmax == 0 or Smax == 0:
             return dp, bt, curr
         dp[:, 0, 0] = prob_log[:, 0, 0]

@@ -38,9 +38,15 @@ struct GemmP {
 enum { EPI_NONE = 0, EPI_GELU = 1 };
 
 template <int EPI, bool VEC_A, int BK, int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(const GemmP p) {
+// 4-wave tiles are register-capped at 128 (accumulators included) so 4 workgroups fit per CU.
+__global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 4 : 2) void gemm_f32_kernel(const GemmP p) {
     constexpr int NT = 64 * WM * WN;
-    constexpr int LDL = BK + 4;
+    // Unpadded BK-float LDS rows with the 16-B chunk index XOR-swizzled by row: chunk' = chunk ^ sw(row).
+    // BK=16: sw = (row>>2)&3 makes every ds_read_b128 lane group (rows {0-3,12-15,20-27} / {4-11,16-19,28-31})
+    // hit 16 distinct 4-bank slots, and every 8-lane ds_write_b128 group (2 rows x 4 chunks) 32 distinct
+    // banks; BK=32: sw = (row>>1)&7 does the same for 128-B rows.  (PMC: the padded layout spent 1/3 of its
+    // LDS cycles in write conflicts.)
+    constexpr int LDL = BK;
     constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
     constexpr int CPR = BK / 4;                 // float4 chunks per row per K-step
     constexpr int LA = BM * CPR / NT;           // A float4 loads per thread
@@ -60,13 +66,21 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(const GemmP p) {
     const float* Wb = p.W + zg * p.sWg;
     const int tid = threadIdx.x;
 
-    int a_row[LA], a_c4[LA], b_row[LB], b_c4[LB];
-    bool b_ok[LB];
+    // Per-thread staging rows are fixed for the whole K loop: precompute their base pointers and the input
+    // time index of tap 0 once, so a K-step only adds the (wave-uniform) tap/channel offset.
+    int a_row[LA], a_c4[LA], b_row[LB], b_c4[LB], a_t0[LA];
+    bool b_ok[LB], a_mok[LA];
+    const float* a_base[LA];
+    const float* b_base[LB];
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
         const int idx = tid + i * NT;
         a_row[i] = idx / CPR;
         a_c4[i] = (idx % CPR) * 4;
+        const int m = tm * BM + a_row[i];
+        a_mok[i] = m < p.M;
+        a_t0[i] = m * p.stride - p.pad;
+        a_base[i] = Ab + (long long)a_t0[i] * p.ldx + a_c4[i];
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
@@ -74,30 +88,35 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(const GemmP p) {
         b_row[i] = idx / CPR;
         b_c4[i] = (idx % CPR) * 4;
         b_ok[i] = tn * BN + b_row[i] < p.N;
+        b_base[i] = Wb + (long long)(tn * BN + b_row[i]) * p.ldw + b_c4[i];
     }
     f32x4 ra[LA], rb[LB];
     auto load_regs = [&](int k0) {
-        const int j = k0 / p.Cg;
-        const int c0 = k0 - j * p.Cg;
+        const int j = k0 / p.Cg;                       // wave-uniform: tap index of this K-step
+        const long long aoff = (long long)j * p.ldx + (k0 - j * p.Cg);
 #pragma unroll
         for (int i = 0; i < LA; ++i) {
-            const int m = tm * BM + a_row[i];
-            const int t = m * p.stride + j - p.pad;
-            const bool ok = (m < p.M) && (t >= 0) && (t < p.Tin);
-            const float* src = Ab + (long long)t * p.ldx + c0 + a_c4[i];
+            const int t = a_t0[i] + j;
+            const bool ok = a_mok[i] && (t >= 0) && (t < p.Tin);
+            // (a guarded load costs an exec-mask branch but fewer VGPRs than a clamped load + select, which
+            // spilled at the 128-register cap; measured: the guarded form is 3-25 % faster)
+            const float* src = a_base[i] + aoff;
             if (VEC_A) ra[i] = ok ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
             else ra[i] = ok ? f32x4{src[0], src[1], src[2], src[3]} : f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int i = 0; i < LB; ++i)
-            rb[i] = b_ok[i] ? *reinterpret_cast<const f32x4*>(Wb + (long long)(tn * BN + b_row[i]) * p.ldw + k0 + b_c4[i])
-                            : f32x4{0.f, 0.f, 0.f, 0.f};
+            rb[i] = b_ok[i] ? *reinterpret_cast<const f32x4*>(b_base[i] + k0) : f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    auto swz = [](int row, int c4) {   // float offset of logical (row, float c4) in the swizzled image
+        constexpr int SH = (CPR == 4) ? 2 : 1;
+        return row * LDL + ((((c4 >> 2) ^ (row >> SH)) & (CPR - 1)) << 2);
     };
     auto store_lds = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < LA; ++i) *reinterpret_cast<f32x4*>(&sA[buf][a_row[i] * LDL + a_c4[i]]) = ra[i];
+        for (int i = 0; i < LA; ++i) *reinterpret_cast<f32x4*>(&sA[buf][swz(a_row[i], a_c4[i])]) = ra[i];
 #pragma unroll
-        for (int i = 0; i < LB; ++i) *reinterpret_cast<f32x4*>(&sB[buf][b_row[i] * LDL + b_c4[i]]) = rb[i];
+        for (int i = 0; i < LB; ++i) *reinterpret_cast<f32x4*>(&sB[buf][swz(b_row[i], b_c4[i])]) = rb[i];
     };
 
     const int wave = tid >> 6, lane = tid & 63;
@@ -123,10 +142,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(const GemmP p) {
             f32x4 a[TI], b[TJ];
 #pragma unroll
             for (int i = 0; i < TI; ++i)
-                a[i] = *reinterpret_cast<const f32x4*>(&sA[cur][(wm * (BM / WM) + i * 32 + r32) * LDL + kk * 8 + h * 4]);
+                a[i] = *reinterpret_cast<const f32x4*>(&sA[cur][swz(wm * (BM / WM) + i * 32 + r32, kk * 8 + h * 4)]);
 #pragma unroll
             for (int j = 0; j < TJ; ++j)
-                b[j] = *reinterpret_cast<const f32x4*>(&sB[cur][(wn * (BN / WN) + j * 32 + r32) * LDL + kk * 8 + h * 4]);
+                b[j] = *reinterpret_cast<const f32x4*>(&sB[cur][swz(wn * (BN / WN) + j * 32 + r32, kk * 8 + h * 4)]);
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -139,20 +158,25 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(const GemmP p) {
         __syncthreads();
     }
 
-    // epilogue: C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    // epilogue: C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+    // GELU uses the branch-free erf (hfa::erf_nb), so lanes in different erf ranges never split.  (A separate
+    // unguarded interior-tile path with batched residual loads measured slower: it pushed the 128-VGPR tile
+    // into spills.)
     float* Cb = p.C + zb * p.sCb + zg * p.sCg;
     const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
     const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+    const int row0 = tm * BM + wm * (BM / WM) + 4 * h;
+    const int col0 = tn * BN + wn * (BN / WN) + r32;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
-        const int col = tn * BN + wn * (BN / WN) + j * 32 + r32;
+        const int col = col0 + j * 32;
         if (col >= p.N) continue;
         const float bv = biasb ? biasb[col] : 0.0f;
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const int row = tm * BM + wm * (BM / WM) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                const int row = row0 + i * 32 + (e & 3) + 8 * (e >> 2);
                 if (row >= p.M) continue;
                 float v = acc[i][j][e] + bv;
                 if (EPI == EPI_GELU) v = hfa::gelu_erf(v);
@@ -165,7 +189,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_f32_kernel(const GemmP p) {
 
 // Tile configurations (BM x BN, WM x WN waves); scripts/gemm_bench.py measures each on the workload's shapes.
 enum { CFG_AUTO = 0, CFG_128x128 = 1, CFG_128x64 = 2, CFG_256x128 = 3, CFG_128x256 = 4, CFG_256x128_W4 = 5,
-       CFG_128x256_W4 = 6, CFG_COUNT = 7 };
+       CFG_128x256_W4 = 6, CFG_256x256 = 7, CFG_COUNT = 8 };
 int g_force_bk = 0, g_force_cfg = 0;   // tuning overrides (hfa_gemm_tuning), 0 = automatic
 
 template <int EPI, int BK, int BM, int BN, int WM, int WN>
@@ -191,6 +215,7 @@ int launch_bk(int cfg, const GemmP& p, int Z, bool vec_a, hipStream_t st) {
         case CFG_128x256: return launch_cfg<EPI, BK, 128, 256, 2, 4>(p, Z, vec_a, st);
         case CFG_256x128_W4: return launch_cfg<EPI, BK, 256, 128, 2, 2>(p, Z, vec_a, st);
         case CFG_128x256_W4: return launch_cfg<EPI, BK, 128, 256, 2, 2>(p, Z, vec_a, st);
+        case CFG_256x256: return launch_cfg<EPI, BK, 256, 256, 4, 2>(p, Z, vec_a, st);
         default: return launch_cfg<EPI, BK, 128, 128, 2, 2>(p, Z, vec_a, st);
     }
 }

@@ -49,9 +49,32 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// Branch-free erf: the two ranges of ROCm's device erff (|x| < 1: odd polynomial in x^2; |x| >= 1:
+// 1 - exp(-q(|x|))) are both evaluated with the same constants and fma order and then selected, so the
+// result is bit-identical to erff (tests/test_kernels_gpu.py) while lanes of a wave never diverge.
+__device__ __forceinline__ float erf_nb(float x) {
+    const float ax = fabsf(x);
+    const float t = x * x;
+    float s = fmaf(t, __uint_as_float(0xba1345e1u), __uint_as_float(0x3ba10414u));
+    s = fmaf(t, s, __uint_as_float(0xbcdac9b8u));
+    s = fmaf(t, s, __uint_as_float(0x3de703beu));
+    s = fmaf(t, s, __uint_as_float(0xbec09330u));
+    s = fmaf(t, s, __uint_as_float(0x3e0375d0u));
+    s = fmaf(ax, s, ax);
+    float q = fmaf(ax, __uint_as_float(0x378e98abu), __uint_as_float(0xb9c68948u));
+    q = fmaf(ax, q, __uint_as_float(0x3b7cd369u));
+    q = fmaf(ax, q, __uint_as_float(0xbcc618b2u));
+    q = fmaf(ax, q, __uint_as_float(0x3dda74e4u));
+    q = fmaf(ax, q, __uint_as_float(0x3f228afdu));
+    q = fmaf(ax, q, __uint_as_float(0x3e03c728u));
+    q = fmaf(ax, q, ax);
+    const float l = 1.0f - expf(-q);
+    return copysignf(ax < 1.0f ? s : l, x);
+}
+
 // erf-GELU exactly as torch's default F.gelu / HF ACT2FN["gelu"]: 0.5 x (1 + erf(x / sqrt 2)).
 __device__ __forceinline__ float gelu_erf(float x) {
-    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+    return 0.5f * x * (1.0f + erf_nb(x * 0.70710678118654752440f));
 }
 
 // torch Hardswish: x * relu6(x + 3) / 6.

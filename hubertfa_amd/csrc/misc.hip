@@ -78,6 +78,14 @@ __global__ __launch_bounds__(256) void add_kernel(long long n4, const f32x4* __r
     for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) o[i] = a[i] + b[i];
 }
 
+__global__ __launch_bounds__(256) void erf_check_kernel(long long n, const float* __restrict__ x,
+                                                        float* __restrict__ y_nb, float* __restrict__ y_ref) {
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        y_nb[i] = hfa::erf_nb(x[i]);
+        y_ref[i] = erff(x[i]);
+    }
+}
+
 inline int grid1d(long long n, int per = 256, int cap = 8192) {
     long long g = (n + per - 1) / per;
     return (int)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -121,6 +129,17 @@ int hfa_pad_rows_f32(int B, int N, const float* x, long long x_bs, int left, int
     hipLaunchKernelGGL(pad_rows_kernel, dim3(grid1d(N_out, 256, 1024), B), dim3(256), 0, stream, N, x, x_bs, left,
                        N_out, y, y_bs);
     return hfa::check_launch("hfa_pad_rows_f32");
+}
+
+// Self-test: the branch-free erf used by every GELU epilogue vs the device library's erff.
+int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hipStream_t stream) {
+    if (n < 0 || !x || !y_nb || !y_ref) {
+        hfa::set_error("hfa_selftest_erf: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (n == 0) return HFA_OK;
+    hipLaunchKernelGGL(erf_check_kernel, dim3(grid1d(n)), dim3(256), 0, stream, n, x, y_nb, y_ref);
+    return hfa::check_launch("hfa_selftest_erf");
 }
 
 int hfa_add_f32(long long n, const float* a, const float* b, float* out, hipStream_t stream) {

@@ -45,8 +45,11 @@ def gather_boundaries(dev_out: dict, dst_world: int | None = None):
     if world == 1:
         return {k: dev_out[k] for k in keys}
     out = {}
+    host_side = dist.get_backend() == "gloo"   # gloo moves host tensors; RCCL moves device tensors over xGMI
     for k in keys:
         t = dev_out[k].contiguous()
+        if host_side:
+            t = t.cpu()
         buf = torch.empty((world * t.shape[0], *t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(buf, t)
         out[k] = buf

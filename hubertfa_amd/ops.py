@@ -134,6 +134,7 @@ _lib.register("hfa_units_gather_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _I_, _I_, 
 _lib.register("hfa_wav_normalize_f32", [_I_, _I_, _P_, _LL_, _F_, _P_, _LL_, _P_])
 _lib.register("hfa_pad_rows_f32", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _LL_, _P_])
 _lib.register("hfa_add_f32", [_LL_, _P_, _P_, _P_, _P_])
+_lib.register("hfa_selftest_erf", [_LL_, _P_, _P_, _P_, _P_])
 _lib.register("hfa_resample_workspace_bytes", [_I_, _I_, _I_, _I_], ctypes.c_longlong)
 _lib.register("hfa_resample_f32", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _I_, _I_, _P_, _P_, _LL_, _P_])
 
@@ -144,11 +145,18 @@ class KernelProbe:
     ``name`` is the rocprof kernel symbol stem, e.g. ``gemm_f32_kernel<1, true>``; per launch the algorithmic
     FLOPs are recorded next to the event pair, so achieved = sum(flops) / sum(durations)."""
 
-    def __init__(self, name: str):
-        self.name = name
+    def __init__(self, name: str | None):
+        self.name = name            # None: census mode (no events; FLOPs tallied per instantiation)
         self.records = []
+        self.census = {}
+
+    def dominant(self) -> str:
+        return max(self.census, key=self.census.get)
 
     def __call__(self, name: str, flops: float, launch):
+        if self.name is None:
+            self.census[name] = self.census.get(name, 0.0) + flops
+            return launch()
         if name != self.name:
             return launch()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -123,6 +123,8 @@ int hfa_wav_normalize_f32(int B, int N, const float* x, long long x_bs, float ep
 /* Zero padding of rows (networks/hubert/model.py:77 F.pad 40/40; resampler edge padding). */
 int hfa_pad_rows_f32(int B, int N, const float* x, long long x_bs, int left, int N_out, float* y, long long y_bs,
                      hipStream_t stream);
+/* Self-test: y_nb = the branch-free erf of every GELU epilogue, y_ref = device erff (must be bit-identical). */
+int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hipStream_t stream);
 /* out = a + b (UNet skip connection, networks/layer/backbone/unet.py:114). */
 int hfa_add_f32(long long n, const float* a, const float* b, float* out, hipStream_t stream);
 /* torchaudio.transforms.Resample (sinc_interp_hann) as pad + MFMA GEMM (tools/load_wav.py:7,

@@ -64,7 +64,7 @@ def main():
     ap.add_argument("--variants", default="16:1,16:2,16:3,16:4,16:5,16:6")
     args = ap.parse_args()
     names = {1: "128x128/2x2", 2: "128x64/2x2", 3: "256x128/4x2", 4: "128x256/2x4", 5: "256x128/2x2",
-             6: "128x256/2x2"}
+             6: "128x256/2x2", 7: "256x256/4x2"}
     variants = [tuple(int(v) for v in s.split(":")) for s in args.variants.split(",")]
     for shape in SHAPES:
         for bk, cfg in variants:

@@ -69,7 +69,7 @@ def test_conv_gemm_vs_conv1d(Cin, Cout, k, s, pad, T, G):
     _close(out, ref, 5e-5, 5e-5)
 
 
-@pytest.mark.parametrize("bk,bn", [(16, c) for c in range(1, 7)] + [(32, 1), (32, 3)])
+@pytest.mark.parametrize("bk,bn", [(16, c) for c in range(1, 8)] + [(32, 1), (32, 3)])
 def test_gemm_tile_variants(bk, bn):
     """Every tile instantiation is exact on a conv and a Linear shape with tails in M and N."""
     from hubertfa_amd import ops, _lib
@@ -88,6 +88,16 @@ def test_gemm_tile_variants(bk, bn):
         _close(ops.linear(x2.to(d), w2.to(d)), x2.double() @ w2.double().T, 2e-5, 2e-5)
     finally:
         _lib.lib().hfa_gemm_tuning(0, 0)
+
+
+def test_branch_free_erf_bit_identical():
+    from hubertfa_amd import ops, _lib
+    d = torch.device("cuda")
+    x = torch.cat([torch.linspace(-12, 12, 1 << 20), _r(1 << 18, seed=30) * 3,
+                   torch.tensor([0.0, -0.0, 1.0, -1.0, 0.99999994, 1.0000001, float("inf"), -float("inf")])]).to(d)
+    y_nb, y_ref = torch.empty_like(x), torch.empty_like(x)
+    _lib.call("hfa_selftest_erf", x.numel(), ops._ptr(x), ops._ptr(y_nb), ops._ptr(y_ref), ops._stream(d))
+    assert torch.equal(y_nb.view(torch.int32), y_ref.view(torch.int32))
 
 
 @pytest.mark.parametrize("B,H,L", [(2, 12, 499), (1, 16, 49), (3, 12, 64), (1, 12, 1)])
