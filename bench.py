@@ -33,6 +33,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "aligned audio sec/sec (RTF^-1) + frames/sec, Hubert-base, 1/2/4/8 MI355X"
 F32_MFMA_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBPS = 8000.0             # MI355X HBM3E, MI355X_MICROARCH.md
 
 
 def parse():
@@ -117,6 +118,33 @@ def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s, encoder="cnhuber
                       f"(oracle: torch-CPU fp32 resample + {encoder} + UNet, C Viterbi), {el:.1f} s wall"}
 
 
+SECONDARY = ("viterbi_forward_kernel", "hfa_conv0_f32", "attn_fwd_f32_kernel")
+
+
+def secondary_rooflines(probe, T, S):
+    """SURVEY §8(d) secondary figures: the DP (HBM-accounted latency-bound scan, also µs per time step),
+    conv0+GroupNorm+GELU (HBM) and flash attention (MFMA), each timed live with HIP events."""
+    out = []
+    for name in SECONDARY:
+        ps = probe.summary(name)
+        if not ps["launches"]:
+            continue
+        rate = ps["avg_work"] / (ps["avg_ms"] * 1e-3)
+        if name == "attn_fwd_f32_kernel":
+            e = {"kernel": name, "bound": "mfma", "achieved": rate / 1e12, "peak": F32_MFMA_PEAK_TFLOPS,
+                 "unit": "TFLOP/s", "frac": rate / 1e12 / F32_MFMA_PEAK_TFLOPS}
+        else:
+            e = {"kernel": name, "bound": "hbm" if name != "viterbi_forward_kernel" else "latency",
+                 "achieved": rate / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": rate / 1e9 / HBM_PEAK_GBPS,
+                 "bytes_per_launch": ps["avg_work"]}
+            if name == "viterbi_forward_kernel":
+                e["us_per_time_step"] = ps["avg_ms"] * 1e3 / T
+                e["states"] = S
+        e.update({"launches": ps["launches"], "avg_launch_ms": ps["avg_ms"]})
+        out.append(e)
+    return out
+
+
 def main():
     args = parse()
     import numpy as np
@@ -171,7 +199,7 @@ def main():
     ops.PROBE = None
     torch.cuda.synchronize()
     probe_name = census.dominant() if args.probe == "auto" else args.probe
-    probe = ops.KernelProbe(probe_name)
+    probe = ops.KernelProbe(probe_name, extra=SECONDARY)
     ops.PROBE = probe
     if world > 1:
         dist.barrier()
@@ -227,6 +255,7 @@ def main():
                      "traffic": traffic, "launches": ps["launches"], "avg_launch_ms": ps["avg_ms"],
                      "flops_per_launch": ps["avg_flops"]},
     }
+    out["secondary"] = secondary_rooflines(probe, n_frames, len(ph_seqs[0]))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wav_np, ph_seqs, word_seqs, p2ws, ckpt, args.cpu_sample_s, encoder)
     if rank == 0:

@@ -14,11 +14,13 @@
 //   z = zb*G + zg (batch x group), W[z] = W + zg*sWg (row n at n*ldw, K-contiguous = [Cout][k][Cin] im2col order)
 //
 // f32-in MFMA is bit-for-bit an fmaf chain (exact f32, no TF32 on gfx950), so this is the fp32 parity path.
-// Tile BM x BN x BK with WM x WN waves, each wave (BM/WM) x (BN/WN) = TI x TJ MFMA 32x32 tiles; A and W tiles
-// are register-staged into double-buffered LDS whose rows are padded to BK+4 floats (ds_read_b128
-// conflict-free).  A lane's ds_read_b128 brings 4 consecutive k of its row; the 4 MFMAs of a k-octet consume
-// one element each, with the same permutation on the W side, so every k is summed exactly once.
-// Block ids are remapped so consecutive logical tiles (same A rows, adjacent W columns) share an XCD's L2.
+// Tile BM x BN x 16 with WM x WN waves, each wave (BM/WM) x (BN/WN) = TI x TJ MFMA 32x32 tiles.  A and W
+// tiles are staged global -> LDS by buffer_load ... lds (LDS-DMA, 2-3 stages, no VALU in the main loop; the
+// default) or register-staged (fallback for unaligned A / spans past 31-bit offsets) into an XOR-swizzled
+// [row][16] image read with conflict-free ds_read_b128.  A lane's ds_read_b128 brings 4 consecutive k of its
+// row; the 4 MFMAs of a k-octet consume one element each, with the same permutation on the W side, so every k is
+// summed exactly once.  Block ids are remapped so consecutive logical tiles (same A rows, adjacent W columns)
+// share an XCD's L2.
 #include "hfa_common.h"
 
 namespace {
@@ -36,6 +38,38 @@ struct GemmP {
 };
 
 enum { EPI_NONE = 0, EPI_GELU = 1 };
+
+// Epilogue shared by both kernels: C/D layout of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) +
+// 4*(lane>>5).  GELU uses the branch-free erf (hfa::erf_nb), so lanes in different erf ranges never split.  (A
+// separate unguarded interior-tile path with batched residual loads measured slower: it pushed the 128-VGPR tile
+// into spills.)
+template <int EPI, int TI, int TJ>
+__device__ __forceinline__ void store_tile(const GemmP& p, const f32x16 (&acc)[TI][TJ], int zb, int zg, int wrow0,
+                                           int wcol0, int lane) {
+    float* Cb = p.C + zb * p.sCb + zg * p.sCg;
+    const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
+    const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+    const int row0 = wrow0 + 4 * (lane >> 5);
+    const int col0 = wcol0 + (lane & 31);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+        const int col = col0 + j * 32;
+        if (col >= p.N) continue;
+        const float bv = biasb ? biasb[col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = row0 + i * 32 + (e & 3) + 8 * (e >> 2);
+                if (row >= p.M) continue;
+                float v = acc[i][j][e] + bv;
+                if (EPI == EPI_GELU) v = hfa::gelu_erf(v);
+                if (Rb) v += Rb[(long long)row * p.ldr + col];
+                Cb[(long long)row * p.ldc + col] = v;
+            }
+        }
+    }
+}
 
 template <int EPI, bool VEC_A, int BK, int BM, int BN, int WM, int WN>
 // 4-wave tiles are register-capped at 128 (accumulators included) so 4 workgroups fit per CU.
@@ -130,22 +164,201 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 4 : 2) void gemm_f32
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
+    // Read offsets in float4 units: the swizzle depends on row bits that the 32-row sub-tile offsets leave
+    // unchanged, so one per-lane offset per k-octet serves every sub-tile (i*32*CPR folds into the immediate).
+    // Indexing whole f32x4 elements keeps the 16-B alignment visible, so every read is one ds_read_b128 (byte
+    // arithmetic on a float* let the compiler split half of them into ds_read2_b32 pairs: 2x the LDS cycles
+    // plus bank conflicts under the 32-bank rule).
+    int rdA[BK / 8], rdB[BK / 8];
+#pragma unroll
+    for (int kk = 0; kk < BK / 8; ++kk) {
+        rdA[kk] = swz(wm * (BM / WM) + r32, kk * 8 + h * 4) >> 2;
+        rdB[kk] = swz(wn * (BN / WN) + r32, kk * 8 + h * 4) >> 2;
+    }
+
     const int nk = p.K / BK;
     load_regs(0);
     store_lds(0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
+#ifndef HFA_ABL_NOGLOBAL
         if (kt + 1 < nk) load_regs((kt + 1) * BK);
+#endif
+        const f32x4* sA4 = reinterpret_cast<const f32x4*>(sA[cur]);
+        const f32x4* sB4 = reinterpret_cast<const f32x4*>(sB[cur]);
 #pragma unroll
         for (int kk = 0; kk < BK / 8; ++kk) {
             f32x4 a[TI], b[TJ];
 #pragma unroll
-            for (int i = 0; i < TI; ++i)
-                a[i] = *reinterpret_cast<const f32x4*>(&sA[cur][swz(wm * (BM / WM) + i * 32 + r32, kk * 8 + h * 4)]);
+            for (int i = 0; i < TI; ++i) a[i] = sA4[rdA[kk] + i * 32 * CPR];
 #pragma unroll
-            for (int j = 0; j < TJ; ++j)
-                b[j] = *reinterpret_cast<const f32x4*>(&sB[cur][swz(wn * (BN / WN) + j * 32 + r32, kk * 8 + h * 4)]);
+            for (int j = 0; j < TJ; ++j) b[j] = sB4[rdB[kk] + j * 32 * CPR];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int i = 0; i < TI; ++i)
+#pragma unroll
+                    for (int j = 0; j < TJ; ++j)
+#ifdef HFA_GEMM_SETPRIO
+                        {
+                            if (e == 0 && i == 0 && j == 0) __builtin_amdgcn_s_setprio(1);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+                            if (e == 3 && i == TI - 1 && j == TJ - 1) __builtin_amdgcn_s_setprio(0);
+                        }
+#else
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+#endif
+        }
+#ifndef HFA_ABL_NOLDSWRITE
+        if (kt + 1 < nk) store_lds(cur ^ 1);
+#endif
+#ifndef HFA_ABL_NOBARRIER
+        __syncthreads();
+#endif
+    }
+
+    store_tile<EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane);
+}
+
+// ---- LDS-DMA pipeline ------------------------------------------------------------------------------------------
+// On gfx950 the f32 MFMA runs at the f32 VECTOR rate, so every VALU instruction in the main loop costs MFMA
+// cycles (ablation, scripts/gpu_gemm_abl.sh: dropping the register-staged loads + ds_writes alone took conv1 from
+// 125 to 143 TFLOP/s).  This kernel stages A and W with buffer_load_dwordx4 ... lds (global -> LDS, no VGPR
+// data, no ds_write) from per-lane byte offsets fixed for a whole tap; the K-step advance is a scalar soffset,
+// so the main loop is 32 MFMAs + 8 ds_read_b128 + (DA+DB) DMA issues + one counted wait/barrier per K-step, with
+// no vector ALU work.  NS LDS stages (NS-1 K-steps in flight across the barrier).  The LDS image is the same
+// XOR-swizzled [row][16] image as above: one DMA wave-instruction writes 1 KiB lane-linearly (16 rows x 4
+// chunks), so the swizzle is applied on the SOURCE side (lane l loads chunk (l&3) ^ sw(row)).
+// Out-of-range conv taps (padding) read through a voffset beyond the buffer's num_records, which the range check
+// turns into zeros (scripts/probes/dma_oob.hip); rows past M / N are clamped (their outputs are never stored).
+__device__ __forceinline__ unsigned lds_addr(const void* ptr) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)ptr;
+}
+
+__device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned soff, unsigned lds) {
+    unsigned keep;   // M0 is compiler-reserved: set and restore it inside the statement that uses it
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+    // this wave's DMAs except the newest N landed, its LDS reads retired, then every wave of the block
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "i"(N) : "memory");
+}
+
+constexpr unsigned DMA_OOB = 0x80000000u;
+
+template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP p) {
+    constexpr int BK = 16, CPR = 4, NW = WM * WN;
+    constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
+    constexpr int DA = BM / 16 / NW, DB = BN / 16 / NW;       // 1-KiB DMA wave-instructions per K-step
+    static_assert(DA * 16 * NW == BM && DB * 16 * NW == BN, "tile/DMA mismatch");
+    constexpr int STAGE = (BM + BN) * BK;                     // floats per stage (A image, then W image)
+    __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];   // one LDS object (no extra waits)
+
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+    const int tm = wgid / p.n_tiles, tn = wgid - tm * p.n_tiles;
+    const int zb = blockIdx.z / p.G, zg = blockIdx.z - zb * p.G;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    // buffer descriptors over this (batch, group)'s A rows and W rows (host checks both spans fit 31 bits)
+    const float* Ab = p.A + zb * p.sAb + zg * p.sAg;
+    const float* Wb = p.W + zg * p.sWg;
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)Ab, (short)0, (int)(((long long)(p.Tin - 1) * p.ldx + p.Cg) * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)Wb, (short)0, (int)(((long long)(p.N - 1) * p.ldw + p.K) * 4), 0x00020000);
+
+    // per-lane source: DMA d of this wave fills tile rows (wave*D + d)*16 + lane/4, LDS chunk slot lane&3
+    int a_t0[DA], a_c[DA];
+    unsigned voffA[DA], voffW[DB];
+#pragma unroll
+    for (int d = 0; d < DA; ++d) {
+        const int row = (wave * DA + d) * 16 + (lane >> 2);
+        int m = tm * BM + row;
+        m = m < p.M ? m : p.M - 1;
+        a_t0[d] = m * p.stride - p.pad;
+        a_c[d] = ((lane & 3) ^ ((row >> 2) & 3)) * 4;
+    }
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+        const int row = (wave * DB + d) * 16 + (lane >> 2);
+        int n = tn * BN + row;
+        n = n < p.N ? n : p.N - 1;
+        voffW[d] = (unsigned)((n * p.ldw + ((lane & 3) ^ ((row >> 2) & 3)) * 4) * 4);
+    }
+    auto set_tap = [&](int j) {      // once per conv tap (every Cg/16 K-steps)
+#pragma unroll
+        for (int d = 0; d < DA; ++d) {
+            const int t = a_t0[d] + j;
+            voffA[d] = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + a_c[d]) * 4) : DMA_OOB;
+        }
+    };
+    const unsigned lds0 = lds_addr(smem);
+    // K-step cursor: tap j, channel offset c0 inside the tap, absolute k0
+    int cur_j = 0, cur_c0 = 0, cur_k0 = 0;
+    set_tap(0);
+    auto issue = [&](int stage) {
+        const unsigned a_dst = lds0 + stage * STAGE * 4 + wave * DA * 1024;
+        const unsigned w_dst = lds0 + (stage * STAGE + BM * BK) * 4 + wave * DB * 1024;
+#pragma unroll
+        for (int d = 0; d < DA; ++d) dma16(voffA[d], rA, (unsigned)cur_c0 * 4, a_dst + d * 1024);
+#pragma unroll
+        for (int d = 0; d < DB; ++d) dma16(voffW[d], rW, (unsigned)cur_k0 * 4, w_dst + d * 1024);
+        cur_k0 += BK;
+        cur_c0 += BK;
+        if (cur_c0 == p.Cg) {
+            cur_c0 = 0;
+            set_tap(++cur_j);
+        }
+    };
+
+    const int wm = wave / WN, wn = wave % WN;
+    const int r32 = lane & 31, h = lane >> 5;
+    int rdA[2], rdB[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 2 + h;
+        rdA[kk] = (wm * (BM / WM) + r32) * CPR + (c ^ ((r32 >> 2) & 3));
+        rdB[kk] = BM * CPR + (wn * (BN / WN) + r32) * CPR + (c ^ ((r32 >> 2) & 3));
+    }
+    f32x16 acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+    const int nk = p.K / BK;
+    // prologue: NS-1 K-steps in flight, wait for the first
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < nk) issue(s);
+    if (nk >= NS - 1) wait_vm_barrier<(NS - 2) * (DA + DB)>();
+    else wait_vm_barrier<0>();
+
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(smem);
+    int stage = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+        // refill the stage read NS-1 steps ago (every wave passed the barrier after its reads)
+        const bool more = kt + NS - 1 < nk;
+        if (more) issue(stage == 0 ? NS - 1 : stage - 1);
+        const f32x4* st = s4 + stage * (STAGE / 4);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            f32x4 a[TI], b[TJ];
+#pragma unroll
+            for (int i = 0; i < TI; ++i) a[i] = st[rdA[kk] + i * 32 * CPR];
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) b[j] = st[rdB[kk] + j * 32 * CPR];
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -154,46 +367,88 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 4 : 2) void gemm_f32
                     for (int j = 0; j < TJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < nk) store_lds(cur ^ 1);
-        __syncthreads();
-    }
-
-    // epilogue: C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-    // GELU uses the branch-free erf (hfa::erf_nb), so lanes in different erf ranges never split.  (A separate
-    // unguarded interior-tile path with batched residual loads measured slower: it pushed the 128-VGPR tile
-    // into spills.)
-    float* Cb = p.C + zb * p.sCb + zg * p.sCg;
-    const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
-    const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
-    const int row0 = tm * BM + wm * (BM / WM) + 4 * h;
-    const int col0 = tn * BN + wn * (BN / WN) + r32;
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-        const int col = col0 + j * 32;
-        if (col >= p.N) continue;
-        const float bv = biasb ? biasb[col] : 0.0f;
-#pragma unroll
-        for (int i = 0; i < TI; ++i) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int row = row0 + i * 32 + (e & 3) + 8 * (e >> 2);
-                if (row >= p.M) continue;
-                float v = acc[i][j][e] + bv;
-                if (EPI == EPI_GELU) v = hfa::gelu_erf(v);
-                if (Rb) v += Rb[(long long)row * p.ldr + col];
-                Cb[(long long)row * p.ldc + col] = v;
-            }
+        if (kt + 1 < nk) {
+            if (more) wait_vm_barrier<(NS - 2) * (DA + DB)>();   // K-step kt+1 landed, kt+2.. still in flight
+            else wait_vm_barrier<0>();
         }
+        stage = stage + 1 == NS ? 0 : stage + 1;
     }
+    store_tile<EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane);
 }
 
 // Tile configurations (BM x BN, WM x WN waves); scripts/gemm_bench.py measures each on the workload's shapes.
 enum { CFG_AUTO = 0, CFG_128x128 = 1, CFG_128x64 = 2, CFG_256x128 = 3, CFG_128x256 = 4, CFG_256x128_W4 = 5,
        CFG_128x256_W4 = 6, CFG_256x256 = 7, CFG_COUNT = 8 };
-int g_force_bk = 0, g_force_cfg = 0;   // tuning overrides (hfa_gemm_tuning), 0 = automatic
+// Pipelines: register-staged BK 16 / 32, LDS-DMA with 2 or 3 stages.
+enum { PIPE_AUTO = 0, PIPE_REG16 = 16, PIPE_REG32 = 32, PIPE_DMA2 = 102, PIPE_DMA3 = 103 };
+int g_force_pipe = 0, g_force_cfg = 0;   // tuning overrides (hfa_gemm_tuning), 0 = automatic
 
-template <int EPI, int BK, int BM, int BN, int WM, int WN>
-int launch_cfg(GemmP p, int Z, bool vec_a, hipStream_t st) {
+// workgroups per CU a DMA instantiation is register-capped for: 128x128 3-stage (48 KiB LDS) -> 3, 2-stage and
+// 128x64 -> 4 (a 5th 2-stage workgroup measured no faster), 8-wave 128x256 -> 2 (64 accumulators per lane)
+constexpr int dma_occ(int BN, int NW, int NS) {
+    return NW == 4 ? (NS == 3 && BN == 128 ? 3 : 4) : 2;
+}
+
+struct Plan {
+    int pipe, cfg;
+    bool vec_a;
+};
+
+inline bool al16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
+
+// LDS-DMA eligibility: 16-B aligned A rows, and both buffer spans addressable by a 31-bit byte offset.
+inline bool dma_ok(const GemmP& p, bool vec_a) {
+    const long long a_span = ((long long)(p.Tin - 1) * p.ldx + p.Cg) * 4;
+    const long long w_span = ((long long)(p.N - 1) * p.ldw + p.K) * 4;
+    return vec_a && p.Tin >= 1 && a_span < 0x7fffffffLL && w_span < 0x7fffffffLL;
+}
+
+inline Plan make_plan(const GemmP& p, int Z, bool vec_a) {
+    // measured (scripts/gemm_bench.py, scripts/gpu_gemm_abl.sh): the LDS-DMA pipeline beats register staging by
+    // 8-12 % on every workload shape; 2 stages at 4 workgroups/CU beat 3 stages at 3 for the 128x128 tile; the
+    // 64-wide N tile (3 stages) wins for N <= 64 (grouped positional conv: 2x the 128-wide tile) and for grids
+    // too small to fill 256 CUs twice (UNet: +33 %); the 8-wave 128x256 tile no longer wins anywhere.
+    Plan pl;
+    pl.vec_a = vec_a;
+    const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
+    pl.cfg = (p.N <= 64 || blocks128 < 512) ? CFG_128x64 : CFG_128x128;
+    if (g_force_cfg > 0 && g_force_cfg < CFG_COUNT) pl.cfg = g_force_cfg;
+    const bool dma_cfg = pl.cfg == CFG_128x128 || pl.cfg == CFG_128x64 || pl.cfg == CFG_128x256;
+    pl.pipe = PIPE_REG16;
+    if (dma_cfg && dma_ok(p, vec_a)) pl.pipe = pl.cfg == CFG_128x64 ? PIPE_DMA3 : PIPE_DMA2;
+    if (g_force_pipe == PIPE_REG16) pl.pipe = PIPE_REG16;
+    if (g_force_pipe == PIPE_REG32 && p.K % 32 == 0 && p.Cg % 32 == 0) pl.pipe = PIPE_REG32;
+    if ((g_force_pipe == PIPE_DMA2 || g_force_pipe == PIPE_DMA3) && dma_cfg && dma_ok(p, vec_a))
+        pl.pipe = g_force_pipe;
+    return pl;
+}
+
+inline void cfg_shape(int cfg, int& BM, int& BN, int& WM, int& WN) {
+    switch (cfg) {
+        case CFG_128x64: BM = 128; BN = 64; WM = 2; WN = 2; break;
+        case CFG_256x128: BM = 256; BN = 128; WM = 4; WN = 2; break;
+        case CFG_128x256: BM = 128; BN = 256; WM = 2; WN = 4; break;
+        case CFG_256x128_W4: BM = 256; BN = 128; WM = 2; WN = 2; break;
+        case CFG_128x256_W4: BM = 128; BN = 256; WM = 2; WN = 2; break;
+        case CFG_256x256: BM = 256; BN = 256; WM = 4; WN = 2; break;
+        default: BM = 128; BN = 128; WM = 2; WN = 2; break;
+    }
+}
+
+// rocprof symbol stem of the instantiation a plan launches (bench.py's probe keys on it)
+inline void plan_name(const Plan& pl, int epi, char* buf, int len) {
+    int BM, BN, WM, WN;
+    cfg_shape(pl.cfg, BM, BN, WM, WN);
+    if (pl.pipe == PIPE_DMA2 || pl.pipe == PIPE_DMA3) {
+        const int ns = pl.pipe - 100, occ = dma_occ(BN, WM * WN, ns);
+        snprintf(buf, len, "gemm_dma_kernel<%d, %d, %d, %d, %d, %d, %d>", epi, BM, BN, WM, WN, ns, occ);
+    } else {
+        snprintf(buf, len, "gemm_f32_kernel<%d, %s, %d, %d, %d, %d, %d>", epi, pl.vec_a ? "true" : "false",
+                 pl.pipe == PIPE_REG32 ? 32 : 16, BM, BN, WM, WN);
+    }
+}
+
+inline int set_grid(GemmP& p, int BM, int BN, dim3& grid, int Z) {
     p.m_tiles = (p.M + BM - 1) / BM;
     p.n_tiles = (p.N + BN - 1) / BN;
     const long long tiles = (long long)p.m_tiles * p.n_tiles;
@@ -201,51 +456,62 @@ int launch_cfg(GemmP p, int Z, bool vec_a, hipStream_t st) {
         hfa::set_error("hfa_conv_gemm_f32: grid too large");
         return HFA_EINVAL;
     }
-    dim3 grid((unsigned)tiles, 1, Z);
+    grid = dim3((unsigned)tiles, 1, Z);
+    return HFA_OK;
+}
+
+template <int EPI, int BK, int BM, int BN, int WM, int WN>
+int launch_reg(GemmP p, int Z, bool vec_a, hipStream_t st) {
+    dim3 grid;
+    if (int rc = set_grid(p, BM, BN, grid, Z)) return rc;
     if (vec_a) hipLaunchKernelGGL((gemm_f32_kernel<EPI, true, BK, BM, BN, WM, WN>), grid, dim3(64 * WM * WN), 0, st, p);
     else hipLaunchKernelGGL((gemm_f32_kernel<EPI, false, BK, BM, BN, WM, WN>), grid, dim3(64 * WM * WN), 0, st, p);
     return hfa::check_launch("hfa_conv_gemm_f32");
 }
 
+template <int EPI, int BM, int BN, int WM, int WN, int NS>
+int launch_dma(GemmP p, int Z, hipStream_t st) {
+    constexpr int OCC = dma_occ(BN, WM * WN, NS);
+    dim3 grid;
+    if (int rc = set_grid(p, BM, BN, grid, Z)) return rc;
+    hipLaunchKernelGGL((gemm_dma_kernel<EPI, BM, BN, WM, WN, NS, OCC>), grid, dim3(64 * WM * WN), 0, st, p);
+    return hfa::check_launch("hfa_conv_gemm_f32");
+}
+
 template <int EPI, int BK>
-int launch_bk(int cfg, const GemmP& p, int Z, bool vec_a, hipStream_t st) {
+int launch_reg_cfg(int cfg, const GemmP& p, int Z, bool vec_a, hipStream_t st) {
     switch (cfg) {
-        case CFG_128x64: return launch_cfg<EPI, BK, 128, 64, 2, 2>(p, Z, vec_a, st);
-        case CFG_256x128: return launch_cfg<EPI, BK, 256, 128, 4, 2>(p, Z, vec_a, st);
-        case CFG_128x256: return launch_cfg<EPI, BK, 128, 256, 2, 4>(p, Z, vec_a, st);
-        case CFG_256x128_W4: return launch_cfg<EPI, BK, 256, 128, 2, 2>(p, Z, vec_a, st);
-        case CFG_128x256_W4: return launch_cfg<EPI, BK, 128, 256, 2, 2>(p, Z, vec_a, st);
-        case CFG_256x256: return launch_cfg<EPI, BK, 256, 256, 4, 2>(p, Z, vec_a, st);
-        default: return launch_cfg<EPI, BK, 128, 128, 2, 2>(p, Z, vec_a, st);
+        case CFG_128x64: return launch_reg<EPI, BK, 128, 64, 2, 2>(p, Z, vec_a, st);
+        case CFG_256x128: return launch_reg<EPI, BK, 256, 128, 4, 2>(p, Z, vec_a, st);
+        case CFG_128x256: return launch_reg<EPI, BK, 128, 256, 2, 4>(p, Z, vec_a, st);
+        case CFG_256x128_W4: return launch_reg<EPI, BK, 256, 128, 2, 2>(p, Z, vec_a, st);
+        case CFG_128x256_W4: return launch_reg<EPI, BK, 128, 256, 2, 2>(p, Z, vec_a, st);
+        case CFG_256x256: return launch_reg<EPI, BK, 256, 256, 4, 2>(p, Z, vec_a, st);
+        default: return launch_reg<EPI, BK, 128, 128, 2, 2>(p, Z, vec_a, st);
+    }
+}
+
+template <int EPI, int NS>
+int launch_dma_cfg(int cfg, const GemmP& p, int Z, hipStream_t st) {
+    switch (cfg) {
+        case CFG_128x64: return launch_dma<EPI, 128, 64, 2, 2, NS>(p, Z, st);
+        case CFG_128x256: return launch_dma<EPI, 128, 256, 2, 4, NS>(p, Z, st);
+        default: return launch_dma<EPI, 128, 128, 2, 2, NS>(p, Z, st);
     }
 }
 
 template <int EPI>
-int launch(const GemmP& p, int Z, bool vec_a, hipStream_t st) {
-    // measured (scripts/gemm_bench.py): BK=16 keeps 3 blocks/CU and wins on every workload shape; the 64-wide
-    // N tile wins for N <= 64 (grouped positional conv) and for grids too small to fill 256 CUs twice (UNet).
-    // The 8-wave 128x256 tile wins on the extractor convs (long K over overlapping rows, M*Z >= 30k rows:
-    // +3..29 %) and loses on the transformer's Linear shapes (-5..-20 %).
-    const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
-    int cfg = (p.N <= 64 || blocks128 < 512) ? CFG_128x64 : CFG_128x128;
-    if (cfg == CFG_128x128 && p.N >= 512 && p.K >= 1024 && (long long)p.M * Z >= 30000 && p.stride > 1)
-        cfg = CFG_128x256;
-    if (g_force_cfg > 0 && g_force_cfg < CFG_COUNT) cfg = g_force_cfg;
-    const bool bk32_ok = p.K % 32 == 0 && p.Cg % 32 == 0;
-    if (g_force_bk == 32 && bk32_ok) return launch_bk<EPI, 32>(cfg, p, Z, vec_a, st);
-    return launch_bk<EPI, 16>(cfg, p, Z, vec_a, st);
+int launch(const GemmP& p, int Z, const Plan& pl, hipStream_t st) {
+    switch (pl.pipe) {
+        case PIPE_DMA3: return launch_dma_cfg<EPI, 3>(pl.cfg, p, Z, st);
+        case PIPE_DMA2: return launch_dma_cfg<EPI, 2>(pl.cfg, p, Z, st);
+        case PIPE_REG32: return launch_reg_cfg<EPI, 32>(pl.cfg, p, Z, pl.vec_a, st);
+        default: return launch_reg_cfg<EPI, 16>(pl.cfg, p, Z, pl.vec_a, st);
+    }
 }
 
-inline bool al16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
-
-}  // namespace
-
-extern "C" {
-
-int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg, int ldx,
-                      int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
-                      const float* bias, long long sBg, const float* R, long long sRb, long long sRg, int ldr,
-                      float* C, long long sCb, long long sCg, int ldc, int epilogue, hipStream_t stream) {
+int check_args(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg, int ldx,
+               int stride, int Cg, const float* W, long long sWg, int ldw, const float* C, int epilogue) {
     if (M < 0 || N < 0 || K < 0 || Zb < 0 || G < 1 || stride < 1 || Cg < 1) {
         hfa::set_error("hfa_conv_gemm_f32: bad sizes M=%d N=%d K=%d Zb=%d G=%d", M, N, K, Zb, G);
         return HFA_EINVAL;
@@ -271,21 +537,58 @@ int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long l
         hfa::set_error("hfa_conv_gemm_f32: Zb*G=%lld exceeds the grid z limit", (long long)Zb * G);
         return HFA_EINVAL;
     }
-    const bool vec_a = al16(A) && ldx % 4 == 0 && sAb % 4 == 0 && sAg % 4 == 0;
+    return HFA_OK;
+}
+
+GemmP make_params(int M, int N, int K, int G, const float* A, long long sAb, long long sAg, int ldx, int stride,
+                  int pad, int Cg, int Tin, const float* W, long long sWg, int ldw) {
     GemmP p;
     p.M = M; p.N = N; p.K = K; p.G = G;
-    p.m_tiles = p.n_tiles = 0;   // set per tile configuration in launch_cfg
+    p.m_tiles = p.n_tiles = 0;   // set per tile configuration at launch
     p.A = A; p.sAb = sAb; p.sAg = sAg; p.ldx = ldx; p.stride = stride; p.pad = pad; p.Cg = Cg; p.Tin = Tin;
     p.W = W; p.sWg = sWg; p.ldw = ldw;
+    p.bias = nullptr; p.sBg = 0;
+    p.R = nullptr; p.sRb = p.sRg = 0; p.ldr = 0;
+    p.C = nullptr; p.sCb = p.sCg = 0; p.ldc = 0;
+    return p;
+}
+
+inline bool vec_a_of(const float* A, int ldx, long long sAb, long long sAg) {
+    return al16(A) && ldx % 4 == 0 && sAb % 4 == 0 && sAg % 4 == 0;
+}
+
+thread_local char g_name[128];
+
+}  // namespace
+
+extern "C" {
+
+int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg, int ldx,
+                      int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
+                      const float* bias, long long sBg, const float* R, long long sRb, long long sRg, int ldr,
+                      float* C, long long sCb, long long sCg, int ldc, int epilogue, hipStream_t stream) {
+    if (int rc = check_args(M, N, K, Zb, G, A, sAb, sAg, ldx, stride, Cg, W, sWg, ldw, C, epilogue)) return rc;
+    if (M == 0 || N == 0 || Zb == 0) return HFA_OK;
+    GemmP p = make_params(M, N, K, G, A, sAb, sAg, ldx, stride, pad, Cg, Tin, W, sWg, ldw);
     p.bias = bias; p.sBg = sBg;
     p.R = R; p.sRb = sRb; p.sRg = sRg; p.ldr = ldr;
     p.C = C; p.sCb = sCb; p.sCg = sCg; p.ldc = ldc;
     const int Z = Zb * G;
-    return epilogue == EPI_GELU ? launch<EPI_GELU>(p, Z, vec_a, stream) : launch<EPI_NONE>(p, Z, vec_a, stream);
+    const Plan pl = make_plan(p, Z, vec_a_of(A, ldx, sAb, sAg));
+    return epilogue == EPI_GELU ? launch<EPI_GELU>(p, Z, pl, stream) : launch<EPI_NONE>(p, Z, pl, stream);
 }
 
-int hfa_gemm_tuning(int force_bk, int force_cfg) {
-    g_force_bk = force_bk;
+const char* hfa_gemm_kernel_name(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg,
+                                 int ldx, int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
+                                 int epilogue) {
+    GemmP p = make_params(M, N, K, G, A, sAb, sAg, ldx, stride, pad, Cg, Tin, W, sWg, ldw);
+    const Plan pl = make_plan(p, Zb * G, vec_a_of(A, ldx, sAb, sAg));
+    plan_name(pl, epilogue, g_name, sizeof(g_name));
+    return g_name;
+}
+
+int hfa_gemm_tuning(int force_pipe, int force_cfg) {
+    g_force_pipe = force_pipe;
     g_force_cfg = force_cfg;
     return HFA_OK;
 }

@@ -54,9 +54,16 @@ def viterbi_forward(prob_log, not_edge_log, edge_log, curr, dp, bt, ph_seq_id, T
     assert dp.shape == prob_log.shape and bt.shape == prob_log.shape
     assert curr.shape == (B, Smax) and ph_seq_id.shape == (B, Smax)
     assert not_edge_log.shape == (B, Tmax) and edge_log.shape == (B, Tmax)
-    _lib.call("hfa_viterbi_forward", B, Tmax, Smax, _ptr(T), _ptr(S), _ptr(pad), _ptr(prob_log),
-              _ptr(not_edge_log), _ptr(edge_log), _ptr(curr), _ptr(dp), _ptr(bt), _ptr(ph_seq_id),
-              _stream(prob_log.device))
+
+    def launch():
+        _lib.call("hfa_viterbi_forward", B, Tmax, Smax, _ptr(T), _ptr(S), _ptr(pad), _ptr(prob_log),
+                  _ptr(not_edge_log), _ptr(edge_log), _ptr(curr), _ptr(dp), _ptr(bt), _ptr(ph_seq_id),
+                  _stream(prob_log.device))
+    if PROBE is None:
+        return launch()
+    # SURVEY §8(d) algorithmic bytes: prob_log in + dp out (4 B each) + bt out (1 B) per cell, 8 B edge terms
+    # per frame; counted on the padded planes (exact when every utterance of the batch fills them).
+    PROBE("viterbi_forward_kernel", B * (9.0 * Tmax * Smax + 8.0 * Tmax), launch, kind="bytes")
 
 
 def viterbi_backtrack(dp, bt, ph_seq_id, T, S):
@@ -123,6 +130,8 @@ _P_, _I_, _LL_, _F_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c
 _lib.register("hfa_conv_gemm_f32", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_, _LL_, _I_,
                                     _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _I_, _P_])
 _lib.register("hfa_gemm_tuning", [_I_, _I_])
+_lib.register("hfa_gemm_kernel_name", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_, _LL_,
+                                       _I_, _I_], ctypes.c_char_p)
 _lib.register("hfa_gemm_f32", [_I_, _I_, _I_, _P_, _I_, _P_, _I_, _P_, _P_, _I_, _P_, _I_, _I_, _P_])
 _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_,
                                     _LL_, _I_, _P_])
@@ -140,52 +149,55 @@ _lib.register("hfa_resample_f32", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _I_, _I_,
 
 
 class KernelProbe:
-    """Times every launch of one kernel instantiation with HIP events on the launching stream (bench.py).
+    """Times every launch of the watched kernels with HIP events on the launching stream (bench.py).
 
-    ``name`` is the rocprof kernel symbol stem, e.g. ``gemm_f32_kernel<1, true>``; per launch the algorithmic
-    FLOPs are recorded next to the event pair, so achieved = sum(flops) / sum(durations)."""
+    ``name`` is the rocprof kernel symbol stem of the dominant kernel, e.g. ``gemm_f32_kernel<1, true, ...>``;
+    ``extra`` names further kernels to time (the DP, conv0, attention).  Per launch the algorithmic work (FLOPs
+    for MFMA kernels, bytes for HBM/latency-bound ones) is recorded next to the event pair, so
+    achieved = sum(work) / sum(durations).  Census mode (name None) times nothing and tallies FLOPs per
+    MFMA instantiation so bench.py can pick the dominant one."""
 
-    def __init__(self, name: str | None):
-        self.name = name            # None: census mode (no events; FLOPs tallied per instantiation)
-        self.records = []
+    def __init__(self, name: str | None, extra=()):
+        self.name = name
+        self.watch = set(extra) | ({name} if name else set())
+        self.records = {}
         self.census = {}
 
     def dominant(self) -> str:
         return max(self.census, key=self.census.get)
 
-    def __call__(self, name: str, flops: float, launch):
+    def __call__(self, name: str, work: float, launch, kind: str = "flops"):
         if self.name is None:
-            self.census[name] = self.census.get(name, 0.0) + flops
+            if kind == "flops":
+                self.census[name] = self.census.get(name, 0.0) + work
             return launch()
-        if name != self.name:
+        if name not in self.watch:
             return launch()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         launch()
         e.record()
-        self.records.append((s, e, flops))
+        self.records.setdefault(name, []).append((s, e, work))
 
-    def summary(self):
+    def summary(self, name: str | None = None):
         torch.cuda.synchronize()
-        n = len(self.records)
-        ms = sum(s.elapsed_time(e) for s, e, _ in self.records)
-        fl = sum(f for _, _, f in self.records)
-        return {"launches": n, "total_ms": ms, "avg_ms": ms / max(n, 1), "flops": fl,
-                "avg_flops": fl / max(n, 1)}
+        recs = self.records.get(name or self.name, [])
+        n = len(recs)
+        ms = sum(s.elapsed_time(e) for s, e, _ in recs)
+        w = sum(f for _, _, f in recs)
+        return {"launches": n, "total_ms": ms, "avg_ms": ms / max(n, 1), "work": w, "avg_work": w / max(n, 1),
+                "flops": w, "avg_flops": w / max(n, 1)}
 
 
 PROBE = None
 
 
-def _gemm_name(epilogue: int, A, ldx: int, sAb: int, sAg: int, M: int, N: int, K: int, Z: int,
-               stride: int) -> str:
-    """rocprof symbol of the instantiation hfa_conv_gemm_f32 dispatches to (mirrors gemm.hip launch())."""
-    vec = A.data_ptr() % 16 == 0 and ldx % 4 == 0 and sAb % 4 == 0 and sAg % 4 == 0
-    blocks128 = -(-M // 128) * -(-N // 128) * Z
-    tile = "128, 64, 2, 2" if (N <= 64 or blocks128 < 512) else "128, 128, 2, 2"
-    if tile == "128, 128, 2, 2" and N >= 512 and K >= 1024 and M * Z >= 30000 and stride > 1:
-        tile = "128, 256, 2, 4"
-    return f"gemm_f32_kernel<{epilogue}, {'true' if vec else 'false'}, 16, {tile}>"
+def _gemm_name(epilogue: int, A, W, M: int, N: int, K: int, Zb: int, G: int, sAb: int, sAg: int, ldx: int,
+               stride: int, pad: int, Cg: int, Tin: int, sWg: int, ldw: int) -> str:
+    """rocprof symbol stem of the instantiation hfa_conv_gemm_f32 dispatches to (asked from the library)."""
+    name = _lib.lib().hfa_gemm_kernel_name(M, N, K, Zb, G, _ptr(A), sAb, sAg, ldx, stride, pad, Cg, Tin, _ptr(W),
+                                           sWg, ldw, epilogue)
+    return name.decode()
 
 
 def conv_gemm(A, W, C, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None, Tin=None, sWg=0,
@@ -200,7 +212,9 @@ def conv_gemm(A, W, C, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0
                   _ptr(R), sRb, sRg, ldr, _ptr(C), sCb, sCg, ldc, epilogue, _stream(C.device))
     if PROBE is None:
         return launch()
-    PROBE(_gemm_name(epilogue, A, ldx, sAb, sAg, M, N, K, Zb * G, stride), 2.0 * M * N * K * Zb * G, launch)
+    PROBE(_gemm_name(epilogue, A, W, M, N, K, Zb, G, sAb, sAg, ldx, stride, pad, Cg or K,
+                     Tin if Tin is not None else M, sWg, ldw if ldw is not None else K),
+          2.0 * M * N * K * Zb * G, launch)
 
 
 def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
@@ -221,13 +235,19 @@ def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
     if PROBE is None:
         launch()
     else:
-        PROBE(_gemm_name(epilogue, x2, x2.stride(0), 0, 0, M, N, K, 1, 1), 2.0 * M * N * K, launch)
+        PROBE(_gemm_name(epilogue, x2, W, M, N, K, 1, 1, 0, 0, x2.stride(0), 1, 0, K, M, 0, W.stride(0)),
+              2.0 * M * N * K, launch)
     return out
 
 
 def attention(q, k, v, out, *, B, H, L, head_dim, scale, q_bs, q_ld, k_bs, k_ld, v_bs, v_ld, o_bs, o_ld):
-    _lib.call("hfa_attention_f32", B, H, L, head_dim, float(scale), _ptr(q), q_bs, q_ld, _ptr(k), k_bs, k_ld,
-              _ptr(v), v_bs, v_ld, _ptr(out), o_bs, o_ld, _stream(out.device))
+    def launch():
+        _lib.call("hfa_attention_f32", B, H, L, head_dim, float(scale), _ptr(q), q_bs, q_ld, _ptr(k), k_bs, k_ld,
+                  _ptr(v), v_bs, v_ld, _ptr(out), o_bs, o_ld, _stream(out.device))
+    if PROBE is None:
+        launch()
+    else:                       # QK^T and PV: 2 * 2 * L * L * head_dim per (batch, head)
+        PROBE("attn_fwd_f32_kernel", 4.0 * B * H * L * L * head_dim, launch, kind="flops_aux")
     return out
 
 
@@ -264,8 +284,14 @@ def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, worksp
     if norm and workspace is None:
         nbytes = _lib.lib().hfa_conv0_workspace_bytes(B, N)
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
-    _lib.call("hfa_conv0_f32", B, N, _ptr(x), x.stride(0), _ptr(w0), _ptr(bias), 1 if norm else 0, _ptr(gamma),
-              _ptr(beta), float(eps), _ptr(workspace), _ptr(out), out.stride(0), _stream(x.device))
+    def launch():
+        _lib.call("hfa_conv0_f32", B, N, _ptr(x), x.stride(0), _ptr(w0), _ptr(bias), 1 if norm else 0,
+                  _ptr(gamma), _ptr(beta), float(eps), _ptr(workspace), _ptr(out), out.stride(0),
+                  _stream(x.device))
+    if PROBE is None:
+        launch()
+    else:                       # wave in (4 B/sample) + activations out (4 B x 512 x T0)
+        PROBE("hfa_conv0_f32", B * (4.0 * N + 4.0 * 512 * T0), launch, kind="bytes")
     return out
 
 

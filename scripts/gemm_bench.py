@@ -61,17 +61,23 @@ def run(shape, bk, cfg, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--variants", default="16:1,16:2,16:3,16:4,16:5,16:6")
+    ap.add_argument("--variants", default="16:1,16:2,16:4,103:1,103:2,103:4",
+                    help="pipe:cfg pairs; pipe 16/32 register-staged BK, 102/103 LDS-DMA 2/3 stages")
+    ap.add_argument("--shapes", default="", help="comma-separated subset of shape names")
     args = ap.parse_args()
+    keep = set(args.shapes.split(",")) if args.shapes else None
     names = {1: "128x128/2x2", 2: "128x64/2x2", 3: "256x128/4x2", 4: "128x256/2x4", 5: "256x128/2x2",
              6: "128x256/2x2", 7: "256x256/4x2"}
     variants = [tuple(int(v) for v in s.split(":")) for s in args.variants.split(",")]
     for shape in SHAPES:
+        if keep is not None and shape[0] not in keep:
+            continue
         for bk, cfg in variants:
             if bk == 32 and (shape[2] // shape[7]) % 32:
                 continue
             ms, tf = run(shape, bk, cfg, args.reps)
-            print(f"{shape[0]:10s} bk={bk:2d} {names[cfg]:12s} {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+            pipe = {16: "reg16", 32: "reg32", 102: "dma2", 103: "dma3"}.get(bk, str(bk))
+            print(f"{shape[0]:10s} {pipe:6s} {names[cfg]:12s} {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
     _lib.lib().hfa_gemm_tuning(0, 0)
 
 

@@ -69,9 +69,11 @@ def test_conv_gemm_vs_conv1d(Cin, Cout, k, s, pad, T, G):
     _close(out, ref, 5e-5, 5e-5)
 
 
-@pytest.mark.parametrize("bk,bn", [(16, c) for c in range(1, 8)] + [(32, 1), (32, 3)])
+@pytest.mark.parametrize("bk,bn", [(16, c) for c in range(1, 8)] + [(32, 1), (32, 3)] +
+                         [(p, c) for p in (102, 103) for c in (1, 2, 4)])
 def test_gemm_tile_variants(bk, bn):
-    """Every tile instantiation is exact on a conv and a Linear shape with tails in M and N."""
+    """Every tile instantiation (register-staged BK 16/32, LDS-DMA 2/3 stages) is exact on a conv and a Linear
+    shape with tails in M and N."""
     from hubertfa_amd import ops, _lib
     _lib.lib().hfa_gemm_tuning(bk, bn)
     try:
