@@ -1,16 +1,18 @@
 // attention.hip — fp32 flash attention on MFMA (v_mfma_f32_32x32x2_f32), head_dim 64, no mask (key length
-// masking only), scale applied to Q (exact for power-of-two scales such as 64^-0.5 = 1/8).
+// masking only); scale * log2(e) is folded into Q (softmax evaluated as exp2, same value up to rounding).
 //
 // Replaces: torch scaled_dot_product_attention / nn.MultiheadAttention fast path in the bshall encoder
 // (networks/hubert/model.py:27-32) and transformers HubertAttention eager path
 // (modeling_hubert.py eager_attention_forward: softmax(q k^T * head_dim^-0.5) v).
 //
 // Structure: one workgroup = 4 waves = 128 queries of one (batch, head); each wave owns 32 queries.
-// K/V tiles of 32 keys are staged through double-buffered LDS and shared by the 4 waves.
+// K/V tiles of 32 keys arrive by LDS-DMA (buffer_load ... lds, NS-stage ring, no VALU staging work: the f32 MFMA
+// shares the vector ALU's issue, so VALU work in the loop costs MFMA time) and are shared by the 4 waves.
 // The score tile is computed TRANSPOSED (S^T = K Q^T) so each lane holds one query column and 16 keys in its
 // accumulator registers: the per-query max/sum is an in-register reduction plus one xor-32 lane swap, and the
 // S^T accumulator registers are directly the B operand of O^T += V^T P^T (no LDS round trip for P).
-// Online softmax (running max/sum per query) avoids materialising the L x L matrix.
+// Online softmax in the log2 domain: scale*log2(e) is folded into Q, so p = exp2(s - m) is one v_exp_f32;
+// the running output is rescaled only when some query's running max moved (wave-uniform skip; x*1 is exact).
 #include "hfa_common.h"
 
 namespace {
@@ -22,7 +24,11 @@ constexpr int DH = 64;
 constexpr int KB = 32;          // keys per tile
 constexpr int QW = 32;          // queries per wave
 constexpr int NW = 4;           // waves per workgroup
-constexpr int LDK = DH + 4;     // padded LDS row (ds_read_b128 conflict-free)
+#ifndef HFA_ATTN_NS
+#define HFA_ATTN_NS 2
+#endif
+constexpr int NS = HFA_ATTN_NS; // LDS stages (NS-1 key tiles in flight)
+constexpr int TILE = KB * DH;   // floats per K (or V) tile image
 
 struct AttnP {
     int B, H, L;
@@ -34,52 +40,61 @@ struct AttnP {
 };
 
 __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
-    __shared__ __attribute__((aligned(16))) float sK[2][KB * LDK];
-    __shared__ __attribute__((aligned(16))) float sV[2][KB * LDK];
+    // stage s: K image [32 rows][64] with 16-B chunks XOR-swizzled by (row & 15) (ds_read_b128 row reads by 32
+    // rows stay conflict-free), then V image [32][64] unswizzled (read by ds_read2_b32 along rows)
+    __shared__ __attribute__((aligned(16))) float smem[NS * 2 * TILE];
 
-    const int bh = blockIdx.y;
+    // XCD-aware bijective remap (as in gemm.hip): the q-blocks of one (batch, head) get consecutive ids and so
+    // share an XCD's L2 for their K/V tiles
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, xq = nwg >> 3, xr = nwg & 7;
+    const int wgid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (orig >> 3);
+    const int nqb = (p.L + QW * NW - 1) / (QW * NW);
+    const int bh = wgid / nqb, qb = wgid - bh * nqb;
     const int b = bh / p.H, hd = bh - b * p.H;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r32 = lane & 31, half = lane >> 5;
-    const int q0 = blockIdx.x * (QW * NW) + wave * QW;
+    const int q0 = qb * (QW * NW) + wave * QW;
     const int qi = q0 + r32;
 
     const float* Q = p.q + b * p.q_bs + hd * DH;
     const float* Kp = p.k + b * p.k_bs + hd * DH;
     const float* Vp = p.v + b * p.v_bs + hd * DH;
+    const __amdgpu_buffer_rsrc_t rK = hfa::make_rsrc(Kp, ((long long)(p.L - 1) * p.k_ld + DH) * 4);
+    const __amdgpu_buffer_rsrc_t rV = hfa::make_rsrc(Vp, ((long long)(p.L - 1) * p.v_ld + DH) * 4);
 
-    // Q fragments: lane holds Q[qi][kk*8 + half*4 + e] * scale, kk = 0..7, e = 0..3
+    // Q fragments: lane holds Q[qi][kk*8 + half*4 + e] * scale * log2(e), kk = 0..7, e = 0..3
+    const float qscale = p.scale * 1.44269504088896340736f;
     f32x4 qf[DH / 8];
 #pragma unroll
     for (int kk = 0; kk < DH / 8; ++kk) {
         if (qi < p.L) {
             f32x4 v = *reinterpret_cast<const f32x4*>(Q + (long long)qi * p.q_ld + kk * 8 + half * 4);
-            qf[kk] = v * p.scale;
+            qf[kk] = v * qscale;
         } else {
             qf[kk] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     }
 
-    // K/V staging: 32 rows x 64 floats each = 512 float4 per matrix; 256 threads x 2 each
-    f32x4 rk[2], rv[2];
-    auto load_tile = [&](int key0) {
+    // DMA geometry: 8 x 1 KiB wave-instructions per 32 x 64 image, 2 per wave; instruction d covers rows
+    // (wave*2 + d)*4 + lane/16, LDS slot lane&15
+    int rowd[2], kcol[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int idx = tid + i * NW * 64;
-            const int row = idx >> 4, c4 = (idx & 15) * 4;
-            const int key = key0 + row;
+    for (int d = 0; d < 2; ++d) {
+        rowd[d] = (wave * 2 + d) * 4 + (lane >> 4);
+        kcol[d] = ((lane & 15) ^ (rowd[d] & 15)) * 4;
+    }
+    const unsigned lds0 = hfa::lds_addr(smem);
+    auto issue = [&](int stage, int key0) {
+        const unsigned kdst = lds0 + stage * 2 * TILE * 4 + wave * 2 * 1024;
+        const unsigned vdst = kdst + TILE * 4;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            const int key = key0 + rowd[d];
             const bool ok = key < p.L;
-            rk[i] = ok ? *reinterpret_cast<const f32x4*>(Kp + (long long)key * p.k_ld + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-            rv[i] = ok ? *reinterpret_cast<const f32x4*>(Vp + (long long)key * p.v_ld + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-    };
-    auto store_tile = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int idx = tid + i * NW * 64;
-            const int row = idx >> 4, c4 = (idx & 15) * 4;
-            *reinterpret_cast<f32x4*>(&sK[buf][row * LDK + c4]) = rk[i];
-            *reinterpret_cast<f32x4*>(&sV[buf][row * LDK + c4]) = rv[i];
+            hfa::dma16(ok ? (unsigned)((key * p.k_ld + kcol[d]) * 4) : hfa::DMA_OOB, rK, 0u, kdst + d * 1024);
+            hfa::dma16(ok ? (unsigned)((key * p.v_ld + (lane & 15) * 4) * 4) : hfa::DMA_OOB, rV, 0u, vdst + d * 1024);
         }
     };
 
@@ -88,81 +103,96 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
     for (int e = 0; e < 16; ++e) { oacc[0][e] = 0.f; oacc[1][e] = 0.f; }
     float m_run = -__builtin_inff(), l_run = 0.0f;
 
+    // per-lane LDS read offsets (floats): K row r32 chunk (kk*2 + half) swizzled; V row j(e, half), column r32
+    int krd[DH / 8];
+#pragma unroll
+    for (int kk = 0; kk < DH / 8; ++kk) krd[kk] = r32 * DH + (((kk * 2 + half) ^ (r32 & 15)) << 2);
+
     const int nkb = (p.L + KB - 1) / KB;
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < NS - 1; ++st)
+        if (st < nkb) issue(st, st * KB);
+    if (nkb >= NS - 1) hfa::wait_vm_barrier<(NS - 2) * 4>();
+    else hfa::wait_vm_barrier<0>();
+    int stage = 0;
     for (int kb = 0; kb < nkb; ++kb) {
-        const int cur = kb & 1;
-        if (kb + 1 < nkb) load_tile((kb + 1) * KB);
-        // S^T[j][i] = sum_d K[j][d] * Qs[i][d]
+        const bool more = kb + NS - 1 < nkb;
+        if (more) issue(stage == 0 ? NS - 1 : stage - 1, (kb + NS - 1) * KB);
+        const float* sK = smem + stage * 2 * TILE;
+        const float* sV = sK + TILE;
+        // S^T[j][i] = sum_d K[j][d] * Qs[i][d]  (log2 units)
         f32x16 s;
 #pragma unroll
         for (int e = 0; e < 16; ++e) s[e] = 0.f;
 #pragma unroll
         for (int kk = 0; kk < DH / 8; ++kk) {
-            const f32x4 kf = *reinterpret_cast<const f32x4*>(&sK[cur][r32 * LDK + kk * 8 + half * 4]);
+            const f32x4 kf = *reinterpret_cast<const f32x4*>(sK + krd[kk]);
 #pragma unroll
             for (int e = 0; e < 4; ++e) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[e], qf[kk][e], s, 0, 0, 0);
         }
-        // mask keys beyond L; block max per query (this lane's 16 keys + partner lane's 16)
         const int key0 = kb * KB;
-        float bm = -__builtin_inff();
+        if (key0 + KB > p.L) {          // last, partial tile: keys >= L do not exist
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int j = key0 + (e & 3) + 8 * (e >> 2) + 4 * half;
-            if (j >= p.L) s[e] = -__builtin_inff();
-            bm = fmaxf(bm, s[e]);
+            for (int e = 0; e < 16; ++e)
+                if (key0 + (e & 3) + 8 * (e >> 2) + 4 * half >= p.L) s[e] = -__builtin_inff();
         }
+        float bm = s[0];
+#pragma unroll
+        for (int e = 1; e < 16; ++e) bm = fmaxf(bm, s[e]);
         bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
         const float m_new = fmaxf(m_run, bm);
-        const float alpha = expf(m_run - m_new);
+        if (__builtin_amdgcn_ballot_w64(m_new != m_run)) {     // some query's max moved: rescale
+            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+            l_run *= alpha;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) { oacc[0][e] *= alpha; oacc[1][e] *= alpha; }
+            m_run = m_new;
+        }
         float ls = 0.0f;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            s[e] = expf(s[e] - m_new);
+            s[e] = __builtin_amdgcn_exp2f(s[e] - m_run);
             ls += s[e];
         }
         ls += __shfl_xor(ls, 32, 64);
-        l_run = l_run * alpha + ls;
-        m_run = m_new;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) { oacc[0][e] *= alpha; oacc[1][e] *= alpha; }
+        l_run += ls;
         // O^T[d][i] += sum_j V[j][d] * P^T[j][i]; MFMA e uses key j(e, half) = (e&3) + 8(e>>2) + 4 half
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int j = (e & 3) + 8 * (e >> 2) + 4 * half;
-            const float v0 = sV[cur][j * LDK + r32];
-            const float v1 = sV[cur][j * LDK + 32 + r32];
+            const float v0 = sV[j * DH + r32];
+            const float v1 = sV[j * DH + 32 + r32];
             oacc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0, s[e], oacc[0], 0, 0, 0);
             oacc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, s[e], oacc[1], 0, 0, 0);
         }
-        if (kb + 1 < nkb) store_tile(cur ^ 1);
-        __syncthreads();
+        if (kb + 1 < nkb) {                     // next tile landed; every wave done with this stage
+            if (more) hfa::wait_vm_barrier<(NS - 2) * 4>();
+            else hfa::wait_vm_barrier<0>();
+        }
+        stage = stage + 1 == NS ? 0 : stage + 1;
     }
 
-    // normalise and stage O[i][d] through LDS (reuse sK: 4 waves x 32 queries x 68 floats fits in 2*32*68)
+    // normalise and stage O[i][d] through LDS (each wave a private 32 x 33 slab), row-contiguous stores
+    __syncthreads();
     const float inv = 1.0f / l_run;
-    float* stage = &sK[0][0] + wave * (QW * LDK / 2);  // 32 x 34? -> use two passes of 32 dims
+    float* slab = smem + wave * (QW * 33);
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) {
-        // each wave writes its 32 queries x 32 dims (dims dt*32..) into a private 32 x 33 slab
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int d = (e & 3) + 8 * (e >> 2) + 4 * half;
-            stage[r32 * 33 + d] = oacc[dt][e] * inv;
+            slab[r32 * 33 + d] = oacc[dt][e] * inv;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        // 32 rows x 32 floats = 256 float4 -> 4 per lane, row-contiguous global stores
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int idx = lane + i * 64;
             const int row = idx >> 3, c4 = (idx & 7) * 4;
             const int qq = q0 + row;
             if (qq < p.L) {
-                f32x4 v{stage[row * 33 + c4], stage[row * 33 + c4 + 1], stage[row * 33 + c4 + 2],
-                        stage[row * 33 + c4 + 3]};
+                f32x4 v{slab[row * 33 + c4], slab[row * 33 + c4 + 1], slab[row * 33 + c4 + 2],
+                        slab[row * 33 + c4 + 3]};
                 *reinterpret_cast<f32x4*>(p.o + b * p.o_bs + (long long)qq * p.o_ld + hd * DH + dt * 32 + c4) = v;
             }
         }
@@ -191,8 +221,17 @@ int hfa_attention_f32(int B, int H, int L, int head_dim, float scale, const floa
         hfa::set_error("hfa_attention_f32: operands must be 16-byte aligned with strides multiple of 4");
         return HFA_EINVAL;
     }
+    if (((long long)(L - 1) * k_ld + DH) * 4 >= 0x7fffffffLL || ((long long)(L - 1) * v_ld + DH) * 4 >= 0x7fffffffLL) {
+        hfa::set_error("hfa_attention_f32: K/V span exceeds 31-bit buffer offsets");
+        return HFA_EINVAL;
+    }
     AttnP p{B, H, L, scale, q, q_bs, q_ld, k, k_bs, k_ld, v, v_bs, v_ld, o, o_bs, o_ld};
-    dim3 grid((L + QW * NW - 1) / (QW * NW), B * H);
+    const long long nblk = (long long)((L + QW * NW - 1) / (QW * NW)) * B * H;
+    if (nblk > 0x7fffffffLL) {
+        hfa::set_error("hfa_attention_f32: grid too large");
+        return HFA_EINVAL;
+    }
+    dim3 grid((unsigned)nblk);
     hipLaunchKernelGGL(attn_fwd_f32_kernel, grid, dim3(NW * 64), 0, stream, p);
     return hfa::check_launch("hfa_attention_f32");
 }

@@ -232,24 +232,6 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 4 : 2) void gemm_f32
 // chunks), so the swizzle is applied on the SOURCE side (lane l loads chunk (l&3) ^ sw(row)).
 // Out-of-range conv taps (padding) read through a voffset beyond the buffer's num_records, which the range check
 // turns into zeros (scripts/probes/dma_oob.hip); rows past M / N are clamped (their outputs are never stored).
-__device__ __forceinline__ unsigned lds_addr(const void* ptr) {
-    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)ptr;
-}
-
-__device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned soff, unsigned lds) {
-    unsigned keep;   // M0 is compiler-reserved: set and restore it inside the statement that uses it
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds) : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm_barrier() {
-    // this wave's DMAs except the newest N landed, its LDS reads retired, then every wave of the block
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "i"(N) : "memory");
-}
-
-constexpr unsigned DMA_OOB = 0x80000000u;
 
 template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP p) {
@@ -298,10 +280,10 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP
 #pragma unroll
         for (int d = 0; d < DA; ++d) {
             const int t = a_t0[d] + j;
-            voffA[d] = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + a_c[d]) * 4) : DMA_OOB;
+            voffA[d] = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + a_c[d]) * 4) : hfa::DMA_OOB;
         }
     };
-    const unsigned lds0 = lds_addr(smem);
+    const unsigned lds0 = hfa::lds_addr(smem);
     // K-step cursor: tap j, channel offset c0 inside the tap, absolute k0
     int cur_j = 0, cur_c0 = 0, cur_k0 = 0;
     set_tap(0);
@@ -309,9 +291,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP
         const unsigned a_dst = lds0 + stage * STAGE * 4 + wave * DA * 1024;
         const unsigned w_dst = lds0 + (stage * STAGE + BM * BK) * 4 + wave * DB * 1024;
 #pragma unroll
-        for (int d = 0; d < DA; ++d) dma16(voffA[d], rA, (unsigned)cur_c0 * 4, a_dst + d * 1024);
+        for (int d = 0; d < DA; ++d) hfa::dma16(voffA[d], rA, (unsigned)cur_c0 * 4, a_dst + d * 1024);
 #pragma unroll
-        for (int d = 0; d < DB; ++d) dma16(voffW[d], rW, (unsigned)cur_k0 * 4, w_dst + d * 1024);
+        for (int d = 0; d < DB; ++d) hfa::dma16(voffW[d], rW, (unsigned)cur_k0 * 4, w_dst + d * 1024);
         cur_k0 += BK;
         cur_c0 += BK;
         if (cur_c0 == p.Cg) {
@@ -342,8 +324,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) issue(s);
-    if (nk >= NS - 1) wait_vm_barrier<(NS - 2) * (DA + DB)>();
-    else wait_vm_barrier<0>();
+    if (nk >= NS - 1) hfa::wait_vm_barrier<(NS - 2) * (DA + DB)>();
+    else hfa::wait_vm_barrier<0>();
 
     const f32x4* s4 = reinterpret_cast<const f32x4*>(smem);
     int stage = 0;
@@ -368,8 +350,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
         }
         if (kt + 1 < nk) {
-            if (more) wait_vm_barrier<(NS - 2) * (DA + DB)>();   // K-step kt+1 landed, kt+2.. still in flight
-            else wait_vm_barrier<0>();
+            if (more) hfa::wait_vm_barrier<(NS - 2) * (DA + DB)>();   // K-step kt+1 landed, kt+2.. still in flight
+            else hfa::wait_vm_barrier<0>();
         }
         stage = stage + 1 == NS ? 0 : stage + 1;
     }

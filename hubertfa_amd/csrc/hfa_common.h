@@ -30,6 +30,32 @@ inline int check_launch(const char* what) {
 
 constexpr int kWave = 64;
 
+// ---- LDS-DMA (buffer_load_dwordx4 ... lds): one wave-instruction copies 64 x 16 B from per-lane byte offsets
+// into 1 KiB of LDS at a wave-uniform address (lane-linear).  An offset past the descriptor's num_records reads
+// zeros (scripts/probes/dma_oob.hip).  Completion is tracked only by vmcnt: wait_vm_barrier<N> then read.
+__device__ __forceinline__ unsigned lds_addr(const void* ptr) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)ptr;
+}
+
+__device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned soff, unsigned lds) {
+    unsigned keep;   // M0 is compiler-reserved: set and restore it inside the statement that uses it
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+    // this wave's DMAs except the newest N landed, its LDS reads retired, then every wave of the block
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "i"(N) : "memory");
+}
+
+constexpr unsigned DMA_OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
 __device__ __forceinline__ float neg_inf() { return -__builtin_inff(); }
 
 // Wave-wide reductions over 64 lanes (ds_swizzle/DPP via __shfl_xor).

@@ -1,0 +1,46 @@
+"""Flash-attention microbenchmark on the workload's shapes (run on the GPU box).
+
+python scripts/attn_bench.py [--reps 20]  -> ms and TFLOP/s (4*B*H*L*L*64 algorithmic FLOPs) per shape
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from hubertfa_amd import ops  # noqa: E402
+
+SHAPES = [("base B32 L499", 32, 12, 499), ("large B32 L499", 32, 16, 499), ("long B1 L14999", 1, 12, 14999)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    d = torch.device("cuda")
+    for name, B, H, L in SHAPES:
+        D = 64
+        qkv = torch.randn(B, L, 3 * H * D, device=d)
+        out = torch.empty(B, L, H * D, device=d)
+
+        def go():
+            ops.attention(qkv, qkv[..., H * D:], qkv[..., 2 * H * D:], out, B=B, H=H, L=L, head_dim=D,
+                          scale=D ** -0.5, q_bs=L * 3 * H * D, q_ld=3 * H * D, k_bs=L * 3 * H * D, k_ld=3 * H * D,
+                          v_bs=L * 3 * H * D, v_ld=3 * H * D, o_bs=L * H * D, o_ld=H * D)
+        for _ in range(3):
+            go()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            go()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.reps
+        print(f"{name:16s} {ms:8.3f} ms  {4.0 * B * H * L * L * D / ms / 1e9:7.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
