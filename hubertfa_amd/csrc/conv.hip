@@ -117,8 +117,8 @@ __global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const fl
         float va = conv10(wa, xs + t * ST);
         float vb = conv10(wb, xs + t * ST);
         if (MODE == 0) {
-            va = hfa::gelu_erf((va - ma) * ra * sa + ha);
-            vb = hfa::gelu_erf((vb - mb) * rb * sb + hb);
+            va = hfa::gelu_fast((va - ma) * ra * sa + ha);
+            vb = hfa::gelu_fast((vb - mb) * rb * sb + hb);
         } else {
             va += ha;
             vb += hb;

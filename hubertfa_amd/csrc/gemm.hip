@@ -40,7 +40,7 @@ struct GemmP {
 enum { EPI_NONE = 0, EPI_GELU = 1 };
 
 // Epilogue shared by both kernels: C/D layout of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) +
-// 4*(lane>>5).  GELU uses the branch-free erf (hfa::erf_nb), so lanes in different erf ranges never split.  (A
+// 4*(lane>>5).  GELU is hfa::gelu_fast (branch-free, 17 VALU ops).  (A
 // separate unguarded interior-tile path with batched residual loads measured slower: it pushed the 128-VGPR tile
 // into spills.)
 template <int EPI, int TI, int TJ>
@@ -63,7 +63,7 @@ __device__ __forceinline__ void store_tile(const GemmP& p, const f32x16 (&acc)[T
                 const int row = row0 + i * 32 + (e & 3) + 8 * (e >> 2);
                 if (row >= p.M) continue;
                 float v = acc[i][j][e] + bv;
-                if (EPI == EPI_GELU) v = hfa::gelu_erf(v);
+                if (EPI == EPI_GELU) v = hfa::gelu_fast(v);
                 if (Rb) v += Rb[(long long)row * p.ldr + col];
                 Cb[(long long)row * p.ldc + col] = v;
             }

@@ -98,9 +98,33 @@ __device__ __forceinline__ float erf_nb(float x) {
     return copysignf(ax < 1.0f ? s : l, x);
 }
 
-// erf-GELU exactly as torch's default F.gelu / HF ACT2FN["gelu"]: 0.5 x (1 + erf(x / sqrt 2)).
+// erf-GELU as torch's default F.gelu / HF ACT2FN["gelu"]: 0.5 x (1 + erf(x / sqrt 2)), with the device erff
+// (two-range, ~32 VALU ops).  Kept as the bit-exact reference of gelu_fast's self-test.
 __device__ __forceinline__ float gelu_erf(float x) {
     return 0.5f * x * (1.0f + erf_nb(x * 0.70710678118654752440f));
+}
+
+// The GELU of every fused epilogue.  erf(z) = sign(z) (1 - exp(-q(|z|))) with q(a) = a + a P8(a) fitted to
+// -log(1 - erf(a)) on [0, 3.95] (abs-error weighted least squares, scripts/fit_gelu_erf.py; f64 fit error
+// 4.3e-9), |z| clamped at 3.95 where f32 erf is already 1.  In f32 its GELU differs from the same formula with a
+// correctly rounded erf by <= 2 |x| 2^-24 (that formula's own cancellation floor, which torch's CPU GELU shares)
+// and is bit-identical to it on 93 % of inputs; 17 VALU ops instead of ~32, which the f32 MFMA main loops feel
+// (the VALU and the f32 MFMA share issue).
+__device__ __forceinline__ float gelu_fast(float x) {
+    const float z = x * 0.70710678118654752440f;
+    const float a = fminf(fabsf(z), 3.95f);
+    float q = __uint_as_float(0xb6fcc2dfu);
+    q = fmaf(q, a, __uint_as_float(0x38d50244u));
+    q = fmaf(q, a, __uint_as_float(0xba160ee5u));
+    q = fmaf(q, a, __uint_as_float(0x3acb0addu));
+    q = fmaf(q, a, __uint_as_float(0xb8060160u));
+    q = fmaf(q, a, __uint_as_float(0xbc9d8a4eu));
+    q = fmaf(q, a, __uint_as_float(0x3dd28a28u));
+    q = fmaf(q, a, __uint_as_float(0x3f22f942u));
+    q = fmaf(q, a, __uint_as_float(0x3e0375dfu));
+    q = fmaf(a, q, a);
+    const float e = 1.0f - __builtin_amdgcn_exp2f(q * -1.44269504088896340736f);
+    return 0.5f * x * (1.0f + copysignf(e, z));
 }
 
 // torch Hardswish: x * relu6(x + 3) / 6.

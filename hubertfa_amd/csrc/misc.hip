@@ -86,6 +86,11 @@ __global__ __launch_bounds__(256) void erf_check_kernel(long long n, const float
     }
 }
 
+__global__ __launch_bounds__(256) void gelu_check_kernel(long long n, const float* __restrict__ x,
+                                                         float* __restrict__ y) {
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) y[i] = hfa::gelu_fast(x[i]);
+}
+
 inline int grid1d(long long n, int per = 256, int cap = 8192) {
     long long g = (n + per - 1) / per;
     return (int)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -140,6 +145,17 @@ int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hip
     if (n == 0) return HFA_OK;
     hipLaunchKernelGGL(erf_check_kernel, dim3(grid1d(n)), dim3(256), 0, stream, n, x, y_nb, y_ref);
     return hfa::check_launch("hfa_selftest_erf");
+}
+
+// Self-test: the GELU every fused epilogue applies (hfa::gelu_fast), element-wise.
+int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream) {
+    if (n < 0 || !x || !y) {
+        hfa::set_error("hfa_selftest_gelu: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (n == 0) return HFA_OK;
+    hipLaunchKernelGGL(gelu_check_kernel, dim3(grid1d(n)), dim3(256), 0, stream, n, x, y);
+    return hfa::check_launch("hfa_selftest_gelu");
 }
 
 int hfa_add_f32(long long n, const float* a, const float* b, float* out, hipStream_t stream) {

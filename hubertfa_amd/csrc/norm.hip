@@ -17,7 +17,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_HARDSWISH = 2 };
 
 __device__ __forceinline__ float act_apply(float v, int act) {
-    if (act == ACT_GELU) return hfa::gelu_erf(v);
+    if (act == ACT_GELU) return hfa::gelu_fast(v);
     if (act == ACT_HARDSWISH) return hfa::hardswish(v);
     return v;
 }

@@ -144,6 +144,7 @@ _lib.register("hfa_wav_normalize_f32", [_I_, _I_, _P_, _LL_, _F_, _P_, _LL_, _P_
 _lib.register("hfa_pad_rows_f32", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _LL_, _P_])
 _lib.register("hfa_add_f32", [_LL_, _P_, _P_, _P_, _P_])
 _lib.register("hfa_selftest_erf", [_LL_, _P_, _P_, _P_, _P_])
+_lib.register("hfa_selftest_gelu", [_LL_, _P_, _P_, _P_])
 _lib.register("hfa_resample_workspace_bytes", [_I_, _I_, _I_, _I_], ctypes.c_longlong)
 _lib.register("hfa_resample_f32", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _I_, _I_, _P_, _P_, _LL_, _P_])
 

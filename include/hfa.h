@@ -131,6 +131,8 @@ int hfa_pad_rows_f32(int B, int N, const float* x, long long x_bs, int left, int
                      hipStream_t stream);
 /* Self-test: y_nb = the branch-free erf of every GELU epilogue, y_ref = device erff (must be bit-identical). */
 int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hipStream_t stream);
+/* Self-test: y = the GELU applied by every fused epilogue (GEMM, LayerNorm/GroupNorm act, conv0). */
+int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream);
 /* out = a + b (UNet skip connection, networks/layer/backbone/unet.py:114). */
 int hfa_add_f32(long long n, const float* a, const float* b, float* out, hipStream_t stream);
 /* torchaudio.transforms.Resample (sinc_interp_hann) as pad + MFMA GEMM (tools/load_wav.py:7,

@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--variants", default="16:1,16:2,16:4,103:1,103:2,103:4",
                     help="pipe:cfg pairs; pipe 16/32 register-staged BK, 102/103 LDS-DMA 2/3 stages")
     ap.add_argument("--shapes", default="", help="comma-separated subset of shape names")
+    ap.add_argument("--epi", type=int, default=-1, help="force the epilogue (0 none, 1 GELU) on every shape")
     args = ap.parse_args()
     keep = set(args.shapes.split(",")) if args.shapes else None
     names = {1: "128x128/2x2", 2: "128x64/2x2", 3: "256x128/4x2", 4: "128x256/2x4", 5: "256x128/2x2",
@@ -75,6 +76,8 @@ def main():
         for bk, cfg in variants:
             if bk == 32 and (shape[2] // shape[7]) % 32:
                 continue
+            if args.epi >= 0:
+                shape = shape[:8] + (args.epi,)
             ms, tf = run(shape, bk, cfg, args.reps)
             pipe = {16: "reg16", 32: "reg32", 102: "dma2", 103: "dma3"}.get(bk, str(bk))
             print(f"{shape[0]:10s} {pipe:6s} {names[cfg]:12s} {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)

@@ -102,6 +102,24 @@ def test_branch_free_erf_bit_identical():
     assert torch.equal(y_nb.view(torch.int32), y_ref.view(torch.int32))
 
 
+def test_epilogue_gelu_accuracy():
+    """hfa::gelu_fast vs fp64 GELU: within 4 |x| 2^-24 + 1e-37 everywhere (the f32 formula 0.5x(1+erf)'s own
+    cancellation floor is 2 |x| 2^-24; scripts/fit_gelu_erf.py), and within 12 ulp where 1+erf is not small."""
+    from hubertfa_amd import ops, _lib
+    d = torch.device("cuda")
+    x = torch.cat([torch.linspace(-12, 12, 1 << 21), _r(1 << 20, seed=31) * 3,
+                   torch.tensor([0.0, -0.0, 1e-30, -1e-30, 3.95 * 2 ** 0.5, 1e6, -1e6])]).to(d)
+    y = torch.empty_like(x)
+    _lib.call("hfa_selftest_gelu", x.numel(), ops._ptr(x), ops._ptr(y), ops._stream(d))
+    xd, yd = x.cpu().double(), y.cpu().double()
+    ref = 0.5 * xd * (1 + torch.erf(xd / math.sqrt(2)))
+    err = (yd - ref).abs()
+    assert bool((err <= 4 * xd.abs() * 2.0 ** -24 + 1e-37).all()), float((err / (xd.abs() * 2.0 ** -24 + 1e-37)).max())
+    m = xd > -1.5
+    ulp = torch.from_numpy(np.spacing(ref[m].abs().float().numpy())).double()
+    assert float((err[m] / ulp).max()) <= 12
+
+
 @pytest.mark.parametrize("B,H,L", [(2, 12, 499), (1, 16, 49), (3, 12, 64), (1, 12, 1)])
 def test_attention(B, H, L):
     from hubertfa_amd import ops
