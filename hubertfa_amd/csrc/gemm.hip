@@ -71,6 +71,58 @@ __device__ __forceinline__ void store_tile(const GemmP& p, const f32x16 (&acc)[T
     }
 }
 
+// Epilogue through LDS (DMA kernel, 16-B aligned C/R rows): each 32x32 accumulator sub-tile (+bias, GELU) is
+// transposed through a per-wave [32][36] slab so that every lane stores (and adds the residual to) 4 consecutive
+// columns with one dwordx4: 4 stores + 4 residual loads per sub-tile instead of 16 + 16 scalar ones, each of
+// which also cost a 64-bit address computation on the VALU the f32 MFMAs share (measured: the scalar stores
+// cost 2-4 % of a GEMM).
+template <int EPI, int TI, int TJ>
+__device__ __forceinline__ void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TI][TJ], int zb, int zg,
+                                               int wrow0, int wcol0, int lane, float* slab) {
+    float* Cb = p.C + zb * p.sCb + zg * p.sCg;
+    const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
+    const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+    const int r32 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+        const int col0 = wcol0 + j * 32;
+        if (col0 >= p.N) continue;                       // wave-uniform
+        const float bv = (biasb && col0 + r32 < p.N) ? biasb[col0 + r32] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const int row0 = wrow0 + i * 32;
+            if (row0 >= p.M) continue;                   // wave-uniform
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                float v = acc[i][j][e] + bv;
+                if (EPI == EPI_GELU) v = hfa::gelu_fast(v);
+                slab[((e & 3) + 8 * (e >> 2) + 4 * h) * 36 + r32] = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int idx = lane + k * 64;
+                const int r = idx >> 3, c4 = (idx & 7) * 4;
+                const int row = row0 + r, col = col0 + c4;
+                if (row < p.M) {
+                    f32x4 v = *reinterpret_cast<const f32x4*>(slab + r * 36 + c4);
+                    float* dst = Cb + (long long)row * p.ldc + col;
+                    if (col + 3 < p.N) {
+                        if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + (long long)row * p.ldr + col);
+                        *reinterpret_cast<f32x4*>(dst) = v;
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            if (col + t < p.N) dst[t] = v[t] + (Rb ? Rb[(long long)row * p.ldr + col + t] : 0.0f);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
 template <int EPI, bool VEC_A, int BK, int BM, int BN, int WM, int WN>
 // 4-wave tiles are register-capped at 128 (accumulators included) so 4 workgroups fit per CU.
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 4 : 2) void gemm_f32_kernel(const GemmP p) {
@@ -233,7 +285,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 4 : 2) void gemm_f32
 // Out-of-range conv taps (padding) read through a voffset beyond the buffer's num_records, which the range check
 // turns into zeros (scripts/probes/dma_oob.hip); rows past M / N are clamped (their outputs are never stored).
 
-template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC>
+template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool VEC_C>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP p) {
     constexpr int BK = 16, CPR = 4, NW = WM * WN;
     constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
@@ -355,7 +407,14 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP
         }
         stage = stage + 1 == NS ? 0 : stage + 1;
     }
-    store_tile<EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane);
+    if constexpr (VEC_C) {
+        static_assert(NW * 32 * 36 <= NS * STAGE, "epilogue slabs exceed the staging LDS");
+        __syncthreads();                                 // every wave done reading the last stage
+        store_tile_lds<EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
+                                    smem + wave * (32 * 36));
+    } else {
+        store_tile<EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane);
+    }
 }
 
 // Tile configurations (BM x BN, WM x WN waves); scripts/gemm_bench.py measures each on the workload's shapes.
@@ -367,13 +426,15 @@ int g_force_pipe = 0, g_force_cfg = 0;   // tuning overrides (hfa_gemm_tuning), 
 
 // workgroups per CU a DMA instantiation is register-capped for: 128x128 3-stage (48 KiB LDS) -> 3, 2-stage and
 // 128x64 -> 4 (a 5th 2-stage workgroup measured no faster), 8-wave 128x256 -> 2 (64 accumulators per lane)
+// (4-wave 256x128 / 128x256 tiles, 64x128 per wave at 3 workgroups/CU, measured no faster on any workload shape
+// and 20-25 % slower on the 768-wide Linear ones)
 constexpr int dma_occ(int BN, int NW, int NS) {
     return NW == 4 ? (NS == 3 && BN == 128 ? 3 : 4) : 2;
 }
 
 struct Plan {
     int pipe, cfg;
-    bool vec_a;
+    bool vec_a, vec_c;   // 16-B aligned A rows (DMA-able) / C and R rows (dwordx4 epilogue)
 };
 
 inline bool al16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
@@ -392,6 +453,8 @@ inline Plan make_plan(const GemmP& p, int Z, bool vec_a) {
     // too small to fill 256 CUs twice (UNet: +33 %); the 8-wave 128x256 tile no longer wins anywhere.
     Plan pl;
     pl.vec_a = vec_a;
+    pl.vec_c = al16(p.C) && p.ldc % 4 == 0 && p.sCb % 4 == 0 && p.sCg % 4 == 0 &&
+               (!p.R || (al16(p.R) && p.ldr % 4 == 0 && p.sRb % 4 == 0 && p.sRg % 4 == 0));
     const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
     pl.cfg = (p.N <= 64 || blocks128 < 512) ? CFG_128x64 : CFG_128x128;
     if (g_force_cfg > 0 && g_force_cfg < CFG_COUNT) pl.cfg = g_force_cfg;
@@ -423,7 +486,8 @@ inline void plan_name(const Plan& pl, int epi, char* buf, int len) {
     cfg_shape(pl.cfg, BM, BN, WM, WN);
     if (pl.pipe == PIPE_DMA2 || pl.pipe == PIPE_DMA3) {
         const int ns = pl.pipe - 100, occ = dma_occ(BN, WM * WN, ns);
-        snprintf(buf, len, "gemm_dma_kernel<%d, %d, %d, %d, %d, %d, %d>", epi, BM, BN, WM, WN, ns, occ);
+        snprintf(buf, len, "gemm_dma_kernel<%d, %d, %d, %d, %d, %d, %d, %s>", epi, BM, BN, WM, WN, ns, occ,
+                 pl.vec_c ? "true" : "false");
     } else {
         snprintf(buf, len, "gemm_f32_kernel<%d, %s, %d, %d, %d, %d, %d>", epi, pl.vec_a ? "true" : "false",
                  pl.pipe == PIPE_REG32 ? 32 : 16, BM, BN, WM, WN);
@@ -452,11 +516,12 @@ int launch_reg(GemmP p, int Z, bool vec_a, hipStream_t st) {
 }
 
 template <int EPI, int BM, int BN, int WM, int WN, int NS>
-int launch_dma(GemmP p, int Z, hipStream_t st) {
+int launch_dma(GemmP p, int Z, bool vec_c, hipStream_t st) {
     constexpr int OCC = dma_occ(BN, WM * WN, NS);
     dim3 grid;
     if (int rc = set_grid(p, BM, BN, grid, Z)) return rc;
-    hipLaunchKernelGGL((gemm_dma_kernel<EPI, BM, BN, WM, WN, NS, OCC>), grid, dim3(64 * WM * WN), 0, st, p);
+    if (vec_c) hipLaunchKernelGGL((gemm_dma_kernel<EPI, BM, BN, WM, WN, NS, OCC, true>), grid, dim3(64 * WM * WN), 0, st, p);
+    else hipLaunchKernelGGL((gemm_dma_kernel<EPI, BM, BN, WM, WN, NS, OCC, false>), grid, dim3(64 * WM * WN), 0, st, p);
     return hfa::check_launch("hfa_conv_gemm_f32");
 }
 
@@ -474,19 +539,19 @@ int launch_reg_cfg(int cfg, const GemmP& p, int Z, bool vec_a, hipStream_t st) {
 }
 
 template <int EPI, int NS>
-int launch_dma_cfg(int cfg, const GemmP& p, int Z, hipStream_t st) {
+int launch_dma_cfg(int cfg, const GemmP& p, int Z, bool vec_c, hipStream_t st) {
     switch (cfg) {
-        case CFG_128x64: return launch_dma<EPI, 128, 64, 2, 2, NS>(p, Z, st);
-        case CFG_128x256: return launch_dma<EPI, 128, 256, 2, 4, NS>(p, Z, st);
-        default: return launch_dma<EPI, 128, 128, 2, 2, NS>(p, Z, st);
+        case CFG_128x64: return launch_dma<EPI, 128, 64, 2, 2, NS>(p, Z, vec_c, st);
+        case CFG_128x256: return launch_dma<EPI, 128, 256, 2, 4, NS>(p, Z, vec_c, st);
+        default: return launch_dma<EPI, 128, 128, 2, 2, NS>(p, Z, vec_c, st);
     }
 }
 
 template <int EPI>
 int launch(const GemmP& p, int Z, const Plan& pl, hipStream_t st) {
     switch (pl.pipe) {
-        case PIPE_DMA3: return launch_dma_cfg<EPI, 3>(pl.cfg, p, Z, st);
-        case PIPE_DMA2: return launch_dma_cfg<EPI, 2>(pl.cfg, p, Z, st);
+        case PIPE_DMA3: return launch_dma_cfg<EPI, 3>(pl.cfg, p, Z, pl.vec_c, st);
+        case PIPE_DMA2: return launch_dma_cfg<EPI, 2>(pl.cfg, p, Z, pl.vec_c, st);
         case PIPE_REG32: return launch_reg_cfg<EPI, 32>(pl.cfg, p, Z, pl.vec_a, st);
         default: return launch_reg_cfg<EPI, 16>(pl.cfg, p, Z, pl.vec_a, st);
     }
@@ -562,8 +627,12 @@ int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long l
 
 const char* hfa_gemm_kernel_name(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg,
                                  int ldx, int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
-                                 int epilogue) {
+                                 const float* bias, long long sBg, const float* R, long long sRb, long long sRg,
+                                 int ldr, float* C, long long sCb, long long sCg, int ldc, int epilogue) {
     GemmP p = make_params(M, N, K, G, A, sAb, sAg, ldx, stride, pad, Cg, Tin, W, sWg, ldw);
+    p.bias = bias; p.sBg = sBg;
+    p.R = R; p.sRb = sRb; p.sRg = sRg; p.ldr = ldr;
+    p.C = C; p.sCb = sCb; p.sCg = sCg; p.ldc = ldc;
     const Plan pl = make_plan(p, Zb * G, vec_a_of(A, ldx, sAb, sAg));
     plan_name(pl, epilogue, g_name, sizeof(g_name));
     return g_name;

@@ -131,7 +131,7 @@ _lib.register("hfa_conv_gemm_f32", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _I
                                     _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _I_, _P_])
 _lib.register("hfa_gemm_tuning", [_I_, _I_])
 _lib.register("hfa_gemm_kernel_name", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_, _LL_,
-                                       _I_, _I_], ctypes.c_char_p)
+                                       _I_, _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _I_], ctypes.c_char_p)
 _lib.register("hfa_gemm_f32", [_I_, _I_, _I_, _P_, _I_, _P_, _I_, _P_, _P_, _I_, _P_, _I_, _I_, _P_])
 _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_,
                                     _LL_, _I_, _P_])
@@ -193,12 +193,10 @@ class KernelProbe:
 PROBE = None
 
 
-def _gemm_name(epilogue: int, A, W, M: int, N: int, K: int, Zb: int, G: int, sAb: int, sAg: int, ldx: int,
-               stride: int, pad: int, Cg: int, Tin: int, sWg: int, ldw: int) -> str:
-    """rocprof symbol stem of the instantiation hfa_conv_gemm_f32 dispatches to (asked from the library)."""
-    name = _lib.lib().hfa_gemm_kernel_name(M, N, K, Zb, G, _ptr(A), sAb, sAg, ldx, stride, pad, Cg, Tin, _ptr(W),
-                                           sWg, ldw, epilogue)
-    return name.decode()
+def _gemm_name(*args) -> str:
+    """rocprof symbol stem of the instantiation hfa_conv_gemm_f32 dispatches to for these arguments (the
+    library answers from the same plan it launches)."""
+    return _lib.lib().hfa_gemm_kernel_name(*args).decode()
 
 
 def conv_gemm(A, W, C, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None, Tin=None, sWg=0,
@@ -207,15 +205,15 @@ def conv_gemm(A, W, C, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0
     for t, n in ((A, "A"), (W, "W"), (C, "C")):
         _need(t, torch.float32, n, contiguous=False)
 
+    args = (M, N, K, Zb, G, _ptr(A), sAb, sAg, ldx, stride, pad, Cg or K, Tin if Tin is not None else M, _ptr(W),
+            sWg, ldw if ldw is not None else K, _ptr(bias), sBg, _ptr(R), sRb, sRg, ldr, _ptr(C), sCb, sCg, ldc,
+            epilogue)
+
     def launch():
-        _lib.call("hfa_conv_gemm_f32", M, N, K, Zb, G, _ptr(A), sAb, sAg, ldx, stride, pad, Cg or K,
-                  Tin if Tin is not None else M, _ptr(W), sWg, ldw if ldw is not None else K, _ptr(bias), sBg,
-                  _ptr(R), sRb, sRg, ldr, _ptr(C), sCb, sCg, ldc, epilogue, _stream(C.device))
+        _lib.call("hfa_conv_gemm_f32", *args, _stream(C.device))
     if PROBE is None:
         return launch()
-    PROBE(_gemm_name(epilogue, A, W, M, N, K, Zb, G, sAb, sAg, ldx, stride, pad, Cg or K,
-                     Tin if Tin is not None else M, sWg, ldw if ldw is not None else K),
-          2.0 * M * N * K * Zb * G, launch)
+    PROBE(_gemm_name(*args), 2.0 * M * N * K * Zb * G, launch)
 
 
 def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
@@ -230,14 +228,17 @@ def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
     r2 = residual.reshape(-1, N) if residual is not None else None
     _need(W, torch.float32, "W")
 
+    args = (M, N, K, _ptr(x2), x2.stride(0), _ptr(W), W.stride(0), _ptr(bias), _ptr(r2),
+            r2.stride(0) if r2 is not None else 0, _ptr(o2), o2.stride(0), epilogue)
+
     def launch():
-        _lib.call("hfa_gemm_f32", M, N, K, _ptr(x2), x2.stride(0), _ptr(W), W.stride(0), _ptr(bias), _ptr(r2),
-                  r2.stride(0) if r2 is not None else 0, _ptr(o2), o2.stride(0), epilogue, _stream(x.device))
+        _lib.call("hfa_gemm_f32", *args, _stream(x.device))
     if PROBE is None:
         launch()
-    else:
-        PROBE(_gemm_name(epilogue, x2, W, M, N, K, 1, 1, 0, 0, x2.stride(0), 1, 0, K, M, 0, W.stride(0)),
-              2.0 * M * N * K, launch)
+    else:                       # hfa_gemm_f32 is hfa_conv_gemm_f32 with Zb = G = 1, stride 1, Cg = K, Tin = M
+        PROBE(_gemm_name(M, N, K, 1, 1, _ptr(x2), 0, 0, x2.stride(0), 1, 0, K, M, _ptr(W), 0, W.stride(0), _ptr(bias),
+                         0, _ptr(r2), 0, 0, r2.stride(0) if r2 is not None else 0, _ptr(o2), 0, 0, o2.stride(0),
+                         epilogue), 2.0 * M * N * K, launch)
     return out
 
 

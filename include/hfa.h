@@ -78,11 +78,12 @@ int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long l
 /* Tuning hook for benchmarks: force the staging pipeline of hfa_conv_gemm_f32 (16/32 = register-staged K-step,
  * 102/103 = LDS-DMA with 2/3 stages) and the tile configuration (1..7, see gemm.hip); 0 = automatic. */
 int hfa_gemm_tuning(int force_pipe, int force_cfg);
-/* Name (rocprof symbol stem) of the kernel instantiation hfa_conv_gemm_f32 launches for these arguments, e.g.
- * "gemm_dma_kernel<1, 128, 128, 2, 2, 3, 3>"; thread-local storage, valid until the next call. */
+/* Name (rocprof symbol stem) of the kernel instantiation hfa_conv_gemm_f32 launches for the same arguments, e.g.
+ * "gemm_dma_kernel<1, 128, 128, 2, 2, 2, 4, true>"; thread-local storage, valid until the next call. */
 const char* hfa_gemm_kernel_name(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg,
                                  int ldx, int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
-                                 int epilogue);
+                                 const float* bias, long long sBg, const float* R, long long sRb, long long sRg,
+                                 int ldr, float* C, long long sCb, long long sCg, int ldc, int epilogue);
 /* Plain Linear: C[M,N] = epi(A[M,K] W[N,K]^T + bias) + R. */
 int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, int ldw, const float* bias,
                  const float* R, int ldr, float* C, int ldc, int epilogue, hipStream_t stream);

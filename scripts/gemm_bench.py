@@ -67,7 +67,7 @@ def main():
     ap.add_argument("--epi", type=int, default=-1, help="force the epilogue (0 none, 1 GELU) on every shape")
     args = ap.parse_args()
     keep = set(args.shapes.split(",")) if args.shapes else None
-    names = {1: "128x128/2x2", 2: "128x64/2x2", 3: "256x128/4x2", 4: "128x256/2x4", 5: "256x128/2x2",
+    names = {0: "auto", 1: "128x128/2x2", 2: "128x64/2x2", 3: "256x128/4x2", 4: "128x256/2x4", 5: "256x128/2x2",
              6: "128x256/2x2", 7: "256x256/4x2"}
     variants = [tuple(int(v) for v in s.split(":")) for s in args.variants.split(",")]
     for shape in SHAPES:
@@ -79,7 +79,7 @@ def main():
             if args.epi >= 0:
                 shape = shape[:8] + (args.epi,)
             ms, tf = run(shape, bk, cfg, args.reps)
-            pipe = {16: "reg16", 32: "reg32", 102: "dma2", 103: "dma3"}.get(bk, str(bk))
+            pipe = {0: "auto", 16: "reg16", 32: "reg32", 102: "dma2", 103: "dma3"}.get(bk, str(bk))
             print(f"{shape[0]:10s} {pipe:6s} {names[cfg]:12s} {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
     _lib.lib().hfa_gemm_tuning(0, 0)
 

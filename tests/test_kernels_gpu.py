@@ -92,6 +92,25 @@ def test_gemm_tile_variants(bk, bn):
         _lib.lib().hfa_gemm_tuning(0, 0)
 
 
+@pytest.mark.parametrize("N,ldc,res", [(198, 200, True), (198, 200, False), (61, 64, True), (130, 131, True)])
+def test_gemm_epilogue_tails(N, ldc, res):
+    """Vector (dwordx4 through LDS) and scalar epilogues: N tails inside an aligned row, unaligned rows, residual."""
+    from hubertfa_amd import ops
+    d = torch.device("cuda")
+    M, K = 333, 256
+    x, w, b = _r(M, K, seed=41), _r(N, K, seed=42, scale=K ** -0.5), _r(N, seed=43)
+    r = _r(M, ldc, seed=44)
+    out = torch.full((M, ldc), 7.0, device=d)
+    rd = r.to(d)
+    ops.conv_gemm(x.to(d), w.to(d), out, M=M, N=N, K=K, ldx=K, bias=b.to(d), R=rd if res else None, ldr=ldc,
+                  ldc=ldc, epilogue=ops.EPI_GELU)
+    ref = F.gelu(x.double() @ w.double().T + b.double())
+    if res:
+        ref = ref + r.double()[:, :N]
+    _close(out[:, :N], ref, 2e-5, 2e-5)
+    assert bool((out[:, N:] == 7.0).all()), "wrote past N"
+
+
 def test_branch_free_erf_bit_identical():
     from hubertfa_amd import ops, _lib
     d = torch.device("cuda")
