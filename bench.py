@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--device", type=int, default=None, help="force every rank onto this device (rehearsal)")
     ap.add_argument("--probe", default="auto",
                     help="kernel instantiation to time; auto = the one carrying the most FLOPs in a warmup census")
+    ap.add_argument("--serial", action="store_true", help="one stream per step (no head/encoder overlap)")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -174,11 +175,15 @@ def main():
     wav = torch.from_numpy(wav_np).to(dev)
 
     def launch():
-        """GPU half of one step (+ the boundary gather) and the async D2H of its results."""
-        dev_out = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False)
-        if world > 1:
-            gather_boundaries(dev_out)
-        return task.decoder.fetch(dev_out)
+        """GPU half of one step (+ the boundary gather) and the async D2H of its results: the encoder on the main
+        stream, head + DP on a side stream overlapping the next step's encoder (task.submit)."""
+        if args.serial:
+            dev_out = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False)
+            if world > 1:
+                gather_boundaries(dev_out)
+            return task.decoder.fetch(dev_out)
+        return task.submit(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000,
+                           on_device=gather_boundaries if world > 1 else None)
 
     def finish(handle):
         return task.decoder.assemble(handle, ph_seqs, word_seqs, p2ws)

@@ -94,11 +94,8 @@ class ForcedAlignmentTask:
         return self._upsamplers[sr]
 
     @torch.no_grad()
-    def align_batch(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
-                    host: bool = True):
-        """B equal-length waveforms [B, N] (at melspec sample_rate, or ``wav_sr`` to resample first, like
-        load_wav) -> list of decode results (dicts with ph_seq / ph_intervals / word_seq / word_intervals /
-        confidence / raw path)."""
+    def encode_batch(self, waves: torch.Tensor, wav_sr: int | None = None):
+        """Device half 1 (current stream): waves [B, N] -> (features [B, T_pad, C], DP frame count, wav lengths)."""
         self.on_predict_start()
         sr = self.melspec_config["sample_rate"]
         hop = self.melspec_config["hop_length"]
@@ -107,10 +104,46 @@ class ForcedAlignmentTask:
             waves = self.upsampler(wav_sr)(waves)
         n = waves.shape[-1]
         feats, n_frames = self.unitsEncoder.encode_frames(waves, sr, hop, pad_to=self.head.divisible)
+        return feats, n_frames, [n / sr] * waves.shape[0]
+
+    def decode_device(self, feats, n_frames, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
+        """Device half 2 (current stream): UNet head + lattice + Viterbi -> the decoder's device outputs."""
         logits = self.head.logits(feats)
         frame, edge, _ = LatticeHead.split(logits[:, :n_frames])
-        wl = [n / sr] * waves.shape[0]
-        return self.decoder.decode_batch(frame, edge, wl, ph_seqs, word_seqs, p2ws, host=host)
+        return self.decoder.decode_batch(frame, edge, wav_lengths, ph_seqs, word_seqs, p2ws, host=False)
+
+    def align_batch(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
+                    host: bool = True):
+        """B equal-length waveforms [B, N] (at melspec sample_rate, or ``wav_sr`` to resample first, like
+        load_wav) -> list of decode results (dicts with ph_seq / ph_intervals / word_seq / word_intervals /
+        confidence / raw path)."""
+        feats, n_frames, wl = self.encode_batch(waves, wav_sr)
+        dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
+        if not host:
+            return dev_out
+        return self.decoder.assemble(dev_out, ph_seqs, word_seqs, p2ws)
+
+    def submit(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
+               on_device=None):
+        """Two-stream pipelined device pass; returns the decoder's fetch handle (``decoder.assemble`` completes it).
+
+        The encoder runs on the caller's current stream and the head + lattice + Viterbi on a side stream that
+        waits for it, so a batch's small-grid tail (UNet GEMMs on a few hundred workgroups, one DP workgroup per
+        utterance) overlaps the next batch's extractor convs instead of idling most of the chip.  ``on_device``
+        (e.g. the RCCL boundary gather) runs on the side stream after the backtrack."""
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        feats, n_frames, wl = self.encode_batch(waves, wav_sr)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ready)
+            feats.record_stream(self._side)      # the caching allocator must not recycle it under the side stream
+            dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
+            if on_device is not None:
+                on_device(dev_out)
+            return self.decoder.fetch(dev_out)
 
 
 def synth_checkpoint(path: str | None = None, *, encoder="cnhubert", model_path="synth:0", seed=1,
