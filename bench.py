@@ -119,6 +119,15 @@ def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s, encoder="cnhuber
                       f"(oracle: torch-CPU fp32 resample + {encoder} + UNet, C Viterbi), {el:.1f} s wall"}
 
 
+def config_name(encoder: str, world: int, B: int) -> str:
+    """Which BASELINE.json config this run's geometry is (configs[1..3]); weak scaling keeps B per GPU fixed."""
+    if encoder == "large":
+        return "config 4 geometry" + ("" if world * B == 256 else f" (global batch {world * B}, config 4 is 256)")
+    if world == 1:
+        return "config 2" if B == 32 else f"config 2 geometry (B={B}, config 2 is 32)"
+    return "config 3 geometry" + ("" if world * B == 512 else f" (global batch {world * B}, config 3 is 512)")
+
+
 SECONDARY = ("viterbi_forward_kernel", "hfa_conv0_f32", "attn_fwd_f32_kernel")
 
 
@@ -244,7 +253,7 @@ def main():
         "metric": METRIC, "value": value, "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"config {'4' if args.encoder == 'large' else ('3' if world > 1 else '2')}: "
+        "config": {"workload": f"{config_name(args.encoder, world, B)}: "
                                f"B={B} x {args.seconds:g} s 16 kHz utterances per GPU, "
                                f"{ {'base': 'Hubert-base (cnhubert arch)', 'large': 'Hubert-large (cnhubert-large arch)', 'soft': 'HubertSoft'}[args.encoder]}"
                                f" + UNet head + Viterbi; full infer path wave(HBM)->boundaries(host), host assembly "
