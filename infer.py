@@ -29,17 +29,30 @@ def _predict(task, dataset, batch_size: int):
     for it in items:
         buckets.setdefault((len(it[1]), it[2]), []).append(it)
     out = {}
+
+    def finish(job):
+        handle, chunk, n44 = job
+        res = task.decoder.assemble(handle, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk])
+        for c, r in zip(chunk, res):
+            out[str(c[0])] = (c[0], n44 / sr, r["confidence"], r["ph_seq"], r["ph_intervals"], r["word_seq"],
+                              r["word_intervals"])
+
+    # one batch in flight: the host assembles batch i while the GPU runs batch i+1 (task.submit: encoder on the
+    # main stream, head + Viterbi on a side stream)
+    pending = None
     for (_, file_sr), group in buckets.items():
         for i in range(0, len(group), batch_size):
             chunk = group[i:i + batch_size]
             wav = torch.from_numpy(__import__("numpy").stack([c[1] for c in chunk])).to(task.device)
-            res = task.align_batch(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
-                                   wav_sr=file_sr)
+            handle = task.submit(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
+                                 wav_sr=file_sr)
             g = math.gcd(sr, file_sr)
             n44 = math.ceil((sr // g) * wav.shape[-1] / (file_sr // g)) if file_sr != sr else wav.shape[-1]
-            for c, r in zip(chunk, res):
-                out[str(c[0])] = (c[0], n44 / sr, r["confidence"], r["ph_seq"], r["ph_intervals"], r["word_seq"],
-                                  r["word_intervals"])
+            if pending is not None:
+                finish(pending)
+            pending = (handle, chunk, n44)
+    if pending is not None:
+        finish(pending)
     return [out[str(it[0])] for it in items if str(it[0]) in out]
 
 
