@@ -417,9 +417,152 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP
     }
 }
 
+// ---- 48-wide tile on 16x16x4 MFMAs (the grouped positional conv: 48 output channels per group) -------------
+// A 64-wide tile wastes a quarter of its MFMAs on N = 48.  Here each of 4 waves owns 32 rows x 48 columns =
+// 2 x 3 blocks of v_mfma_f32_16x16x4_f32 (lane l: A[l&15][k=l>>4], B[k=l>>4][l&15]; D: col l&15,
+// row 4(l>>4)+r).  A lane's ds_read_b128 brings 4 consecutive k of its row (chunk l>>4 of the 16-k step), and
+// MFMA e consumes element e, the same permutation on both operands.  The 16-row read groups need their own
+// chunk swizzle: chunk' = chunk ^ F[(row>>2)&3] with F = {0,2,3,1} keeps every ds_read_b128 lane group on 16
+// distinct 16-B slots (the 32-row tiles' F = identity does not).  DMA: A 2 x 1 KiB per wave, W 3 x 1 KiB on
+// waves 0-2; stages as in gemm_dma_kernel.
+constexpr int swz48(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }    // F = {0, 2, 3, 1}
+
+template <int EPI, int NS>
+__global__ __launch_bounds__(256, 4) void gemm_dma_n48_kernel(const GemmP p) {
+    constexpr int BM = 128, BN = 48, BK = 16, NW = 4;
+    constexpr int STAGE = (BM + BN) * BK;
+    __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
+
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+    const int tm = wgid / p.n_tiles, tn = wgid - tm * p.n_tiles;
+    const int zb = blockIdx.z / p.G, zg = blockIdx.z - zb * p.G;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    const float* Ab = p.A + zb * p.sAb + zg * p.sAg;
+    const float* Wb = p.W + zg * p.sWg;
+    const __amdgpu_buffer_rsrc_t rA = hfa::make_rsrc(Ab, ((long long)(p.Tin - 1) * p.ldx + p.Cg) * 4);
+    const __amdgpu_buffer_rsrc_t rW = hfa::make_rsrc(Wb, ((long long)(p.N - 1) * p.ldw + p.K) * 4);
+
+    int a_t0[2], a_c[2];
+    unsigned voffA[2], voffW = 0;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+        const int row = (wave * 2 + d) * 16 + (lane >> 2);
+        int m = tm * BM + row;
+        m = m < p.M ? m : p.M - 1;
+        a_t0[d] = m * p.stride - p.pad;
+        a_c[d] = ((lane & 3) ^ swz48(row)) * 4;
+    }
+    {
+        const int row = wave * 16 + (lane >> 2);          // waves 0-2: W rows 0..47
+        int n = tn * BN + row;
+        n = n < p.N ? n : p.N - 1;
+        voffW = (unsigned)((n * p.ldw + ((lane & 3) ^ swz48(row)) * 4) * 4);
+    }
+    auto set_tap = [&](int j) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            const int t = a_t0[d] + j;
+            voffA[d] = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + a_c[d]) * 4) : hfa::DMA_OOB;
+        }
+    };
+    const unsigned lds0 = hfa::lds_addr(smem);
+    int cur_j = 0, cur_c0 = 0, cur_k0 = 0;
+    set_tap(0);
+    auto issue = [&](int stage) {
+        const unsigned a_dst = lds0 + stage * STAGE * 4 + wave * 2 * 1024;
+        hfa::dma16(voffA[0], rA, (unsigned)cur_c0 * 4, a_dst);
+        hfa::dma16(voffA[1], rA, (unsigned)cur_c0 * 4, a_dst + 1024);
+        if (wave < 3) hfa::dma16(voffW, rW, (unsigned)cur_k0 * 4, lds0 + (stage * STAGE + BM * BK) * 4 + wave * 1024);
+        cur_k0 += BK;
+        cur_c0 += BK;
+        if (cur_c0 == p.Cg) {
+            cur_c0 = 0;
+            set_tap(++cur_j);
+        }
+    };
+    // this wave's DMAs per K-step: 3 (waves 0-2) or 2 (wave 3); the counted wait differs per wave
+    auto wait_steps_in_flight = [&](bool keep) {
+        if (!keep) hfa::wait_vm_barrier<0>();
+        else if (wave < 3) hfa::wait_vm_barrier<(NS - 2) * 3>();
+        else hfa::wait_vm_barrier<(NS - 2) * 2>();
+    };
+
+    const int r16 = lane & 15, g = lane >> 4;
+    int rdA[2], rdB[3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int row = wave * 32 + i * 16 + r16;
+        rdA[i] = row * 4 + (g ^ swz48(row));
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int row = j * 16 + r16;
+        rdB[j] = BM * 4 + row * 4 + (g ^ swz48(row));
+    }
+    f32x4 acc[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = p.K / BK;
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < nk) issue(s);
+    wait_steps_in_flight(nk >= NS - 1);
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(smem);
+    int stage = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+        const bool more = kt + NS - 1 < nk;
+        if (more) issue(stage == 0 ? NS - 1 : stage - 1);
+        const f32x4* st = s4 + stage * (STAGE / 4);
+        f32x4 a[2], b[3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = st[rdA[i]];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) b[j] = st[rdB[j]];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+        if (kt + 1 < nk) wait_steps_in_flight(more);
+        stage = stage + 1 == NS ? 0 : stage + 1;
+    }
+
+    // epilogue: D col = lane&15, row = 4(lane>>4) + r
+    float* Cb = p.C + zb * p.sCb + zg * p.sCg;
+    const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
+    const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int col = tn * BN + j * 16 + r16;
+        if (col >= p.N) continue;
+        const float bv = biasb ? biasb[col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = tm * BM + wave * 32 + i * 16 + 4 * g + r;
+                if (row >= p.M) continue;
+                float v = acc[i][j][r] + bv;
+                if (EPI == EPI_GELU) v = hfa::gelu_fast(v);
+                if (Rb) v += Rb[(long long)row * p.ldr + col];
+                Cb[(long long)row * p.ldc + col] = v;
+            }
+        }
+    }
+}
+
 // Tile configurations (BM x BN, WM x WN waves); scripts/gemm_bench.py measures each on the workload's shapes.
 enum { CFG_AUTO = 0, CFG_128x128 = 1, CFG_128x64 = 2, CFG_256x128 = 3, CFG_128x256 = 4, CFG_256x128_W4 = 5,
-       CFG_128x256_W4 = 6, CFG_256x256 = 7, CFG_COUNT = 8 };
+       CFG_128x256_W4 = 6, CFG_256x256 = 7, CFG_128x48 = 8, CFG_COUNT = 9 };
 // Pipelines: register-staged BK 16 / 32, LDS-DMA with 2 or 3 stages.
 enum { PIPE_AUTO = 0, PIPE_REG16 = 16, PIPE_REG32 = 32, PIPE_DMA2 = 102, PIPE_DMA3 = 103 };
 int g_force_pipe = 0, g_force_cfg = 0;   // tuning overrides (hfa_gemm_tuning), 0 = automatic
@@ -457,10 +600,14 @@ inline Plan make_plan(const GemmP& p, int Z, bool vec_a) {
                (!p.R || (al16(p.R) && p.ldr % 4 == 0 && p.sRb % 4 == 0 && p.sRg % 4 == 0));
     const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
     pl.cfg = (p.N <= 64 || blocks128 < 512) ? CFG_128x64 : CFG_128x128;
+    if (p.N > 32 && p.N <= 48 && dma_ok(p, vec_a)) pl.cfg = CFG_128x48;
     if (g_force_cfg > 0 && g_force_cfg < CFG_COUNT) pl.cfg = g_force_cfg;
-    const bool dma_cfg = pl.cfg == CFG_128x128 || pl.cfg == CFG_128x64 || pl.cfg == CFG_128x256;
+    if (pl.cfg == CFG_128x48 && (p.N > 48 || !dma_ok(p, vec_a))) pl.cfg = CFG_128x64;
+    const bool dma_cfg = pl.cfg == CFG_128x128 || pl.cfg == CFG_128x64 || pl.cfg == CFG_128x256 ||
+                         pl.cfg == CFG_128x48;
     pl.pipe = PIPE_REG16;
-    if (dma_cfg && dma_ok(p, vec_a)) pl.pipe = pl.cfg == CFG_128x64 ? PIPE_DMA3 : PIPE_DMA2;
+    if (dma_cfg && dma_ok(p, vec_a)) pl.pipe = (pl.cfg == CFG_128x64 || pl.cfg == CFG_128x48) ? PIPE_DMA3 : PIPE_DMA2;
+    if (pl.cfg == CFG_128x48) return pl;        // DMA-only tile
     if (g_force_pipe == PIPE_REG16) pl.pipe = PIPE_REG16;
     if (g_force_pipe == PIPE_REG32 && p.K % 32 == 0 && p.Cg % 32 == 0) pl.pipe = PIPE_REG32;
     if ((g_force_pipe == PIPE_DMA2 || g_force_pipe == PIPE_DMA3) && dma_cfg && dma_ok(p, vec_a))
@@ -476,6 +623,7 @@ inline void cfg_shape(int cfg, int& BM, int& BN, int& WM, int& WN) {
         case CFG_256x128_W4: BM = 256; BN = 128; WM = 2; WN = 2; break;
         case CFG_128x256_W4: BM = 128; BN = 256; WM = 2; WN = 2; break;
         case CFG_256x256: BM = 256; BN = 256; WM = 4; WN = 2; break;
+        case CFG_128x48: BM = 128; BN = 48; WM = 4; WN = 1; break;
         default: BM = 128; BN = 128; WM = 2; WN = 2; break;
     }
 }
@@ -484,7 +632,9 @@ inline void cfg_shape(int cfg, int& BM, int& BN, int& WM, int& WN) {
 inline void plan_name(const Plan& pl, int epi, char* buf, int len) {
     int BM, BN, WM, WN;
     cfg_shape(pl.cfg, BM, BN, WM, WN);
-    if (pl.pipe == PIPE_DMA2 || pl.pipe == PIPE_DMA3) {
+    if (pl.cfg == CFG_128x48) {
+        snprintf(buf, len, "gemm_dma_n48_kernel<%d, %d>", epi, pl.pipe - 100);
+    } else if (pl.pipe == PIPE_DMA2 || pl.pipe == PIPE_DMA3) {
         const int ns = pl.pipe - 100, occ = dma_occ(BN, WM * WN, ns);
         snprintf(buf, len, "gemm_dma_kernel<%d, %d, %d, %d, %d, %d, %d, %s>", epi, BM, BN, WM, WN, ns, occ,
                  pl.vec_c ? "true" : "false");
@@ -539,8 +689,17 @@ int launch_reg_cfg(int cfg, const GemmP& p, int Z, bool vec_a, hipStream_t st) {
 }
 
 template <int EPI, int NS>
+int launch_n48(GemmP p, int Z, hipStream_t st) {
+    dim3 grid;
+    if (int rc = set_grid(p, 128, 48, grid, Z)) return rc;
+    hipLaunchKernelGGL((gemm_dma_n48_kernel<EPI, NS>), grid, dim3(256), 0, st, p);
+    return hfa::check_launch("hfa_conv_gemm_f32");
+}
+
+template <int EPI, int NS>
 int launch_dma_cfg(int cfg, const GemmP& p, int Z, bool vec_c, hipStream_t st) {
     switch (cfg) {
+        case CFG_128x48: return launch_n48<EPI, NS>(p, Z, st);
         case CFG_128x64: return launch_dma<EPI, 128, 64, 2, 2, NS>(p, Z, vec_c, st);
         case CFG_128x256: return launch_dma<EPI, 128, 256, 2, 4, NS>(p, Z, vec_c, st);
         default: return launch_dma<EPI, 128, 128, 2, 2, NS>(p, Z, vec_c, st);

@@ -92,6 +92,37 @@ def test_gemm_tile_variants(bk, bn):
         _lib.lib().hfa_gemm_tuning(0, 0)
 
 
+@pytest.mark.parametrize("Cg,Ng,k,pad,T,G,epi", [(48, 48, 7, 3, 150, 4, 1), (48, 48, 128, 64, 499, 2, 1),
+                                                  (64, 40, 3, 1, 77, 3, 0), (96, 33, 1, 0, 300, 1, 1)])
+def test_gemm_n48_tile(Cg, Ng, k, pad, T, G, epi):
+    """The 48-wide 16x16x4-MFMA tile (32 < N <= 48): grouped padded convs with M tails, GELU and residual."""
+    from hubertfa_amd import ops
+    d = torch.device("cuda")
+    B = 2
+    Cin, Cout = Cg * G, Ng * G
+    x = _r(B, T, Cin, seed=51)
+    w = _r(Cout, Cg, k, seed=52, scale=(Cg * k) ** -0.5)
+    b = _r(Cout, seed=53)
+    ref = F.conv1d(x.double().transpose(1, 2), w.double(), b.double(), padding=pad, groups=G)[..., :T]
+    if epi:
+        ref = F.gelu(ref)
+    ref = ref.transpose(1, 2)
+    r = _r(B, T, Cout, seed=54)
+    ref = ref + r.double()
+    out = torch.empty(B, T, Cout, device=d)
+    wk = w.permute(0, 2, 1).contiguous().to(d)
+    args = dict(M=T, N=Ng, K=k * Cg, Zb=B, G=G, sAb=T * Cin, sAg=Cg, ldx=Cin, stride=1, pad=pad, Cg=Cg, Tin=T,
+                sWg=Ng * k * Cg, bias=b.to(d), sBg=Ng, R=r.to(d), sRb=T * Cout, sRg=Ng, ldr=Cout, sCb=T * Cout,
+                sCg=Ng, ldc=Cout, epilogue=epi)
+    xd = x.to(d)
+    name = ops._gemm_name(T, Ng, k * Cg, B, G, ops._ptr(xd), T * Cin, Cg, Cin, 1, pad, Cg, T, ops._ptr(wk),
+                          Ng * k * Cg, k * Cg, ops._ptr(b), Ng, ops._ptr(r), T * Cout, Ng, Cout, ops._ptr(out),
+                          T * Cout, Ng, Cout, epi)
+    assert name.startswith("gemm_dma_n48_kernel"), name
+    ops.conv_gemm(xd, wk, out, **args)
+    _close(out, ref, 5e-5, 5e-5)
+
+
 @pytest.mark.parametrize("N,ldc,res", [(198, 200, True), (198, 200, False), (61, 64, True), (130, 131, True)])
 def test_gemm_epilogue_tails(N, ldc, res):
     """Vector (dwordx4 through LDS) and scalar epilogues: N tails inside an aligned row, unaligned rows, residual."""
