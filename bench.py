@@ -201,11 +201,16 @@ def main():
         """k steps, software-pipelined: the host assembles batch i while the GPU runs batch i+1."""
         pending, res = None, None
         for _ in range(k):
+            t0 = time.perf_counter()
             h = launch()
+            t1 = time.perf_counter()
             if pending is not None:
                 res = finish(pending)
+            host_t.append((t1 - t0, time.perf_counter() - t1))
             pending = h
         return finish(pending) if pending is not None else res
+
+    host_t = []   # (enqueue, wait + assemble) seconds per step, reported on stderr
 
     census = ops.KernelProbe(None)
     ops.PROBE = census
@@ -273,6 +278,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wav_np, ph_seqs, word_seqs, p2ws, ckpt, args.cpu_sample_s, encoder)
     if rank == 0:
+        ht = host_t[-args.steps:]
+        print(f"host per step: enqueue {1e3 * sum(a for a, _ in ht) / len(ht):.2f} ms, wait+assemble "
+              f"{1e3 * sum(b for _, b in ht) / len(ht):.2f} ms", file=sys.stderr, flush=True)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

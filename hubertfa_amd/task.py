@@ -108,8 +108,8 @@ class ForcedAlignmentTask:
 
     def decode_device(self, feats, n_frames, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
         """Device half 2 (current stream): UNet head + lattice + Viterbi -> the decoder's device outputs."""
-        logits = self.head.logits(feats)
-        frame, edge, _ = LatticeHead.split(logits[:, :n_frames])
+        logits = self.head.logits(feats)[:, :n_frames]
+        frame, edge = logits[:, :, 2:], logits[:, :, 0]      # LatticeHead.split without the unused ctc logits
         return self.decoder.decode_batch(frame, edge, wav_lengths, ph_seqs, word_seqs, p2ws, host=False)
 
     def align_batch(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,

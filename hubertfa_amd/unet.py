@@ -130,7 +130,8 @@ class LatticeHead:
     @staticmethod
     def split(logits: torch.Tensor):
         """(ph_frame_logits, ph_edge_logits, ctc_logits) views, forced_alignment.py:287-292."""
-        return logits[:, :, 2:], logits[:, :, 0], torch.cat([logits[:, :, [1]], logits[:, :, 3:]], dim=-1)
+        # (basic slicing only: a list index would upload an index tensor through a synchronising pageable copy)
+        return logits[:, :, 2:], logits[:, :, 0], torch.cat([logits[:, :, 1:2], logits[:, :, 3:]], dim=-1)
 
     def flops(self, T_pad: int) -> float:
         a = self.arch
