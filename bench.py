@@ -119,8 +119,10 @@ def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s, encoder="cnhuber
                       f"(oracle: torch-CPU fp32 resample + {encoder} + UNet, C Viterbi), {el:.1f} s wall"}
 
 
-def config_name(encoder: str, world: int, B: int) -> str:
-    """Which BASELINE.json config this run's geometry is (configs[1..3]); weak scaling keeps B per GPU fixed."""
+def config_name(encoder: str, world: int, B: int, seconds: float = 10.0) -> str:
+    """Which BASELINE.json config this run's geometry is (configs[1..4]); weak scaling keeps B per GPU fixed."""
+    if seconds >= 60:
+        return f"config 5 geometry (long-form, {seconds:g} s unchunked, {B} per GPU)"
     if encoder == "large":
         return "config 4 geometry" + ("" if world * B == 256 else f" (global batch {world * B}, config 4 is 256)")
     if world == 1:
@@ -263,7 +265,7 @@ def main():
         "metric": METRIC, "value": value, "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"{config_name(args.encoder, world, B)}: "
+        "config": {"workload": f"{config_name(args.encoder, world, B, args.seconds)}: "
                                f"B={B} x {args.seconds:g} s 16 kHz utterances per GPU, "
                                f"{ {'base': 'Hubert-base (cnhubert arch)', 'large': 'Hubert-large (cnhubert-large arch)', 'soft': 'HubertSoft'}[args.encoder]}"
                                f" + UNet head + Viterbi; full infer path wave(HBM)->boundaries(host), host assembly "

@@ -114,7 +114,8 @@ class AlignmentDecoder:
         B, Tl, V = frame_logits.shape
         Ts = [self.num_frames(w, Tl) for w in wav_lengths]
         ids = [self.ph_ids(p) for p in ph_seqs]
-        Smax = max(len(i) for i in ids)
+        # state pitch padded to a multiple of 8 so the DP kernel moves each lane's states as vectors
+        Smax = -(-max(len(i) for i in ids) // 8) * 8
         ids_pad = np.zeros((B, Smax), np.int32)
         for b, i in enumerate(ids):
             ids_pad[b, :len(i)] = i

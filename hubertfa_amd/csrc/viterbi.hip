@@ -25,7 +25,16 @@ using hfa::neg_inf;
 // One workgroup per utterance: NW waves x 64 lanes, each lane owning K contiguous states; G time steps of
 // emissions are prefetched one group ahead.  With NW > 1 the two boundary q values of each wave's last lane
 // cross to the next wave through a double-buffered LDS slot (one barrier per time step).
-template <int K, int NW, int G>
+// q of the lane one below (DPP wave_shr:1: a one-cycle VALU move, where __shfl_up is an LDS ds_bpermute on
+// the step's critical path); lane 0 receives -inf.
+__device__ __forceinline__ float from_lane_below(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(neg_inf()), __float_as_int(v), 0x138, 0xF, 0xF,
+                                                      false));
+}
+
+// VEC: Smax % K == 0 and aligned planes, so a lane's K contiguous states are loaded and stored as vectors
+// (dp K x f32, bt K bytes) instead of 2K scattered narrow accesses per time step.
+template <int K, int NW, int G, bool VEC>
 __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
     const int32_t* __restrict__ padv, const float* __restrict__ prob_log,
@@ -76,8 +85,23 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
             const bool tv = t < T;
             E[u] = tv ? Ep[t] : 0.0f;
             nE[u] = tv ? nEp[t] : 0.0f;
+            if (VEC && K >= 2) {
+                if (tv && s0 < Smax) {
+                    const float* src = pl + (size_t)t * Smax + s0;
 #pragma unroll
-            for (int k = 0; k < K; ++k) L[u][k] = (tv && valid[k]) ? pl[(size_t)t * Smax + s0 + k] : 0.0f;
+                    for (int k = 0; k < K; k += 2) {
+                        const float2 v = *reinterpret_cast<const float2*>(src + k);
+                        L[u][k] = v.x;
+                        L[u][k + 1] = v.y;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) L[u][k] = 0.0f;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k) L[u][k] = (tv && valid[k]) ? pl[(size_t)t * Smax + s0 + k] : 0.0f;
+            }
         }
     };
     load_group(1, Lc, Ec, nEc);
@@ -97,10 +121,8 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
                 q[k] = (float)__dadd_rn((double)a2, __dmul_rn(curr[k], ratio));          //  + C*T/S   (f64)
             }
             // left neighbour lane's last two q values (states s0-1, s0-2)
-            float qm1 = __shfl_up(q[K - 1], 1, 64);
-            float qm2 = (K >= 2) ? __shfl_up(q[K >= 2 ? K - 2 : 0], 1, 64) : __shfl_up(q[0], 2, 64);
-            if (lane < 1) qm1 = neg_inf();
-            if (K >= 2 ? lane < 1 : lane < 2) qm2 = neg_inf();
+            float qm1 = from_lane_below(q[K - 1]);
+            float qm2 = (K >= 2) ? from_lane_below(q[K >= 2 ? K - 2 : 0]) : from_lane_below(qm1);
             if (NW > 1) {
                 if (lane == 63) {
                     xq[t & 1][wave][0] = q[K - 1];
@@ -113,6 +135,8 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
                 }
             }
             const size_t row = (size_t)t * Smax;
+            float bestv[K];
+            unsigned long long bidx = 0;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const int s = s0 + k;
@@ -125,7 +149,10 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
                 int idx = 0;
                 if (p2 > best) { best = p2; idx = 1; }
                 if (p3 > best) { best = p3; idx = 2; }
-                if (valid[k]) {
+                if (VEC) {
+                    bestv[k] = best;
+                    bidx |= (unsigned long long)idx << (8 * k);
+                } else if (valid[k]) {
                     d[row + s] = best;
                     bb[row + s] = (int8_t)idx;
                 }
@@ -134,6 +161,24 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
                 else curr[k] = Ld;                                       // (:224)
                 if (zero[k]) curr[k] = 0.0;                              // (:226-228)
                 dprev[k] = best;
+            }
+            if (VEC && s0 < Smax) {     // states past S inside the Smax pitch get don't-care values
+                float* drow = d + row + s0;
+                if (K == 1) {
+                    drow[0] = bestv[0];
+                    bb[row + s0] = (int8_t)bidx;
+                } else if (K == 2) {
+                    *reinterpret_cast<float2*>(drow) = make_float2(bestv[0], bestv[K > 1 ? 1 : 0]);
+                    *reinterpret_cast<uint16_t*>(bb + row + s0) = (uint16_t)bidx;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < K; k += 4)
+                        *reinterpret_cast<float4*>(drow + k) =
+                            make_float4(bestv[k], bestv[k + 1 < K ? k + 1 : 0], bestv[k + 2 < K ? k + 2 : 0],
+                                        bestv[k + 3 < K ? k + 3 : 0]);
+                    if (K == 4) *reinterpret_cast<uint32_t*>(bb + row + s0) = (uint32_t)bidx;
+                    else *reinterpret_cast<unsigned long long*>(bb + row + s0) = bidx;
+                }
             }
         }
 #pragma unroll
@@ -318,8 +363,14 @@ template <int K, int NW, int G>
 int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const int32_t* pad,
                    const float* prob_log, const float* nE, const float* E, double* curr, float* dp, int8_t* bt,
                    const int32_t* ids, hipStream_t st) {
-    hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T, S, pad,
-                       prob_log, nE, E, curr, dp, bt, ids);
+    const bool vec = Smax % K == 0 && ((uintptr_t)prob_log % 16 == 0) && ((uintptr_t)dp % 16 == 0) &&
+                     ((uintptr_t)bt % 8 == 0);
+    if (vec)
+        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, true>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
+                           S, pad, prob_log, nE, E, curr, dp, bt, ids);
+    else
+        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, false>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
+                           S, pad, prob_log, nE, E, curr, dp, bt, ids);
     return hfa::check_launch("hfa_viterbi_forward");
 }
 
