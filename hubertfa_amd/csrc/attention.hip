@@ -37,6 +37,7 @@ struct AttnP {
     const float* k; long long k_bs; int k_ld;
     const float* v; long long v_bs; int v_ld;
     float* o; long long o_bs; int o_ld;
+    const int32_t* key_len;     // optional [B]: per-row sequence lengths of a variable-length batch
 };
 
 __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
@@ -52,6 +53,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
     const int nqb = (p.L + QW * NW - 1) / (QW * NW);
     const int bh = wgid / nqb, qb = wgid - bh * nqb;
     const int b = bh / p.H, hd = bh - b * p.H;
+    const int L = p.key_len ? p.key_len[b] : p.L;       // this row's length (queries and keys beyond: padding)
+    if (qb * (QW * NW) >= L) return;                     // whole workgroup is padding (uniform exit)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r32 = lane & 31, half = lane >> 5;
@@ -61,15 +64,15 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
     const float* Q = p.q + b * p.q_bs + hd * DH;
     const float* Kp = p.k + b * p.k_bs + hd * DH;
     const float* Vp = p.v + b * p.v_bs + hd * DH;
-    const __amdgpu_buffer_rsrc_t rK = hfa::make_rsrc(Kp, ((long long)(p.L - 1) * p.k_ld + DH) * 4);
-    const __amdgpu_buffer_rsrc_t rV = hfa::make_rsrc(Vp, ((long long)(p.L - 1) * p.v_ld + DH) * 4);
+    const __amdgpu_buffer_rsrc_t rK = hfa::make_rsrc(Kp, ((long long)(L - 1) * p.k_ld + DH) * 4);
+    const __amdgpu_buffer_rsrc_t rV = hfa::make_rsrc(Vp, ((long long)(L - 1) * p.v_ld + DH) * 4);
 
     // Q fragments: lane holds Q[qi][kk*8 + half*4 + e] * scale * log2(e), kk = 0..7, e = 0..3
     const float qscale = p.scale * 1.44269504088896340736f;
     f32x4 qf[DH / 8];
 #pragma unroll
     for (int kk = 0; kk < DH / 8; ++kk) {
-        if (qi < p.L) {
+        if (qi < L) {
             f32x4 v = *reinterpret_cast<const f32x4*>(Q + (long long)qi * p.q_ld + kk * 8 + half * 4);
             qf[kk] = v * qscale;
         } else {
@@ -92,7 +95,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
             const int key = key0 + rowd[d];
-            const bool ok = key < p.L;
+            const bool ok = key < L;
             hfa::dma16(ok ? (unsigned)((key * p.k_ld + kcol[d]) * 4) : hfa::DMA_OOB, rK, 0u, kdst + d * 1024);
             hfa::dma16(ok ? (unsigned)((key * p.v_ld + (lane & 15) * 4) * 4) : hfa::DMA_OOB, rV, 0u, vdst + d * 1024);
         }
@@ -108,7 +111,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
 #pragma unroll
     for (int kk = 0; kk < DH / 8; ++kk) krd[kk] = r32 * DH + (((kk * 2 + half) ^ (r32 & 15)) << 2);
 
-    const int nkb = (p.L + KB - 1) / KB;
+    const int nkb = (L + KB - 1) / KB;
 #pragma unroll
     for (int st = 0; st < NS - 1; ++st)
         if (st < nkb) issue(st, st * KB);
@@ -131,10 +134,10 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
             for (int e = 0; e < 4; ++e) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[e], qf[kk][e], s, 0, 0, 0);
         }
         const int key0 = kb * KB;
-        if (key0 + KB > p.L) {          // last, partial tile: keys >= L do not exist
+        if (key0 + KB > L) {          // last, partial tile: keys >= L do not exist
 #pragma unroll
             for (int e = 0; e < 16; ++e)
-                if (key0 + (e & 3) + 8 * (e >> 2) + 4 * half >= p.L) s[e] = -__builtin_inff();
+                if (key0 + (e & 3) + 8 * (e >> 2) + 4 * half >= L) s[e] = -__builtin_inff();
         }
         float bm = s[0];
 #pragma unroll
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
             const int idx = lane + i * 64;
             const int row = idx >> 3, c4 = (idx & 7) * 4;
             const int qq = q0 + row;
-            if (qq < p.L) {
+            if (qq < L) {
                 f32x4 v{slab[row * 33 + c4], slab[row * 33 + c4 + 1], slab[row * 33 + c4 + 2],
                         slab[row * 33 + c4 + 3]};
                 *reinterpret_cast<f32x4*>(p.o + b * p.o_bs + (long long)qq * p.o_ld + hd * DH + dt * 32 + c4) = v;
@@ -206,7 +209,7 @@ extern "C" {
 
 int hfa_attention_f32(int B, int H, int L, int head_dim, float scale, const float* q, long long q_bs, int q_ld,
                       const float* k, long long k_bs, int k_ld, const float* v, long long v_bs, int v_ld, float* o,
-                      long long o_bs, int o_ld, hipStream_t stream) {
+                      long long o_bs, int o_ld, const int32_t* key_len, hipStream_t stream) {
     if (head_dim != DH) {
         hfa::set_error("hfa_attention_f32: head_dim=%d unsupported (64 only)", head_dim);
         return HFA_EINVAL;
@@ -225,7 +228,7 @@ int hfa_attention_f32(int B, int H, int L, int head_dim, float scale, const floa
         hfa::set_error("hfa_attention_f32: K/V span exceeds 31-bit buffer offsets");
         return HFA_EINVAL;
     }
-    AttnP p{B, H, L, scale, q, q_bs, q_ld, k, k_bs, k_ld, v, v_bs, v_ld, o, o_bs, o_ld};
+    AttnP p{B, H, L, scale, q, q_bs, q_ld, k, k_bs, k_ld, v, v_bs, v_ld, o, o_bs, o_ld, key_len};
     const long long nblk = (long long)((L + QW * NW - 1) / (QW * NW)) * B * H;
     if (nblk > 0x7fffffffLL) {
         hfa::set_error("hfa_attention_f32: grid too large");

@@ -39,11 +39,13 @@ __device__ __forceinline__ void stage_chunk(float* xs, const float* xb, int t0, 
 }
 
 __global__ __launch_bounds__(NT) void conv0_stats_kernel(int N, int T0, const float* __restrict__ x, long long x_bs,
-                                                         const float* __restrict__ w0, double* __restrict__ part) {
+                                                         const float* __restrict__ w0, double* __restrict__ part,
+                                                         const int32_t* __restrict__ t0_len) {
     __shared__ float xs[CH * ST + KW];
     const int b = blockIdx.y, chunk = blockIdx.x;
     const int t0 = chunk * CH;
-    const int nt = min(CH, T0 - t0);
+    const int T0b = t0_len ? t0_len[b] : T0;       // a variable-length batch: statistics over this row's frames
+    const int nt = max(0, min(CH, T0b - t0));
     stage_chunk(xs, x + b * x_bs, t0, nt, N);
     const int c0 = threadIdx.x * 2;
     float wa[KW], wb[KW];
@@ -65,8 +67,10 @@ __global__ __launch_bounds__(NT) void conv0_stats_kernel(int N, int T0, const fl
 }
 
 __global__ __launch_bounds__(NT) void conv0_reduce_kernel(int T0, int nchunk, const double* __restrict__ part,
-                                                          float eps, float* __restrict__ stats) {
+                                                          float eps, float* __restrict__ stats,
+                                                          const int32_t* __restrict__ t0_len) {
     const int b = blockIdx.x;
+    if (t0_len) T0 = t0_len[b];
     for (int c = threadIdx.x; c < C0; c += NT) {
         double s = 0.0, q = 0.0;
         for (int k = 0; k < nchunk; ++k) {
@@ -139,10 +143,11 @@ long long hfa_conv0_workspace_bytes(int B, int N) {
 
 // x [B, N] (row stride x_bs) -> y [B, T0, 512] channels-last (row stride 512, batch stride y_bs).
 // norm = 1: GroupNorm(512,512)+GELU (gamma/beta required, workspace of hfa_conv0_workspace_bytes);
-// norm = 0: raw conv + bias (bias may be NULL).
+// norm = 0: raw conv + bias (bias may be NULL).  t0_len (optional, device [B]): per-row frame counts of a
+// variable-length batch — the GroupNorm statistics cover frames < t0_len[b] only (rows beyond are don't-care).
 int hfa_conv0_f32(int B, int N, const float* x, long long x_bs, const float* w0, const float* bias, int norm,
                   const float* gamma, const float* beta, float eps, void* workspace, float* y, long long y_bs,
-                  hipStream_t stream) {
+                  const int32_t* t0_len, hipStream_t stream) {
     if (B < 0 || N < KW) {
         hfa::set_error("hfa_conv0_f32: need N >= %d samples (got %d)", KW, N);
         return HFA_EINVAL;
@@ -158,8 +163,8 @@ int hfa_conv0_f32(int B, int N, const float* x, long long x_bs, const float* w0,
     if (norm) {
         double* part = reinterpret_cast<double*>(workspace);
         float* stats = reinterpret_cast<float*>(part + (size_t)B * nchunk * C0 * 2);
-        hipLaunchKernelGGL(conv0_stats_kernel, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, part);
-        hipLaunchKernelGGL(conv0_reduce_kernel, dim3(B), dim3(NT), 0, stream, T0, nchunk, part, eps, stats);
+        hipLaunchKernelGGL(conv0_stats_kernel, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, part, t0_len);
+        hipLaunchKernelGGL(conv0_reduce_kernel, dim3(B), dim3(NT), 0, stream, T0, nchunk, part, eps, stats, t0_len);
         hipLaunchKernelGGL(conv0_apply_kernel<0>, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats, gamma, beta,
                            bias, y, y_bs);
     } else {

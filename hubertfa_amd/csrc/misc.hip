@@ -19,30 +19,49 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void units_gather_kernel(int U, int C, const float* __restrict__ units,
                                                            long long u_bs, int u_ld, int n_frames, int T_pad,
                                                            float ratio, float* __restrict__ out, long long o_bs,
-                                                           int o_ld) {
+                                                           int o_ld, const int32_t* __restrict__ nf_b,
+                                                           const int32_t* __restrict__ U_b) {
     const int b = blockIdx.y;
     const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (k >= T_pad) return;
+    const int nf = nf_b ? nf_b[b] : n_frames;      // per-utterance lengths of a variable-length batch
+    const int Ub = U_b ? U_b[b] : U;
     float* orow = out + b * o_bs + (long long)k * o_ld;
-    if (k >= n_frames) {
+    if (k >= nf) {
         for (int c = lane * 4; c < C; c += 256) *reinterpret_cast<f32x4*>(orow + c) = f32x4{0.f, 0.f, 0.f, 0.f};
         return;
     }
     int idx = (int)rintf(__fmul_rn(ratio, (float)k));
-    idx = idx < U - 1 ? idx : U - 1;
+    idx = idx < Ub - 1 ? idx : Ub - 1;
     const float* irow = units + b * u_bs + (long long)idx * u_ld;
     for (int c = lane * 4; c < C; c += 256) *reinterpret_cast<f32x4*>(orow + c) = *reinterpret_cast<const f32x4*>(irow + c);
+}
+
+// Zero rows t >= lens[b] of a [B, T, C] tensor (the padding rows of a variable-length batch, which convs with
+// padding and GroupNorm must see as zeros / not at all).
+__global__ __launch_bounds__(256) void mask_rows_kernel(int T, int C, float* __restrict__ x, long long x_bs, int ldx,
+                                                        const int32_t* __restrict__ lens) {
+    const int b = blockIdx.y;
+    const int t0 = lens[b];
+    const long long n = (long long)(T - t0) * C;
+    float* xb = x + b * x_bs;
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const int t = t0 + (int)(i / C), c = (int)(i % C);
+        xb[(long long)t * ldx + c] = 0.0f;
+    }
 }
 
 // Wav2Vec2FeatureExtractor zero_mean_unit_var_norm (transformers feature_extraction_wav2vec2.py): per row
 // (x - mean) / sqrt(var + 1e-7), biased variance.  One workgroup per row, f64 statistics.
 __global__ __launch_bounds__(256) void wav_normalize_kernel(int N, const float* __restrict__ x, long long x_bs,
-                                                            float eps, float* __restrict__ y, long long y_bs) {
+                                                            float eps, float* __restrict__ y, long long y_bs,
+                                                            const int32_t* __restrict__ lens) {
     const int b = blockIdx.x;
+    const int Nb = lens ? lens[b] : N;                // statistics over this utterance's samples only
     const float* xr = x + b * x_bs;
     double s = 0.0, ss = 0.0;
-    for (int i = threadIdx.x; i < N; i += 256) {
+    for (int i = threadIdx.x; i < Nb; i += 256) {
         const double v = xr[i];
         s += v;
         ss += v * v;
@@ -54,13 +73,13 @@ __global__ __launch_bounds__(256) void wav_normalize_kernel(int N, const float* 
     __syncthreads();
     const double S = red[0][0] + red[0][1] + red[0][2] + red[0][3];
     const double SS = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-    const double mean = S / N;
-    double var = SS / N - mean * mean;
+    const double mean = Nb > 0 ? S / Nb : 0.0;
+    double var = Nb > 0 ? SS / Nb - mean * mean : 0.0;
     if (var < 0) var = 0;
     const float meanf = (float)mean;
     const float den = (float)sqrt((double)(float)var + (double)eps);
     float* yr = y + b * y_bs;
-    for (int i = threadIdx.x; i < N; i += 256) yr[i] = (xr[i] - meanf) / den;
+    for (int i = threadIdx.x; i < N; i += 256) yr[i] = i < Nb ? (xr[i] - meanf) / den : 0.0f;
 }
 
 // y[b, i] = x[b, i - left] inside [0, N), else 0, for i < N_out.
@@ -101,7 +120,8 @@ inline int grid1d(long long n, int per = 256, int cap = 8192) {
 extern "C" {
 
 int hfa_units_gather_f32(int B, int U, int C, const float* units, long long u_bs, int u_ld, int n_frames, int T_pad,
-                         float ratio, float* out, long long o_bs, int o_ld, hipStream_t stream) {
+                         float ratio, float* out, long long o_bs, int o_ld, const int32_t* n_frames_b,
+                         const int32_t* U_b, hipStream_t stream) {
     if (B < 0 || U < 1 || C <= 0 || C % 4 || n_frames < 0 || T_pad < n_frames || u_ld % 4 || o_ld % 4 ||
         u_bs % 4 || o_bs % 4 || (((uintptr_t)units | (uintptr_t)out) & 15)) {
         hfa::set_error("hfa_units_gather_f32: bad arguments");
@@ -109,18 +129,30 @@ int hfa_units_gather_f32(int B, int U, int C, const float* units, long long u_bs
     }
     if (B == 0 || T_pad == 0) return HFA_OK;
     hipLaunchKernelGGL(units_gather_kernel, dim3((T_pad + 3) / 4, B), dim3(256), 0, stream, U, C, units, u_bs, u_ld,
-                       n_frames, T_pad, ratio, out, o_bs, o_ld);
+                       n_frames, T_pad, ratio, out, o_bs, o_ld, n_frames_b, U_b);
     return hfa::check_launch("hfa_units_gather_f32");
 }
 
+int hfa_mask_rows_f32(int B, int T, int C, float* x, long long x_bs, int ldx, const int32_t* lens,
+                      hipStream_t stream) {
+    if (B < 0 || T < 0 || C < 1 || !x || !lens || ldx < C) {
+        hfa::set_error("hfa_mask_rows_f32: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (B == 0 || T == 0) return HFA_OK;
+    hipLaunchKernelGGL(mask_rows_kernel, dim3(grid1d((long long)T * C, 256, 512), B), dim3(256), 0, stream, T, C, x,
+                       x_bs, ldx, lens);
+    return hfa::check_launch("hfa_mask_rows_f32");
+}
+
 int hfa_wav_normalize_f32(int B, int N, const float* x, long long x_bs, float eps, float* y, long long y_bs,
-                          hipStream_t stream) {
+                          const int32_t* lens, hipStream_t stream) {
     if (B < 0 || N <= 0 || !x || !y) {
         hfa::set_error("hfa_wav_normalize_f32: bad arguments");
         return HFA_EINVAL;
     }
     if (B == 0) return HFA_OK;
-    hipLaunchKernelGGL(wav_normalize_kernel, dim3(B), dim3(256), 0, stream, N, x, x_bs, eps, y, y_bs);
+    hipLaunchKernelGGL(wav_normalize_kernel, dim3(B), dim3(256), 0, stream, N, x, x_bs, eps, y, y_bs, lens);
     return hfa::check_launch("hfa_wav_normalize_f32");
 }
 

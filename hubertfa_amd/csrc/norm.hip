@@ -28,10 +28,16 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
                                                         const float* __restrict__ res, long long ldr,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps, int act,
-                                                        float* __restrict__ y, long long ldy) {
+                                                        float* __restrict__ y, long long ldy, int T,
+                                                        const int32_t* __restrict__ t_len) {
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wave >= rows) return;
+    if (t_len && wave % T >= t_len[wave / T]) {     // padding row of a variable-length batch: zeros
+        float* yr = y + wave * ldy;
+        for (int c = lane * 4; c < C; c += 256) *reinterpret_cast<f32x4*>(yr + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+        return;
+    }
     const float* xr = x + wave * ldx;
     const float* rr = res ? res + wave * ldr : nullptr;
     f32x4 v[VPL];
@@ -83,12 +89,14 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
 __global__ __launch_bounds__(256) void groupnorm_kernel(int T, int C, int G, const float* __restrict__ x,
                                                         long long x_bs, int ldx, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps, int act,
-                                                        float* __restrict__ y, long long y_bs, int ldy) {
+                                                        float* __restrict__ y, long long y_bs, int ldy,
+                                                        const int32_t* __restrict__ t_len) {
     const int b = blockIdx.y, g = blockIdx.x;
     const int Cg = C / G;
     const float* xb = x + b * x_bs + g * Cg;
     float* yb = y + b * y_bs + g * Cg;
-    const int n = T * Cg;
+    const int Tb = t_len ? t_len[b] : T;            // variable-length batch: this row's frames only
+    const int n = Tb * Cg;
     double s = 0.0, ss = 0.0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int t = i / Cg, c = i - t * Cg;
@@ -109,8 +117,8 @@ __global__ __launch_bounds__(256) void groupnorm_kernel(int T, int C, int G, con
         S += red[0][w];
         SS += red[1][w];
     }
-    const double mean_d = S / n;
-    double var_d = SS / n - mean_d * mean_d;
+    const double mean_d = n > 0 ? S / n : 0.0;
+    double var_d = n > 0 ? SS / n - mean_d * mean_d : 0.0;
     if (var_d < 0) var_d = 0;
     const float mean = (float)mean_d;
     const float rstd = (float)(1.0 / sqrt(var_d + (double)eps));
@@ -119,6 +127,10 @@ __global__ __launch_bounds__(256) void groupnorm_kernel(int T, int C, int G, con
         const float v = xb[(long long)t * ldx + c];
         yb[(long long)t * ldy + c] = act_apply((v - mean) * rstd * gamma[g * Cg + c] + beta[g * Cg + c], act);
     }
+    for (int i = n + threadIdx.x; i < T * Cg; i += blockDim.x) {   // padding rows -> zeros
+        const int t = i / Cg, c = i - t * Cg;
+        yb[(long long)t * ldy + c] = 0.0f;
+    }
 }
 
 }  // namespace
@@ -126,8 +138,12 @@ __global__ __launch_bounds__(256) void groupnorm_kernel(int T, int C, int G, con
 extern "C" {
 
 int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const float* res, long long ldr,
-                      const float* gamma, const float* beta, float eps, int act, float* y, long long ldy,
-                      hipStream_t stream) {
+                      const float* gamma, const float* beta, float eps, int act, float* y, long long ldy, int T,
+                      const int32_t* t_len, hipStream_t stream) {
+    if (t_len && (T <= 0 || rows % T)) {
+        hfa::set_error("hfa_layernorm_f32: t_len needs rows = B * T (T=%d, rows=%d)", T, rows);
+        return HFA_EINVAL;
+    }
     if (rows < 0 || C <= 0 || C % 4 || C > 4096 || act < 0 || act > 2) {
         hfa::set_error("hfa_layernorm_f32: bad sizes rows=%d C=%d (C%%4==0, C<=4096)", rows, C);
         return HFA_EINVAL;
@@ -142,7 +158,7 @@ int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const floa
     const int vpl = (C + 255) / 256;
 #define HFA_LN(V)                                                                                               \
     hipLaunchKernelGGL(layernorm_kernel<V>, dim3(blocks), dim3(256), 0, stream, rows, C, x, ldx, res, ldr, gamma, \
-                       beta, eps, act, y, ldy)
+                       beta, eps, act, y, ldy, T, t_len)
     if (vpl <= 1) HFA_LN(1);
     else if (vpl <= 2) HFA_LN(2);
     else if (vpl <= 3) HFA_LN(3);
@@ -154,7 +170,8 @@ int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const floa
 }
 
 int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,
-                      const float* beta, float eps, int act, float* y, long long y_bs, int ldy, hipStream_t stream) {
+                      const float* beta, float eps, int act, float* y, long long y_bs, int ldy, const int32_t* t_len,
+                      hipStream_t stream) {
     if (B < 0 || T < 0 || C <= 0 || G <= 0 || C % G || act < 0 || act > 2) {
         hfa::set_error("hfa_groupnorm_f32: bad sizes");
         return HFA_EINVAL;
@@ -165,7 +182,7 @@ int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs
         return HFA_EINVAL;
     }
     hipLaunchKernelGGL(groupnorm_kernel, dim3(G, B), dim3(256), 0, stream, T, C, G, x, x_bs, ldx, gamma, beta, eps,
-                       act, y, y_bs, ldy);
+                       act, y, y_bs, ldy, t_len);
     return hfa::check_launch("hfa_groupnorm_f32");
 }
 

@@ -15,12 +15,14 @@ a bshall checkpoint (``torch.load(path)["hubert"]``), or ``synth:<seed>`` for se
 from __future__ import annotations
 
 import json
+import math
 import os
 
 import torch
 
 from . import ops, synth
 from .hubert import HubertEncoder
+from .hubert import dev_lengths
 from .resample import Resampler
 
 
@@ -98,23 +100,54 @@ class UnitsEncoder:
         ratio = (hop_size / sample_rate) / (self.encoder_hop_size / self.encoder_sample_rate)
         return n_frames, ratio
 
+    def resampled_lengths(self, lengths, sample_rate: int):
+        """Per-row sample counts after resampling to the encoder rate (torchaudio: ceil(new * n / orig))."""
+        if sample_rate == self.encoder_sample_rate:
+            return [int(n) for n in lengths]
+        g = math.gcd(int(sample_rate), int(self.encoder_sample_rate))
+        orig, new = int(sample_rate) // g, int(self.encoder_sample_rate) // g
+        return [-(-new * int(n) // orig) for n in lengths]
+
     @torch.no_grad()
-    def units(self, audio: torch.Tensor, sample_rate: int) -> torch.Tensor:
+    def units(self, audio: torch.Tensor, sample_rate: int, lengths=None) -> torch.Tensor:
+        """[B, N] -> units [B, L, C].  ``lengths``: per-row sample counts of a zero-padded variable-length batch
+        (every row's units then equal what that utterance gives alone)."""
         audio = audio.to(self.device).float()
         if audio.dim() == 1:
             audio = audio[None]
         audio_res = self._resample(audio, sample_rate)
-        if audio_res.size(-1) < 400:   # reference pads the ORIGINAL audio here (encoder.py:51-52)
-            audio_res = torch.nn.functional.pad(audio, (0, 400 - audio_res.size(-1)))
-        return self.model(audio_res.contiguous())
+        if lengths is None:
+            if audio_res.size(-1) < 400:   # reference pads the ORIGINAL audio here (encoder.py:51-52)
+                audio_res = torch.nn.functional.pad(audio, (0, 400 - audio_res.size(-1)))
+            return self.model(audio_res.contiguous())
+        lens16 = self.resampled_lengths(lengths, sample_rate)
+        if min(lens16) < 400:
+            raise ValueError("utterances shorter than 400 encoder samples take the reference's padding quirk "
+                             "(encoder.py:51-52) and must be aligned alone")
+        audio_res = audio_res.contiguous()
+        if any(n != audio_res.shape[-1] for n in lens16):   # the resampler's sinc tails spill past each row's end
+            ops.mask_rows(audio_res, dev_lengths(lens16, audio_res.device))
+        return self.model(audio_res, lengths=lens16)
 
     @torch.no_grad()
-    def encode_frames(self, audio: torch.Tensor, sample_rate: int, hop_size: int, pad_to: int = 1):
-        """[B, N] -> (features [B, T_pad, C] channels-last, n_frames); rows >= n_frames are zero."""
-        units = self.units(audio, sample_rate)
-        n_frames, ratio = self.grid(audio.shape[-1], sample_rate, hop_size)
-        T_pad = (n_frames + pad_to - 1) // pad_to * pad_to
-        return ops.units_gather(units.contiguous(), n_frames, T_pad, ratio), n_frames
+    def encode_frames(self, audio: torch.Tensor, sample_rate: int, hop_size: int, pad_to: int = 1, lengths=None):
+        """[B, N] -> (features [B, T_pad, C] channels-last, n_frames); rows >= n_frames are zero.
+
+        With ``lengths`` (per-row sample counts of a zero-padded batch) n_frames is a list (one per row) and
+        rows >= n_frames[b] of row b are zero; T_pad covers the longest row."""
+        units = self.units(audio, sample_rate, lengths)
+        if lengths is None:
+            n_frames, ratio = self.grid(audio.shape[-1], sample_rate, hop_size)
+            T_pad = (n_frames + pad_to - 1) // pad_to * pad_to
+            return ops.units_gather(units.contiguous(), n_frames, T_pad, ratio), n_frames
+        nfs = [self.grid(int(n), sample_rate, hop_size)[0] for n in lengths]
+        _, ratio = self.grid(int(lengths[0]), sample_rate, hop_size)
+        Ls = [self.model.frame_lengths(n) for n in self.resampled_lengths(lengths, sample_rate)]
+        T_pad = (max(nfs) + pad_to - 1) // pad_to * pad_to
+        dev = units.device
+        feats = ops.units_gather(units.contiguous(), max(nfs), T_pad, ratio, n_frames_b=dev_lengths(nfs, dev),
+                                 U_b=dev_lengths(Ls, dev))
+        return feats, nfs
 
     def encode(self, audio, sample_rate, hop_size):
         feats, n = self.encode_frames(audio, sample_rate, hop_size)

@@ -56,6 +56,12 @@ class _Layer:
     __slots__ = ("wqkv", "bqkv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w", "ln2_b")
 
 
+def dev_lengths(values, device) -> torch.Tensor:
+    """Host ints -> int32 device tensor through pinned memory and a non-blocking copy (a pageable upload would
+    synchronise the stream and stall the pipelined host)."""
+    return torch.tensor([int(v) for v in values], dtype=torch.int32).pin_memory().to(device, non_blocking=True)
+
+
 class HubertEncoder:
     """Hubert forward on HIP kernels.  ``forward(wav[B, N]) -> units[B, L, C_out]`` (f32, channels-last)."""
 
@@ -123,14 +129,24 @@ class HubertEncoder:
             self._ws[name] = buf
         return buf
 
-    def feature_extractor(self, x: torch.Tensor) -> torch.Tensor:
-        """[B, N] -> [B, L, 512] (channels-last); GELU applied after every conv."""
+    def frame_lengths(self, n_samples: int) -> int:
+        """Hubert frames of an n-sample input (after wav_pad), through the CNN extractor's valid convs."""
+        a = self.arch
+        t = n_samples + 2 * a.wav_pad
+        for k, st in zip(a.conv_kernel, a.conv_stride):
+            t = (t - k) // st + 1 if t >= k else 0
+        return t
+
+    def feature_extractor(self, x: torch.Tensor, t0_len: torch.Tensor | None = None) -> torch.Tensor:
+        """[B, N] -> [B, L, 512] (channels-last); GELU applied after every conv.  ``t0_len`` [B] int32: conv0
+        frames per row of a variable-length batch (GroupNorm statistics); later convs need no lengths (their
+        valid rows only read valid rows)."""
         a = self.arch
         B, N = x.shape
         ln0 = self.conv_ln[0]
         if a.feat_extract_norm == "group":
             ws = self._workspace("conv0", ops._lib.lib().hfa_conv0_workspace_bytes(B, N))
-            h = ops.conv0(x, self.conv_w[0], gamma=ln0[0], beta=ln0[1], eps=1e-5, workspace=ws)
+            h = ops.conv0(x, self.conv_w[0], gamma=ln0[0], beta=ln0[1], eps=1e-5, workspace=ws, t0_len=t0_len)
         else:
             h = ops.conv0(x, self.conv_w[0], bias=self.conv_b[0])
             h = ops.layernorm(h, ln0[0], ln0[1], a.layer_norm_eps, act=ops.ACT_GELU, out=h)
@@ -150,19 +166,22 @@ class HubertEncoder:
             h = out
         return h
 
-    def positional(self, h: torch.Tensor) -> torch.Tensor:
-        """h + GELU(grouped conv k128 pad64 (+bias), last frame dropped) — one GEMM launch over (batch, group)."""
+    def positional(self, h: torch.Tensor, lens: torch.Tensor | None = None) -> torch.Tensor:
+        """h + GELU(grouped conv k128 pad64 (+bias), last frame dropped) — one GEMM launch over (batch, group).
+        With ``lens`` the padding rows are zeroed first: the conv's padding must read zeros past each row's end."""
         a = self.arch
         B, L, H = h.shape
         G, k = a.pos_groups, a.pos_kernel
         Cg = H // G
+        if lens is not None:
+            ops.mask_rows(h, lens)
         out = torch.empty_like(h)
         ops.conv_gemm(h, self.pos_w, out, M=L, N=Cg, K=k * Cg, Zb=B, G=G, sAb=L * H, sAg=Cg, ldx=H, stride=1,
                       pad=k // 2, Cg=Cg, Tin=L, sWg=Cg * k * Cg, bias=self.pos_b, sBg=Cg, R=h, sRb=L * H, sRg=Cg,
                       ldr=H, sCb=L * H, sCg=Cg, ldc=H, epilogue=ops.EPI_GELU)
         return out
 
-    def attention_block(self, h_in: torch.Tensor, L_: _Layer) -> torch.Tensor:
+    def attention_block(self, h_in: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None) -> torch.Tensor:
         a = self.arch
         B, L, H = h_in.shape
         nh = a.heads
@@ -171,13 +190,13 @@ class HubertEncoder:
         o = torch.empty((B, L, H), dtype=torch.float32, device=h_in.device)
         ops.attention(qkv, qkv[..., H:], qkv[..., 2 * H:], o, B=B, H=nh, L=L, head_dim=dh, scale=dh ** -0.5,
                       q_bs=L * 3 * H, q_ld=3 * H, k_bs=L * 3 * H, k_ld=3 * H, v_bs=L * 3 * H, v_ld=3 * H,
-                      o_bs=L * H, o_ld=H)
+                      o_bs=L * H, o_ld=H, key_len=lens)
         return o
 
-    def layer(self, h: torch.Tensor, L_: _Layer) -> torch.Tensor:
+    def layer(self, h: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None) -> torch.Tensor:
         eps = self.arch.layer_norm_eps
         if not self.arch.stable_layer_norm:   # post-LN (HubertEncoderLayer / nn.TransformerEncoderLayer)
-            o = self.attention_block(h, L_)
+            o = self.attention_block(h, L_, lens)
             h1 = ops.linear(o, L_.wo, L_.bo, residual=h)
             h1 = ops.layernorm(h1, L_.ln1_w, L_.ln1_b, eps, out=h1)
             f = ops.linear(h1, L_.w1, L_.b1, epilogue=ops.EPI_GELU)
@@ -185,30 +204,42 @@ class HubertEncoder:
             return ops.layernorm(h2, L_.ln2_w, L_.ln2_b, eps, out=h2)
         # pre-LN (HubertEncoderLayerStableLayerNorm)
         a_ = ops.layernorm(h, L_.ln1_w, L_.ln1_b, eps)
-        o = self.attention_block(a_, L_)
+        o = self.attention_block(a_, L_, lens)
         h = ops.linear(o, L_.wo, L_.bo, residual=h)
         a_ = ops.layernorm(h, L_.ln2_w, L_.ln2_b, eps)
         f = ops.linear(a_, L_.w1, L_.b1, epilogue=ops.EPI_GELU)
         return ops.linear(f, L_.w2, L_.b2, residual=h)
 
     @torch.no_grad()
-    def forward(self, wav: torch.Tensor, n_layers: int | None = None) -> torch.Tensor:
+    def forward(self, wav: torch.Tensor, n_layers: int | None = None, lengths=None) -> torch.Tensor:
+        """wav [B, N] -> units [B, L, C].  ``lengths`` (optional, host ints [B]): samples per row of a
+        variable-length batch (rows zero-padded to N); row b's units are valid for frame_lengths(lengths[b])
+        frames and equal what that utterance gives alone."""
         a = self.arch
         x = wav.float().contiguous()
         if x.dim() == 1:
             x = x[None]
+        B, N = x.shape
+        if lengths is not None and all(int(n) == N for n in lengths):
+            lengths = None
+        ns = lens0 = lensL = None
+        if lengths is not None:
+            ns = dev_lengths(lengths, x.device)
+            lens0 = dev_lengths([(int(n) + 2 * a.wav_pad - a.conv_kernel[0]) // a.conv_stride[0] + 1
+                                 for n in lengths], x.device)
+            lensL = dev_lengths([self.frame_lengths(int(n)) for n in lengths], x.device)
         if a.do_normalize:
-            x = ops.wav_normalize(x, 1e-7)
+            x = ops.wav_normalize(x, 1e-7, lens=ns)
         if a.wav_pad:
             x = ops.pad_rows(x, a.wav_pad, x.shape[1] + 2 * a.wav_pad)
-        feats = self.feature_extractor(x)
+        feats = self.feature_extractor(x, lens0)
         fln = ops.layernorm(feats, self.fp_ln[0], self.fp_ln[1], a.layer_norm_eps)
         h = ops.linear(fln, self.fp_w, self.fp_b)
-        h = self.positional(h)
+        h = self.positional(h, lensL)
         if not a.stable_layer_norm:
             h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
         for L_ in self.layers[:n_layers]:
-            h = self.layer(h, L_)
+            h = self.layer(h, L_, lensL)
         if a.stable_layer_norm:
             h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
         if self.proj is not None:

@@ -134,13 +134,15 @@ _lib.register("hfa_gemm_kernel_name", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_,
                                        _I_, _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _I_], ctypes.c_char_p)
 _lib.register("hfa_gemm_f32", [_I_, _I_, _I_, _P_, _I_, _P_, _I_, _P_, _P_, _I_, _P_, _I_, _I_, _P_])
 _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_,
-                                    _LL_, _I_, _P_])
-_lib.register("hfa_layernorm_f32", [_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _P_])
-_lib.register("hfa_groupnorm_f32", [_I_, _I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_])
+                                    _LL_, _I_, _P_, _P_])
+_lib.register("hfa_layernorm_f32", [_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_])
+_lib.register("hfa_groupnorm_f32", [_I_, _I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_,
+                                    _P_])
 _lib.register("hfa_conv0_workspace_bytes", [_I_, _I_], ctypes.c_longlong)
-_lib.register("hfa_conv0_f32", [_I_, _I_, _P_, _LL_, _P_, _P_, _I_, _P_, _P_, _F_, _P_, _P_, _LL_, _P_])
-_lib.register("hfa_units_gather_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_])
-_lib.register("hfa_wav_normalize_f32", [_I_, _I_, _P_, _LL_, _F_, _P_, _LL_, _P_])
+_lib.register("hfa_conv0_f32", [_I_, _I_, _P_, _LL_, _P_, _P_, _I_, _P_, _P_, _F_, _P_, _P_, _LL_, _P_, _P_])
+_lib.register("hfa_units_gather_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _P_, _P_])
+_lib.register("hfa_mask_rows_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_])
+_lib.register("hfa_wav_normalize_f32", [_I_, _I_, _P_, _LL_, _F_, _P_, _LL_, _P_, _P_])
 _lib.register("hfa_pad_rows_f32", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _LL_, _P_])
 _lib.register("hfa_add_f32", [_LL_, _P_, _P_, _P_, _P_])
 _lib.register("hfa_selftest_erf", [_LL_, _P_, _P_, _P_, _P_])
@@ -242,10 +244,22 @@ def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
     return out
 
 
-def attention(q, k, v, out, *, B, H, L, head_dim, scale, q_bs, q_ld, k_bs, k_ld, v_bs, v_ld, o_bs, o_ld):
+def _lens(lens):
+    """Optional per-row lengths of a variable-length batch: None or an int32 device tensor [B]."""
+    if lens is None:
+        return None
+    _need(lens, torch.int32, "lengths")
+    return lens
+
+
+def attention(q, k, v, out, *, B, H, L, head_dim, scale, q_bs, q_ld, k_bs, k_ld, v_bs, v_ld, o_bs, o_ld,
+              key_len=None):
+    """Flash attention; ``key_len`` [B] int32 (optional): per-row lengths (keys and queries beyond are padding)."""
+    kl = _lens(key_len)
+
     def launch():
         _lib.call("hfa_attention_f32", B, H, L, head_dim, float(scale), _ptr(q), q_bs, q_ld, _ptr(k), k_bs, k_ld,
-                  _ptr(v), v_bs, v_ld, _ptr(out), o_bs, o_ld, _stream(out.device))
+                  _ptr(v), v_bs, v_ld, _ptr(out), o_bs, o_ld, _ptr(kl), _stream(out.device))
     if PROBE is None:
         launch()
     else:                       # QK^T and PV: 2 * 2 * L * L * head_dim per (batch, head)
@@ -253,31 +267,37 @@ def attention(q, k, v, out, *, B, H, L, head_dim, scale, q_bs, q_ld, k_bs, k_ld,
     return out
 
 
-def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None):
+def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None, t_len=None):
+    """Row LayerNorm (+act) over the last dim; with ``t_len`` [B] (x is [B, T, C]) rows t >= t_len[b] -> 0."""
     C = x.shape[-1]
     x2 = x.reshape(-1, C)
     if out is None:
         out = torch.empty_like(x)
     o2 = out.view(-1, C)
     r2 = residual.reshape(-1, C) if residual is not None else None
+    tl = _lens(t_len)
+    T = x.shape[-2] if (tl is not None and x.dim() == 3) else 0
     _lib.call("hfa_layernorm_f32", x2.shape[0], C, _ptr(x2), x2.stride(0), _ptr(r2),
               r2.stride(0) if r2 is not None else 0, _ptr(gamma), _ptr(beta), float(eps), act, _ptr(o2),
-              o2.stride(0), _stream(x.device))
+              o2.stride(0), T, _ptr(tl), _stream(x.device))
     return out
 
 
-def groupnorm(x, G, gamma, beta, eps=1e-5, act=ACT_NONE, out=None):
-    """GroupNorm over channels-last x [B, T, C] (stats over T x C/G per group)."""
+def groupnorm(x, G, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, t_len=None):
+    """GroupNorm over channels-last x [B, T, C] (stats over T x C/G per group; over t_len[b] rows if given,
+    padding rows -> 0)."""
     B, T, C = x.shape
     if out is None:
         out = torch.empty_like(x)
+    tl = _lens(t_len)
     _lib.call("hfa_groupnorm_f32", B, T, C, G, _ptr(x), x.stride(0), x.stride(1), _ptr(gamma), _ptr(beta),
-              float(eps), act, _ptr(out), out.stride(0), out.stride(1), _stream(x.device))
+              float(eps), act, _ptr(out), out.stride(0), out.stride(1), _ptr(tl), _stream(x.device))
     return out
 
 
-def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, workspace=None):
-    """First extractor conv (1->512, k10, s5) -> [B, T0, 512]; GroupNorm+GELU when gamma/beta are given."""
+def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, workspace=None, t0_len=None):
+    """First extractor conv (1->512, k10, s5) -> [B, T0, 512]; GroupNorm+GELU when gamma/beta are given
+    (statistics over t0_len[b] frames if given)."""
     B, N = x.shape
     T0 = (N - 10) // 5 + 1
     if out is None:
@@ -286,9 +306,11 @@ def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, worksp
     if norm and workspace is None:
         nbytes = _lib.lib().hfa_conv0_workspace_bytes(B, N)
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+    tl = _lens(t0_len)
+
     def launch():
         _lib.call("hfa_conv0_f32", B, N, _ptr(x), x.stride(0), _ptr(w0), _ptr(bias), 1 if norm else 0,
-                  _ptr(gamma), _ptr(beta), float(eps), _ptr(workspace), _ptr(out), out.stride(0),
+                  _ptr(gamma), _ptr(beta), float(eps), _ptr(workspace), _ptr(out), out.stride(0), _ptr(tl),
                   _stream(x.device))
     if PROBE is None:
         launch()
@@ -297,20 +319,35 @@ def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, worksp
     return out
 
 
-def units_gather(units, n_frames, T_pad, ratio, out=None):
+def units_gather(units, n_frames, T_pad, ratio, out=None, n_frames_b=None, U_b=None):
     B, U, C = units.shape
     if out is None:
         out = torch.empty((B, T_pad, C), dtype=torch.float32, device=units.device)
+    nf, ub = _lens(n_frames_b), _lens(U_b)
     _lib.call("hfa_units_gather_f32", B, U, C, _ptr(units), units.stride(0), units.stride(1), n_frames, T_pad,
-              float(ratio), _ptr(out), out.stride(0), out.stride(1), _stream(units.device))
+              float(ratio), _ptr(out), out.stride(0), out.stride(1), _ptr(nf), _ptr(ub), _stream(units.device))
     return out
 
 
-def wav_normalize(x, eps=1e-7, out=None):
+def mask_rows(x, lens):
+    """Zero rows t >= lens[b] of x [B, T, C] (or [B, N] as C = 1), in place."""
+    ln = _lens(lens)
+    if x.dim() == 2:
+        B, T = x.shape
+        C, ld = 1, 1
+    else:
+        B, T, C = x.shape
+        ld = x.stride(1)
+    _lib.call("hfa_mask_rows_f32", B, T, C, _ptr(x), x.stride(0), ld, _ptr(ln), _stream(x.device))
+    return x
+
+
+def wav_normalize(x, eps=1e-7, out=None, lens=None):
     B, N = x.shape
     if out is None:
         out = torch.empty_like(x)
-    _lib.call("hfa_wav_normalize_f32", B, N, _ptr(x), x.stride(0), float(eps), _ptr(out), out.stride(0),
+    ln = _lens(lens)
+    _lib.call("hfa_wav_normalize_f32", B, N, _ptr(x), x.stride(0), float(eps), _ptr(out), out.stride(0), _ptr(ln),
               _stream(x.device))
     return out
 

@@ -10,14 +10,17 @@ UNet+head, lattice prologue, DP, backtrack), the path the benchmark and the batc
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import torch
 import yaml
 
-from . import synth
+from . import ops, synth
 from .alignment_decoder import AlignmentDecoder
 from .encoder import UnitsEncoder
 from .resample import Resampler
+from .hubert import dev_lengths
 from .unet import LatticeHead
 from .wav_io import load_wav
 
@@ -94,37 +97,54 @@ class ForcedAlignmentTask:
         return self._upsamplers[sr]
 
     @torch.no_grad()
-    def encode_batch(self, waves: torch.Tensor, wav_sr: int | None = None):
-        """Device half 1 (current stream): waves [B, N] -> (features [B, T_pad, C], DP frame count, wav lengths)."""
+    def encode_batch(self, waves: torch.Tensor, wav_sr: int | None = None, lengths=None):
+        """Device half 1 (current stream): waves [B, N] -> (features [B, T_pad, C], DP frames, wav lengths).
+
+        ``lengths`` (optional host ints [B]): samples per row of a variable-length batch, rows zero-padded to N
+        at ``wav_sr``; then DP frames is a per-row list and every row aligns exactly as it would alone."""
         self.on_predict_start()
         sr = self.melspec_config["sample_rate"]
         hop = self.melspec_config["hop_length"]
         waves = waves.to(self.device).float()
+        if lengths is not None and all(int(n) == waves.shape[-1] for n in lengths):
+            lengths = None
         if wav_sr is not None and wav_sr != sr:
-            waves = self.upsampler(wav_sr)(waves)
+            up = self.upsampler(wav_sr)
+            waves = up(waves)
+            if lengths is not None:
+                g = math.gcd(int(wav_sr), int(sr))
+                lengths = [-(-(sr // g) * int(n) // (int(wav_sr) // g)) for n in lengths]
+                waves = waves.contiguous()
+                ops.mask_rows(waves, dev_lengths(lengths, waves.device))   # sinc tails past each row's end
         n = waves.shape[-1]
-        feats, n_frames = self.unitsEncoder.encode_frames(waves, sr, hop, pad_to=self.head.divisible)
-        return feats, n_frames, [n / sr] * waves.shape[0]
+        feats, n_frames = self.unitsEncoder.encode_frames(waves, sr, hop, pad_to=self.head.divisible,
+                                                          lengths=lengths)
+        wl = [n / sr] * waves.shape[0] if lengths is None else [int(m) / sr for m in lengths]
+        return feats, n_frames, wl
 
     def decode_device(self, feats, n_frames, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
         """Device half 2 (current stream): UNet head + lattice + Viterbi -> the decoder's device outputs."""
-        logits = self.head.logits(feats)[:, :n_frames]
+        if isinstance(n_frames, (list, tuple)):          # variable-length batch
+            t_pad = [self.head.padded_len(int(t)) for t in n_frames]
+            logits = self.head.logits(feats, t_pad)[:, :max(n_frames)]
+        else:
+            logits = self.head.logits(feats)[:, :n_frames]
         frame, edge = logits[:, :, 2:], logits[:, :, 0]      # LatticeHead.split without the unused ctc logits
         return self.decoder.decode_batch(frame, edge, wav_lengths, ph_seqs, word_seqs, p2ws, host=False)
 
     def align_batch(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
-                    host: bool = True):
-        """B equal-length waveforms [B, N] (at melspec sample_rate, or ``wav_sr`` to resample first, like
-        load_wav) -> list of decode results (dicts with ph_seq / ph_intervals / word_seq / word_intervals /
-        confidence / raw path)."""
-        feats, n_frames, wl = self.encode_batch(waves, wav_sr)
+                    host: bool = True, lengths=None):
+        """B waveforms [B, N] (at melspec sample_rate, or ``wav_sr`` to resample first, like load_wav) ->
+        list of decode results (dicts with ph_seq / ph_intervals / word_seq / word_intervals / confidence / raw
+        path).  Rows of different lengths: zero-pad to N and pass ``lengths``."""
+        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths)
         dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
         if not host:
             return dev_out
         return self.decoder.assemble(dev_out, ph_seqs, word_seqs, p2ws)
 
     def submit(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
-               on_device=None):
+               on_device=None, lengths=None):
         """Two-stream pipelined device pass; returns the decoder's fetch handle (``decoder.assemble`` completes it).
 
         The encoder runs on the caller's current stream and the head + lattice + Viterbi on a side stream that
@@ -134,7 +154,7 @@ class ForcedAlignmentTask:
         main = torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
-        feats, n_frames, wl = self.encode_batch(waves, wav_sr)
+        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths)
         ready = torch.cuda.Event()
         ready.record(main)
         with torch.cuda.stream(self._side):

@@ -35,18 +35,22 @@ class _Block:
         self.sc = P("shortcut.0.weight") if pre + "shortcut.0.weight" in sd else None
         self.ln = (P("out.0.weight"), P("out.0.bias"))
 
-    def __call__(self, x):
+    def __call__(self, x, lens=None):
+        """lens [B] int32 (variable-length batch): rows >= lens[b] are padding — zeroed on the way in (the k3
+        convs must read zeros there) and excluded from the GroupNorm statistics, zero on the way out."""
         B, T, _ = x.shape
+        if lens is not None:
+            ops.mask_rows(x, lens)
         h = torch.empty((B, T, self.hid), dtype=torch.float32, device=x.device)
         ops.conv_gemm(x, self.w1, h, M=T, N=self.hid, K=3 * self.cin, Zb=B, sAb=T * self.cin, ldx=self.cin, stride=1,
                       pad=1, Cg=self.cin, Tin=T, sCb=T * self.hid, ldc=self.hid)
-        h = ops.groupnorm(h, self.n_groups, self.gn[0], self.gn[1], 1e-5, act=ops.ACT_HARDSWISH, out=h)
+        h = ops.groupnorm(h, self.n_groups, self.gn[0], self.gn[1], 1e-5, act=ops.ACT_HARDSWISH, out=h, t_len=lens)
         sc = x if self.sc is None else ops.linear(x, self.sc)
         y = torch.empty((B, T, self.cout), dtype=torch.float32, device=x.device)
         ops.conv_gemm(h, self.w2, y, M=T, N=self.cout, K=3 * self.hid, Zb=B, sAb=T * self.hid, ldx=self.hid, stride=1,
                       pad=1, Cg=self.hid, Tin=T, R=sc, sRb=T * self.cout, ldr=self.cout, sCb=T * self.cout,
                       ldc=self.cout)
-        return ops.layernorm(y, self.ln[0], self.ln[1], 1e-5, act=ops.ACT_HARDSWISH, out=y)
+        return ops.layernorm(y, self.ln[0], self.ln[1], 1e-5, act=ops.ACT_HARDSWISH, out=y, t_len=lens)
 
 
 class _Down:
@@ -56,7 +60,7 @@ class _Down:
         self.w = w.permute(0, 2, 1).reshape(self.cout, -1).contiguous().to(dev)
         self.b = _t(sd[pre + "conv.bias"]).float().contiguous().to(dev)
 
-    def __call__(self, x):
+    def __call__(self, x, lens=None):
         B, T, _ = x.shape
         assert T % self.f == 0, "T is pre-padded to a multiple of factor**times (unet.py:103-106)"
         To = T // self.f
@@ -75,7 +79,7 @@ class _Up:
         b = _t(sd[pre + "conv.bias"]).float()
         self.b = b.repeat(self.f).contiguous().to(dev)
 
-    def __call__(self, x):
+    def __call__(self, x, lens=None):
         B, T, _ = x.shape
         y = ops.linear(x, self.w, self.b)
         return y.view(B, T * self.f, self.cout)
@@ -107,25 +111,34 @@ class LatticeHead:
         return T if r == 0 else T + self.divisible - r
 
     @staticmethod
-    def _seq(mods, x):
+    def _seq(mods, x, lens=None):
         for m in mods:
-            x = m(x)
+            x = m(x, lens)
         return x
 
     @torch.no_grad()
-    def backbone(self, x: torch.Tensor) -> torch.Tensor:
-        """x [B, T_pad, C_in] with T_pad % factor**times == 0 (zero rows beyond the real T)."""
+    def backbone(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
+        """x [B, T_pad, C_in] with T_pad % factor**times == 0 (zero rows beyond the real T).  ``t_pad`` (optional
+        host ints [B]): each row's own padded length (a multiple of factor**times) in a variable-length batch; the
+        reference runs each utterance alone at that length (unet.py:103-106), so every level masks beyond it."""
+        lv = None
+        if t_pad is not None and any(int(t) != x.shape[1] for t in t_pad):
+            from .hubert import dev_lengths
+            lv = [dev_lengths([int(t) // self.arch.factor ** i for t in t_pad], x.device)
+                  for i in range(self.arch.times + 1)]
+        L = (lambda i: None) if lv is None else (lambda i: lv[i])
         h = [x]
-        for enc in self.encoders:
-            h.append(self._seq(enc, h[-1]))
-        y = self._seq(self.bottleneck, h[-1])
+        for i, enc in enumerate(self.encoders):
+            h.append(self._seq(enc, h[-1], L(i)))
+        bott = self.bottleneck
+        y = bott[2](bott[1](bott[0](h[-1]), L(self.arch.times)))
         for i, dec in enumerate(self.decoders):
-            y = self._seq(dec, ops.add(y, h[-1 - i]))
+            y = self._seq(dec, ops.add(y, h[-1 - i]), L(self.arch.times - 1 - i))
         return y
 
     @torch.no_grad()
-    def logits(self, x: torch.Tensor) -> torch.Tensor:
-        return ops.linear(self.backbone(x), self.head_w, self.head_b)
+    def logits(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
+        return ops.linear(self.backbone(x, t_pad), self.head_w, self.head_b)
 
     @staticmethod
     def split(logits: torch.Tensor):

@@ -9,6 +9,11 @@
  *     call can be captured into a hipGraph.
  *   - plain pointers and sizes only (no torch types); layouts are row-major with the strides named.
  *
+ *   - variable-length batches: the optional `const int32_t*` length arrays ([B], device) give each row's own
+ *     length; statistics (GroupNorm, conv0's GroupNorm, wave normalisation) and attention keys cover that
+ *     length only, and padding rows come out as zeros (or don't-care where stated), so every utterance gets
+ *     the result it would get alone — the reference runs one utterance at a time.  NULL = all rows full.
+ *
  * Each entry cites the reference interface it replaces (paths relative to the HubertFA repository).
  */
 #ifndef HFA_H_
@@ -95,7 +100,7 @@ int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, i
  * modeling_hubert.py HubertAttention (eager_attention_forward). */
 int hfa_attention_f32(int B, int H, int L, int head_dim, float scale, const float* q, long long q_bs, int q_ld,
                       const float* k, long long k_bs, int k_ld, const float* v, long long v_bs, int v_ld, float* o,
-                      long long o_bs, int o_ld, hipStream_t stream);
+                      long long o_bs, int o_ld, const int32_t* key_len, hipStream_t stream);
 
 /* ---- normalisation (hubertfa_amd/csrc/norm.hip); act: 0 none, 1 erf-GELU, 2 Hardswish -----------------------
  * y = act(LayerNorm(x (+ res)) * gamma + beta) over rows of C <= 4096 (C % 4 == 0).
@@ -103,12 +108,13 @@ int hfa_attention_f32(int B, int H, int L, int head_dim, float scale, const floa
  * transformers HubertFeatureProjection/HubertEncoder(*StableLayerNorm)/HubertLayerNormConvLayer,
  * networks/layer/block/resnet_block.py:170-173 (LN + Hardswish). */
 int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const float* res, long long ldr,
-                      const float* gamma, const float* beta, float eps, int act, float* y, long long ldy,
-                      hipStream_t stream);
+                      const float* gamma, const float* beta, float eps, int act, float* y, long long ldy, int T,
+                      const int32_t* t_len, hipStream_t stream);
 /* GroupNorm(G, C) over a channels-last [B, T, C] tensor (+act).  Replaces resnet_block.py:153-154
  * (nn.GroupNorm(16, C) + nn.Hardswish). */
 int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,
-                      const float* beta, float eps, int act, float* y, long long y_bs, int ldy, hipStream_t stream);
+                      const float* beta, float eps, int act, float* y, long long y_bs, int ldy, const int32_t* t_len,
+                      hipStream_t stream);
 
 /* ---- extractor conv0 (hubertfa_amd/csrc/conv.hip) ------------------------------------------------------------
  * x [B, N] -> y [B, T0, 512] channels-last, T0 = (N-10)/5+1.  norm=1: GroupNorm(512,512) + GELU
@@ -117,16 +123,21 @@ int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs
 long long hfa_conv0_workspace_bytes(int B, int N);
 int hfa_conv0_f32(int B, int N, const float* x, long long x_bs, const float* w0, const float* bias, int norm,
                   const float* gamma, const float* beta, float eps, void* workspace, float* y, long long y_bs,
-                  hipStream_t stream);
+                  const int32_t* t0_len, hipStream_t stream);
 
 /* ---- glue (hubertfa_amd/csrc/misc.hip) -----------------------------------------------------------------------
  * Nearest-frame gather onto the DP grid, tools/encoder.py:56-59: idx[k] = min(rint(f32(ratio)*k), U-1),
  * out[b,k,:] = units[b,idx[k],:] for k < n_frames, zero rows up to T_pad (unet.py:103-106 padding). */
 int hfa_units_gather_f32(int B, int U, int C, const float* units, long long u_bs, int u_ld, int n_frames, int T_pad,
-                         float ratio, float* out, long long o_bs, int o_ld, hipStream_t stream);
+                         float ratio, float* out, long long o_bs, int o_ld, const int32_t* n_frames_b,
+                         const int32_t* U_b, hipStream_t stream);
 /* Wav2Vec2FeatureExtractor zero-mean/unit-variance normalisation (tools/encoder.py:94-95). */
 int hfa_wav_normalize_f32(int B, int N, const float* x, long long x_bs, float eps, float* y, long long y_bs,
-                          hipStream_t stream);
+                          const int32_t* lens, hipStream_t stream);
+/* Zero rows t >= lens[b] of a [B, T, C] tensor (row t of batch b at x + b*x_bs + t*ldx): the padding rows of a
+ * variable-length batch, which padded convs must read as zeros (reference: each utterance runs alone, B=1). */
+int hfa_mask_rows_f32(int B, int T, int C, float* x, long long x_bs, int ldx, const int32_t* lens,
+                      hipStream_t stream);
 /* Zero padding of rows (networks/hubert/model.py:77 F.pad 40/40; resampler edge padding). */
 int hfa_pad_rows_f32(int B, int N, const float* x, long long x_bs, int left, int N_out, float* y, long long y_bs,
                      hipStream_t stream);

@@ -3,7 +3,8 @@
     python infer.py -c model.ckpt -f segments [-g Dictionary] [-d dictionary/opencpop-extension.txt] [-sc]
 
 Same flags and defaults as the reference; extra flags: ``--hubert_path`` (override hubert_config.model_path, e.g.
-``synth:0``), ``--batch_size`` (utterances of identical length are aligned together), ``--out_path``.
+``synth:0``), ``--batch_size`` (utterances per GPU batch: sorted by length, zero-padded, aligned with per-row
+lengths so every result equals the one-utterance run), ``--out_path``.
 Launched under ``torchrun --nproc-per-node N`` it shards the wav files across ranks by estimated cost (LPT);
 rank 0 gathers the per-utterance results and writes the TextGrids / confidence.csv.
 """
@@ -16,41 +17,62 @@ import click
 
 
 def _predict(task, dataset, batch_size: int):
+    import numpy as np
     import torch
     from hubertfa_amd.wav_io import read_wav
 
+    task.on_predict_start()
     sr = task.melspec_config["sample_rate"]
     items = []
     for wav_path, ph_seq, word_seq, p2w in dataset:
         x, file_sr = read_wav(wav_path)
         items.append((wav_path, x[0], file_sr, ph_seq, word_seq, p2w))
-    # bucket identical (length, rate) so GroupNorm/attention statistics stay per-utterance exact
-    buckets = {}
+    # variable-length batches: per sample rate, sorted by length (little padding), rows zero-padded and aligned
+    # with per-row lengths, which keeps every utterance's result identical to aligning it alone (the reference's
+    # B=1); utterances too short for the encoder's 400-sample window take the reference's padding quirk alone
+    by_sr = {}
     for it in items:
-        buckets.setdefault((len(it[1]), it[2]), []).append(it)
+        by_sr.setdefault(it[2], []).append(it)
     out = {}
 
     def finish(job):
-        handle, chunk, n44 = job
+        handle, chunk, n44s = job
         res = task.decoder.assemble(handle, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk])
-        for c, r in zip(chunk, res):
+        for c, r, n44 in zip(chunk, res, n44s):
             out[str(c[0])] = (c[0], n44 / sr, r["confidence"], r["ph_seq"], r["ph_intervals"], r["word_seq"],
                               r["word_intervals"])
+
+    def batches():
+        for file_sr, group in by_sr.items():
+            group = sorted(group, key=lambda c: len(c[1]))
+            enc_len = task.unitsEncoder.resampled_lengths([len(c[1]) for c in group], file_sr) if group else []
+            if file_sr != sr:   # lengths at the encoder rate go through 44.1 kHz first (load_wav)
+                g = math.gcd(sr, file_sr)
+                n44 = [-(-(sr // g) * len(c[1]) // (file_sr // g)) for c in group]
+                enc_len = task.unitsEncoder.resampled_lengths(n44, sr)
+            short = [c for c, e in zip(group, enc_len) if e < 400]
+            rest = [c for c, e in zip(group, enc_len) if e >= 400]
+            for c in short:
+                yield file_sr, [c]
+            for i in range(0, len(rest), batch_size):
+                yield file_sr, rest[i:i + batch_size]
 
     # one batch in flight: the host assembles batch i while the GPU runs batch i+1 (task.submit: encoder on the
     # main stream, head + Viterbi on a side stream)
     pending = None
-    for (_, file_sr), group in buckets.items():
-        for i in range(0, len(group), batch_size):
-            chunk = group[i:i + batch_size]
-            wav = torch.from_numpy(__import__("numpy").stack([c[1] for c in chunk])).to(task.device)
-            handle = task.submit(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
-                                 wav_sr=file_sr)
-            g = math.gcd(sr, file_sr)
-            n44 = math.ceil((sr // g) * wav.shape[-1] / (file_sr // g)) if file_sr != sr else wav.shape[-1]
-            if pending is not None:
-                finish(pending)
-            pending = (handle, chunk, n44)
+    for file_sr, chunk in batches():
+        lens = [len(c[1]) for c in chunk]
+        wav_np = np.zeros((len(chunk), max(lens)), np.float32)
+        for r, c in enumerate(chunk):
+            wav_np[r, :lens[r]] = c[1]
+        wav = torch.from_numpy(wav_np).to(task.device)
+        handle = task.submit(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
+                             wav_sr=file_sr, lengths=lens if len(chunk) > 1 else None)
+        g = math.gcd(sr, file_sr)
+        n44s = [math.ceil((sr // g) * n / (file_sr // g)) if file_sr != sr else n for n in lens]
+        if pending is not None:
+            finish(pending)
+        pending = (handle, chunk, n44s)
     if pending is not None:
         finish(pending)
     return [out[str(it[0])] for it in items if str(it[0]) in out]
@@ -64,7 +86,7 @@ def _predict(task, dataset, batch_size: int):
 @click.option("--dictionary", "-d", default="dictionary/opencpop-extension.txt", type=str,
               help="(only used when --g2p=='Dictionary') path to the dictionary")
 @click.option("--hubert_path", default=None, type=str, help="override hubert_config.model_path")
-@click.option("--batch_size", default=32, type=int, help="max utterances per GPU batch (equal lengths only)")
+@click.option("--batch_size", default=32, type=int, help="max utterances per GPU batch (variable lengths; results equal B=1)")
 @click.option("--out_path", default=None, type=str, help="write TextGrids under this folder instead")
 def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, **kwargs):
     import os
