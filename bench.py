@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--probe", default="auto",
                     help="kernel instantiation to time; auto = the one carrying the most FLOPs in a warmup census")
     ap.add_argument("--serial", action="store_true", help="one stream per step (no head/encoder overlap)")
+    ap.add_argument("--chunk-seconds", type=float, default=None,
+                    help="long-form: encode overlapping windows of this length (config 5 chunked; B=1 only)")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -122,7 +124,7 @@ def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s, encoder="cnhuber
 def config_name(encoder: str, world: int, B: int, seconds: float = 10.0) -> str:
     """Which BASELINE.json config this run's geometry is (configs[1..4]); weak scaling keeps B per GPU fixed."""
     if seconds >= 60:
-        return f"config 5 geometry (long-form, {seconds:g} s unchunked, {B} per GPU)"
+        return f"config 5 geometry (long-form, {seconds:g} s, {B} per GPU)"
     if encoder == "large":
         return "config 4 geometry" + ("" if world * B == 256 else f" (global batch {world * B}, config 4 is 256)")
     if world == 1:
@@ -194,12 +196,13 @@ def main():
         """GPU half of one step (+ the boundary gather) and the async D2H of its results: the encoder on the main
         stream, head + DP on a side stream overlapping the next step's encoder (task.submit)."""
         if args.serial:
-            dev_out = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False)
+            dev_out = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False,
+                                       chunk_seconds=args.chunk_seconds)
             if world > 1:
                 gather_boundaries(dev_out)
             return task.decoder.fetch(dev_out)
         return task.submit(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000,
-                           on_device=gather_boundaries if world > 1 else None)
+                           on_device=gather_boundaries if world > 1 else None, chunk_seconds=args.chunk_seconds)
 
     def finish(handle):
         return task.decoder.assemble(handle, ph_seqs, word_seqs, p2ws)
@@ -265,7 +268,8 @@ def main():
         "metric": METRIC, "value": value, "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"{config_name(args.encoder, world, B, args.seconds)}: "
+        "config": {"workload": f"{config_name(args.encoder, world, B, args.seconds)}"
+                               f"{'' if args.chunk_seconds is None else f', chunked {args.chunk_seconds:g} s windows'}: "
                                f"B={B} x {args.seconds:g} s 16 kHz utterances per GPU, "
                                f"{ {'base': 'Hubert-base (cnhubert arch)', 'large': 'Hubert-large (cnhubert-large arch)', 'soft': 'HubertSoft'}[args.encoder]}"
                                f" + UNet head + Viterbi; full infer path wave(HBM)->boundaries(host), host assembly "
@@ -285,8 +289,8 @@ def main():
     ops.PROBE = iso
     for _ in range(2):
         torch.cuda.synchronize()
-        task.decoder.assemble(task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False),
-                              ph_seqs, word_seqs, p2ws)
+        task.decoder.assemble(task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False,
+                                               chunk_seconds=args.chunk_seconds), ph_seqs, word_seqs, p2ws)
     torch.cuda.synchronize()
     ops.PROBE = None
     out["secondary"] = secondary_rooflines(iso, probe, n_frames, len(ph_seqs[0]))

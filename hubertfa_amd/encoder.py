@@ -18,6 +18,7 @@ import json
 import math
 import os
 
+import numpy as np
 import torch
 
 from . import ops, synth
@@ -130,12 +131,55 @@ class UnitsEncoder:
         return self.model(audio_res, lengths=lens16)
 
     @torch.no_grad()
-    def encode_frames(self, audio: torch.Tensor, sample_rate: int, hop_size: int, pad_to: int = 1, lengths=None):
+    def units_chunked(self, audio: torch.Tensor, chunk_frames: int, overlap_frames: int) -> torch.Tensor:
+        """Long-form units of ONE utterance [1, N] at the encoder rate from overlapping windows (BASELINE config 5).
+
+        Window k covers global Hubert frames [kC - O, (k+1)C + O) (C = chunk_frames, O = overlap_frames, clipped
+        to [0, L)); frame j of the utterance covers samples [320 j - pad, 320 j + 400 - pad) (pad = the layout's
+        wave padding), so a window is the sample span of its frames and yields exactly its frame count.  All
+        windows run as ONE variable-length batch (every GEMM and attention launch covers all of them) and the
+        core frames [kC, (k+1)C) of each are stitched back in order.  Attention then costs O(L (C + 2O)) instead of
+        O(L^2); the price is context: each frame sees its window only, and conv0's GroupNorm statistics are per
+        window.  The reference has no chunking — the unchunked path stays the parity anchor."""
+        m = self.model
+        hop, rf, pad = 320, 400, m.arch.wav_pad
+        x = audio.to(self.device).float().reshape(1, -1)
+        N = x.shape[-1]
+        L = m.frame_lengths(N)
+        C, O = int(chunk_frames), int(overlap_frames)
+        if L <= C + O:
+            return m(x.contiguous())
+        wins = []
+        for k in range(-(-L // C)):
+            a, b = max(0, k * C - O), min(L, (k + 1) * C + O)
+            wins.append((k * C, min(L, (k + 1) * C), a, b))
+        n_win = [hop * (b - a - 1) + rf - 2 * pad for _, _, a, b in wins]
+        xs = x[0]
+        batch = torch.zeros((len(wins), max(n_win)), dtype=torch.float32, device=x.device)
+        for i, (_, _, a, b) in enumerate(wins):
+            s0 = hop * a - pad
+            lo, hi = max(0, s0), min(N, s0 + n_win[i])
+            if hi > lo:
+                batch[i, lo - s0:hi - s0] = xs[lo:hi]
+        units = m(batch, lengths=n_win)                   # [K, Wmax, C]
+        idx = np.concatenate([i * units.shape[1] + np.arange(c0 - a, c1 - a) for i, (c0, c1, a, _) in
+                              enumerate(wins)])
+        flat = units.reshape(-1, units.shape[-1])
+        take = torch.from_numpy(idx.astype(np.int64)).pin_memory().to(x.device, non_blocking=True)
+        return flat.index_select(0, take)[None]
+
+    @torch.no_grad()
+    def encode_frames(self, audio: torch.Tensor, sample_rate: int, hop_size: int, pad_to: int = 1, lengths=None,
+                      chunk_frames: int | None = None, overlap_frames: int = 100):
         """[B, N] -> (features [B, T_pad, C] channels-last, n_frames); rows >= n_frames are zero.
 
         With ``lengths`` (per-row sample counts of a zero-padded batch) n_frames is a list (one per row) and
         rows >= n_frames[b] of row b are zero; T_pad covers the longest row."""
-        units = self.units(audio, sample_rate, lengths)
+        if chunk_frames is not None and lengths is None and audio.shape[0] == 1:
+            audio_res = self._resample(audio.to(self.device).float(), sample_rate)
+            units = self.units_chunked(audio_res.contiguous(), chunk_frames, overlap_frames)
+        else:
+            units = self.units(audio, sample_rate, lengths)
         if lengths is None:
             n_frames, ratio = self.grid(audio.shape[-1], sample_rate, hop_size)
             T_pad = (n_frames + pad_to - 1) // pad_to * pad_to

@@ -97,11 +97,14 @@ class ForcedAlignmentTask:
         return self._upsamplers[sr]
 
     @torch.no_grad()
-    def encode_batch(self, waves: torch.Tensor, wav_sr: int | None = None, lengths=None):
+    def encode_batch(self, waves: torch.Tensor, wav_sr: int | None = None, lengths=None,
+                     chunk_seconds: float | None = None):
         """Device half 1 (current stream): waves [B, N] -> (features [B, T_pad, C], DP frames, wav lengths).
 
         ``lengths`` (optional host ints [B]): samples per row of a variable-length batch, rows zero-padded to N
-        at ``wav_sr``; then DP frames is a per-row list and every row aligns exactly as it would alone."""
+        at ``wav_sr``; then DP frames is a per-row list and every row aligns exactly as it would alone.
+        ``chunk_seconds`` (one long utterance): encode overlapping windows of that length as one batch
+        (UnitsEncoder.units_chunked) — long-form speed at the cost of per-window attention context."""
         self.on_predict_start()
         sr = self.melspec_config["sample_rate"]
         hop = self.melspec_config["hop_length"]
@@ -117,8 +120,9 @@ class ForcedAlignmentTask:
                 waves = waves.contiguous()
                 ops.mask_rows(waves, dev_lengths(lengths, waves.device))   # sinc tails past each row's end
         n = waves.shape[-1]
+        chunk = None if chunk_seconds is None else max(1, int(round(chunk_seconds * 50)))
         feats, n_frames = self.unitsEncoder.encode_frames(waves, sr, hop, pad_to=self.head.divisible,
-                                                          lengths=lengths)
+                                                          lengths=lengths, chunk_frames=chunk)
         wl = [n / sr] * waves.shape[0] if lengths is None else [int(m) / sr for m in lengths]
         return feats, n_frames, wl
 
@@ -133,18 +137,18 @@ class ForcedAlignmentTask:
         return self.decoder.decode_batch(frame, edge, wav_lengths, ph_seqs, word_seqs, p2ws, host=False)
 
     def align_batch(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
-                    host: bool = True, lengths=None):
+                    host: bool = True, lengths=None, chunk_seconds: float | None = None):
         """B waveforms [B, N] (at melspec sample_rate, or ``wav_sr`` to resample first, like load_wav) ->
         list of decode results (dicts with ph_seq / ph_intervals / word_seq / word_intervals / confidence / raw
         path).  Rows of different lengths: zero-pad to N and pass ``lengths``."""
-        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths)
+        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds)
         dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
         if not host:
             return dev_out
         return self.decoder.assemble(dev_out, ph_seqs, word_seqs, p2ws)
 
     def submit(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
-               on_device=None, lengths=None):
+               on_device=None, lengths=None, chunk_seconds: float | None = None):
         """Two-stream pipelined device pass; returns the decoder's fetch handle (``decoder.assemble`` completes it).
 
         The encoder runs on the caller's current stream and the head + lattice + Viterbi on a side stream that
@@ -154,7 +158,7 @@ class ForcedAlignmentTask:
         main = torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
-        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths)
+        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds)
         ready = torch.cuda.Event()
         ready.record(main)
         with torch.cuda.stream(self._side):

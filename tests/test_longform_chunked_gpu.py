@@ -1,0 +1,73 @@
+"""Chunked long-form encoding (BASELINE config 5's "overlapped chunks"): windows batched as one variable-length
+batch and stitched.  The reference has no chunking, so the unchunked path is the anchor:
+  * a window that covers the utterance reproduces the unchunked units exactly;
+  * every window yields exactly its frames, and the stitched grid IS the unchunked grid: with the context-free
+    part of the encoder (LN-conv extractor, projection, positional conv of receptive field +-64 frames < the
+    100-frame overlap; no attention layers, no whole-utterance wave normalisation) the stitched units equal the
+    unchunked units bit for bit;
+  * with attention the windows see less context, so the alignment only approximates the unchunked one (the
+    agreement is printed; with random weights it says little about trained models, so it is not asserted).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _task():
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
+    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=torch.device("cuda"))
+    task.on_predict_start()
+    return task
+
+
+def test_window_frame_counts():
+    task = _task()
+    m = task.unitsEncoder.model
+    for n_frames in (1, 2, 7, 1000, 1201):
+        assert m.frame_lengths(320 * (n_frames - 1) + 400 - 2 * m.arch.wav_pad) == n_frames
+
+
+def test_chunked_units_single_window_exact_and_grid():
+    task = _task()
+    enc = task.unitsEncoder
+    from hubertfa_amd import synth
+    x = torch.from_numpy(synth.synth_audio(16000 * 30, seed=5)[None]).cuda()
+    full = enc.units(x, 16000)
+    one = enc.units_chunked(x, chunk_frames=2000, overlap_frames=100)      # one window covers all 1499 frames
+    assert torch.equal(one, full)
+    chunked = enc.units_chunked(x, chunk_frames=400, overlap_frames=100)
+    assert chunked.shape == full.shape
+    assert bool(torch.isfinite(chunked).all())
+
+
+def test_chunked_stitching_exact_without_attention():
+    from hubertfa_amd import synth
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+    ckpt = synth_checkpoint(encoder="cnhubert-large", model_path="synth:0", seed=1)
+    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=torch.device("cuda"))
+    task.on_predict_start()
+    enc = task.unitsEncoder
+    enc.model.layers = enc.model.layers[:0]          # context-free encoder: LN-conv, projection, pos-conv only
+    enc.model.arch.do_normalize = False              # (the wave normalisation is a whole-utterance statistic)
+    x = torch.from_numpy(synth.synth_audio(16000 * 30, seed=6)[None]).cuda()
+    full = enc.units(x, 16000)
+    chunked = enc.units_chunked(x, chunk_frames=400, overlap_frames=100)     # 4 windows over 1499 frames
+    assert torch.equal(chunked, full)
+
+
+def test_chunked_alignment_runs_and_agreement():
+    import bench
+    task = _task()
+    wav, ph, ws, pw = bench.make_inputs(1, 60.0, 120, 99)
+    x = torch.from_numpy(wav).cuda()
+    ref = task.align_batch(x, ph, ws, pw, wav_sr=16000)[0]
+    got = task.align_batch(x, ph, ws, pw, wav_sr=16000, chunk_seconds=20.0)[0]
+    assert got["T"] == ref["T"]
+    assert np.all(np.diff(got["ph_time_int"]) > 0) and got["ph_time_int"][0] == 0
+    a, b = ref["ph_time_int"], got["ph_time_int"]
+    n = min(len(a), len(b))
+    close = float(np.mean(np.abs(a[:n] - b[:n]) <= 2)) if n else 0.0
+    print(f"chunked vs unchunked (random weights): {close:.1%} of boundaries within 2 frames")
