@@ -26,6 +26,7 @@ _SIGS = {
     "hfa_viterbi_forward": [I, I, I, P, P, P, P, P, P, P, P, P, P, P],
     "hfa_viterbi_backtrack": [I, I, I, P, P, P, P, P, P, P, P, P, P],
     "hfa_lattice_prologue": [I, I, I, I, P, P, P, LL, LL, P, LL, LL, P, P, P, P, P, P, P, P, P],
+    "hfa_viterbi_tuning": [I],
 }
 _RESTYPE = {"hfa_last_error": ctypes.c_char_p, "hfa_build_arch": ctypes.c_char_p}
 

@@ -133,6 +133,70 @@ __global__ __launch_bounds__(256) void groupnorm_kernel(int T, int C, int G, con
     }
 }
 
+// Long sequences with few (batch, group) pairs (a 5-minute utterance: B = 1, 16 groups) would leave the chip
+// idle with one workgroup per pair: split T into P parts.  Pass 1 writes per-part f64 partial sums, pass 2
+// reduces the P partials of its pair (P <= 64, same order in every block) and applies its part.
+__global__ __launch_bounds__(256) void groupnorm_partial_kernel(int T, int C, int G, int P,
+                                                                const float* __restrict__ x, long long x_bs,
+                                                                int ldx, const int32_t* __restrict__ t_len,
+                                                                double* __restrict__ part) {
+    const int g = blockIdx.x, b = blockIdx.y, pi = blockIdx.z;
+    const int Cg = C / G;
+    const int Tb = t_len ? t_len[b] : T;
+    const int rows = (Tb + P - 1) / P;
+    const int t0 = pi * rows, t1 = min(Tb, t0 + rows);
+    const float* xb = x + b * x_bs + g * Cg;
+    double s = 0.0, ss = 0.0;
+    const int n = max(0, t1 - t0) * Cg;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int t = t0 + i / Cg, c = i % Cg;
+        const double v = xb[(long long)t * ldx + c];
+        s += v;
+        ss += v * v;
+    }
+    __shared__ double red[2][4];
+    s = hfa::wave_sum_d(s);
+    ss = hfa::wave_sum_d(ss);
+    if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = s; red[1][threadIdx.x >> 6] = ss; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double* pp = part + (((size_t)b * G + g) * P + pi) * 2;
+        pp[0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        pp[1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    }
+}
+
+__global__ __launch_bounds__(256) void groupnorm_apply_kernel(int T, int C, int G, int P, const float* __restrict__ x,
+                                                              long long x_bs, int ldx, const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float eps, int act,
+                                                              float* __restrict__ y, long long y_bs, int ldy,
+                                                              const int32_t* __restrict__ t_len,
+                                                              const double* __restrict__ part) {
+    const int g = blockIdx.x, b = blockIdx.y, pi = blockIdx.z;
+    const int Cg = C / G;
+    const int Tb = t_len ? t_len[b] : T;
+    const double* pp = part + ((size_t)b * G + g) * P * 2;
+    double S = 0.0, SS = 0.0;
+    for (int k = 0; k < P; ++k) { S += pp[2 * k]; SS += pp[2 * k + 1]; }
+    const long long n = (long long)Tb * Cg;
+    const double mean_d = n > 0 ? S / n : 0.0;
+    double var_d = n > 0 ? SS / n - mean_d * mean_d : 0.0;
+    if (var_d < 0) var_d = 0;
+    const float mean = (float)mean_d;
+    const float rstd = (float)(1.0 / sqrt(var_d + (double)eps));
+    const int rows = (T + P - 1) / P;                // this block's share of ALL T rows (padding rows -> 0)
+    const int t0 = pi * rows, t1 = min(T, t0 + rows);
+    const float* xb = x + b * x_bs + g * Cg;
+    float* yb = y + b * y_bs + g * Cg;
+    const int m = max(0, t1 - t0) * Cg;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        const int t = t0 + i / Cg, c = i % Cg;
+        float o = 0.0f;
+        if (t < Tb) o = act_apply((xb[(long long)t * ldx + c] - mean) * rstd * gamma[g * Cg + c] + beta[g * Cg + c], act);
+        yb[(long long)t * ldy + c] = o;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -169,9 +233,14 @@ int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const floa
     return hfa::check_launch("hfa_layernorm_f32");
 }
 
+long long hfa_groupnorm_workspace_bytes(int B, int T, int C, int G) {
+    (void)T; (void)C;
+    return (long long)B * G * 64 * 2 * sizeof(double) + 64;
+}
+
 int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,
                       const float* beta, float eps, int act, float* y, long long y_bs, int ldy, const int32_t* t_len,
-                      hipStream_t stream) {
+                      void* workspace, hipStream_t stream) {
     if (B < 0 || T < 0 || C <= 0 || G <= 0 || C % G || act < 0 || act > 2) {
         hfa::set_error("hfa_groupnorm_f32: bad sizes");
         return HFA_EINVAL;
@@ -181,8 +250,24 @@ int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs
         hfa::set_error("hfa_groupnorm_f32: null pointer");
         return HFA_EINVAL;
     }
-    hipLaunchKernelGGL(groupnorm_kernel, dim3(G, B), dim3(256), 0, stream, T, C, G, x, x_bs, ldx, gamma, beta, eps,
-                       act, y, y_bs, ldy, t_len);
+    // split T when the (group, batch) grid alone cannot fill the chip and the rows are long
+    const long long per_pair = (long long)T * (C / G);
+    int P = 1;
+    if (workspace && (long long)B * G < 512 && per_pair > 65536) {
+        P = (int)min(64LL, max(1LL, 1024LL / ((long long)B * G)));
+        P = (int)min((long long)P, max(1LL, per_pair / 16384));
+    }
+    if (P > 1) {
+        double* part = reinterpret_cast<double*>(workspace);
+        // (the apply pass writes y in place of x only after every partial of its pair is complete: separate launch)
+        hipLaunchKernelGGL(groupnorm_partial_kernel, dim3(G, B, P), dim3(256), 0, stream, T, C, G, P, x, x_bs, ldx,
+                           t_len, part);
+        hipLaunchKernelGGL(groupnorm_apply_kernel, dim3(G, B, P), dim3(256), 0, stream, T, C, G, P, x, x_bs, ldx,
+                           gamma, beta, eps, act, y, y_bs, ldy, t_len, part);
+    } else {
+        hipLaunchKernelGGL(groupnorm_kernel, dim3(G, B), dim3(256), 0, stream, T, C, G, x, x_bs, ldx, gamma, beta,
+                           eps, act, y, y_bs, ldy, t_len);
+    }
     return hfa::check_launch("hfa_groupnorm_f32");
 }
 

@@ -232,17 +232,30 @@ __global__ __launch_bounds__(kBtThreads) void viterbi_backtrack_kernel(
             s = S - 2;
         s_cur = s;
     }
-    const int rows_per_chunk = max(1, kBtChunkBytes / Smax);
-    for (int hi = T - 1; hi >= 0; hi -= rows_per_chunk) {
-        const int lo = max(0, hi - rows_per_chunk + 1);
-        const int nbytes = (hi - lo + 1) * Smax;
-        const int8_t* src = bb + (size_t)lo * Smax;
-        for (int i = tid; i < nbytes; i += kBtThreads) chunk[i] = src[i];
+    // The chased state drops by at most 2 per step, so R rows of the chase only touch columns
+    // [s_top - 2R, s_top]: stage that R x (2R+1) window instead of whole rows (long lattices: S = 1801 moves
+    // 29 KB per 120 steps instead of 32 KB per 18).  Short rows (Smax <= 2R+1) stage whole rows as before.
+    int R = kBtChunkBytes / Smax;
+    if (R < 1 || 2 * R + 1 < Smax) {
+        R = 1;
+        while (2 * (R + 1) + 1 <= Smax && (R + 1) * (2 * (R + 1) + 1) <= kBtChunkBytes) ++R;
+    }
+    __syncthreads();
+    for (int hi = T - 1; hi >= 0; hi -= R) {
+        const int lo = max(0, hi - R + 1);
+        const int top = s_cur;
+        const int c0 = max(0, top - 2 * (hi - lo));
+        const int W = min(Smax - c0, 2 * (hi - lo) + 1);
+        const int nbytes = (hi - lo + 1) * W;
+        for (int i = tid; i < nbytes; i += kBtThreads) {
+            const int r = i / W, c = i - r * W;
+            chunk[i] = bb[(size_t)(lo + r) * Smax + c0 + c];
+        }
         __syncthreads();
         if (tid == 0) {
-            int s = s_cur;
+            int s = top;
             for (int t = hi; t >= lo; --t) {
-                const int code = (t == 0) ? -1 : (int)chunk[(t - lo) * Smax + s];
+                const int code = (t == 0) ? -1 : (int)chunk[(t - lo) * W + (s - c0)];
                 const int emit = code != 0;
                 path[t] = (uint16_t)(s | (emit << 15));
                 if (emit) s -= code;
@@ -359,6 +372,8 @@ __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
     }
 }
 
+int g_force_k = 0;   // hfa_viterbi_tuning: states per lane of the multi-wave DP (0 = automatic)
+
 template <int K, int NW, int G>
 int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const int32_t* pad,
                    const float* prob_log, const float* nE, const float* E, double* curr, float* dp, int8_t* bt,
@@ -388,7 +403,8 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
         return HFA_EINVAL;
     }
     if (B == 0 || Tmax == 0 || Smax == 0) return HFA_OK;
-    // one wave while a lane holds <= 8 states; beyond that 8 states per lane over up to 16 waves
+    // one wave while a lane holds <= 8 states; beyond that K states per lane over up to 16 waves (K = 8 by
+    // default, or forced to 2/4 by hfa_viterbi_tuning: more waves, fewer states each, one barrier per step)
 #define HFA_FWD(K, NW, G)                                                                                       \
     return launch_forward<K, NW, G>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log, edge_log, curr, \
                                     dp, bt, ph_seq_id, stream)
@@ -396,7 +412,25 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
     if (per_lane <= 1) HFA_FWD(1, 1, 8);
     if (per_lane <= 2) HFA_FWD(2, 1, 8);
     if (per_lane <= 4) HFA_FWD(4, 1, 8);
-    if (per_lane <= 8) HFA_FWD(8, 1, 4);
+    if (per_lane <= 8 && g_force_k == 0) HFA_FWD(8, 1, 4);
+    // measured (scripts/dp_bench.py, T = 25 839, S = 1 801): 2 states per lane over 16 waves 0.76 us/step,
+    // 4 over 8 0.78, 8 over 4 1.08 — the per-step critical path (VALU chain of one lane's K states) wins over
+    // the extra barrier participants
+    const int kk = g_force_k ? g_force_k : (Smax <= 2048 ? 2 : (Smax <= 4096 ? 4 : 8));
+    if (kk == 2 && Smax <= 2048) {
+        const int w = (Smax + 127) / 128;
+        if (w <= 2) HFA_FWD(2, 2, 8);
+        if (w <= 4) HFA_FWD(2, 4, 8);
+        if (w <= 8) HFA_FWD(2, 8, 8);
+        HFA_FWD(2, 16, 8);
+    }
+    if (kk == 4 && Smax <= 4096) {
+        const int w = (Smax + 255) / 256;
+        if (w <= 2) HFA_FWD(4, 2, 4);
+        if (w <= 4) HFA_FWD(4, 4, 4);
+        if (w <= 8) HFA_FWD(4, 8, 4);
+        HFA_FWD(4, 16, 4);
+    }
     const int waves = (Smax + 511) / 512;
     if (waves <= 2) HFA_FWD(8, 2, 4);
     if (waves <= 4) HFA_FWD(8, 4, 4);
@@ -405,6 +439,11 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
 #undef HFA_FWD
     hfa::set_error("hfa_viterbi_forward: Smax=%d exceeds 8192 states per utterance", Smax);
     return HFA_EINVAL;
+}
+
+int hfa_viterbi_tuning(int force_k) {
+    g_force_k = (force_k == 2 || force_k == 4 || force_k == 8) ? force_k : 0;
+    return HFA_OK;
 }
 
 int hfa_viterbi_backtrack(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const float* dp,

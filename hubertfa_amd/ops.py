@@ -137,7 +137,8 @@ _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_
                                     _LL_, _I_, _P_, _P_])
 _lib.register("hfa_layernorm_f32", [_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_])
 _lib.register("hfa_groupnorm_f32", [_I_, _I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_,
-                                    _P_])
+                                    _P_, _P_])
+_lib.register("hfa_groupnorm_workspace_bytes", [_I_, _I_, _I_, _I_], ctypes.c_longlong)
 _lib.register("hfa_conv0_workspace_bytes", [_I_, _I_], ctypes.c_longlong)
 _lib.register("hfa_conv0_f32", [_I_, _I_, _P_, _LL_, _P_, _P_, _I_, _P_, _P_, _F_, _P_, _P_, _LL_, _P_, _P_])
 _lib.register("hfa_units_gather_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _P_, _P_])
@@ -290,8 +291,11 @@ def groupnorm(x, G, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, t_len=None):
     if out is None:
         out = torch.empty_like(x)
     tl = _lens(t_len)
+    ws = None
+    if B * G < 512 and T * (C // G) > 65536:          # long rows: the split-T path needs a small workspace
+        ws = torch.empty(_lib.lib().hfa_groupnorm_workspace_bytes(B, T, C, G), dtype=torch.uint8, device=x.device)
     _lib.call("hfa_groupnorm_f32", B, T, C, G, _ptr(x), x.stride(0), x.stride(1), _ptr(gamma), _ptr(beta),
-              float(eps), act, _ptr(out), out.stride(0), out.stride(1), _ptr(tl), _stream(x.device))
+              float(eps), act, _ptr(out), out.stride(0), out.stride(1), _ptr(tl), _ptr(ws), _stream(x.device))
     return out
 
 

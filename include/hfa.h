@@ -46,6 +46,10 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
                         const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,
                         hipStream_t stream);
 
+/* Tuning hook (benchmarks): states per lane of the multi-wave forward DP, 2 / 4 / 8, 0 = automatic (2 up to 2048
+ * states, 4 up to 4096, then 8). */
+int hfa_viterbi_tuning(int force_k);
+
 /* hfa_viterbi_backtrack replaces the backward half of AlignmentDecoder._decode,
  * tools/alignment_decoder.py:263-288: end state, serial backtrack, frame_confidence = exp(diff([0]+dp_path)).
  * Outputs: ph_idx_seq/ph_time_int [B,Tmax] i32 (first n_out[b] valid, ascending t), frame_conf [B,Tmax] f32.
@@ -114,7 +118,10 @@ int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const floa
  * (nn.GroupNorm(16, C) + nn.Hardswish). */
 int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,
                       const float* beta, float eps, int act, float* y, long long y_bs, int ldy, const int32_t* t_len,
-                      hipStream_t stream);
+                      void* workspace, hipStream_t stream);
+/* Workspace for hfa_groupnorm_f32's split-T path (long rows, few (batch, group) pairs); NULL workspace = one
+ * workgroup per pair. */
+long long hfa_groupnorm_workspace_bytes(int B, int T, int C, int G);
 
 /* ---- extractor conv0 (hubertfa_amd/csrc/conv.hip) ------------------------------------------------------------
  * x [B, N] -> y [B, T0, 512] channels-last, T0 = (N-10)/5+1.  norm=1: GroupNorm(512,512) + GELU

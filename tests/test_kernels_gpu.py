@@ -202,15 +202,24 @@ def test_layernorm(C, act):
     _close(got, ref, 1e-5, 2e-5)
 
 
-def test_groupnorm_hardswish():
+@pytest.mark.parametrize("B,T,C", [(3, 864, 192), (1, 30000, 192), (2, 9000, 384)])
+def test_groupnorm_hardswish(B, T, C):
+    """Single-pass and split-T (long rows, few (batch, group) pairs) GroupNorm + Hardswish."""
     from hubertfa_amd import ops
-    B, T, C = 3, 864, 192
     x = _r(B, T, C, seed=12, scale=2.0) + 0.3
     g, b = _r(C, seed=13) * 0.1 + 1, _r(C, seed=14) * 0.1
     ref = F.hardswish(F.group_norm(x.double().transpose(1, 2), 16, g.double(), b.double(), 1e-5)).transpose(1, 2)
     d = torch.device("cuda")
     got = ops.groupnorm(x.to(d), 16, g.to(d), b.to(d), 1e-5, act=ops.ACT_HARDSWISH)
     _close(got, ref, 1e-5, 2e-5)
+    lens = torch.tensor([T // 2 + 7 * i for i in range(B)], dtype=torch.int32)
+    got = ops.groupnorm(x.to(d), 16, g.to(d), b.to(d), 1e-5, act=ops.ACT_HARDSWISH, t_len=lens.to(d))
+    for i in range(B):
+        n = int(lens[i])
+        ref_i = F.hardswish(F.group_norm(x[i:i + 1, :n].double().transpose(1, 2), 16, g.double(), b.double(),
+                                         1e-5)).transpose(1, 2)
+        _close(got[i:i + 1, :n], ref_i, 1e-5, 2e-5)
+        assert bool((got[i, n:] == 0).all())
 
 
 def test_conv0_groupnorm_gelu():

@@ -72,10 +72,15 @@ def test_forward_batched_bit_exact():
         np.testing.assert_allclose(fc[b, :Ts[b]], z[p + "frame_confidence"], rtol=2e-6, atol=0, equal_nan=True)
 
 
-@pytest.mark.parametrize("T,S", [(700, 300), (1200, 513), (3000, 1801), (2500, 4100), (4200, 8000)])
-def test_forward_many_states_vs_oracle(T, S):
-    """Single- and multi-wave DP variants (S up to 8192) bit-exact with the pinned C oracle."""
-    from hubertfa_amd import ops
+@pytest.mark.parametrize("T,S,force_k,pitch8", [(700, 300, 0, False), (1200, 513, 0, False), (3000, 1801, 0, False),
+                                                (2500, 4100, 0, False), (4200, 8000, 0, False),
+                                                (3000, 1801, 0, True), (1200, 513, 2, True), (3000, 1801, 2, True),
+                                                (3000, 1801, 4, True), (3000, 1801, 8, True), (2500, 4100, 4, False),
+                                                (700, 300, 2, False)])
+def test_forward_many_states_vs_oracle(T, S, force_k, pitch8):
+    """Single- and multi-wave DP variants (S up to 8192; 2/4/8 states per lane; scalar and vector state pitch)
+    bit-exact with the pinned C oracle, and the windowed backtrack with it."""
+    from hubertfa_amd import ops, _lib
     from oracle import decode as od
     r = np.random.default_rng(T * 7 + S)
     V = 63
@@ -87,17 +92,27 @@ def test_forward_many_states_vs_oracle(T, S):
     edge = np.clip(r.uniform(-0.2, 1.2, T), 0, 1)
     pl, E, nE, cu, dp, bt, pad = od.lattice_inputs(ids, ph_prob_log, edge)
     d_ref, b_ref, c_ref = od.forward_pass(T, S, pl, nE, E, cu.copy(), dp.copy(), bt.copy(), ids, pad)
+    P = -(-S // 8) * 8 if pitch8 else S                 # state pitch (the decoder pads it to 8)
+
+    def padded(a, fill):
+        out = np.full(a.shape[:-1] + (P,), fill, dtype=a.dtype)
+        out[..., :S] = a
+        return out
     dev = torch.device("cuda")
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a))[None].to(dev)
-    dp_t, cu_t = t(dp), t(cu)
-    bt_t = torch.full((1, T, S), -1, dtype=torch.int8, device=dev)
-    ids_t = t(ids.astype(np.int32))
+    dp_t, cu_t = t(padded(dp, -np.inf)), t(padded(cu, -np.inf))
+    bt_t = torch.full((1, T, P), -1, dtype=torch.int8, device=dev)
+    ids_t = t(padded(ids.astype(np.int32), 0))
     Tt = torch.tensor([T], dtype=torch.int32, device=dev)
     St = torch.tensor([S], dtype=torch.int32, device=dev)
-    ops.viterbi_forward(t(pl), t(nE), t(E), cu_t, dp_t, bt_t, ids_t, Tt, St)
-    assert np.array_equal(dp_t[0].cpu().numpy().view(np.int32), d_ref.view(np.int32))
-    assert np.array_equal(bt_t[0, 1:].cpu().numpy().astype(np.int32), b_ref[1:])
-    assert np.array_equal(cu_t[0].cpu().numpy().view(np.int64), c_ref.view(np.int64))
+    _lib.lib().hfa_viterbi_tuning(force_k)
+    try:
+        ops.viterbi_forward(t(padded(pl, 0.0)), t(nE), t(E), cu_t, dp_t, bt_t, ids_t, Tt, St)
+    finally:
+        _lib.lib().hfa_viterbi_tuning(0)
+    assert np.array_equal(dp_t[0, :, :S].cpu().numpy().view(np.int32), d_ref.view(np.int32))
+    assert np.array_equal(bt_t[0, 1:, :S].cpu().numpy().astype(np.int32), b_ref[1:])
+    assert np.array_equal(cu_t[0, :S].cpu().numpy().view(np.int64), c_ref.view(np.int64))
     idx, tint, n, fc = ops.viterbi_backtrack(dp_t, bt_t, ids_t, Tt, St)
     i_ref, t_ref, f_ref = od.backtrack(d_ref, b_ref, ids)
     k = int(n[0])
