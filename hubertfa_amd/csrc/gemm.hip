@@ -289,8 +289,13 @@ template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool VEC_C>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP p) {
     constexpr int BK = 16, CPR = 4, NW = WM * WN;
     constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
-    constexpr int DA = BM / 16 / NW, DB = BN / 16 / NW;       // 1-KiB DMA wave-instructions per K-step
-    static_assert(DA * 16 * NW == BM && DB * 16 * NW == BN, "tile/DMA mismatch");
+    // 1-KiB DMA wave-instructions per K-step: IA = BM/16 for A, IW = BN/16 for W, instruction i on wave i % NW;
+    // a wave issues at most DA / DB of them.  Uneven shares (BN = 96 over 4 waves) need NS = 2, whose waits
+    // drain to vmcnt(0); the counted waits of NS = 3 assume every wave issues the same number.
+    constexpr int IA = BM / 16, IW = BN / 16;
+    constexpr int DA = (IA + NW - 1) / NW, DB = (IW + NW - 1) / NW;
+    static_assert(IA * 16 == BM && IW * 16 == BN, "tile/DMA mismatch");
+    static_assert(NS == 2 || (IA % NW == 0 && IW % NW == 0), "uneven DMA shares need the 2-stage pipeline");
     constexpr int STAGE = (BM + BN) * BK;                     // floats per stage (A image, then W image)
     __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];   // one LDS object (no extra waits)
 
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP
     unsigned voffA[DA], voffW[DB];
 #pragma unroll
     for (int d = 0; d < DA; ++d) {
-        const int row = (wave * DA + d) * 16 + (lane >> 2);
+        const int row = (wave + d * NW) * 16 + (lane >> 2);
         int m = tm * BM + row;
         m = m < p.M ? m : p.M - 1;
         a_t0[d] = m * p.stride - p.pad;
@@ -323,7 +328,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP
     }
 #pragma unroll
     for (int d = 0; d < DB; ++d) {
-        const int row = (wave * DB + d) * 16 + (lane >> 2);
+        const int row = (wave + d * NW) * 16 + (lane >> 2);
         int n = tn * BN + row;
         n = n < p.N ? n : p.N - 1;
         voffW[d] = (unsigned)((n * p.ldw + ((lane & 3) ^ ((row >> 2) & 3)) * 4) * 4);
@@ -340,12 +345,16 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_dma_kernel(const GemmP
     int cur_j = 0, cur_c0 = 0, cur_k0 = 0;
     set_tap(0);
     auto issue = [&](int stage) {
-        const unsigned a_dst = lds0 + stage * STAGE * 4 + wave * DA * 1024;
-        const unsigned w_dst = lds0 + (stage * STAGE + BM * BK) * 4 + wave * DB * 1024;
+        const unsigned a_dst = lds0 + stage * STAGE * 4 + wave * 1024;
+        const unsigned w_dst = lds0 + (stage * STAGE + BM * BK) * 4 + wave * 1024;
 #pragma unroll
-        for (int d = 0; d < DA; ++d) hfa::dma16(voffA[d], rA, (unsigned)cur_c0 * 4, a_dst + d * 1024);
+        for (int d = 0; d < DA; ++d)
+            if (IA % NW == 0 || wave + d * NW < IA)
+                hfa::dma16(voffA[d], rA, (unsigned)cur_c0 * 4, a_dst + d * NW * 1024);
 #pragma unroll
-        for (int d = 0; d < DB; ++d) hfa::dma16(voffW[d], rW, (unsigned)cur_k0 * 4, w_dst + d * 1024);
+        for (int d = 0; d < DB; ++d)
+            if (IW % NW == 0 || wave + d * NW < IW)
+                hfa::dma16(voffW[d], rW, (unsigned)cur_k0 * 4, w_dst + d * NW * 1024);
         cur_k0 += BK;
         cur_c0 += BK;
         if (cur_c0 == p.Cg) {
@@ -562,7 +571,7 @@ __global__ __launch_bounds__(256, 4) void gemm_dma_n48_kernel(const GemmP p) {
 
 // Tile configurations (BM x BN, WM x WN waves); scripts/gemm_bench.py measures each on the workload's shapes.
 enum { CFG_AUTO = 0, CFG_128x128 = 1, CFG_128x64 = 2, CFG_256x128 = 3, CFG_128x256 = 4, CFG_256x128_W4 = 5,
-       CFG_128x256_W4 = 6, CFG_256x256 = 7, CFG_128x48 = 8, CFG_COUNT = 9 };
+       CFG_128x256_W4 = 6, CFG_256x256 = 7, CFG_128x48 = 8, CFG_128x96 = 9, CFG_COUNT = 10 };
 // Pipelines: register-staged BK 16 / 32, LDS-DMA with 2 or 3 stages.
 enum { PIPE_AUTO = 0, PIPE_REG16 = 16, PIPE_REG32 = 32, PIPE_DMA2 = 102, PIPE_DMA3 = 103 };
 int g_force_pipe = 0, g_force_cfg = 0;   // tuning overrides (hfa_gemm_tuning), 0 = automatic
@@ -604,10 +613,17 @@ inline Plan make_plan(const GemmP& p, int Z, bool vec_a) {
     if (g_force_cfg > 0 && g_force_cfg < CFG_COUNT) pl.cfg = g_force_cfg;
     if (pl.cfg == CFG_128x48 && (p.N > 48 || !dma_ok(p, vec_a))) pl.cfg = CFG_128x64;
     const bool dma_cfg = pl.cfg == CFG_128x128 || pl.cfg == CFG_128x64 || pl.cfg == CFG_128x256 ||
-                         pl.cfg == CFG_128x48;
+                         pl.cfg == CFG_128x48 || pl.cfg == CFG_128x96;
     pl.pipe = PIPE_REG16;
     if (dma_cfg && dma_ok(p, vec_a)) pl.pipe = (pl.cfg == CFG_128x64 || pl.cfg == CFG_128x48) ? PIPE_DMA3 : PIPE_DMA2;
-    if (pl.cfg == CFG_128x48) return pl;        // DMA-only tile
+    if (pl.cfg == CFG_128x48) return pl;        // DMA-only tiles
+    if (pl.cfg == CFG_128x96) {
+        if (pl.pipe != PIPE_REG16) {
+            pl.pipe = PIPE_DMA2;
+            return pl;
+        }
+        pl.cfg = CFG_128x128;
+    }
     if (g_force_pipe == PIPE_REG16) pl.pipe = PIPE_REG16;
     if (g_force_pipe == PIPE_REG32 && p.K % 32 == 0 && p.Cg % 32 == 0) pl.pipe = PIPE_REG32;
     if ((g_force_pipe == PIPE_DMA2 || g_force_pipe == PIPE_DMA3) && dma_cfg && dma_ok(p, vec_a))
@@ -624,6 +640,7 @@ inline void cfg_shape(int cfg, int& BM, int& BN, int& WM, int& WN) {
         case CFG_128x256_W4: BM = 128; BN = 256; WM = 2; WN = 2; break;
         case CFG_256x256: BM = 256; BN = 256; WM = 4; WN = 2; break;
         case CFG_128x48: BM = 128; BN = 48; WM = 4; WN = 1; break;
+        case CFG_128x96: BM = 128; BN = 96; WM = 4; WN = 1; break;
         default: BM = 128; BN = 128; WM = 2; WN = 2; break;
     }
 }
@@ -702,6 +719,7 @@ int launch_dma_cfg(int cfg, const GemmP& p, int Z, bool vec_c, hipStream_t st) {
         case CFG_128x48: return launch_n48<EPI, NS>(p, Z, st);
         case CFG_128x64: return launch_dma<EPI, 128, 64, 2, 2, NS>(p, Z, vec_c, st);
         case CFG_128x256: return launch_dma<EPI, 128, 256, 2, 4, NS>(p, Z, vec_c, st);
+        case CFG_128x96: return launch_dma<EPI, 128, 96, 4, 1, 2>(p, Z, vec_c, st);     // uneven W DMA: 2 stages
         default: return launch_dma<EPI, 128, 128, 2, 2, NS>(p, Z, vec_c, st);
     }
 }

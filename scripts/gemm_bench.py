@@ -68,7 +68,7 @@ def main():
     args = ap.parse_args()
     keep = set(args.shapes.split(",")) if args.shapes else None
     names = {0: "auto", 1: "128x128/2x2", 2: "128x64/2x2", 3: "256x128/4x2", 4: "128x256/2x4", 5: "256x128/2x2",
-             6: "128x256/2x2", 7: "256x256/4x2"}
+             6: "128x256/2x2", 7: "256x256/4x2", 8: "128x48/4x1", 9: "128x96/4x1"}
     variants = [tuple(int(v) for v in s.split(":")) for s in args.variants.split(",")]
     for shape in SHAPES:
         if keep is not None and shape[0] not in keep:

@@ -70,7 +70,7 @@ def test_conv_gemm_vs_conv1d(Cin, Cout, k, s, pad, T, G):
 
 
 @pytest.mark.parametrize("bk,bn", [(16, c) for c in range(1, 8)] + [(32, 1), (32, 3)] +
-                         [(p, c) for p in (102, 103) for c in (1, 2, 4)])
+                         [(p, c) for p in (102, 103) for c in (1, 2, 4)] + [(102, 9)])
 def test_gemm_tile_variants(bk, bn):
     """Every tile instantiation (register-staged BK 16/32, LDS-DMA 2/3 stages) is exact on a conv and a Linear
     shape with tails in M and N."""
