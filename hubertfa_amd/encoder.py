@@ -76,6 +76,20 @@ def load_hubert(encoder: str, encoder_ckpt: str, device) -> HubertEncoder:
     raise ValueError(f" [x] Unknown units encoder: {encoder}")
 
 
+def plan_windows(L: int, C: int, O: int):
+    """Long-form windows over L Hubert frames: (core_lo, core_hi, win_lo, win_hi) per window, cores C frames
+    tiling [0, L) in order, each window its core plus up to O frames of context on either side."""
+    out = []
+    for k in range(-(-L // C)):
+        out.append((k * C, min(L, (k + 1) * C), max(0, k * C - O), min(L, (k + 1) * C + O)))
+    return out
+
+
+def window_samples(a: int, b: int, hop: int = 320, rf: int = 400, pad: int = 0) -> int:
+    """Samples whose extractor output is exactly frames [a, b) (frame j covers [hop j - pad, hop j + rf - pad))."""
+    return hop * (b - a - 1) + rf - 2 * pad
+
+
 class UnitsEncoder:
     def __init__(self, encoder, encoder_ckpt, encoder_sample_rate=16000, encoder_hop_size=320, device=None):
         if device is None:
@@ -149,11 +163,8 @@ class UnitsEncoder:
         C, O = int(chunk_frames), int(overlap_frames)
         if L <= C + O:
             return m(x.contiguous())
-        wins = []
-        for k in range(-(-L // C)):
-            a, b = max(0, k * C - O), min(L, (k + 1) * C + O)
-            wins.append((k * C, min(L, (k + 1) * C), a, b))
-        n_win = [hop * (b - a - 1) + rf - 2 * pad for _, _, a, b in wins]
+        wins = plan_windows(L, C, O)
+        n_win = [window_samples(a, b, hop, rf, pad) for _, _, a, b in wins]
         xs = x[0]
         batch = torch.zeros((len(wins), max(n_win)), dtype=torch.float32, device=x.device)
         for i, (_, _, a, b) in enumerate(wins):

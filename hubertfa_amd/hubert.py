@@ -56,6 +56,15 @@ class _Layer:
     __slots__ = ("wqkv", "bqkv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w", "ln2_b")
 
 
+def frame_count(arch: HubertArch, n_samples: int) -> int:
+    """Hubert frames of an n-sample input (after the layout's wave padding) through the CNN extractor's valid
+    convs (receptive field 400 samples, hop 320 for every layout here)."""
+    t = n_samples + 2 * arch.wav_pad
+    for k, st in zip(arch.conv_kernel, arch.conv_stride):
+        t = (t - k) // st + 1 if t >= k else 0
+    return t
+
+
 def dev_lengths(values, device) -> torch.Tensor:
     """Host ints -> int32 device tensor through pinned memory and a non-blocking copy (a pageable upload would
     synchronise the stream and stall the pipelined host)."""
@@ -131,11 +140,7 @@ class HubertEncoder:
 
     def frame_lengths(self, n_samples: int) -> int:
         """Hubert frames of an n-sample input (after wav_pad), through the CNN extractor's valid convs."""
-        a = self.arch
-        t = n_samples + 2 * a.wav_pad
-        for k, st in zip(a.conv_kernel, a.conv_stride):
-            t = (t - k) // st + 1 if t >= k else 0
-        return t
+        return frame_count(self.arch, n_samples)
 
     def feature_extractor(self, x: torch.Tensor, t0_len: torch.Tensor | None = None) -> torch.Tensor:
         """[B, N] -> [B, L, 512] (channels-last); GELU applied after every conv.  ``t0_len`` [B] int32: conv0

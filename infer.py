@@ -10,7 +10,6 @@ rank 0 gathers the per-utterance results and writes the TextGrids / confidence.c
 """
 from __future__ import annotations
 
-import math
 import pathlib
 
 import click
@@ -19,6 +18,7 @@ import click
 def _predict(task, dataset, batch_size: int):
     import numpy as np
     import torch
+    from hubertfa_amd.batching import plan_batches, resampled_length
     from hubertfa_amd.wav_io import read_wav
 
     task.on_predict_start()
@@ -27,13 +27,11 @@ def _predict(task, dataset, batch_size: int):
     for wav_path, ph_seq, word_seq, p2w in dataset:
         x, file_sr = read_wav(wav_path)
         items.append((wav_path, x[0], file_sr, ph_seq, word_seq, p2w))
-    # variable-length batches: per sample rate, sorted by length (little padding), rows zero-padded and aligned
-    # with per-row lengths, which keeps every utterance's result identical to aligning it alone (the reference's
-    # B=1); utterances too short for the encoder's 400-sample window take the reference's padding quirk alone
-    by_sr = {}
-    for it in items:
-        by_sr.setdefault(it[2], []).append(it)
+    # variable-length batches (hubertfa_amd.batching.plan_batches): per sample rate, sorted by length, rows
+    # zero-padded and aligned with per-row lengths, which keeps every utterance's result identical to aligning it
+    # alone (the reference's B=1); files too short for the encoder's 400-sample window are aligned alone
     out = {}
+    by_key = {i: it for i, it in enumerate(items)}
 
     def finish(job):
         handle, chunk, n44s = job
@@ -43,19 +41,10 @@ def _predict(task, dataset, batch_size: int):
                               r["word_intervals"])
 
     def batches():
-        for file_sr, group in by_sr.items():
-            group = sorted(group, key=lambda c: len(c[1]))
-            enc_len = task.unitsEncoder.resampled_lengths([len(c[1]) for c in group], file_sr) if group else []
-            if file_sr != sr:   # lengths at the encoder rate go through 44.1 kHz first (load_wav)
-                g = math.gcd(sr, file_sr)
-                n44 = [-(-(sr // g) * len(c[1]) // (file_sr // g)) for c in group]
-                enc_len = task.unitsEncoder.resampled_lengths(n44, sr)
-            short = [c for c, e in zip(group, enc_len) if e < 400]
-            rest = [c for c, e in zip(group, enc_len) if e >= 400]
-            for c in short:
-                yield file_sr, [c]
-            for i in range(0, len(rest), batch_size):
-                yield file_sr, rest[i:i + batch_size]
+        plan = plan_batches([(i, len(it[1]), it[2]) for i, it in by_key.items()], batch_size, sr,
+                            task.unitsEncoder.encoder_sample_rate)
+        for file_sr, keys in plan:
+            yield file_sr, [by_key[k] for k in keys]
 
     # one batch in flight: the host assembles batch i while the GPU runs batch i+1 (task.submit: encoder on the
     # main stream, head + Viterbi on a side stream)
@@ -65,11 +54,10 @@ def _predict(task, dataset, batch_size: int):
         wav_np = np.zeros((len(chunk), max(lens)), np.float32)
         for r, c in enumerate(chunk):
             wav_np[r, :lens[r]] = c[1]
-        wav = torch.from_numpy(wav_np).to(task.device)
+        wav = torch.from_numpy(wav_np).pin_memory().to(task.device, non_blocking=True)   # no host sync
         handle = task.submit(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
                              wav_sr=file_sr, lengths=lens if len(chunk) > 1 else None)
-        g = math.gcd(sr, file_sr)
-        n44s = [math.ceil((sr // g) * n / (file_sr // g)) if file_sr != sr else n for n in lens]
+        n44s = [resampled_length(n, file_sr, sr) for n in lens]
         if pending is not None:
             finish(pending)
         pending = (handle, chunk, n44s)

@@ -145,3 +145,40 @@ def test_boundary_gather_world2_gloo():
     assert np.array(res["ph_idx_seq"]).shape == (6, 7)
     assert np.array(res["n"]).tolist() == [1, 1, 1, 2, 2, 2]
     assert np.array(res["ph_time_int"])[3, 0] == 100
+
+
+def test_resampled_and_encoder_lengths():
+    from hubertfa_amd.batching import encoder_length, resampled_length
+    assert resampled_length(160000, 16000, 44100) == 441000
+    assert resampled_length(441000, 44100, 16000) == 160000
+    assert resampled_length(1, 16000, 44100) == 3                   # ceil(441 / 160)
+    assert resampled_length(12345, 44100, 44100) == 12345
+    assert encoder_length(160000, 16000) == 160000
+    assert encoder_length(48000, 48000) == resampled_length(resampled_length(48000, 48000, 44100), 44100, 16000)
+
+
+def test_plan_batches_sorted_short_alone():
+    from hubertfa_amd.batching import plan_batches
+    items = [("a", 50000, 16000), ("b", 20000, 16000), ("c", 100, 16000), ("d", 90000, 16000),
+             ("e", 30000, 44100), ("f", 70000, 16000), ("g", 60000, 16000)]
+    plan = plan_batches(items, batch_size=2)
+    assert (16000, ["c"]) in plan                                    # 100 samples -> < 400 at the encoder: alone
+    b16 = [keys for sr, keys in plan if sr == 16000 and keys != ["c"]]
+    assert b16 == [["b", "a"], ["g", "f"], ["d"]]                    # sorted by length, batch_size 2
+    assert (44100, ["e"]) in plan
+    assert sorted(k for _, ks in plan for k in ks) == sorted(i[0] for i in items)
+
+
+def test_longform_window_plan_and_spans():
+    from hubertfa_amd import synth
+    from hubertfa_amd.encoder import plan_windows, window_samples
+    from hubertfa_amd.hubert import frame_count
+    for L, C, O in ((1499, 400, 100), (25839, 1000, 100), (1000, 1000, 50), (7, 3, 2)):
+        wins = plan_windows(L, C, O)
+        cores = [i for c0, c1, _, _ in wins for i in range(c0, c1)]
+        assert cores == list(range(L))                                # cores tile [0, L) once, in order
+        for c0, c1, a, b in wins:
+            assert 0 <= a <= c0 < c1 <= b <= L and c0 - a <= O and b - c1 <= O
+    for arch in (synth.arch_cnhubert_base(), synth.arch_cnhubert_large(), synth.arch_hubertsoft()):
+        for a, b in ((0, 1), (0, 400), (300, 1601), (5, 6)):
+            assert frame_count(arch, window_samples(a, b, pad=arch.wav_pad)) == b - a
