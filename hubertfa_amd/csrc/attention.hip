@@ -12,7 +12,8 @@
 // accumulator registers: the per-query max/sum is an in-register reduction plus one xor-32 lane swap, and the
 // S^T accumulator registers are directly the B operand of O^T += V^T P^T (no LDS round trip for P).
 // Online softmax in the log2 domain: scale*log2(e) is folded into Q, so p = exp2(s - m) is one v_exp_f32;
-// the running output is rescaled only when some query's running max moved (wave-uniform skip; x*1 is exact).
+// the running reference max moves only when a query's max exceeds it by more than 8 (log2 units), so the
+// output rescale runs about once per row.
 #include "hfa_common.h"
 
 namespace {
@@ -29,6 +30,7 @@ constexpr int NW = 4;           // waves per workgroup
 #endif
 constexpr int NS = HFA_ATTN_NS; // LDS stages (NS-1 key tiles in flight)
 constexpr int TILE = KB * DH;   // floats per K (or V) tile image
+constexpr float kSlack = 8.0f;  // stale-max slack of the online softmax (log2 units)
 
 struct AttnP {
     int B, H, L;
@@ -143,8 +145,15 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
 #pragma unroll
         for (int e = 1; e < 16; ++e) bm = fmaxf(bm, s[e]);
         bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-        const float m_new = fmaxf(m_run, bm);
-        if (__builtin_amdgcn_ballot_w64(m_new != m_run)) {     // some query's max moved: rescale
+        // Stale-max online softmax: the running reference m_run moves only when a query's max exceeds it by more
+        // than kSlack (log2 units), so p = exp2(s - m_run) <= 2^kSlack stays far from overflow while the O/l
+        // rescale (64 multiplies per lane) runs about once per row instead of on almost every 32-key tile (with
+        // 32 queries per wave, SOME query's max moves on most tiles).  O and l share the reference, so the
+        // normalised result is the same softmax; f32 keeps its relative precision at 2^8 as at 1.
+        const float m_cand = fmaxf(m_run, bm);
+        const bool move = m_cand > m_run + kSlack;          // first tile: m_run = -inf moves
+        if (__builtin_amdgcn_ballot_w64(move)) {
+            const float m_new = move ? m_cand : m_run;
             const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
             l_run *= alpha;
 #pragma unroll
