@@ -148,6 +148,8 @@ class AlignmentDecoder:
         if keep_frame_probs:
             src["edge_prob"] = dev_out["lattice"]["edge_prob"]
             src["ph_frame_pred"] = dev_out["lattice"]["ph_frame_pred"]
+        if "split_oflow" in dev_out:             # the split-precision range guard (task._guard)
+            src["split_oflow"] = dev_out["split_oflow"]
         host = {}
         for k, t in src.items():
             h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
@@ -155,7 +157,10 @@ class AlignmentDecoder:
             host[k] = h
         ev = torch.cuda.Event()
         ev.record()
-        return {"T": dev_out["T"], "host": host, "event": ev}
+        out = {"T": dev_out["T"], "host": host, "event": ev}
+        if "redo" in dev_out:
+            out["redo"] = dev_out["redo"]
+        return out
 
     def assemble(self, dev_out, ph_seqs, word_seqs=None, p2ws=None, keep_frame_probs: bool = False):
         """Host half of decode for a batch (from ``decode_batch(host=False)`` or ``fetch``): per-utterance
@@ -164,6 +169,9 @@ class AlignmentDecoder:
             dev_out = self.fetch(dev_out, keep_frame_probs)
         dev_out["event"].synchronize()
         hd = {k: v.numpy() for k, v in dev_out["host"].items()}
+        if "split_oflow" in hd and int(hd["split_oflow"][0]) and "redo" in dev_out:
+            # a split-f16 operand left f16 range: this batch is recomputed with f32 GEMMs
+            return dev_out["redo"]()
         Ts = dev_out["T"]
         idx_h, tint_h, n_h, fc_h, ed_h = (hd[k] for k in self._FETCH_KEYS)
         ep_h = hd.get("edge_prob") if keep_frame_probs else None

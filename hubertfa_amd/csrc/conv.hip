@@ -86,13 +86,17 @@ __global__ __launch_bounds__(NT) void conv0_reduce_kernel(int T0, int nchunk, co
     }
 }
 
-// mode 0: GroupNorm(stats) + affine + GELU; mode 1: + bias, no norm, no act (LN variant feeds a LayerNorm)
-template <int MODE>
+// mode 0: GroupNorm(stats) + affine + GELU; mode 1: + bias, no norm, no act (LN variant feeds a LayerNorm).
+// OUTS: write the output as split-f16 planes (gemm.hip gemm_split_kernel operand: hi = f16(v), lo = f16((v - hi)
+// * 2^11), plane 1 at +y_sp halves) instead of f32 — the same bytes, and conv1 then runs on the f16 MFMA.
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+template <int MODE, bool OUTS>
 __global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const float* __restrict__ x, long long x_bs,
                                                          const float* __restrict__ w0, const float* __restrict__ stats,
                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                         const float* __restrict__ bias, float* __restrict__ y,
-                                                         long long y_bs) {
+                                                         const float* __restrict__ bias, void* __restrict__ yv,
+                                                         long long y_bs, long long y_sp, int* __restrict__ oflow) {
     __shared__ float xs[CH * ST + KW];
     const int b = blockIdx.y, chunk = blockIdx.x;
     const int t0 = chunk * CH;
@@ -116,7 +120,9 @@ __global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const fl
         hb = bias ? bias[c0 + 1] : 0.f;
     }
     __syncthreads();
-    float* yb = y + b * y_bs + (long long)t0 * C0 + c0;
+    float* yb = reinterpret_cast<float*>(yv) + b * y_bs + (long long)t0 * C0 + c0;
+    _Float16* yh = reinterpret_cast<_Float16*>(yv) + b * y_bs + (long long)t0 * C0 + c0;
+    bool bad = false;
     for (int t = 0; t < nt; ++t) {
         float va = conv10(wa, xs + t * ST);
         float vb = conv10(wb, xs + t * ST);
@@ -127,8 +133,20 @@ __global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const fl
             va += ha;
             vb += hb;
         }
-        *reinterpret_cast<float2*>(yb + (long long)t * C0) = make_float2(va, vb);
+        if constexpr (OUTS) {
+            bad |= !(__builtin_fabsf(va) < 65504.0f) || !(__builtin_fabsf(vb) < 65504.0f);
+            f16x2 v1, v2;
+            v1[0] = (_Float16)va;
+            v1[1] = (_Float16)vb;
+            v2[0] = (_Float16)((va - (float)v1[0]) * 2048.0f);
+            v2[1] = (_Float16)((vb - (float)v1[1]) * 2048.0f);
+            *reinterpret_cast<f16x2*>(yh + (long long)t * C0) = v1;
+            *reinterpret_cast<f16x2*>(yh + (long long)t * C0 + y_sp) = v2;
+        } else {
+            *reinterpret_cast<float2*>(yb + (long long)t * C0) = make_float2(va, vb);
+        }
     }
+    if (OUTS && bad && oflow) *oflow = 1;
 }
 
 }  // namespace
@@ -141,20 +159,19 @@ long long hfa_conv0_workspace_bytes(int B, int N) {
     return (long long)B * nchunk * C0 * 2 * sizeof(double) + (long long)B * C0 * 2 * sizeof(float) + 64;
 }
 
-// x [B, N] (row stride x_bs) -> y [B, T0, 512] channels-last (row stride 512, batch stride y_bs).
-// norm = 1: GroupNorm(512,512)+GELU (gamma/beta required, workspace of hfa_conv0_workspace_bytes);
-// norm = 0: raw conv + bias (bias may be NULL).  t0_len (optional, device [B]): per-row frame counts of a
-// variable-length batch — the GroupNorm statistics cover frames < t0_len[b] only (rows beyond are don't-care).
-int hfa_conv0_f32(int B, int N, const float* x, long long x_bs, const float* w0, const float* bias, int norm,
-                  const float* gamma, const float* beta, float eps, void* workspace, float* y, long long y_bs,
-                  const int32_t* t0_len, hipStream_t stream) {
+namespace {
+int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, const float* bias, int norm,
+                 const float* gamma, const float* beta, float eps, void* workspace, void* y, long long y_bs,
+                 long long y_sp, bool outs, int* oflow, const int32_t* t0_len, hipStream_t stream) {
+    const char* fn = outs ? "hfa_conv0_split" : "hfa_conv0_f32";
     if (B < 0 || N < KW) {
-        hfa::set_error("hfa_conv0_f32: need N >= %d samples (got %d)", KW, N);
+        hfa::set_error("%s: need N >= %d samples (got %d)", fn, KW, N);
         return HFA_EINVAL;
     }
     if (B == 0) return HFA_OK;
-    if (!x || !w0 || !y || (norm && (!gamma || !beta || !workspace)) || ((uintptr_t)y & 7) || y_bs % 2) {
-        hfa::set_error("hfa_conv0_f32: bad pointer arguments");
+    if (!x || !w0 || !y || (norm && (!gamma || !beta || !workspace)) || ((uintptr_t)y & 7) || y_bs % 2 ||
+        (outs && y_sp % 2)) {
+        hfa::set_error("%s: bad pointer arguments", fn);
         return HFA_EINVAL;
     }
     const int T0 = (N - KW) / ST + 1;
@@ -165,13 +182,41 @@ int hfa_conv0_f32(int B, int N, const float* x, long long x_bs, const float* w0,
         float* stats = reinterpret_cast<float*>(part + (size_t)B * nchunk * C0 * 2);
         hipLaunchKernelGGL(conv0_stats_kernel, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, part, t0_len);
         hipLaunchKernelGGL(conv0_reduce_kernel, dim3(B), dim3(NT), 0, stream, T0, nchunk, part, eps, stats, t0_len);
-        hipLaunchKernelGGL(conv0_apply_kernel<0>, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats, gamma, beta,
-                           bias, y, y_bs);
+        if (outs)
+            hipLaunchKernelGGL((conv0_apply_kernel<0, true>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats,
+                               gamma, beta, bias, y, y_bs, y_sp, oflow);
+        else
+            hipLaunchKernelGGL((conv0_apply_kernel<0, false>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats,
+                               gamma, beta, bias, y, y_bs, y_sp, oflow);
+    } else if (outs) {
+        hipLaunchKernelGGL((conv0_apply_kernel<1, true>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, nullptr,
+                           nullptr, nullptr, bias, y, y_bs, y_sp, oflow);
     } else {
-        hipLaunchKernelGGL(conv0_apply_kernel<1>, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, nullptr, nullptr,
-                           nullptr, bias, y, y_bs);
+        hipLaunchKernelGGL((conv0_apply_kernel<1, false>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, nullptr,
+                           nullptr, nullptr, bias, y, y_bs, y_sp, oflow);
     }
-    return hfa::check_launch("hfa_conv0_f32");
+    return hfa::check_launch(fn);
+}
+}  // namespace
+
+// x [B, N] (row stride x_bs) -> y [B, T0, 512] channels-last (row stride 512, batch stride y_bs).
+// norm = 1: GroupNorm(512,512)+GELU (gamma/beta required, workspace of hfa_conv0_workspace_bytes);
+// norm = 0: raw conv + bias (bias may be NULL).  t0_len (optional, device [B]): per-row frame counts of a
+// variable-length batch — the GroupNorm statistics cover frames < t0_len[b] only (rows beyond are don't-care).
+int hfa_conv0_f32(int B, int N, const float* x, long long x_bs, const float* w0, const float* bias, int norm,
+                  const float* gamma, const float* beta, float eps, void* workspace, float* y, long long y_bs,
+                  const int32_t* t0_len, hipStream_t stream) {
+    return conv0_launch(B, N, x, x_bs, w0, bias, norm, gamma, beta, eps, workspace, y, y_bs, 0, false, nullptr,
+                        t0_len, stream);
+}
+
+// As hfa_conv0_f32, output as split-f16 planes ys (plane 1 at +y_sp halves; strides in halves); *oflow is raised
+// when an output leaves f16 range.
+int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w0, const float* bias, int norm,
+                    const float* gamma, const float* beta, float eps, void* workspace, uint16_t* ys, long long y_bs,
+                    long long y_sp, int* oflow, const int32_t* t0_len, hipStream_t stream) {
+    return conv0_launch(B, N, x, x_bs, w0, bias, norm, gamma, beta, eps, workspace, ys, y_bs, y_sp, true, oflow,
+                        t0_len, stream);
 }
 
 }  // extern "C"

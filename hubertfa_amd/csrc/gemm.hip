@@ -27,6 +27,8 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 struct GemmP {
     int M, N, K, G, m_tiles, n_tiles;
@@ -35,6 +37,12 @@ struct GemmP {
     const float* bias; long long sBg;
     const float* R; long long sRb, sRg; int ldr;
     float* C; long long sCb, sCg; int ldc;
+    // split-f16 operands (gemm_split_kernel): A / W / output as two f16 planes (hi, lo * 2^11), element strides
+    // as above (halves), plane 1 at +sAp / +sWp / +sCp; Ch set = planes out instead of C; oflow = range flag
+    const _Float16* Ah; long long sAp;
+    const _Float16* Wh; long long sWp;
+    _Float16* Ch; long long sCp;
+    int* oflow;
 };
 
 enum { EPI_NONE = 0, EPI_GELU = 1 };
@@ -569,6 +577,262 @@ __global__ __launch_bounds__(256, 4) void gemm_dma_n48_kernel(const GemmP p) {
     }
 }
 
+// ---- split-f16 GEMM (f32-class accuracy on the f16 MFMA) ---------------------------------------------------------
+// Every f32 operand x is carried as two f16 planes: x1 = f16(x), x2 = f16((x - x1) * 2^11); x1 + 2^-11 x2 keeps 22
+// of f32's 24 significand bits (relative error <= 2^-22, absolute 2^-36 below f16's normal range).  The product
+// a.w is evaluated as a1.w1 + 2^-11 (a1.w2 + a2.w1): every partial product of two f16 is exact in the MFMA's f32
+// accumulator, and the dropped a2.w2 term is 2^-22 relative, so the result is within a few f32 rounding steps of
+// the f32-MFMA result (scripts/split_precision_sim.py: per-frame log-probs 2.2e-5 from an f64 evaluation of the
+// whole path, the plain f32 path 2.0e-5).  v_mfma_f32_32x32x16_f16 does 16x the FLOP per clock of the f32 MFMA, so
+// the 3 products run at 5.3x the f32-MFMA rate.  Two accumulators (main, correction) keep the 2^-11 scale exact.
+// Range: |x| must stay below 65504 (f16 max); the producer of a split operand raises *oflow otherwise, and the host
+// re-runs the batch on the f32 path (ops.SplitOverflow).
+// Tile: the f32 DMA kernel's geometry with 32 halves (64 B) per row per K-step: the same 1-KiB DMA pieces (16 rows
+// x 4 chunks), the same XOR-swizzled [row][64 B] image per plane, 4 planes per stage (A1, A2, W1, W2).  A lane's
+// ds_read_b128 brings 8 consecutive k of its row = one MFMA operand (lane l: row l&31, k 8(l>>5)..+7 of a 16-k
+// sub-step; the same mapping on both operands).
+template <int TI, int TJ>
+__device__ __forceinline__ void store_split_lds(const GemmP& p, const f32x16 (&acc)[TI][TJ], int EPI_, int zb, int zg,
+                                                int wrow0, int wcol0, int lane, float* slab) {
+    _Float16* Cb = p.Ch + zb * p.sCb + zg * p.sCg;
+    const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+    const int r32 = lane & 31, h = lane >> 5;
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+        const int col0 = wcol0 + j * 32;
+        if (col0 >= p.N) continue;
+        const float bv = (biasb && col0 + r32 < p.N) ? biasb[col0 + r32] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const int row0 = wrow0 + i * 32;
+            if (row0 >= p.M) continue;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                float v = acc[i][j][e] + bv;
+                if (EPI_ == EPI_GELU) v = hfa::gelu_fast(v);
+                slab[((e & 3) + 8 * (e >> 2) + 4 * h) * 36 + r32] = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int idx = lane + k * 64;
+                const int r = idx >> 3, c4 = (idx & 7) * 4;
+                const int row = row0 + r, col = col0 + c4;
+                if (row < p.M) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(slab + r * 36 + c4);
+                    f16x4 v1, v2;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        bad |= !(__builtin_fabsf(v[t]) < 65504.0f);
+                        v1[t] = (_Float16)v[t];
+                        v2[t] = (_Float16)((v[t] - (float)v1[t]) * 2048.0f);
+                    }
+                    _Float16* dst = Cb + (long long)row * p.ldc + col;
+                    if (col + 3 < p.N) {
+                        *reinterpret_cast<f16x4*>(dst) = v1;
+                        *reinterpret_cast<f16x4*>(dst + p.sCp) = v2;
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            if (col + t < p.N) {
+                                dst[t] = v1[t];
+                                dst[t + p.sCp] = v2[t];
+                            }
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (bad && p.oflow) *p.oflow = 1;
+}
+
+template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const GemmP p) {
+    constexpr int BK = 32, CPR = 4, NW = WM * WN;            // halves per row per K-step, 16-B chunks per row
+    constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
+    constexpr int IA = BM / 16, IW = BN / 16;                 // 1-KiB DMA pieces per plane per K-step
+    constexpr int DA = IA / NW, DB = IW / NW;
+    static_assert(IA % NW == 0 && IW % NW == 0, "even DMA shares only");
+    constexpr int PA = BM * BK, PW = BN * BK;                 // halves per plane image
+    constexpr int STAGE = 2 * PA + 2 * PW;                    // halves per stage: A1, A2, W1, W2
+    __shared__ __attribute__((aligned(16))) _Float16 smem[NS * STAGE];
+
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+    const int tm = wgid / p.n_tiles, tn = wgid - tm * p.n_tiles;
+    const int zb = blockIdx.z / p.G, zg = blockIdx.z - zb * p.G;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    const _Float16* Ab = p.Ah + zb * p.sAb + zg * p.sAg;
+    const _Float16* Wb = p.Wh + zg * p.sWg;
+    const long long a_bytes = ((long long)(p.Tin - 1) * p.ldx + p.Cg) * 2;
+    const long long w_bytes = ((long long)(p.N - 1) * p.ldw + p.K) * 2;
+    const __amdgpu_buffer_rsrc_t rA1 = hfa::make_rsrc(Ab, a_bytes);
+    const __amdgpu_buffer_rsrc_t rA2 = hfa::make_rsrc(Ab + p.sAp, a_bytes);
+    const __amdgpu_buffer_rsrc_t rW1 = hfa::make_rsrc(Wb, w_bytes);
+    const __amdgpu_buffer_rsrc_t rW2 = hfa::make_rsrc(Wb + p.sWp, w_bytes);
+
+    // DMA d of this wave fills rows (wave + d*NW)*16 + lane/4 of each plane, chunk slot lane&3 (swizzled source)
+    int a_t0[DA], a_c[DA];
+    unsigned voffA[DA], voffW[DB];
+#pragma unroll
+    for (int d = 0; d < DA; ++d) {
+        const int row = (wave + d * NW) * 16 + (lane >> 2);
+        int m = tm * BM + row;
+        m = m < p.M ? m : p.M - 1;
+        a_t0[d] = m * p.stride - p.pad;
+        a_c[d] = ((lane & 3) ^ ((row >> 2) & 3)) * 8;
+    }
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+        const int row = (wave + d * NW) * 16 + (lane >> 2);
+        int n = tn * BN + row;
+        n = n < p.N ? n : p.N - 1;
+        voffW[d] = (unsigned)((n * p.ldw + ((lane & 3) ^ ((row >> 2) & 3)) * 8) * 2);
+    }
+    auto set_tap = [&](int j) {
+#pragma unroll
+        for (int d = 0; d < DA; ++d) {
+            const int t = a_t0[d] + j;
+            voffA[d] = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + a_c[d]) * 2) : hfa::DMA_OOB;
+        }
+    };
+    const unsigned lds0 = hfa::lds_addr(smem);
+    int cur_j = 0, cur_c0 = 0, cur_k0 = 0;
+    set_tap(0);
+    auto issue = [&](int stage) {
+        const unsigned base = lds0 + stage * STAGE * 2 + wave * 1024;
+#pragma unroll
+        for (int d = 0; d < DA; ++d) {
+            hfa::dma16(voffA[d], rA1, (unsigned)cur_c0 * 2, base + d * NW * 1024);
+            hfa::dma16(voffA[d], rA2, (unsigned)cur_c0 * 2, base + PA * 2 + d * NW * 1024);
+        }
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+            hfa::dma16(voffW[d], rW1, (unsigned)cur_k0 * 2, base + 2 * PA * 2 + d * NW * 1024);
+            hfa::dma16(voffW[d], rW2, (unsigned)cur_k0 * 2, base + (2 * PA + PW) * 2 + d * NW * 1024);
+        }
+        cur_k0 += BK;
+        cur_c0 += BK;
+        if (cur_c0 == p.Cg) {
+            cur_c0 = 0;
+            set_tap(++cur_j);
+        }
+    };
+    constexpr int DN = 2 * (DA + DB);                       // DMA issues per wave per K-step
+
+    const int wm = wave / WN, wn = wave % WN;
+    const int r32 = lane & 31, h = lane >> 5;
+    int rdA[2], rdB[2];                                      // f16x8 (16-B) units within a stage
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 2 + h;
+        rdA[kk] = (wm * (BM / WM) + r32) * CPR + (c ^ ((r32 >> 2) & 3));
+        rdB[kk] = 2 * PA / 8 + (wn * (BN / WN) + r32) * CPR + (c ^ ((r32 >> 2) & 3));
+    }
+    f32x16 accM[TI][TJ], accC[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) accM[i][j][e] = accC[i][j][e] = 0.0f;
+
+    const int nk = p.K / BK;
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < nk) issue(s);
+    if (nk >= NS - 1) hfa::wait_vm_barrier<(NS - 2) * DN>();
+    else hfa::wait_vm_barrier<0>();
+
+    const f16x8* s8 = reinterpret_cast<const f16x8*>(smem);
+    int stage = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+        const bool more = kt + NS - 1 < nk;
+        if (more) issue(stage == 0 ? NS - 1 : stage - 1);
+        const f16x8* st = s8 + stage * (STAGE / 8);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            f16x8 a1[TI], a2[TI], w1[TJ], w2[TJ];
+#pragma unroll
+            for (int i = 0; i < TI; ++i) {
+                a1[i] = st[rdA[kk] + i * 32 * CPR];
+                a2[i] = st[rdA[kk] + PA / 8 + i * 32 * CPR];
+            }
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) {
+                w1[j] = st[rdB[kk] + j * 32 * CPR];
+                w2[j] = st[rdB[kk] + PW / 8 + j * 32 * CPR];
+            }
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j) {
+                    accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w1[j], accM[i][j], 0, 0, 0);
+                    accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w2[j], accC[i][j], 0, 0, 0);
+                    accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accC[i][j], 0, 0, 0);
+                }
+        }
+        if (kt + 1 < nk) {
+            if (more) hfa::wait_vm_barrier<(NS - 2) * DN>();
+            else hfa::wait_vm_barrier<0>();
+        }
+        stage = stage + 1 == NS ? 0 : stage + 1;
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) accM[i][j][e] = __builtin_fmaf(accC[i][j][e], 1.0f / 2048.0f, accM[i][j][e]);
+    static_assert(NW * 32 * 36 * 4 <= NS * STAGE * 2, "epilogue slabs exceed the staging LDS");
+    __syncthreads();
+    float* slab = reinterpret_cast<float*>(smem) + wave * (32 * 36);
+    if constexpr (OUT_SPLIT)
+        store_split_lds<TI, TJ>(p, accM, EPI, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane, slab);
+    else
+        store_tile_lds<EPI, TI, TJ>(p, accM, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane, slab);
+}
+
+// f32 -> (hi, lo * 2^11) f16 planes, row-wise with 4-element vectors where aligned; raises *oflow for |x| >= 65504
+// or a non-finite x.
+__global__ __launch_bounds__(256) void split_f16_kernel(int rows, int cols, const float* __restrict__ x, long long ldx,
+                                                        _Float16* __restrict__ y, long long ldy, long long sp,
+                                                        int* __restrict__ oflow) {
+    const int c4 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    const int r = blockIdx.y;
+    if (r >= rows || c4 >= cols) return;
+    const float* src = x + (long long)r * ldx + c4;
+    _Float16* dst = y + (long long)r * ldy + c4;
+    bool bad = false;
+    if (c4 + 3 < cols && ((ldx | ldy | sp) & 3) == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(src);
+        f16x4 v1, v2;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            bad |= !(__builtin_fabsf(v[t]) < 65504.0f);
+            v1[t] = (_Float16)v[t];
+            v2[t] = (_Float16)((v[t] - (float)v1[t]) * 2048.0f);
+        }
+        *reinterpret_cast<f16x4*>(dst) = v1;
+        *reinterpret_cast<f16x4*>(dst + sp) = v2;
+    } else {
+        for (int t = 0; t < 4 && c4 + t < cols; ++t) {
+            const float v = src[t];
+            bad |= !(__builtin_fabsf(v) < 65504.0f);
+            const _Float16 v1 = (_Float16)v;
+            dst[t] = v1;
+            dst[t + sp] = (_Float16)((v - (float)v1) * 2048.0f);
+        }
+    }
+    if (bad && oflow) *oflow = 1;
+}
+
 // Tile configurations (BM x BN, WM x WN waves); scripts/gemm_bench.py measures each on the workload's shapes.
 enum { CFG_AUTO = 0, CFG_128x128 = 1, CFG_128x64 = 2, CFG_256x128 = 3, CFG_128x256 = 4, CFG_256x128_W4 = 5,
        CFG_128x256_W4 = 6, CFG_256x256 = 7, CFG_128x48 = 8, CFG_128x96 = 9, CFG_COUNT = 10 };
@@ -673,6 +937,41 @@ inline int set_grid(GemmP& p, int BM, int BN, dim3& grid, int Z) {
     return HFA_OK;
 }
 
+// ---- split-f16 dispatch --------------------------------------------------------------------------------------
+enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_COUNT = 4 };
+int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
+
+inline int split_cfg(const GemmP& p, int Z) {
+    if (g_split_cfg > 0 && g_split_cfg < SCFG_COUNT) return g_split_cfg;
+    const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
+    return (p.N <= 64 || blocks128 < 256) ? SCFG_128x64 : SCFG_128x128;
+}
+
+inline void split_name(int cfg, int epi, bool outs, char* buf, int len) {
+    const int BM = cfg == SCFG_256x128 ? 256 : 128, BN = cfg == SCFG_128x64 ? 64 : 128;
+    const int WM = cfg == SCFG_256x128 ? 4 : 2, OCC = cfg == SCFG_256x128 ? 1 : 2;
+    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, 2, 2, %d, %s>", epi, BM, BN, WM, OCC, outs ? "true" : "false");
+}
+
+template <int EPI, bool OUTS>
+int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
+    dim3 grid;
+    switch (cfg) {
+        case SCFG_128x64:
+            if (int rc = set_grid(p, 128, 64, grid, Z)) return rc;
+            hipLaunchKernelGGL((gemm_split_kernel<EPI, 128, 64, 2, 2, 2, 2, OUTS>), grid, dim3(256), 0, st, p);
+            break;
+        case SCFG_256x128:
+            if (int rc = set_grid(p, 256, 128, grid, Z)) return rc;
+            hipLaunchKernelGGL((gemm_split_kernel<EPI, 256, 128, 4, 2, 2, 1, OUTS>), grid, dim3(512), 0, st, p);
+            break;
+        default:
+            if (int rc = set_grid(p, 128, 128, grid, Z)) return rc;
+            hipLaunchKernelGGL((gemm_split_kernel<EPI, 128, 128, 2, 2, 2, 2, OUTS>), grid, dim3(256), 0, st, p);
+    }
+    return hfa::check_launch("hfa_conv_gemm_split");
+}
+
 template <int EPI, int BK, int BM, int BN, int WM, int WN>
 int launch_reg(GemmP p, int Z, bool vec_a, hipStream_t st) {
     dim3 grid;
@@ -774,6 +1073,7 @@ GemmP make_params(int M, int N, int K, int G, const float* A, long long sAb, lon
     p.bias = nullptr; p.sBg = 0;
     p.R = nullptr; p.sRb = p.sRg = 0; p.ldr = 0;
     p.C = nullptr; p.sCb = p.sCg = 0; p.ldc = 0;
+    p.Ah = nullptr; p.sAp = 0; p.Wh = nullptr; p.sWp = 0; p.Ch = nullptr; p.sCp = 0; p.oflow = nullptr;
     return p;
 }
 
@@ -825,6 +1125,94 @@ int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, i
                  const float* R, int ldr, float* C, int ldc, int epilogue, hipStream_t stream) {
     return hfa_conv_gemm_f32(M, N, K, 1, 1, A, 0, 0, lda, 1, 0, K, M, W, 0, ldw, bias, 0, R, 0, 0, ldr, C, 0, 0,
                              ldc, epilogue, stream);
+}
+
+// Split-f16 implicit GEMM (gemm_split_kernel): A, W as f16 plane pairs (plane 1 at +sAp / +sWp halves), element
+// strides in halves; output either f32 C (+R) or, with Cs, f16 planes (plane 1 at +sCp; bias/GELU only, no R).
+int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, long long sAp, long long sAb,
+                        long long sAg, int ldx, int stride, int pad, int Cg, int Tin, const uint16_t* W,
+                        long long sWp, long long sWg, int ldw, const float* bias, long long sBg, const float* R,
+                        long long sRb, long long sRg, int ldr, float* C, uint16_t* Cs, long long sCp, long long sCb,
+                        long long sCg, int ldc, int epilogue, int* oflow, hipStream_t stream) {
+    if (M < 0 || N < 0 || K < 0 || Zb < 0 || G < 1 || stride < 1 || Cg < 1 || Tin < 1) {
+        hfa::set_error("hfa_conv_gemm_split: bad sizes M=%d N=%d K=%d Zb=%d G=%d", M, N, K, Zb, G);
+        return HFA_EINVAL;
+    }
+    if (M == 0 || N == 0 || Zb == 0) return HFA_OK;
+    if (!A || !W || (!C == !Cs) || K == 0 || (Cs && R)) {
+        hfa::set_error("hfa_conv_gemm_split: need A, W and exactly one of C / Cs (Cs takes no residual)");
+        return HFA_EINVAL;
+    }
+    if (K % 32 || Cg % 32 || K % Cg) {
+        hfa::set_error("hfa_conv_gemm_split: K=%d and Cg=%d must be multiples of 32 with Cg | K", K, Cg);
+        return HFA_EINVAL;
+    }
+    if (!al16(A) || !al16(W) || (ldx | ldw) % 8 || (sAp | sAb | sAg | sWp | sWg) % 8) {
+        hfa::set_error("hfa_conv_gemm_split: A/W planes must be 16-byte aligned with strides multiple of 8 halves");
+        return HFA_EINVAL;
+    }
+    const long long a_span = ((long long)(Tin - 1) * ldx + Cg) * 2, w_span = ((long long)(N - 1) * ldw + K) * 2;
+    if (a_span >= 0x7fffffffLL || w_span >= 0x7fffffffLL) {
+        hfa::set_error("hfa_conv_gemm_split: operand span past 31-bit buffer offsets");
+        return HFA_EINVAL;
+    }
+    const bool vc = C ? (al16(C) && ldc % 4 == 0 && sCb % 4 == 0 && sCg % 4 == 0 &&
+                         (!R || (al16(R) && ldr % 4 == 0 && sRb % 4 == 0 && sRg % 4 == 0)))
+                      : (((uintptr_t)Cs & 7) == 0 && ldc % 4 == 0 && (sCp | sCb | sCg) % 4 == 0);
+    if (!vc) {
+        hfa::set_error("hfa_conv_gemm_split: C/R (or Cs) rows must be 16-B (8-B) aligned");
+        return HFA_EINVAL;
+    }
+    if (epilogue != EPI_NONE && epilogue != EPI_GELU) {
+        hfa::set_error("hfa_conv_gemm_split: unknown epilogue %d", epilogue);
+        return HFA_EINVAL;
+    }
+    if ((long long)Zb * G > 65535) {
+        hfa::set_error("hfa_conv_gemm_split: Zb*G exceeds the grid z limit");
+        return HFA_EINVAL;
+    }
+    GemmP p = make_params(M, N, K, G, nullptr, sAb, sAg, ldx, stride, pad, Cg, Tin, nullptr, sWg, ldw);
+    p.Ah = reinterpret_cast<const _Float16*>(A); p.sAp = sAp;
+    p.Wh = reinterpret_cast<const _Float16*>(W); p.sWp = sWp;
+    p.bias = bias; p.sBg = sBg;
+    p.R = R; p.sRb = sRb; p.sRg = sRg; p.ldr = ldr;
+    p.C = C; p.Ch = reinterpret_cast<_Float16*>(Cs); p.sCp = sCp; p.sCb = sCb; p.sCg = sCg; p.ldc = ldc;
+    p.oflow = oflow;
+    const int Z = Zb * G, cfg = split_cfg(p, Z);
+    if (Cs) return epilogue == EPI_GELU ? launch_split<EPI_GELU, true>(p, Z, cfg, stream)
+                                        : launch_split<EPI_NONE, true>(p, Z, cfg, stream);
+    return epilogue == EPI_GELU ? launch_split<EPI_GELU, false>(p, Z, cfg, stream)
+                                : launch_split<EPI_NONE, false>(p, Z, cfg, stream);
+}
+
+const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue) {
+    GemmP p = make_params(M, N, 32, 1, nullptr, 0, 0, 0, 1, 0, 32, 1, nullptr, 0, 0);
+    split_name(split_cfg(p, Z), epilogue, out_split != 0, g_name, sizeof(g_name));
+    return g_name;
+}
+
+int hfa_gemm_split_tuning(int cfg) {
+    g_split_cfg = cfg;
+    return HFA_OK;
+}
+
+// x [rows, cols] f32 (row stride ldx) -> planes y (row stride ldy halves, plane 1 at +sp): y1 = f16(x),
+// y2 = f16((x - y1) * 2^11).  Sets *oflow (when given) if any |x| >= 65504 or x is not finite.
+int hfa_split_f16(int rows, int cols, const float* x, long long ldx, uint16_t* y, long long ldy, long long sp,
+                  int* oflow, hipStream_t stream) {
+    if (rows < 0 || cols < 0 || (rows && cols && (!x || !y))) {
+        hfa::set_error("hfa_split_f16: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (!rows || !cols) return HFA_OK;
+    if (rows > 65535 * 64) {
+        hfa::set_error("hfa_split_f16: too many rows");
+        return HFA_EINVAL;
+    }
+    dim3 grid((cols + 1023) / 1024, rows);
+    hipLaunchKernelGGL(split_f16_kernel, grid, dim3(256), 0, stream, rows, cols, x, ldx,
+                       reinterpret_cast<_Float16*>(y), ldy, sp, oflow);
+    return hfa::check_launch("hfa_split_f16");
 }
 
 }  // extern "C"

@@ -53,7 +53,8 @@ def _weight_norm(sd: dict, prefix: str) -> torch.Tensor:
 
 
 class _Layer:
-    __slots__ = ("wqkv", "bqkv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w", "ln2_b")
+    __slots__ = ("wqkv", "bqkv", "wo", "bo", "ln1_w", "ln1_b", "w1", "b1", "w2", "b2", "ln2_w", "ln2_b",
+                 "wqkv_s", "wo_s", "w1_s", "w2_s")
 
 
 def frame_count(arch: HubertArch, n_samples: int) -> int:
@@ -72,10 +73,20 @@ def dev_lengths(values, device) -> torch.Tensor:
 
 
 class HubertEncoder:
-    """Hubert forward on HIP kernels.  ``forward(wav[B, N]) -> units[B, L, C_out]`` (f32, channels-last)."""
+    """Hubert forward on HIP kernels.  ``forward(wav[B, N]) -> units[B, L, C_out]`` (f32, channels-last).
 
-    def __init__(self, arch: HubertArch, state_dict: dict, device: str | torch.device = "cuda"):
+    ``precision``: "split" (default) evaluates every dense contraction whose channel count allows it (K, Cg
+    multiples of 32) on the split-f16 MFMA GEMM (gemm.hip gemm_split_kernel: f32-class accuracy, 2-2.5x the f32
+    MFMA rate), the operands carried as f16 plane pairs written directly by their producers; "f32" runs every
+    GEMM on the f32 MFMA.  A split producer that meets a value outside f16 range raises ops.split_flag(), and
+    the caller re-runs that batch with precision "f32" (task.ForcedAlignmentTask)."""
+
+    def __init__(self, arch: HubertArch, state_dict: dict, device: str | torch.device = "cuda",
+                 precision: str = "split"):
+        if precision not in ("split", "f32"):
+            raise ValueError(f"precision must be 'split' or 'f32', not {precision!r}")
         self.arch = arch
+        self.precision = precision
         self.device = torch.device(device)
         sd = _strip(state_dict)
         dev = self.device
@@ -129,6 +140,17 @@ class HubertEncoder:
             self.layers.append(L)
         self.proj = (P("proj.weight"), P("proj.bias")) if (not hf and arch.proj_dim) else None
         self._ws = {}
+        # split-f16 planes of every GEMM weight (one-time); conv weights only where Cin is a multiple of 32
+        def sp(w):   # weights outside f16 range (none in practice) stay on the f32 GEMM
+            if precision != "split" or self.device.type != "cuda" or not bool(w.abs().max() < 65504):
+                return None
+            return ops.split(w)
+        self.conv_ws = [None] + [sp(w) if arch.conv_dim[i - 1] % 32 == 0 else None
+                                 for i, w in enumerate(self.conv_w) if i > 0]
+        self.fp_ws = sp(self.fp_w) if self.fp_w.shape[1] % 32 == 0 else None
+        for L in self.layers:
+            L.wqkv_s, L.wo_s, L.w1_s, L.w2_s = sp(L.wqkv), sp(L.wo), sp(L.w1), sp(L.w2)
+        self.proj_s = sp(self.proj[0]) if self.proj is not None else None
 
     # ----------------------------------------------------------------------------------------------------------
     def _workspace(self, name, nbytes):
@@ -142,34 +164,61 @@ class HubertEncoder:
         """Hubert frames of an n-sample input (after wav_pad), through the CNN extractor's valid convs."""
         return frame_count(self.arch, n_samples)
 
+    def _split_conv(self, i: int) -> bool:
+        return self.precision == "split" and self.conv_ws[i] is not None
+
     def feature_extractor(self, x: torch.Tensor, t0_len: torch.Tensor | None = None) -> torch.Tensor:
         """[B, N] -> [B, L, 512] (channels-last); GELU applied after every conv.  ``t0_len`` [B] int32: conv0
         frames per row of a variable-length batch (GroupNorm statistics); later convs need no lengths (their
-        valid rows only read valid rows)."""
+        valid rows only read valid rows).  In split precision a conv whose consumer is a split GEMM writes its
+        output as split planes (conv0's apply pass, the GEMM epilogues)."""
         a = self.arch
         B, N = x.shape
         ln0 = self.conv_ln[0]
+        n = len(a.conv_dim)
         if a.feat_extract_norm == "group":
             ws = self._workspace("conv0", ops._lib.lib().hfa_conv0_workspace_bytes(B, N))
-            h = ops.conv0(x, self.conv_w[0], gamma=ln0[0], beta=ln0[1], eps=1e-5, workspace=ws, t0_len=t0_len)
+            h = ops.conv0(x, self.conv_w[0], gamma=ln0[0], beta=ln0[1], eps=1e-5, workspace=ws, t0_len=t0_len,
+                          out_split=n > 1 and self._split_conv(1))
         else:
             h = ops.conv0(x, self.conv_w[0], bias=self.conv_b[0])
             h = ops.layernorm(h, ln0[0], ln0[1], a.layer_norm_eps, act=ops.ACT_GELU, out=h)
-        for i in range(1, len(a.conv_dim)):
+            if n > 1 and self._split_conv(1):
+                h = ops.split(h)
+        for i in range(1, n):
             k, s = a.conv_kernel[i], a.conv_stride[i]
-            Tin, Cin = h.shape[1], h.shape[2]
+            split_in = h.dtype == torch.float16
+            Tin, Cin = h.shape[-2], h.shape[-1]
             Tout = (Tin - k) // s + 1
             Cout = a.conv_dim[i]
-            out = torch.empty((B, Tout, Cout), dtype=torch.float32, device=x.device)
             layer_norm = self.conv_ln[i] is not None
-            ops.conv_gemm(h, self.conv_w[i], out, M=Tout, N=Cout, K=k * Cin, Zb=B, sAb=Tin * Cin, ldx=Cin,
-                          stride=s, Cg=Cin, Tin=Tin, bias=self.conv_b[i], sCb=Tout * Cout, ldc=Cout,
-                          epilogue=ops.EPI_NONE if layer_norm else ops.EPI_GELU)
+            split_out = split_in and not layer_norm and i + 1 < n and self._split_conv(i + 1)
+            out = torch.empty(((2,) if split_out else ()) + (B, Tout, Cout),
+                              dtype=torch.float16 if split_out else torch.float32, device=x.device)
+            kw = dict(M=Tout, N=Cout, K=k * Cin, Zb=B, sAb=Tin * Cin, ldx=Cin, stride=s, Cg=Cin, Tin=Tin,
+                      bias=self.conv_b[i], sCb=Tout * Cout, ldc=Cout,
+                      epilogue=ops.EPI_NONE if layer_norm else ops.EPI_GELU)
+            if split_in:
+                ops.conv_gemm_split(h, self.conv_ws[i], C=None if split_out else out, Cs=out if split_out else None,
+                                    **kw)
+            else:
+                ops.conv_gemm(h, self.conv_w[i], out, **kw)
             if layer_norm:
                 out = ops.layernorm(out, self.conv_ln[i][0], self.conv_ln[i][1], a.layer_norm_eps,
                                     act=ops.ACT_GELU, out=out)
+                if i + 1 < n and self._split_conv(i + 1):
+                    out = ops.split(out)
             h = out
         return h
+
+    def _linear(self, x, w, ws, bias=None, residual=None, epilogue=ops.EPI_NONE, out_split=False, xs=None):
+        """Linear on the split GEMM when this encoder runs split and the weight has planes (x given as f32 and/or
+        as planes xs), else on the f32 GEMM."""
+        if self.precision == "split" and ws is not None:
+            if xs is None:
+                xs = ops.split(x)
+            return ops.linear_split(xs, ws, bias, residual=residual, epilogue=epilogue, out_split=out_split)
+        return ops.linear(x, w, bias, residual=residual, epilogue=epilogue)
 
     def positional(self, h: torch.Tensor, lens: torch.Tensor | None = None) -> torch.Tensor:
         """h + GELU(grouped conv k128 pad64 (+bias), last frame dropped) — one GEMM launch over (batch, group).
@@ -191,7 +240,7 @@ class HubertEncoder:
         B, L, H = h_in.shape
         nh = a.heads
         dh = H // nh
-        qkv = ops.linear(h_in, L_.wqkv, L_.bqkv)
+        qkv = self._linear(h_in, L_.wqkv, L_.wqkv_s, L_.bqkv)
         o = torch.empty((B, L, H), dtype=torch.float32, device=h_in.device)
         ops.attention(qkv, qkv[..., H:], qkv[..., 2 * H:], o, B=B, H=nh, L=L, head_dim=dh, scale=dh ** -0.5,
                       q_bs=L * 3 * H, q_ld=3 * H, k_bs=L * 3 * H, k_ld=3 * H, v_bs=L * 3 * H, v_ld=3 * H,
@@ -200,19 +249,23 @@ class HubertEncoder:
 
     def layer(self, h: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None) -> torch.Tensor:
         eps = self.arch.layer_norm_eps
+        sp = self.precision == "split" and L_.w1_s is not None and L_.w2_s is not None
         if not self.arch.stable_layer_norm:   # post-LN (HubertEncoderLayer / nn.TransformerEncoderLayer)
             o = self.attention_block(h, L_, lens)
-            h1 = ops.linear(o, L_.wo, L_.bo, residual=h)
+            h1 = self._linear(o, L_.wo, L_.wo_s, L_.bo, residual=h)
             h1 = ops.layernorm(h1, L_.ln1_w, L_.ln1_b, eps, out=h1)
-            f = ops.linear(h1, L_.w1, L_.b1, epilogue=ops.EPI_GELU)
-            h2 = ops.linear(f, L_.w2, L_.b2, residual=h1)
+            f = self._linear(h1, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp)
+            h2 = self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h1, xs=f) if sp else \
+                ops.linear(f, L_.w2, L_.b2, residual=h1)
             return ops.layernorm(h2, L_.ln2_w, L_.ln2_b, eps, out=h2)
         # pre-LN (HubertEncoderLayerStableLayerNorm)
         a_ = ops.layernorm(h, L_.ln1_w, L_.ln1_b, eps)
         o = self.attention_block(a_, L_, lens)
-        h = ops.linear(o, L_.wo, L_.bo, residual=h)
+        h = self._linear(o, L_.wo, L_.wo_s, L_.bo, residual=h)
         a_ = ops.layernorm(h, L_.ln2_w, L_.ln2_b, eps)
-        f = ops.linear(a_, L_.w1, L_.b1, epilogue=ops.EPI_GELU)
+        f = self._linear(a_, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp)
+        if sp:
+            return self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h, xs=f)
         return ops.linear(f, L_.w2, L_.b2, residual=h)
 
     @torch.no_grad()
@@ -239,7 +292,7 @@ class HubertEncoder:
             x = ops.pad_rows(x, a.wav_pad, x.shape[1] + 2 * a.wav_pad)
         feats = self.feature_extractor(x, lens0)
         fln = ops.layernorm(feats, self.fp_ln[0], self.fp_ln[1], a.layer_norm_eps)
-        h = ops.linear(fln, self.fp_w, self.fp_b)
+        h = self._linear(fln, self.fp_w, self.fp_ws, self.fp_b)
         h = self.positional(h, lensL)
         if not a.stable_layer_norm:
             h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
@@ -248,7 +301,7 @@ class HubertEncoder:
         if a.stable_layer_norm:
             h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
         if self.proj is not None:
-            h = ops.linear(h, self.proj[0], self.proj[1])
+            h = self._linear(h, self.proj[0], self.proj_s, self.proj[1])
         return h
 
     __call__ = forward

@@ -132,6 +132,12 @@ _lib.register("hfa_conv_gemm_f32", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _I
 _lib.register("hfa_gemm_tuning", [_I_, _I_])
 _lib.register("hfa_gemm_kernel_name", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_, _LL_,
                                        _I_, _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _I_], ctypes.c_char_p)
+_lib.register("hfa_conv_gemm_split", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_,
+                                       _LL_, _LL_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _P_, _LL_, _LL_, _LL_,
+                                       _I_, _I_, _P_, _P_])
+_lib.register("hfa_gemm_split_kernel_name", [_I_, _I_, _I_, _I_, _I_], ctypes.c_char_p)
+_lib.register("hfa_gemm_split_tuning", [_I_])
+_lib.register("hfa_split_f16", [_I_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _P_, _P_])
 _lib.register("hfa_gemm_f32", [_I_, _I_, _I_, _P_, _I_, _P_, _I_, _P_, _P_, _I_, _P_, _I_, _I_, _P_])
 _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_,
                                     _LL_, _I_, _P_, _P_])
@@ -141,6 +147,8 @@ _lib.register("hfa_groupnorm_f32", [_I_, _I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_
 _lib.register("hfa_groupnorm_workspace_bytes", [_I_, _I_, _I_, _I_], ctypes.c_longlong)
 _lib.register("hfa_conv0_workspace_bytes", [_I_, _I_], ctypes.c_longlong)
 _lib.register("hfa_conv0_f32", [_I_, _I_, _P_, _LL_, _P_, _P_, _I_, _P_, _P_, _F_, _P_, _P_, _LL_, _P_, _P_])
+_lib.register("hfa_conv0_split", [_I_, _I_, _P_, _LL_, _P_, _P_, _I_, _P_, _P_, _F_, _P_, _P_, _LL_, _LL_, _P_, _P_,
+                                   _P_])
 _lib.register("hfa_units_gather_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _P_, _P_])
 _lib.register("hfa_mask_rows_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_])
 _lib.register("hfa_wav_normalize_f32", [_I_, _I_, _P_, _LL_, _F_, _P_, _LL_, _P_, _P_])
@@ -245,6 +253,83 @@ def linear(x, W, bias=None, residual=None, out=None, epilogue=EPI_NONE):
     return out
 
 
+# ---- split-f16 operands (gemm.hip gemm_split_kernel) ----------------------------------------------------------
+# A split tensor is a float16 tensor [2, *shape]: plane 0 = f16(x), plane 1 = f16((x - plane0) * 2^11).
+_OFLOW = {}
+
+
+def split_flag(device) -> torch.Tensor:
+    """Device int32 flag the split producers raise when a value leaves f16 range (|x| >= 65504 / non-finite);
+    the caller re-runs that batch on the f32 path (see task.ForcedAlignmentTask)."""
+    key = torch.device(device)
+    if key.type == "cuda" and key.index is None:
+        key = torch.device("cuda", torch.cuda.current_device())
+    if key not in _OFLOW:
+        _OFLOW[key] = torch.zeros(1, dtype=torch.int32, device=key)
+    return _OFLOW[key]
+
+
+def split(x, out=None):
+    """f32 [..., C] (row-strided) -> split planes [2, ..., C]."""
+    _need(x, torch.float32, "x", contiguous=False)
+    C = x.shape[-1]
+    x2 = x.reshape(-1, C) if x.dim() != 2 else x
+    if x2.stride(-1) != 1:
+        raise ValueError("split: last dim must be contiguous")
+    rows = x2.shape[0]
+    if out is None:
+        out = torch.empty((2, *x.shape), dtype=torch.float16, device=x.device)
+    o2 = out.view(2, rows, C)
+    _lib.call("hfa_split_f16", rows, C, _ptr(x2), x2.stride(0), _ptr(o2), o2.stride(1), o2.stride(0),
+              _ptr(split_flag(x.device)), _stream(x.device))
+    return out
+
+
+def _split_name(M, N, Z, out_split, epilogue) -> str:
+    return _lib.lib().hfa_gemm_split_kernel_name(M, N, Z, int(out_split), epilogue).decode()
+
+
+def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None,
+                    Tin=None, sWg=0, ldw=None, bias=None, sBg=0, R=None, sRb=0, sRg=0, ldr=0, sCb=0, sCg=0, ldc,
+                    epilogue=EPI_NONE):
+    """conv_gemm on split operands (As, Ws: [2, ...] f16 planes; strides in elements of one plane).  Output to f32
+    C (+R) or to split planes Cs [2, ...] (bias/GELU epilogue only)."""
+    _need(As, torch.float16, "As", contiguous=False)
+    _need(Ws, torch.float16, "Ws", contiguous=False)
+    if (C is None) == (Cs is None):
+        raise ValueError("conv_gemm_split: exactly one of C / Cs")
+    dev = (C if C is not None else Cs).device
+    args = (M, N, K, Zb, G, _ptr(As), As.stride(0), sAb, sAg, ldx, stride, pad, Cg or K, Tin if Tin is not None else M,
+            _ptr(Ws), Ws.stride(0), sWg, ldw if ldw is not None else K, _ptr(bias), sBg, _ptr(R), sRb, sRg, ldr,
+            _ptr(C), _ptr(Cs), Cs.stride(0) if Cs is not None else 0, sCb, sCg, ldc, epilogue,
+            _ptr(split_flag(dev)))
+
+    def launch():
+        _lib.call("hfa_conv_gemm_split", *args, _stream(dev))
+    if PROBE is None:
+        return launch()
+    PROBE(_split_name(M, N, Zb * G, Cs is not None, epilogue), 2.0 * M * N * K * Zb * G, launch)
+
+
+def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, out_split=False):
+    """y = epi(x @ W^T + bias) (+ residual) with x, W given as split planes [2, ..., K] / [2, N, K]; y f32, or split
+    planes [2, ..., N] when out_split (no residual)."""
+    K = xs.shape[-1]
+    N = Ws.shape[1]
+    lead = xs.shape[1:-1]
+    M = 1
+    for d in lead:
+        M *= d
+    if out is None:
+        out = torch.empty(((2,) if out_split else ()) + (*lead, N), dtype=torch.float16 if out_split else torch.float32,
+                          device=xs.device)
+    r2 = residual.reshape(-1, N) if residual is not None else None
+    conv_gemm_split(xs, Ws, C=None if out_split else out, Cs=out if out_split else None, M=M, N=N, K=K,
+                    ldx=xs.stride(-2) if xs.dim() > 2 else K, bias=bias, R=r2, ldr=r2.stride(0) if r2 is not None else 0,
+                    ldc=N, epilogue=epilogue)
+    return out
+
+
 def _lens(lens):
     """Optional per-row lengths of a variable-length batch: None or an int32 device tensor [B]."""
     if lens is None:
@@ -299,13 +384,15 @@ def groupnorm(x, G, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, t_len=None):
     return out
 
 
-def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, workspace=None, t0_len=None):
+def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, workspace=None, t0_len=None,
+          out_split=False):
     """First extractor conv (1->512, k10, s5) -> [B, T0, 512]; GroupNorm+GELU when gamma/beta are given
-    (statistics over t0_len[b] frames if given)."""
+    (statistics over t0_len[b] frames if given).  out_split: the output as split-f16 planes [2, B, T0, 512]."""
     B, N = x.shape
     T0 = (N - 10) // 5 + 1
     if out is None:
-        out = torch.empty((B, T0, 512), dtype=torch.float32, device=x.device)
+        out = torch.empty(((2,) if out_split else ()) + (B, T0, 512),
+                          dtype=torch.float16 if out_split else torch.float32, device=x.device)
     norm = gamma is not None
     if norm and workspace is None:
         nbytes = _lib.lib().hfa_conv0_workspace_bytes(B, N)
@@ -313,9 +400,14 @@ def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, worksp
     tl = _lens(t0_len)
 
     def launch():
-        _lib.call("hfa_conv0_f32", B, N, _ptr(x), x.stride(0), _ptr(w0), _ptr(bias), 1 if norm else 0,
-                  _ptr(gamma), _ptr(beta), float(eps), _ptr(workspace), _ptr(out), out.stride(0), _ptr(tl),
-                  _stream(x.device))
+        if out_split:
+            _lib.call("hfa_conv0_split", B, N, _ptr(x), x.stride(0), _ptr(w0), _ptr(bias), 1 if norm else 0,
+                      _ptr(gamma), _ptr(beta), float(eps), _ptr(workspace), _ptr(out), out.stride(1), out.stride(0),
+                      _ptr(split_flag(x.device)), _ptr(tl), _stream(x.device))
+        else:
+            _lib.call("hfa_conv0_f32", B, N, _ptr(x), x.stride(0), _ptr(w0), _ptr(bias), 1 if norm else 0,
+                      _ptr(gamma), _ptr(beta), float(eps), _ptr(workspace), _ptr(out), out.stride(0), _ptr(tl),
+                      _stream(x.device))
     if PROBE is None:
         launch()
     else:                       # wave in (4 B/sample) + activations out (4 B x 512 x T0)

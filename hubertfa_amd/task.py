@@ -136,6 +136,28 @@ class ForcedAlignmentTask:
         frame, edge = logits[:, :, 2:], logits[:, :, 0]      # LatticeHead.split without the unused ctc logits
         return self.decoder.decode_batch(frame, edge, wav_lengths, ph_seqs, word_seqs, p2ws, host=False)
 
+    def _guard(self, dev_out, redo_args):
+        """Split-precision range guard: snapshot (and clear) the split-f16 overflow flag the batch's producers
+        raise (ops.split_flag) into the batch's outputs, and attach a re-run of the batch on the f32 GEMMs that
+        ``decoder.assemble`` takes instead when the flag is set."""
+        enc = getattr(self.unitsEncoder, "model", None)
+        if getattr(enc, "precision", "f32") != "split":
+            return dev_out
+        flag = ops.split_flag(self.device)
+        dev_out["split_oflow"] = flag.clone()
+        flag.zero_()
+        dev_out["redo"] = lambda: self._align_f32(*redo_args)
+        return dev_out
+
+    def _align_f32(self, waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds):
+        enc = self.unitsEncoder.model
+        enc.precision = "f32"
+        try:
+            return self.align_batch(waves, ph_seqs, word_seqs, p2ws, wav_sr=wav_sr, lengths=lengths,
+                                    chunk_seconds=chunk_seconds)
+        finally:
+            enc.precision = "split"
+
     def align_batch(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
                     host: bool = True, lengths=None, chunk_seconds: float | None = None):
         """B waveforms [B, N] (at melspec sample_rate, or ``wav_sr`` to resample first, like load_wav) ->
@@ -143,6 +165,7 @@ class ForcedAlignmentTask:
         path).  Rows of different lengths: zero-pad to N and pass ``lengths``."""
         feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds)
         dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
+        dev_out = self._guard(dev_out, (waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds))
         if not host:
             return dev_out
         return self.decoder.assemble(dev_out, ph_seqs, word_seqs, p2ws)
@@ -159,12 +182,16 @@ class ForcedAlignmentTask:
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
         feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds)
+        guard = self._guard({}, (waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds))
         ready = torch.cuda.Event()
         ready.record(main)
         with torch.cuda.stream(self._side):
             self._side.wait_event(ready)
             feats.record_stream(self._side)      # the caching allocator must not recycle it under the side stream
             dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
+            if "split_oflow" in guard:
+                guard["split_oflow"].record_stream(self._side)
+            dev_out.update(guard)
             if on_device is not None:
                 on_device(dev_out)
             return self.decoder.fetch(dev_out)

@@ -97,6 +97,27 @@ const char* hfa_gemm_kernel_name(int M, int N, int K, int Zb, int G, const float
 int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, int ldw, const float* bias,
                  const float* R, int ldr, float* C, int ldc, int epilogue, hipStream_t stream);
 
+/* ---- split-f16 GEMM (gemm.hip gemm_split_kernel) -------------------------------------------------------------
+ * The same contractions as hfa_conv_gemm_f32 with f32-class accuracy on the f16 MFMA: every f32 operand x is
+ * carried as two f16 planes, x1 = f16(x) and x2 = f16((x - x1) * 2^11) (plane 1 at +sAp / +sWp / +sCp halves;
+ * every stride in halves), and A.W = A1.W1 + 2^-11 (A1.W2 + A2.W1), each partial product exact in f32.
+ * Requirements: K, Cg multiples of 32; A/W 16-B aligned with 8-half strides; |x| < 65504 for every split value
+ * (producers raise *oflow otherwise; the caller recomputes on the f32 path).  Output: f32 C (+R, 16-B rows) or,
+ * with Cs non-NULL (C NULL), split planes of epi(acc + bias) (no R). */
+int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, long long sAp, long long sAb,
+                        long long sAg, int ldx, int stride, int pad, int Cg, int Tin, const uint16_t* W,
+                        long long sWp, long long sWg, int ldw, const float* bias, long long sBg, const float* R,
+                        long long sRb, long long sRg, int ldr, float* C, uint16_t* Cs, long long sCp, long long sCb,
+                        long long sCg, int ldc, int epilogue, int* oflow, hipStream_t stream);
+/* rocprof symbol stem of the split instantiation for an M x N output over Z = Zb*G (out_split: planes out). */
+const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue);
+/* Tile override for the split GEMM: 0 auto, 1 128x128, 2 128x64, 3 256x128 (8 waves). */
+int hfa_gemm_split_tuning(int cfg);
+/* x [rows, cols] f32 (row stride ldx) -> split planes y (row stride ldy, plane 1 at +sp); raises *oflow (if
+ * non-NULL) for |x| >= 65504 or a non-finite x. */
+int hfa_split_f16(int rows, int cols, const float* x, long long ldx, uint16_t* y, long long ldy, long long sp,
+                  int* oflow, hipStream_t stream);
+
 /* ---- attention (hubertfa_amd/csrc/attention.hip) -----------------------------------------------------------
  * O = softmax(scale * Q K^T) V per (batch, head), head_dim 64, fp32 MFMA flash attention.
  * Q(b,h,i,d) at q + b*q_bs + i*q_ld + h*64 + d (same for k, v, o).
@@ -131,6 +152,11 @@ long long hfa_conv0_workspace_bytes(int B, int N);
 int hfa_conv0_f32(int B, int N, const float* x, long long x_bs, const float* w0, const float* bias, int norm,
                   const float* gamma, const float* beta, float eps, void* workspace, float* y, long long y_bs,
                   const int32_t* t0_len, hipStream_t stream);
+/* hfa_conv0_f32 with the output written as split-f16 planes (see hfa_conv_gemm_split): ys [2][B][T0][512],
+ * batch stride y_bs and plane stride y_sp in halves; *oflow raised for outputs outside f16 range. */
+int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w0, const float* bias, int norm,
+                    const float* gamma, const float* beta, float eps, void* workspace, uint16_t* ys, long long y_bs,
+                    long long y_sp, int* oflow, const int32_t* t0_len, hipStream_t stream);
 
 /* ---- glue (hubertfa_amd/csrc/misc.hip) -----------------------------------------------------------------------
  * Nearest-frame gather onto the DP grid, tools/encoder.py:56-59: idx[k] = min(rint(f32(ratio)*k), U-1),

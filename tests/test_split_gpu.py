@@ -1,0 +1,144 @@
+"""Split-f16 GEMM path (gemm.hip gemm_split_kernel, hfa_split_f16, conv0 split output) against fp64 CPU references.
+
+The split operand x = x1 + 2^-11 x2 keeps 22 significand bits; the product adds three exact f16 x f16 partial
+products in f32.  Bars: the same tolerances as the f32 MFMA GEMM tests (2e-5 relative + 2e-5 absolute on unit-scale
+data) — the split path is measured at or below the f32 path's own error (scripts/split_gemm_bench.py).
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+F = torch.nn.functional
+
+
+def _r(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+def _close(got, ref, rtol, atol):
+    got = got.detach().cpu().double()
+    ref = ref.detach().cpu().double()
+    err = (got - ref).abs()
+    assert bool((err <= atol + rtol * ref.abs()).all()), f"max err {float(err.max()):.3e}"
+
+
+def test_split_planes_and_flag():
+    from hubertfa_amd import ops
+    d = torch.device("cuda")
+    x = torch.cat([_r(1000, seed=1) * 100, _r(1000, seed=2) * 1e-3, torch.tensor([0.0, 1e-9, -65000.0, 3.0e-5])])
+    x = x.reshape(1, -1)[:, :2000].contiguous()
+    flag = ops.split_flag(d)
+    flag.zero_()
+    s = ops.split(x.to(d)).cpu().float()
+    back = s[0] + s[1] / 2048.0
+    err = (back.double() - x.double()).abs()
+    assert bool((err <= 2.0 ** -22 * x.abs().double() + 2.0 ** -36).all())
+    assert int(flag.item()) == 0
+    for bad in (70000.0, float("inf"), float("nan")):
+        flag.zero_()
+        ops.split(torch.tensor([[1.0, bad, 2.0, 3.0, 4.0]], device=d))
+        assert int(flag.item()) == 1, bad
+    flag.zero_()
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K,epi,res,outs", [(300, 200, 128, 0, False, False), (1000, 768, 768, 1, False, False),
+                                                (257, 72, 192, 0, True, False), (4096, 3072, 768, 1, False, True),
+                                                (130, 2304, 768, 0, False, True), (64, 768, 3072, 0, True, False)])
+def test_split_linear(cfg, M, N, K, epi, res, outs):
+    from hubertfa_amd import ops, _lib
+    d = torch.device("cuda")
+    x, w, b = _r(M, K, seed=1), _r(N, K, seed=2, scale=K ** -0.5), _r(N, seed=3)
+    r = _r(M, N, seed=4) if res else None
+    ref = x.double() @ w.double().T + b.double()
+    if epi:
+        ref = F.gelu(ref)
+    if res:
+        ref = ref + r.double()
+    _lib.lib().hfa_gemm_split_tuning(cfg)
+    try:
+        got = ops.linear_split(ops.split(x.to(d)), ops.split(w.to(d)), b.to(d), residual=r.to(d) if res else None,
+                               epilogue=epi, out_split=outs)
+    finally:
+        _lib.lib().hfa_gemm_split_tuning(0)
+    if outs:
+        got = got[0].float() + got[1].float() / 2048.0
+        _close(got, ref, 2e-5 + 2.0 ** -21, 2e-5)
+    else:
+        _close(got, ref, 2e-5, 2e-5)
+
+
+@pytest.mark.parametrize("Cin,Cout,k,s,pad,T", [(512, 512, 3, 2, 0, 301), (512, 512, 2, 2, 0, 100),
+                                                (192, 192, 3, 1, 1, 64), (192, 384, 2, 2, 0, 40)])
+def test_split_conv_vs_conv1d(Cin, Cout, k, s, pad, T):
+    from hubertfa_amd import ops
+    B = 3
+    d = torch.device("cuda")
+    x = _r(B, T, Cin, seed=5)
+    w = _r(Cout, Cin, k, seed=6, scale=(Cin * k) ** -0.5)
+    b = _r(Cout, seed=7)
+    ref = F.conv1d(x.double().transpose(1, 2), w.double(), b.double(), stride=s, padding=pad).transpose(1, 2)
+    Tout = ref.shape[1]
+    wi = w.permute(0, 2, 1).reshape(Cout, k * Cin).contiguous()
+    y = torch.empty(B, Tout, Cout, device=d)
+    ops.conv_gemm_split(ops.split(x.to(d)), ops.split(wi.to(d)), C=y, M=Tout, N=Cout, K=k * Cin, Zb=B, sAb=T * Cin,
+                        ldx=Cin, stride=s, pad=pad, Cg=Cin, Tin=T, bias=b.to(d), sCb=Tout * Cout, ldc=Cout)
+    _close(y, ref, 2e-5, 2e-5)
+
+
+def test_conv0_split_output_matches_f32():
+    from hubertfa_amd import ops
+    d = torch.device("cuda")
+    B, N = 2, 16000
+    x = _r(B, N, seed=8).to(d)
+    w0 = _r(512, 10, seed=9, scale=0.3).to(d)
+    g, bb = (1 + 0.1 * _r(512, seed=10)).to(d), (0.1 * _r(512, seed=11)).to(d)
+    y32 = ops.conv0(x, w0, gamma=g, beta=bb)
+    ys = ops.conv0(x, w0, gamma=g, beta=bb, out_split=True)
+    hi = ys[0].float()
+    assert torch.equal(hi, y32.half().float())
+    back = hi.double() + ys[1].double() / 2048.0
+    assert float((back - y32.double()).abs().max()) <= 2.0 ** -22 * float(y32.abs().max()) + 1e-9
+
+
+def test_encoder_split_vs_f32_precision():
+    """The whole Hubert-base encoder, split vs f32 GEMMs: units agree to f32-path accuracy."""
+    from hubertfa_amd import synth
+    from hubertfa_amd.hubert import HubertEncoder
+    d = torch.device("cuda")
+    arch = synth.arch_cnhubert_base()
+    sd = synth.synth_hubert_state_dict(arch, seed=0)
+    wav = _r(2, 32000, seed=12).to(d) * 0.1
+    u32 = HubertEncoder(arch, sd, d, precision="f32")(wav)
+    us = HubertEncoder(arch, sd, d, precision="split")(wav)
+    assert float((us - u32).abs().max()) < 2e-4 * max(1.0, float(u32.abs().max()))
+
+
+def test_range_guard_reruns_batch_on_f32():
+    """An activation outside f16 range raises the split flag; assemble returns the f32-GEMM re-run of the batch,
+    identical to running the batch with precision f32."""
+    import bench
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+    d = torch.device("cuda")
+    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
+    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=d)
+    task.on_predict_start()
+    enc = task.unitsEncoder.model
+    enc.conv_ln[0][1][5] = 1.0e5            # GroupNorm beta of one conv0 channel: that channel's output ~1e5
+    wav, ph_seqs, word_seqs, p2ws = bench.make_inputs(2, 2.0, 6, 5)
+    w = torch.from_numpy(wav).to(d)
+    calls = []
+    redo = task._align_f32
+    task._align_f32 = lambda *a: calls.append(1) or redo(*a)
+    got = task.align_batch(w, ph_seqs, word_seqs, p2ws, wav_sr=16000)
+    assert calls == [1]
+    assert enc.precision == "split"
+    enc.precision = "f32"
+    ref = task.align_batch(w, ph_seqs, word_seqs, p2ws, wav_sr=16000)
+    enc.precision = "split"
+    for a, b in zip(got, ref):
+        assert list(a["ph_seq"]) == list(b["ph_seq"])
+        assert (a["ph_intervals"] == b["ph_intervals"]).all()
+    import hubertfa_amd.ops as ops
+    assert int(ops.split_flag(d).item()) == 0
