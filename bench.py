@@ -5,7 +5,9 @@ One step = the whole infer path for one batch, wave in HBM -> phoneme boundaries
   16k->44.1k sinc resample (load_wav) -> 44.1k->16k sinc resample (UnitsEncoder) -> Hubert-base (7 convs,
   projection, positional conv, 12 post-LN layers) -> nearest-frame gather -> UNet + head -> lattice prologue
   -> Viterbi DP -> backtrack -> device->host copy -> interval/word assembly (+ RCCL gather of boundary arrays
-  when N > 1).  All arithmetic is f32 (the parity configuration).  Weights are seeded synthetic (no checkpoint
+  when N > 1).  Arithmetic is f32-class: every dense contraction (GEMMs, convs, attention) carries its f32
+  operands as split-f16 plane pairs on the f16 MFMA (three exact partial products, f32 accumulation; a batch
+  whose values leave f16 range re-runs on the f32 MFMA), everything else is f32.  Weights are seeded synthetic (no checkpoint
   offline), inputs are synthetic harmonic audio + 30 two-phone words (S = 91).
 
 Multi-GPU: one process per GPU (torch.distributed.run); each rank aligns its own B utterances (weak scaling);
@@ -41,7 +43,8 @@ SPLIT_F32EQ_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 
 
 def mfma_peak(kernel: str) -> float:
-    return SPLIT_F32EQ_PEAK_TFLOPS if kernel.startswith("gemm_split_kernel") else F32_MFMA_PEAK_TFLOPS
+    split = kernel.startswith("gemm_split_kernel") or kernel.startswith("attn_fwd_split_kernel")
+    return SPLIT_F32EQ_PEAK_TFLOPS if split else F32_MFMA_PEAK_TFLOPS
 HBM_PEAK_GBPS = 8000.0             # MI355X HBM3E, MI355X_MICROARCH.md
 
 
@@ -141,7 +144,7 @@ def config_name(encoder: str, world: int, B: int, seconds: float = 10.0) -> str:
     return "config 3 geometry" + ("" if world * B == 512 else f" (global batch {world * B}, config 3 is 512)")
 
 
-SECONDARY = ("viterbi_forward_kernel", "hfa_conv0_f32", "attn_fwd_f32_kernel")
+SECONDARY = ("viterbi_forward_kernel", "hfa_conv0_f32", "attn_fwd_split_kernel", "attn_fwd_f32_kernel")
 
 
 def secondary_rooflines(iso, pipe, T, S):
@@ -156,7 +159,7 @@ def secondary_rooflines(iso, pipe, T, S):
         if not ps["launches"]:
             continue
         rate = ps["avg_work"] / (ps["avg_ms"] * 1e-3)
-        if name == "attn_fwd_f32_kernel":
+        if name.startswith("attn_fwd"):
             e = {"kernel": name, "bound": "mfma", "achieved": rate / 1e12, "peak": mfma_peak(name),
                  "unit": "TFLOP/s", "frac": rate / 1e12 / mfma_peak(name)}
         else:
@@ -277,6 +280,8 @@ def main():
         "metric": METRIC, "value": value, "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "arithmetic": "f32 operands as split-f16 pairs (x = x1 + 2^-11 x2) on v_mfma_f32_32x32x16_f16, 3 exact products per "
+                      "f32 MAC, f32 accumulate; norms/softmax/DP in f32 (DP f32/f64 as the reference)",
         "config": {"workload": f"{config_name(args.encoder, world, B, args.seconds)}"
                                f"{'' if args.chunk_seconds is None else f', chunked {args.chunk_seconds:g} s windows'}: "
                                f"B={B} x {args.seconds:g} s 16 kHz utterances per GPU, "

@@ -212,6 +212,263 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
     }
 }
 
+// ---- split-f16 flash attention ---------------------------------------------------------------------------------
+// Q, K, V and O as split-f16 plane pairs (x = x1 + 2^-11 x2, gemm.hip's split scheme): every product is three exact
+// f16 x f16 MFMA products (x1 y1 into a main accumulator, x1 y2 + x2 y1 into a correction accumulator scaled by
+// 2^-11 at the end), so the contractions keep f32-class accuracy while running on v_mfma_f32_32x32x16_f16.
+// Same structure as attn_fwd_f32_kernel (S^T = K Q^T with one query per lane, stale-max online softmax in the
+// exp2 domain, the P accumulator as the B operand of O^T += V^T P^T), with 64-key tiles and:
+//   * K image [64 keys][8 chunks of 16 B] per plane, chunk c of row r at slot c ^ ((r >> 1) & 7): the
+//     ds_read_b128 row reads of the 32x32x16 A operand are conflict-free;
+//   * V image, same shape, chunk c of row r at slot c ^ (((r >> 1) & 1) << 2), read with ds_read_b64_tr_b16
+//     (4 keys x 16 d per 16-lane group, delivered column-major): the V^T operand with no transposing pass;
+//   * P split in registers (p <= 2^8 under the stale max, far inside f16 range); the scale * log2(e) factor
+//     multiplies the f32 score (Q stays exactly the producer's planes);
+//   * O normalised in f32 and written back as split planes for the out-projection's split GEMM.
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int SKB = 64;              // keys per tile
+constexpr int SNS = 2;               // LDS stages
+constexpr int SPLANE = SKB * DH;     // halves per plane image (8 KiB)
+constexpr int SSTAGE = 4 * SPLANE;   // K1, K2, V1, V2
+constexpr float kLo = 1.0f / 2048.0f;
+
+struct AttnSP {
+    int B, H, L;
+    float scale;
+    const _Float16* q; long long q_sp, q_bs; int q_ld;
+    const _Float16* k; long long k_sp, k_bs; int k_ld;
+    const _Float16* v; long long v_sp, v_bs; int v_ld;
+    _Float16* o; long long o_sp, o_bs; int o_ld;
+    const int32_t* key_len;
+};
+
+__device__ __forceinline__ f16x4 lds_tr(const _Float16* base, int byte_off) {
+    const auto* ptr = reinterpret_cast<const __attribute__((address_space(3))) s16x4*>(
+        reinterpret_cast<const __attribute__((address_space(3))) char*>(
+            (const __attribute__((address_space(3))) _Float16*)base) + byte_off);
+    return __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        const_cast<__attribute__((address_space(3))) s16x4*>(ptr)));
+}
+
+__global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP p) {
+    __shared__ __attribute__((aligned(16))) _Float16 smem[SNS * SSTAGE];
+
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, xq = nwg >> 3, xr = nwg & 7;
+    const int wgid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (orig >> 3);
+    const int nqb = (p.L + QW * NW - 1) / (QW * NW);
+    const int bh = wgid / nqb, qb = wgid - bh * nqb;
+    const int b = bh / p.H, hd = bh - b * p.H;
+    const int L = p.key_len ? p.key_len[b] : p.L;
+    if (qb * (QW * NW) >= L) return;                     // whole workgroup is padding (uniform exit)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r32 = lane & 31, half = lane >> 5;
+    const int q0 = qb * (QW * NW) + wave * QW;
+    const int qi = q0 + r32;
+
+    const _Float16* Q = p.q + b * p.q_bs + hd * DH;
+    const _Float16* Kp = p.k + b * p.k_bs + hd * DH;
+    const _Float16* Vp = p.v + b * p.v_bs + hd * DH;
+    const long long kbytes = ((long long)(L - 1) * p.k_ld + DH) * 2, vbytes = ((long long)(L - 1) * p.v_ld + DH) * 2;
+    const __amdgpu_buffer_rsrc_t rK1 = hfa::make_rsrc(Kp, kbytes), rK2 = hfa::make_rsrc(Kp + p.k_sp, kbytes);
+    const __amdgpu_buffer_rsrc_t rV1 = hfa::make_rsrc(Vp, vbytes), rV2 = hfa::make_rsrc(Vp + p.v_sp, vbytes);
+
+    // Q fragments (B operand of S^T = K Q^T): lane holds Q[qi][16 kb + 8 half + j], j = 0..7
+    f16x8 q1[DH / 16], q2[DH / 16];
+#pragma unroll
+    for (int kb = 0; kb < DH / 16; ++kb) {
+        if (qi < L) {
+            const _Float16* src = Q + (long long)qi * p.q_ld + kb * 16 + half * 8;
+            q1[kb] = *reinterpret_cast<const f16x8*>(src);
+            q2[kb] = *reinterpret_cast<const f16x8*>(src + p.q_sp);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) q1[kb][j] = q2[kb][j] = (_Float16)0.0f;
+        }
+    }
+
+    // DMA geometry: per plane 8 x 1 KiB pieces of 8 rows, 2 per wave; lane -> row 8 piece + lane/8, slot lane&7
+    int rowd[2], kch[2], vch[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+        rowd[d] = (wave * 2 + d) * 8 + (lane >> 3);
+        kch[d] = (lane & 7) ^ ((rowd[d] >> 1) & 7);
+        vch[d] = (lane & 7) ^ (((rowd[d] >> 1) & 1) << 2);
+    }
+    const unsigned lds0 = hfa::lds_addr(smem);
+    auto issue = [&](int stage, int key0) {
+        const unsigned base = lds0 + stage * SSTAGE * 2 + wave * 2 * 1024;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            const int key = key0 + rowd[d];
+            const bool ok = key < L;
+            const unsigned ko = ok ? (unsigned)((key * p.k_ld + kch[d] * 8) * 2) : hfa::DMA_OOB;
+            const unsigned vo = ok ? (unsigned)((key * p.v_ld + vch[d] * 8) * 2) : hfa::DMA_OOB;
+            hfa::dma16(ko, rK1, 0u, base + d * 1024);
+            hfa::dma16(ko, rK2, 0u, base + SPLANE * 2 + d * 1024);
+            hfa::dma16(vo, rV1, 0u, base + 2 * SPLANE * 2 + d * 1024);
+            hfa::dma16(vo, rV2, 0u, base + 3 * SPLANE * 2 + d * 1024);
+        }
+    };
+
+    // K row reads: row 32 kt + r32, chunk 2 kb + half (halves within a plane image)
+    int kofs[DH / 16];
+#pragma unroll
+    for (int kb = 0; kb < DH / 16; ++kb) kofs[kb] = r32 * DH + (((kb * 2 + half) ^ ((r32 >> 1) & 7)) << 3);
+    // V transposed reads: 16-lane group g supplies rows r0 + (i >> 2), columns c0 + 4 (i & 3) of its block
+    const int gi = lane & 15, gq = gi >> 2, gp = gi & 3;
+    const int vrow = 4 * half + gq;                                   // row within the (kt, s, jj) 8-row step
+    const int vch0 = 2 * ((lane >> 4) & 1) + (gp >> 1);               // chunk within the 32-column block
+    const int vfx = (((vrow >> 1) & 1) << 2);                         // the row's swizzle (rows r0 = 0 mod 4)
+    int vofs[2];                                                      // bytes, per d-block db
+#pragma unroll
+    for (int db = 0; db < 2; ++db) vofs[db] = vrow * (DH * 2) + (((4 * db + vch0) ^ vfx) << 4) + 8 * (gp & 1);
+
+    f32x16 oM[2], oC[2];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) oM[0][e] = oM[1][e] = oC[0][e] = oC[1][e] = 0.f;
+    float m_run = -__builtin_inff(), l_run = 0.0f;
+    const float qscale = p.scale * 1.44269504088896340736f;
+
+    const int nkb = (L + SKB - 1) / SKB;
+#pragma unroll
+    for (int st = 0; st < SNS - 1; ++st)
+        if (st < nkb) issue(st, st * SKB);
+    if (nkb >= SNS - 1) hfa::wait_vm_barrier<(SNS - 2) * 8>();
+    else hfa::wait_vm_barrier<0>();
+    int stage = 0;
+    for (int kt0 = 0; kt0 < nkb; ++kt0) {
+        const bool more = kt0 + SNS - 1 < nkb;
+        if (more) issue(stage == 0 ? SNS - 1 : stage - 1, (kt0 + SNS - 1) * SKB);
+        const _Float16* sK = smem + stage * SSTAGE;
+        const _Float16* sV = sK + 2 * SPLANE;
+        // S^T[key][query] for two 32-key blocks
+        f32x16 s[2];
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+            f32x16 sM, sC;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) sM[e] = sC[e] = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < DH / 16; ++kb) {
+                const f16x8 k1 = *reinterpret_cast<const f16x8*>(sK + kt * 32 * DH + kofs[kb]);
+                const f16x8 k2 = *reinterpret_cast<const f16x8*>(sK + SPLANE + kt * 32 * DH + kofs[kb]);
+                sM = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q1[kb], sM, 0, 0, 0);
+                sC = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q2[kb], sC, 0, 0, 0);
+                sC = __builtin_amdgcn_mfma_f32_32x32x16_f16(k2, q1[kb], sC, 0, 0, 0);
+            }
+#pragma unroll
+            for (int e = 0; e < 16; ++e) s[kt][e] = __builtin_fmaf(sC[e], kLo, sM[e]) * qscale;
+        }
+        const int key0 = kt0 * SKB;
+        if (key0 + SKB > L) {          // last, partial tile: keys >= L do not exist
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (key0 + kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * half >= L) s[kt][e] = -__builtin_inff();
+        }
+        float bm = fmaxf(s[0][0], s[1][0]);
+#pragma unroll
+        for (int e = 1; e < 16; ++e) bm = fmaxf(bm, fmaxf(s[0][e], s[1][e]));
+        bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+        const float m_cand = fmaxf(m_run, bm);
+        const bool move = m_cand > m_run + kSlack;          // first tile: m_run = -inf moves
+        if (__builtin_amdgcn_ballot_w64(move)) {
+            const float m_new = move ? m_cand : m_run;
+            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+            l_run *= alpha;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                oM[0][e] *= alpha; oM[1][e] *= alpha;
+                oC[0][e] *= alpha; oC[1][e] *= alpha;
+            }
+            m_run = m_new;
+        }
+        float ls = 0.0f;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                s[kt][e] = __builtin_amdgcn_exp2f(s[kt][e] - m_run);
+                ls += s[kt][e];
+            }
+        ls += __shfl_xor(ls, 32, 64);
+        l_run += ls;
+        // O^T[d][q] += sum_key V^T[d][key] P^T[key][q]; k-step (kt, ks) takes P registers 8 ks .. 8 ks + 7 of
+        // block kt, i.e. keys 32 kt + 16 ks + 8 (j >> 2) + 4 half + (j & 3) for element j
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                f16x8 p1, p2;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float pv = s[kt][8 * ks + j];
+                    p1[j] = (_Float16)pv;
+                    p2[j] = (_Float16)((pv - (float)p1[j]) * 2048.0f);
+                }
+                const int rb = (32 * kt + 16 * ks) * (DH * 2);
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    const f16x4 a0 = lds_tr(sV, rb + vofs[db]);
+                    const f16x4 a1 = lds_tr(sV, rb + 8 * DH * 2 + vofs[db]);
+                    const f16x4 b0 = lds_tr(sV + SPLANE, rb + vofs[db]);
+                    const f16x4 b1 = lds_tr(sV + SPLANE, rb + 8 * DH * 2 + vofs[db]);
+                    const f16x8 v1 = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                    const f16x8 v2 = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+                    oM[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, p1, oM[db], 0, 0, 0);
+                    oC[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, p2, oC[db], 0, 0, 0);
+                    oC[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v2, p1, oC[db], 0, 0, 0);
+                }
+            }
+        if (kt0 + 1 < nkb) {                    // next tile landed; every wave done with this stage
+            if (more) hfa::wait_vm_barrier<(SNS - 2) * 8>();
+            else hfa::wait_vm_barrier<0>();
+        }
+        stage = stage + 1 == SNS ? 0 : stage + 1;
+    }
+
+    // normalise and stage O[i][d] through LDS (each wave a private 32 x 33 f32 slab), then row-contiguous split
+    // stores (4 d per lane per plane)
+    __syncthreads();
+    const float inv = 1.0f / l_run;
+    float* slab = reinterpret_cast<float*>(smem) + wave * (QW * 33);
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int d = (e & 3) + 8 * (e >> 2) + 4 * half;
+            slab[r32 * 33 + d] = __builtin_fmaf(oC[db][e], kLo, oM[db][e]) * inv;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int idx = lane + i * 64;
+            const int row = idx >> 3, c4 = (idx & 7) * 4;
+            const int qq = q0 + row;
+            if (qq < L) {
+                f16x4 h1, h2;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float x = slab[row * 33 + c4 + t];
+                    h1[t] = (_Float16)x;
+                    h2[t] = (_Float16)((x - (float)h1[t]) * 2048.0f);
+                }
+                _Float16* dst = p.o + b * p.o_bs + (long long)qq * p.o_ld + hd * DH + db * 32 + c4;
+                *reinterpret_cast<f16x4*>(dst) = h1;
+                *reinterpret_cast<f16x4*>(dst + p.o_sp) = h2;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -246,6 +503,39 @@ int hfa_attention_f32(int B, int H, int L, int head_dim, float scale, const floa
     dim3 grid((unsigned)nblk);
     hipLaunchKernelGGL(attn_fwd_f32_kernel, grid, dim3(NW * 64), 0, stream, p);
     return hfa::check_launch("hfa_attention_f32");
+}
+
+int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const uint16_t* q, long long q_sp,
+                        long long q_bs, int q_ld, const uint16_t* k, long long k_sp, long long k_bs, int k_ld,
+                        const uint16_t* v, long long v_sp, long long v_bs, int v_ld, uint16_t* o, long long o_sp,
+                        long long o_bs, int o_ld, const int32_t* key_len, hipStream_t stream) {
+    if (head_dim != DH) {
+        hfa::set_error("hfa_attention_split: head_dim=%d unsupported (64 only)", head_dim);
+        return HFA_EINVAL;
+    }
+    if (B < 0 || H < 1 || L < 0) {
+        hfa::set_error("hfa_attention_split: bad sizes");
+        return HFA_EINVAL;
+    }
+    if (B == 0 || L == 0) return HFA_OK;
+    if ((((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) || (q_ld | k_ld | v_ld | o_ld) % 8 ||
+        (q_bs | k_bs | v_bs | o_bs | q_sp | k_sp | v_sp | o_sp) % 8) {
+        hfa::set_error("hfa_attention_split: planes must be 16-byte aligned with strides multiple of 8 halves");
+        return HFA_EINVAL;
+    }
+    if (((long long)(L - 1) * k_ld + DH) * 2 >= 0x7fffffffLL || ((long long)(L - 1) * v_ld + DH) * 2 >= 0x7fffffffLL) {
+        hfa::set_error("hfa_attention_split: K/V span exceeds 31-bit buffer offsets");
+        return HFA_EINVAL;
+    }
+    AttnSP p{B, H, L, scale, (const _Float16*)q, q_sp, q_bs, q_ld, (const _Float16*)k, k_sp, k_bs, k_ld,
+             (const _Float16*)v, v_sp, v_bs, v_ld, (_Float16*)o, o_sp, o_bs, o_ld, key_len};
+    const long long nblk = (long long)((L + QW * NW - 1) / (QW * NW)) * B * H;
+    if (nblk > 0x7fffffffLL) {
+        hfa::set_error("hfa_attention_split: grid too large");
+        return HFA_EINVAL;
+    }
+    hipLaunchKernelGGL(attn_fwd_split_kernel, dim3((unsigned)nblk), dim3(NW * 64), 0, stream, p);
+    return hfa::check_launch("hfa_attention_split");
 }
 
 }  // extern "C"

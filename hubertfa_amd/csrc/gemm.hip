@@ -754,7 +754,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     int stage = 0;
     for (int kt = 0; kt < nk; ++kt) {
         const bool more = kt + NS - 1 < nk;
+#ifndef HFA_SABL_NODMA
         if (more) issue(stage == 0 ? NS - 1 : stage - 1);
+#endif
         const f16x8* st = s8 + stage * (STAGE / 8);
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
@@ -774,8 +776,12 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
 #pragma unroll
                 for (int j = 0; j < TJ; ++j) {
                     accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w1[j], accM[i][j], 0, 0, 0);
+#if !defined(HFA_SABL_PRODUCTS) || HFA_SABL_PRODUCTS >= 2   // timing-only ablation builds (scripts/gpu_split_abl.sh)
                     accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w2[j], accC[i][j], 0, 0, 0);
+#endif
+#if !defined(HFA_SABL_PRODUCTS) || HFA_SABL_PRODUCTS >= 3
                     accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accC[i][j], 0, 0, 0);
+#endif
                 }
         }
         if (kt + 1 < nk) {
@@ -938,7 +944,12 @@ inline int set_grid(GemmP& p, int BM, int BN, dim3& grid, int Z) {
 }
 
 // ---- split-f16 dispatch --------------------------------------------------------------------------------------
-enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_COUNT = 4 };
+enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_128x128_NS3 = 4, SCFG_128x128_NS4 = 5,
+       SCFG_256x128_NS3 = 6, SCFG_COUNT = 7 };
+struct SplitGeom { int BM, BN, WM, NS, OCC; };
+constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
+    {128, 128, 2, 2, 2}, {128, 128, 2, 2, 2}, {128, 64, 2, 2, 2}, {256, 128, 4, 2, 1},
+    {128, 128, 2, 3, 1}, {128, 128, 2, 4, 1}, {256, 128, 4, 3, 1}};
 int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 
 inline int split_cfg(const GemmP& p, int Z) {
@@ -948,28 +959,31 @@ inline int split_cfg(const GemmP& p, int Z) {
 }
 
 inline void split_name(int cfg, int epi, bool outs, char* buf, int len) {
-    const int BM = cfg == SCFG_256x128 ? 256 : 128, BN = cfg == SCFG_128x64 ? 64 : 128;
-    const int WM = cfg == SCFG_256x128 ? 4 : 2, OCC = cfg == SCFG_256x128 ? 1 : 2;
-    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, 2, 2, %d, %s>", epi, BM, BN, WM, OCC, outs ? "true" : "false");
+    const SplitGeom& g = kSplitGeom[cfg];
+    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, 2, %d, %d, %s>", epi, g.BM, g.BN, g.WM, g.NS, g.OCC,
+             outs ? "true" : "false");
+}
+
+template <int EPI, bool OUTS, int CFG>
+int launch_split_cfg(GemmP p, int Z, hipStream_t st) {
+    constexpr SplitGeom g = kSplitGeom[CFG];
+    dim3 grid;
+    if (int rc = set_grid(p, g.BM, g.BN, grid, Z)) return rc;
+    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, 2, g.NS, g.OCC, OUTS>), grid, dim3(128 * g.WM), 0, st,
+                       p);
+    return hfa::check_launch("hfa_conv_gemm_split");
 }
 
 template <int EPI, bool OUTS>
 int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
-    dim3 grid;
     switch (cfg) {
-        case SCFG_128x64:
-            if (int rc = set_grid(p, 128, 64, grid, Z)) return rc;
-            hipLaunchKernelGGL((gemm_split_kernel<EPI, 128, 64, 2, 2, 2, 2, OUTS>), grid, dim3(256), 0, st, p);
-            break;
-        case SCFG_256x128:
-            if (int rc = set_grid(p, 256, 128, grid, Z)) return rc;
-            hipLaunchKernelGGL((gemm_split_kernel<EPI, 256, 128, 4, 2, 2, 1, OUTS>), grid, dim3(512), 0, st, p);
-            break;
-        default:
-            if (int rc = set_grid(p, 128, 128, grid, Z)) return rc;
-            hipLaunchKernelGGL((gemm_split_kernel<EPI, 128, 128, 2, 2, 2, 2, OUTS>), grid, dim3(256), 0, st, p);
+        case SCFG_128x64: return launch_split_cfg<EPI, OUTS, SCFG_128x64>(p, Z, st);
+        case SCFG_256x128: return launch_split_cfg<EPI, OUTS, SCFG_256x128>(p, Z, st);
+        case SCFG_128x128_NS3: return launch_split_cfg<EPI, OUTS, SCFG_128x128_NS3>(p, Z, st);
+        case SCFG_128x128_NS4: return launch_split_cfg<EPI, OUTS, SCFG_128x128_NS4>(p, Z, st);
+        case SCFG_256x128_NS3: return launch_split_cfg<EPI, OUTS, SCFG_256x128_NS3>(p, Z, st);
+        default: return launch_split_cfg<EPI, OUTS, SCFG_128x128>(p, Z, st);
     }
-    return hfa::check_launch("hfa_conv_gemm_split");
 }
 
 template <int EPI, int BK, int BM, int BN, int WM, int WN>

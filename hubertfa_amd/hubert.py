@@ -236,10 +236,16 @@ class HubertEncoder:
         return out
 
     def attention_block(self, h_in: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None) -> torch.Tensor:
+        """softmax(QK^T/sqrt(dh))V over the fused QKV projection.  Split precision: QKV written as split planes,
+        attention on the split kernel, O returned as split planes (the out-projection's A operand)."""
         a = self.arch
         B, L, H = h_in.shape
         nh = a.heads
         dh = H // nh
+        if self.precision == "split" and L_.wqkv_s is not None and L_.wo_s is not None and dh == 64:
+            qkv_s = self._linear(h_in, L_.wqkv, L_.wqkv_s, L_.bqkv, out_split=True)
+            o_s = torch.empty((2, B, L, H), dtype=torch.float16, device=h_in.device)
+            return ops.attention_split(qkv_s, o_s, B=B, H=nh, L=L, head_dim=dh, scale=dh ** -0.5, key_len=lens)
         qkv = self._linear(h_in, L_.wqkv, L_.wqkv_s, L_.bqkv)
         o = torch.empty((B, L, H), dtype=torch.float32, device=h_in.device)
         ops.attention(qkv, qkv[..., H:], qkv[..., 2 * H:], o, B=B, H=nh, L=L, head_dim=dh, scale=dh ** -0.5,
@@ -247,12 +253,17 @@ class HubertEncoder:
                       o_bs=L * H, o_ld=H, key_len=lens)
         return o
 
+    def _out_proj(self, o: torch.Tensor, L_: _Layer, residual: torch.Tensor) -> torch.Tensor:
+        if o.dtype == torch.float16:          # split planes from the split attention
+            return self._linear(None, L_.wo, L_.wo_s, L_.bo, residual=residual, xs=o)
+        return self._linear(o, L_.wo, L_.wo_s, L_.bo, residual=residual)
+
     def layer(self, h: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None) -> torch.Tensor:
         eps = self.arch.layer_norm_eps
         sp = self.precision == "split" and L_.w1_s is not None and L_.w2_s is not None
         if not self.arch.stable_layer_norm:   # post-LN (HubertEncoderLayer / nn.TransformerEncoderLayer)
             o = self.attention_block(h, L_, lens)
-            h1 = self._linear(o, L_.wo, L_.wo_s, L_.bo, residual=h)
+            h1 = self._out_proj(o, L_, h)
             h1 = ops.layernorm(h1, L_.ln1_w, L_.ln1_b, eps, out=h1)
             f = self._linear(h1, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp)
             h2 = self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h1, xs=f) if sp else \
@@ -261,7 +272,7 @@ class HubertEncoder:
         # pre-LN (HubertEncoderLayerStableLayerNorm)
         a_ = ops.layernorm(h, L_.ln1_w, L_.ln1_b, eps)
         o = self.attention_block(a_, L_, lens)
-        h = self._linear(o, L_.wo, L_.wo_s, L_.bo, residual=h)
+        h = self._out_proj(o, L_, h)
         a_ = ops.layernorm(h, L_.ln2_w, L_.ln2_b, eps)
         f = self._linear(a_, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp)
         if sp:

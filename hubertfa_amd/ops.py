@@ -141,7 +141,9 @@ _lib.register("hfa_split_f16", [_I_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _P_, _P_])
 _lib.register("hfa_gemm_f32", [_I_, _I_, _I_, _P_, _I_, _P_, _I_, _P_, _P_, _I_, _P_, _I_, _I_, _P_])
 _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_,
                                     _LL_, _I_, _P_, _P_])
-_lib.register("hfa_layernorm_f32", [_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_])
+_lib.register("hfa_attention_split", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _LL_,
+                                      _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _P_])
+_lib.register("hfa_layernorm_f32",[_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_])
 _lib.register("hfa_groupnorm_f32", [_I_, _I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_,
                                     _P_, _P_])
 _lib.register("hfa_groupnorm_workspace_bytes", [_I_, _I_, _I_, _I_], ctypes.c_longlong)
@@ -351,6 +353,30 @@ def attention(q, k, v, out, *, B, H, L, head_dim, scale, q_bs, q_ld, k_bs, k_ld,
     else:                       # QK^T and PV: 2 * 2 * L * L * head_dim per (batch, head)
         PROBE("attn_fwd_f32_kernel", 4.0 * B * H * L * L * head_dim, launch, kind="flops_aux")
     return out
+
+
+def attention_split(qkv_s, out_s, *, B, H, L, head_dim, scale, key_len=None):
+    """Flash attention on split planes (attention.hip attn_fwd_split_kernel): ``qkv_s`` [2, B, L, 3*H*head_dim]
+    f16 planes of the fused QKV projection (Q | K | V column blocks), ``out_s`` [2, B, L, H*head_dim] planes."""
+    _need(qkv_s, torch.float16, "qkv_s")
+    _need(out_s, torch.float16, "out_s")
+    D = H * head_dim
+    if qkv_s.shape != (2, B, L, 3 * D) or out_s.shape != (2, B, L, D):
+        raise ValueError(f"attention_split: qkv_s {tuple(qkv_s.shape)} / out_s {tuple(out_s.shape)} do not match "
+                         f"B={B} L={L} H={H} head_dim={head_dim}")
+    kl = _lens(key_len)
+    sp, bs, ld = qkv_s.stride(0), qkv_s.stride(1), qkv_s.stride(2)
+    base = qkv_s.data_ptr()
+
+    def launch():
+        _lib.call("hfa_attention_split", B, H, L, head_dim, float(scale), _P(base), sp, bs, ld, _P(base + 2 * D),
+                  sp, bs, ld, _P(base + 4 * D), sp, bs, ld, _ptr(out_s), out_s.stride(0), out_s.stride(1),
+                  out_s.stride(2), _ptr(kl), _stream(out_s.device))
+    if PROBE is None:
+        launch()
+    else:
+        PROBE("attn_fwd_split_kernel", 4.0 * B * H * L * L * head_dim, launch, kind="flops_aux")
+    return out_s
 
 
 def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None, t_len=None):

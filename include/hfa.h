@@ -111,7 +111,8 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
                         long long sCg, int ldc, int epilogue, int* oflow, hipStream_t stream);
 /* rocprof symbol stem of the split instantiation for an M x N output over Z = Zb*G (out_split: planes out). */
 const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue);
-/* Tile override for the split GEMM: 0 auto, 1 128x128, 2 128x64, 3 256x128 (8 waves). */
+/* Tile override for the split GEMM: 0 auto, 1 128x128, 2 128x64, 3 256x128 (8 waves), 4/5 128x128 with 3/4
+ * stages (one workgroup per CU), 6 256x128 with 3 stages. */
 int hfa_gemm_split_tuning(int cfg);
 /* x [rows, cols] f32 (row stride ldx) -> split planes y (row stride ldy, plane 1 at +sp); raises *oflow (if
  * non-NULL) for |x| >= 65504 or a non-finite x. */
@@ -126,6 +127,13 @@ int hfa_split_f16(int rows, int cols, const float* x, long long ldx, uint16_t* y
 int hfa_attention_f32(int B, int H, int L, int head_dim, float scale, const float* q, long long q_bs, int q_ld,
                       const float* k, long long k_bs, int k_ld, const float* v, long long v_bs, int v_ld, float* o,
                       long long o_bs, int o_ld, const int32_t* key_len, hipStream_t stream);
+/* The same attention on split-f16 planes (see hfa_conv_gemm_split): Q, K, V read as plane pairs (plane 1 at
+ * +q_sp / +k_sp / +v_sp halves), O written as plane pairs (+o_sp); every contraction is three exact f16 MFMA
+ * products (f32-class accuracy).  Pointers 16-B aligned, strides multiples of 8 halves; |O| <= max |V|. */
+int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const uint16_t* q, long long q_sp,
+                        long long q_bs, int q_ld, const uint16_t* k, long long k_sp, long long k_bs, int k_ld,
+                        const uint16_t* v, long long v_sp, long long v_bs, int v_ld, uint16_t* o, long long o_sp,
+                        long long o_bs, int o_ld, const int32_t* key_len, hipStream_t stream);
 
 /* ---- normalisation (hubertfa_amd/csrc/norm.hip); act: 0 none, 1 erf-GELU, 2 Hardswish -----------------------
  * y = act(LayerNorm(x (+ res)) * gamma + beta) over rows of C <= 4096 (C % 4 == 0).

@@ -25,21 +25,28 @@ def main():
         qkv = torch.randn(B, L, 3 * H * D, device=d)
         out = torch.empty(B, L, H * D, device=d)
 
+        qs = ops.split(qkv)
+        os_ = torch.empty(2, B, L, H * D, dtype=torch.float16, device=d)
+
+        def go_split():
+            ops.attention_split(qs, os_, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5)
+
         def go():
             ops.attention(qkv, qkv[..., H * D:], qkv[..., 2 * H * D:], out, B=B, H=H, L=L, head_dim=D,
                           scale=D ** -0.5, q_bs=L * 3 * H * D, q_ld=3 * H * D, k_bs=L * 3 * H * D, k_ld=3 * H * D,
                           v_bs=L * 3 * H * D, v_ld=3 * H * D, o_bs=L * H * D, o_ld=H * D)
-        for _ in range(3):
-            go()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.reps):
-            go()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / args.reps
-        print(f"{name:16s} {ms:8.3f} ms  {4.0 * B * H * L * L * D / ms / 1e9:7.1f} TFLOP/s", flush=True)
+        for tag, fn in (("f32", go), ("split", go_split)):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / args.reps
+            print(f"{name:16s} {tag:5s} {ms:8.3f} ms  {4.0 * B * H * L * L * D / ms / 1e9:7.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":

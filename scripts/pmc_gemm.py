@@ -18,7 +18,7 @@ def load(d):
     out = defaultdict(dict)
     for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(fn)):
-            if "gemm_f32_kernel" not in r["Kernel_Name"] and "gemm_dma_kernel" not in r["Kernel_Name"]:
+            if not any(t in r["Kernel_Name"] for t in ("gemm_f32_kernel", "gemm_dma_kernel", "gemm_split_kernel")):
                 continue
             k = int(r["Dispatch_Id"])
             e = out[k]

@@ -142,3 +142,68 @@ def test_range_guard_reruns_batch_on_f32():
         assert (a["ph_intervals"] == b["ph_intervals"]).all()
     import hubertfa_amd.ops as ops
     assert int(ops.split_flag(d).item()) == 0
+
+
+def _attn_ref(qkv, B, L, H, D, lens=None):
+    """f64 softmax(QK^T / sqrt(D)) V per (batch, head); with lens, keys >= lens[b] masked (rows past: don't care)."""
+    q, k, v = qkv.double().split(H * D, dim=-1)
+    q, k, v = (t.view(B, L, H, D).transpose(1, 2) for t in (q, k, v))
+    s = (q @ k.transpose(-1, -2)) * D ** -0.5
+    if lens is not None:
+        mask = torch.arange(L)[None, :] >= torch.tensor(lens)[:, None]          # [B, L] keys
+        s = s.masked_fill(mask[:, None, None, :], float("-inf"))
+    return (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B, L, H * D)
+
+
+@pytest.mark.parametrize("B,H,L", [(2, 12, 499), (1, 3, 64), (3, 2, 1), (1, 16, 200), (1, 1, 1500)])
+def test_attention_split(B, H, L):
+    """Split attention vs f64, at the f32 kernel's own tolerance (tests/test_kernels_gpu.py::test_attention)."""
+    from hubertfa_amd import ops
+    D = 64
+    qkv = _r(B, L, 3 * H * D, seed=8, scale=1.5)
+    ref = _attn_ref(qkv, B, L, H, D)
+    d = torch.device("cuda")
+    qs = ops.split(qkv.to(d))
+    out = torch.empty(2, B, L, H * D, dtype=torch.float16, device=d)
+    ops.attention_split(qs, out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5)
+    got = out[0].float() + out[1].float() / 2048.0
+    _close(got, ref, 1e-4, 2e-5)
+
+
+def test_attention_split_varlen():
+    """Per-row key lengths: each row equals its own un-padded attention (rows past the length untouched)."""
+    from hubertfa_amd import ops
+    from hubertfa_amd.hubert import dev_lengths
+    B, H, L, D = 3, 4, 300, 64
+    lens = [300, 129, 65]
+    qkv = _r(B, L, 3 * H * D, seed=9, scale=2.0)
+    ref = _attn_ref(qkv, B, L, H, D, lens)
+    d = torch.device("cuda")
+    qs = ops.split(qkv.to(d))
+    out = torch.zeros(2, B, L, H * D, dtype=torch.float16, device=d)
+    ops.attention_split(qs, out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5, key_len=dev_lengths(lens, d))
+    got = (out[0].float() + out[1].float() / 2048.0).cpu()
+    for b, n in enumerate(lens):
+        _close(got[b, :n], ref[b, :n], 1e-4, 2e-5)
+        assert bool((got[b, n:] == 0).all())
+
+
+def test_attention_split_large_scores():
+    """Peaked softmax (scores ~ +-60): the score's own f32-level rounding dominates both kernels' error; the split
+    kernel stays within 2x the f32 MFMA kernel's error against f64."""
+    from hubertfa_amd import ops
+    B, H, L, D = 1, 2, 777, 64
+    qkv = _r(B, L, 3 * H * D, seed=10, scale=4.0)
+    qkv[..., : H * D] *= 2.5
+    ref = _attn_ref(qkv, B, L, H, D)
+    d = torch.device("cuda")
+    out = torch.empty(2, B, L, H * D, dtype=torch.float16, device=d)
+    ops.attention_split(ops.split(qkv.to(d)), out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5)
+    qd = qkv.to(d)
+    o32 = torch.empty(B, L, H * D, device=d)
+    ld = 3 * H * D
+    ops.attention(qd, qd[..., H * D:], qd[..., 2 * H * D:], o32, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5,
+                  q_bs=L * ld, q_ld=ld, k_bs=L * ld, k_ld=ld, v_bs=L * ld, v_ld=ld, o_bs=L * H * D, o_ld=H * D)
+    e_split = float(((out[0].double() + out[1].double() / 2048.0).cpu() - ref).abs().max())
+    e_f32 = float((o32.double().cpu() - ref).abs().max())
+    assert e_split <= max(2.0 * e_f32, 2e-5), (e_split, e_f32)
