@@ -86,7 +86,8 @@ __device__ __forceinline__ void store_tile(const GemmP& p, const f32x16 (&acc)[T
 // cost 2-4 % of a GEMM).
 template <int EPI, int TI, int TJ>
 __device__ __forceinline__ void store_tile_lds(const GemmP& p, const f32x16 (&acc)[TI][TJ], int zb, int zg,
-                                               int wrow0, int wcol0, int lane, float* slab) {
+                                               int wrow0, int wcol0, int lane, float* slab, bool check = false) {
+    bool bad = false;                                    // check: raise *oflow on a non-finite accumulator
     float* Cb = p.C + zb * p.sCb + zg * p.sCg;
     const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
     const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
@@ -102,6 +103,7 @@ __device__ __forceinline__ void store_tile_lds(const GemmP& p, const f32x16 (&ac
             if (row0 >= p.M) continue;                   // wave-uniform
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
+                if (check) bad |= !__builtin_isfinite(acc[i][j][e]);
                 float v = acc[i][j][e] + bv;
                 if (EPI == EPI_GELU) v = hfa::gelu_fast(v);
                 slab[((e & 3) + 8 * (e >> 2) + 4 * h) * 36 + r32] = v;
@@ -129,6 +131,7 @@ __device__ __forceinline__ void store_tile_lds(const GemmP& p, const f32x16 (&ac
             __builtin_amdgcn_wave_barrier();
         }
     }
+    if (bad && p.oflow) *p.oflow = 1;
 }
 
 template <int EPI, bool VEC_A, int BK, int BM, int BN, int WM, int WN>
@@ -649,7 +652,15 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const f32x16 (&a
     if (bad && p.oflow) *p.oflow = 1;
 }
 
-template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT>
+// GT (general taps): Cg a multiple of 8 but not of 32 (the grouped positional conv, Cg = 48): a K-step's four
+// 16-B chunks can straddle a tap boundary, so every lane tracks its own chunk's (tap, channel) instead of the
+// workgroup-uniform tap + scalar channel offset.
+// ONE (single accumulator): the three products share one accumulator at scale 2^11 -- a1 (2^11 w1) + a1 w2 + a2 w1,
+// with 2^11 w1 formed exactly in registers (v_pk_mul_f16; needs |w| < 32, an overflow shows as a non-finite
+// output, which the epilogue flags) -- and the result is scaled by 2^-11 at the end.  Half the accumulator
+// registers, so a wave can own a 128 x 64 tile: 0.5 LDS fragment reads per MFMA instead of 0.67 (the LDS, shared
+// by the DMA fills and the fragment reads, is what bounds the 64 x 64-per-wave kernel: scripts/gpu_split_abl.sh).
+template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT, bool GT, bool ONE>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const GemmP p) {
     constexpr int BK = 32, CPR = 4, NW = WM * WN;            // halves per row per K-step, 16-B chunks per row
     constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
@@ -678,7 +689,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     const __amdgpu_buffer_rsrc_t rW2 = hfa::make_rsrc(Wb + p.sWp, w_bytes);
 
     // DMA d of this wave fills rows (wave + d*NW)*16 + lane/4 of each plane, chunk slot lane&3 (swizzled source)
-    int a_t0[DA], a_c[DA];
+    int a_t0[DA], a_c[DA], a_tap[DA];
     unsigned voffA[DA], voffW[DB];
 #pragma unroll
     for (int d = 0; d < DA; ++d) {
@@ -686,7 +697,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         int m = tm * BM + row;
         m = m < p.M ? m : p.M - 1;
         a_t0[d] = m * p.stride - p.pad;
-        a_c[d] = ((lane & 3) ^ ((row >> 2) & 3)) * 8;
+        a_c[d] = ((lane & 3) ^ ((row >> 2) & 3)) * 8;        // GT: the chunk's channel within its current tap
+        a_tap[d] = 0;
     }
 #pragma unroll
     for (int d = 0; d < DB; ++d) {
@@ -704,13 +716,25 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     };
     const unsigned lds0 = hfa::lds_addr(smem);
     int cur_j = 0, cur_c0 = 0, cur_k0 = 0;
-    set_tap(0);
+    if constexpr (!GT) set_tap(0);
     auto issue = [&](int stage) {
         const unsigned base = lds0 + stage * STAGE * 2 + wave * 1024;
 #pragma unroll
         for (int d = 0; d < DA; ++d) {
-            hfa::dma16(voffA[d], rA1, (unsigned)cur_c0 * 2, base + d * NW * 1024);
-            hfa::dma16(voffA[d], rA2, (unsigned)cur_c0 * 2, base + PA * 2 + d * NW * 1024);
+            if constexpr (GT) {
+                const int t = a_t0[d] + a_tap[d];
+                const unsigned vo = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + a_c[d]) * 2) : hfa::DMA_OOB;
+                hfa::dma16(vo, rA1, 0u, base + d * NW * 1024);
+                hfa::dma16(vo, rA2, 0u, base + PA * 2 + d * NW * 1024);
+                a_c[d] += BK;
+                if (a_c[d] >= p.Cg) {                     // Cg >= BK: at most one tap boundary per K-step
+                    a_c[d] -= p.Cg;
+                    ++a_tap[d];
+                }
+            } else {
+                hfa::dma16(voffA[d], rA1, (unsigned)cur_c0 * 2, base + d * NW * 1024);
+                hfa::dma16(voffA[d], rA2, (unsigned)cur_c0 * 2, base + PA * 2 + d * NW * 1024);
+            }
         }
 #pragma unroll
         for (int d = 0; d < DB; ++d) {
@@ -718,10 +742,12 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
             hfa::dma16(voffW[d], rW2, (unsigned)cur_k0 * 2, base + (2 * PA + PW) * 2 + d * NW * 1024);
         }
         cur_k0 += BK;
-        cur_c0 += BK;
-        if (cur_c0 == p.Cg) {
-            cur_c0 = 0;
-            set_tap(++cur_j);
+        if constexpr (!GT) {
+            cur_c0 += BK;
+            if (cur_c0 == p.Cg) {
+                cur_c0 = 0;
+                set_tap(++cur_j);
+            }
         }
     };
     constexpr int DN = 2 * (DA + DB);                       // DMA issues per wave per K-step
@@ -735,13 +761,21 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         rdA[kk] = (wm * (BM / WM) + r32) * CPR + (c ^ ((r32 >> 2) & 3));
         rdB[kk] = 2 * PA / 8 + (wn * (BN / WN) + r32) * CPR + (c ^ ((r32 >> 2) & 3));
     }
-    f32x16 accM[TI][TJ], accC[TI][TJ];
+    f32x16 accM[TI][TJ], accC[ONE ? 1 : TI][ONE ? 1 : TJ];
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) accM[i][j][e] = accC[i][j][e] = 0.0f;
+            for (int e = 0; e < 16; ++e) accM[i][j][e] = 0.0f;
+    if constexpr (!ONE) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) accC[i][j][e] = 0.0f;
+    }
 
     const int nk = p.K / BK;
 #pragma unroll
@@ -771,18 +805,32 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
                 w1[j] = st[rdB[kk] + j * 32 * CPR];
                 w2[j] = st[rdB[kk] + PW / 8 + j * 32 * CPR];
             }
+            if constexpr (ONE) {
+                f16x8 w1s[TJ];
 #pragma unroll
-            for (int i = 0; i < TI; ++i)
+                for (int j = 0; j < TJ; ++j) w1s[j] = w1[j] * (_Float16)2048.0f;
 #pragma unroll
-                for (int j = 0; j < TJ; ++j) {
-                    accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w1[j], accM[i][j], 0, 0, 0);
+                for (int i = 0; i < TI; ++i)
+#pragma unroll
+                    for (int j = 0; j < TJ; ++j) {
+                        accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w1s[j], accM[i][j], 0, 0, 0);
+                        accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w2[j], accM[i][j], 0, 0, 0);
+                        accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accM[i][j], 0, 0, 0);
+                    }
+            } else {
+#pragma unroll
+                for (int i = 0; i < TI; ++i)
+#pragma unroll
+                    for (int j = 0; j < TJ; ++j) {
+                        accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w1[j], accM[i][j], 0, 0, 0);
 #if !defined(HFA_SABL_PRODUCTS) || HFA_SABL_PRODUCTS >= 2   // timing-only ablation builds (scripts/gpu_split_abl.sh)
-                    accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w2[j], accC[i][j], 0, 0, 0);
+                        accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w2[j], accC[i][j], 0, 0, 0);
 #endif
 #if !defined(HFA_SABL_PRODUCTS) || HFA_SABL_PRODUCTS >= 3
-                    accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accC[i][j], 0, 0, 0);
+                        accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accC[i][j], 0, 0, 0);
 #endif
-                }
+                    }
+            }
         }
         if (kt + 1 < nk) {
             if (more) hfa::wait_vm_barrier<(NS - 2) * DN>();
@@ -795,14 +843,18 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) accM[i][j][e] = __builtin_fmaf(accC[i][j][e], 1.0f / 2048.0f, accM[i][j][e]);
+            for (int e = 0; e < 16; ++e) {
+                if constexpr (ONE) accM[i][j][e] *= 1.0f / 2048.0f;
+                else accM[i][j][e] = __builtin_fmaf(accC[i][j][e], 1.0f / 2048.0f, accM[i][j][e]);
+            }
     static_assert(NW * 32 * 36 * 4 <= NS * STAGE * 2, "epilogue slabs exceed the staging LDS");
     __syncthreads();
     float* slab = reinterpret_cast<float*>(smem) + wave * (32 * 36);
     if constexpr (OUT_SPLIT)
         store_split_lds<TI, TJ>(p, accM, EPI, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane, slab);
     else
-        store_tile_lds<EPI, TI, TJ>(p, accM, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane, slab);
+        store_tile_lds<EPI, TI, TJ>(p, accM, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane, slab,
+                                    ONE);
 }
 
 // f32 -> (hi, lo * 2^11) f16 planes, row-wise with 4-element vectors where aligned; raises *oflow for |x| >= 65504
@@ -945,43 +997,68 @@ inline int set_grid(GemmP& p, int BM, int BN, dim3& grid, int Z) {
 
 // ---- split-f16 dispatch --------------------------------------------------------------------------------------
 enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_128x128_NS3 = 4, SCFG_128x128_NS4 = 5,
-       SCFG_256x128_NS3 = 6, SCFG_COUNT = 7 };
-struct SplitGeom { int BM, BN, WM, NS, OCC; };
+       SCFG_256x128_NS3 = 6, SCFG_256x256_1 = 7, SCFG_256x128_1 = 8, SCFG_128x128_1 = 9, SCFG_128x64_1 = 10,
+       SCFG_COUNT = 11 };
+struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; };
 constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
-    {128, 128, 2, 2, 2}, {128, 128, 2, 2, 2}, {128, 64, 2, 2, 2}, {256, 128, 4, 2, 1},
-    {128, 128, 2, 3, 1}, {128, 128, 2, 4, 1}, {256, 128, 4, 3, 1}};
+    {128, 128, 2, 2, 2, 2, false}, {128, 128, 2, 2, 2, 2, false}, {128, 64, 2, 2, 2, 2, false},
+    {256, 128, 4, 2, 2, 1, false}, {128, 128, 2, 2, 3, 1, false}, {128, 128, 2, 2, 4, 1, false},
+    {256, 128, 4, 2, 3, 1, false}, {256, 256, 2, 4, 2, 1, true},  {256, 128, 2, 2, 2, 1, true},
+    {128, 128, 2, 2, 2, 2, true},  {128, 64, 2, 2, 2, 2, true}};
 int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 
+// Measured on the workload's shapes (scripts/split_gemm_bench.py, profiles/r01/split_gemm_cfgs.txt): the 256 x 256
+// single-accumulator tile is 7-15 % faster than 128 x 128 on the extractor convs, FFN and out-projection (even at
+// 189 tiles for N = 768) and within 3 % on the QKV projection; small grids keep the narrower tiles.  Every
+// automatic choice is a single-accumulator tile: each output element then sees the same MFMA sequence (same
+// k-blocks, same three products in the same order) whatever the tile, so a row's result does not depend on the
+// batch it is in (variable-length batches stay bit-identical to the reference's B = 1 runs).
 inline int split_cfg(const GemmP& p, int Z) {
     if (g_split_cfg > 0 && g_split_cfg < SCFG_COUNT) return g_split_cfg;
     const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
-    return (p.N <= 64 || blocks128 < 256) ? SCFG_128x64 : SCFG_128x128;
+    const long long blocks256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * Z;
+    if (p.N <= 64 || blocks128 < 256) return SCFG_128x64_1;
+    return (blocks256 >= 128 && p.N >= 512) ? SCFG_256x256_1 : SCFG_128x128_1;
 }
 
-inline void split_name(int cfg, int epi, bool outs, char* buf, int len) {
+inline void split_name(int cfg, int epi, bool outs, bool gt, char* buf, int len) {
+    if (gt) cfg = kSplitGeom[cfg].BN == 64 ? SCFG_128x64_1 : SCFG_128x128_1;
     const SplitGeom& g = kSplitGeom[cfg];
-    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, 2, %d, %d, %s>", epi, g.BM, g.BN, g.WM, g.NS, g.OCC,
-             outs ? "true" : "false");
+    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, %s>", epi, g.BM, g.BN, g.WM, g.WN, g.NS,
+             g.OCC, outs ? "true" : "false", gt ? "true" : "false", g.ONE ? "true" : "false");
 }
 
-template <int EPI, bool OUTS, int CFG>
+template <int EPI, bool OUTS, int CFG, bool GT = false>
 int launch_split_cfg(GemmP p, int Z, hipStream_t st) {
     constexpr SplitGeom g = kSplitGeom[CFG];
     dim3 grid;
     if (int rc = set_grid(p, g.BM, g.BN, grid, Z)) return rc;
-    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, 2, g.NS, g.OCC, OUTS>), grid, dim3(128 * g.WM), 0, st,
-                       p);
+    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE>), grid,
+                       dim3(64 * g.WM * g.WN), 0, st, p);
     return hfa::check_launch("hfa_conv_gemm_split");
 }
 
 template <int EPI, bool OUTS>
 int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
+    if (p.Cg % 32) {                          // general taps (Cg % 8 == 0): the two common tiles only
+        if constexpr (OUTS) {
+            hfa::set_error("hfa_conv_gemm_split: Cg %% 32 != 0 takes no split output");
+            return HFA_EINVAL;
+        } else {
+            return kSplitGeom[cfg].BN == 64 ? launch_split_cfg<EPI, false, SCFG_128x64_1, true>(p, Z, st)
+                                            : launch_split_cfg<EPI, false, SCFG_128x128_1, true>(p, Z, st);
+        }
+    }
     switch (cfg) {
         case SCFG_128x64: return launch_split_cfg<EPI, OUTS, SCFG_128x64>(p, Z, st);
         case SCFG_256x128: return launch_split_cfg<EPI, OUTS, SCFG_256x128>(p, Z, st);
         case SCFG_128x128_NS3: return launch_split_cfg<EPI, OUTS, SCFG_128x128_NS3>(p, Z, st);
         case SCFG_128x128_NS4: return launch_split_cfg<EPI, OUTS, SCFG_128x128_NS4>(p, Z, st);
         case SCFG_256x128_NS3: return launch_split_cfg<EPI, OUTS, SCFG_256x128_NS3>(p, Z, st);
+        case SCFG_256x256_1: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1>(p, Z, st);
+        case SCFG_256x128_1: return launch_split_cfg<EPI, OUTS, SCFG_256x128_1>(p, Z, st);
+        case SCFG_128x128_1: return launch_split_cfg<EPI, OUTS, SCFG_128x128_1>(p, Z, st);
+        case SCFG_128x64_1: return launch_split_cfg<EPI, OUTS, SCFG_128x64_1>(p, Z, st);
         default: return launch_split_cfg<EPI, OUTS, SCFG_128x128>(p, Z, st);
     }
 }
@@ -1157,8 +1234,9 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
         hfa::set_error("hfa_conv_gemm_split: need A, W and exactly one of C / Cs (Cs takes no residual)");
         return HFA_EINVAL;
     }
-    if (K % 32 || Cg % 32 || K % Cg) {
-        hfa::set_error("hfa_conv_gemm_split: K=%d and Cg=%d must be multiples of 32 with Cg | K", K, Cg);
+    if (K % 32 || Cg % 8 || (Cg % 32 && Cg < 32) || K % Cg) {
+        hfa::set_error("hfa_conv_gemm_split: K=%d must be a multiple of 32 and Cg=%d a multiple of 32 (or of 8 and "
+                       ">= 32), with Cg | K", K, Cg);
         return HFA_EINVAL;
     }
     if (!al16(A) || !al16(W) || (ldx | ldw) % 8 || (sAp | sAb | sAg | sWp | sWg) % 8) {
@@ -1199,9 +1277,9 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
                                 : launch_split<EPI_NONE, false>(p, Z, cfg, stream);
 }
 
-const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue) {
+const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue, int Cg) {
     GemmP p = make_params(M, N, 32, 1, nullptr, 0, 0, 0, 1, 0, 32, 1, nullptr, 0, 0);
-    split_name(split_cfg(p, Z), epilogue, out_split != 0, g_name, sizeof(g_name));
+    split_name(split_cfg(p, Z), epilogue, out_split != 0, Cg % 32 != 0, g_name, sizeof(g_name));
     return g_name;
 }
 

@@ -141,13 +141,16 @@ class HubertEncoder:
         self.proj = (P("proj.weight"), P("proj.bias")) if (not hf and arch.proj_dim) else None
         self._ws = {}
         # split-f16 planes of every GEMM weight (one-time); conv weights only where Cin is a multiple of 32
-        def sp(w):   # weights outside f16 range (none in practice) stay on the f32 GEMM
-            if precision != "split" or self.device.type != "cuda" or not bool(w.abs().max() < 65504):
+        def sp(w):   # weights with |w| >= 16 (none in practice) stay on the f32 GEMM: the single-accumulator
+            # split tile forms 2^11 * hi(w) in f16 (gemm.hip gemm_split_kernel ONE)
+            if precision != "split" or self.device.type != "cuda" or not bool(w.abs().max() < 16):
                 return None
             return ops.split(w)
         self.conv_ws = [None] + [sp(w) if arch.conv_dim[i - 1] % 32 == 0 else None
                                  for i, w in enumerate(self.conv_w) if i > 0]
         self.fp_ws = sp(self.fp_w) if self.fp_w.shape[1] % 32 == 0 else None
+        cg = arch.hidden // arch.pos_groups                  # grouped pos conv: per-lane taps when Cg % 32 != 0
+        self.pos_ws = sp(self.pos_w) if (cg % 32 == 0 or (cg % 8 == 0 and cg >= 32)) else None
         for L in self.layers:
             L.wqkv_s, L.wo_s, L.w1_s, L.w2_s = sp(L.wqkv), sp(L.wo), sp(L.w1), sp(L.w2)
         self.proj_s = sp(self.proj[0]) if self.proj is not None else None
@@ -230,9 +233,13 @@ class HubertEncoder:
         if lens is not None:
             ops.mask_rows(h, lens)
         out = torch.empty_like(h)
-        ops.conv_gemm(h, self.pos_w, out, M=L, N=Cg, K=k * Cg, Zb=B, G=G, sAb=L * H, sAg=Cg, ldx=H, stride=1,
-                      pad=k // 2, Cg=Cg, Tin=L, sWg=Cg * k * Cg, bias=self.pos_b, sBg=Cg, R=h, sRb=L * H, sRg=Cg,
-                      ldr=H, sCb=L * H, sCg=Cg, ldc=H, epilogue=ops.EPI_GELU)
+        kw = dict(M=L, N=Cg, K=k * Cg, Zb=B, G=G, sAb=L * H, sAg=Cg, ldx=H, stride=1, pad=k // 2, Cg=Cg, Tin=L,
+                  sWg=Cg * k * Cg, bias=self.pos_b, sBg=Cg, R=h, sRb=L * H, sRg=Cg, ldr=H, sCb=L * H, sCg=Cg, ldc=H,
+                  epilogue=ops.EPI_GELU)
+        if self.precision == "split" and self.pos_ws is not None:
+            ops.conv_gemm_split(ops.split(h), self.pos_ws, C=out, **kw)
+        else:
+            ops.conv_gemm(h, self.pos_w, out, **kw)
         return out
 
     def attention_block(self, h_in: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None) -> torch.Tensor:

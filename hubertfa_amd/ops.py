@@ -135,7 +135,7 @@ _lib.register("hfa_gemm_kernel_name", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_,
 _lib.register("hfa_conv_gemm_split", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_,
                                        _LL_, _LL_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _P_, _LL_, _LL_, _LL_,
                                        _I_, _I_, _P_, _P_])
-_lib.register("hfa_gemm_split_kernel_name", [_I_, _I_, _I_, _I_, _I_], ctypes.c_char_p)
+_lib.register("hfa_gemm_split_kernel_name", [_I_, _I_, _I_, _I_, _I_, _I_], ctypes.c_char_p)
 _lib.register("hfa_gemm_split_tuning", [_I_])
 _lib.register("hfa_split_f16", [_I_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _P_, _P_])
 _lib.register("hfa_gemm_f32", [_I_, _I_, _I_, _P_, _I_, _P_, _I_, _P_, _P_, _I_, _P_, _I_, _I_, _P_])
@@ -287,8 +287,8 @@ def split(x, out=None):
     return out
 
 
-def _split_name(M, N, Z, out_split, epilogue) -> str:
-    return _lib.lib().hfa_gemm_split_kernel_name(M, N, Z, int(out_split), epilogue).decode()
+def _split_name(M, N, Z, out_split, epilogue, Cg) -> str:
+    return _lib.lib().hfa_gemm_split_kernel_name(M, N, Z, int(out_split), epilogue, Cg).decode()
 
 
 def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None,
@@ -310,7 +310,7 @@ def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0
         _lib.call("hfa_conv_gemm_split", *args, _stream(dev))
     if PROBE is None:
         return launch()
-    PROBE(_split_name(M, N, Zb * G, Cs is not None, epilogue), 2.0 * M * N * K * Zb * G, launch)
+    PROBE(_split_name(M, N, Zb * G, Cs is not None, epilogue, Cg or K), 2.0 * M * N * K * Zb * G, launch)
 
 
 def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, out_split=False):

@@ -101,8 +101,10 @@ int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, i
  * The same contractions as hfa_conv_gemm_f32 with f32-class accuracy on the f16 MFMA: every f32 operand x is
  * carried as two f16 planes, x1 = f16(x) and x2 = f16((x - x1) * 2^11) (plane 1 at +sAp / +sWp / +sCp halves;
  * every stride in halves), and A.W = A1.W1 + 2^-11 (A1.W2 + A2.W1), each partial product exact in f32.
- * Requirements: K, Cg multiples of 32; A/W 16-B aligned with 8-half strides; |x| < 65504 for every split value
- * (producers raise *oflow otherwise; the caller recomputes on the f32 path).  Output: f32 C (+R, 16-B rows) or,
+ * Requirements: K a multiple of 32, Cg a multiple of 32 (or of 8 and >= 32: per-lane tap tracking, f32 C only); A/W 16-B aligned with 8-half strides; |x| < 65504 for every split value
+ * (producers raise *oflow otherwise; the caller recomputes on the f32 path) and |w| < 32 for W (the large
+ * single-accumulator tiles form 2^11 * w1 in f16; an overflow there yields a non-finite result, which also raises
+ * *oflow).  Output: f32 C (+R, 16-B rows) or,
  * with Cs non-NULL (C NULL), split planes of epi(acc + bias) (no R). */
 int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, long long sAp, long long sAb,
                         long long sAg, int ldx, int stride, int pad, int Cg, int Tin, const uint16_t* W,
@@ -110,9 +112,11 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
                         long long sRb, long long sRg, int ldr, float* C, uint16_t* Cs, long long sCp, long long sCb,
                         long long sCg, int ldc, int epilogue, int* oflow, hipStream_t stream);
 /* rocprof symbol stem of the split instantiation for an M x N output over Z = Zb*G (out_split: planes out). */
-const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue);
+const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue, int Cg);
 /* Tile override for the split GEMM: 0 auto, 1 128x128, 2 128x64, 3 256x128 (8 waves), 4/5 128x128 with 3/4
- * stages (one workgroup per CU), 6 256x128 with 3 stages. */
+ * stages (one workgroup per CU), 6 256x128 with 3 stages, 7 256x256 single accumulator (8 waves of 128x64),
+ * 8 256x128 single accumulator (4 waves), 9 128x128 single accumulator, 10 128x64 single accumulator.  The
+ * automatic choice uses single-accumulator tiles only (7, 9, 10): results then do not depend on the tile. */
 int hfa_gemm_split_tuning(int cfg);
 /* x [rows, cols] f32 (row stride ldx) -> split planes y (row stride ldy, plane 1 at +sp); raises *oflow (if
  * non-NULL) for |x| >= 65504 or a non-finite x. */

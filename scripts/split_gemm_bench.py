@@ -74,8 +74,11 @@ def main():
         line = f"{name:8s} f32 {flops / ms32 / 1e9:6.1f} TF ({ms32:.3f} ms) err {e32:.1e} | split err {es:.1e}"
         for cfg in (int(c) for c in args.cfgs.split(",")):
             _lib.lib().hfa_gemm_split_tuning(cfg)
+            ys.zero_()
+            spl()
+            ec = (ys[bsel][:, rows].double() - ref).abs().max().item()
             ms = timeit(spl, args.reps)
-            line += f" | cfg{cfg} {flops / ms / 1e9:6.1f} TF"
+            line += f" | cfg{cfg} {flops / ms / 1e9:6.1f} TF e{ec:.0e}"
         _lib.lib().hfa_gemm_split_tuning(0)
         print(line, flush=True)
 

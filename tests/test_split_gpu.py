@@ -42,7 +42,7 @@ def test_split_planes_and_flag():
     flag.zero_()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 7, 8, 9, 10])
 @pytest.mark.parametrize("M,N,K,epi,res,outs", [(300, 200, 128, 0, False, False), (1000, 768, 768, 1, False, False),
                                                 (257, 72, 192, 0, True, False), (4096, 3072, 768, 1, False, True),
                                                 (130, 2304, 768, 0, False, True), (64, 768, 3072, 0, True, False)])
@@ -85,6 +85,73 @@ def test_split_conv_vs_conv1d(Cin, Cout, k, s, pad, T):
     ops.conv_gemm_split(ops.split(x.to(d)), ops.split(wi.to(d)), C=y, M=Tout, N=Cout, K=k * Cin, Zb=B, sAb=T * Cin,
                         ldx=Cin, stride=s, pad=pad, Cg=Cin, Tin=T, bias=b.to(d), sCb=Tout * Cout, ldc=Cout)
     _close(y, ref, 2e-5, 2e-5)
+
+
+@pytest.mark.parametrize("H,G,k,L,cfg", [(768, 16, 128, 499, 0), (768, 16, 128, 77, 1), (96, 2, 8, 40, 0),
+                                         (640, 16, 16, 130, 0)])
+def test_split_grouped_posconv_general_taps(H, G, k, L, cfg):
+    """Grouped positional conv with Cg = H/G not a multiple of 32 (48 at Hubert-base: per-lane tap tracking),
+    GELU + residual epilogue, pad k/2 and the last frame dropped, against f64 conv1d (model.py:132-147)."""
+    from hubertfa_amd import ops, _lib
+    B = 2
+    Cg = H // G
+    d = torch.device("cuda")
+    x = _r(B, L, H, seed=12)
+    w = _r(H, Cg, k, seed=13, scale=(Cg * k) ** -0.5)
+    b = _r(H, seed=14) * 0.1
+    conv = F.conv1d(x.double().transpose(1, 2), w.double(), b.double(), padding=k // 2, groups=G)[..., :L]
+    ref = x.double() + F.gelu(conv.transpose(1, 2))
+    wi = w.permute(0, 2, 1).reshape(H, k * Cg).contiguous()
+    xd = x.to(d)
+    out = torch.empty(B, L, H, device=d)
+    _lib.lib().hfa_gemm_split_tuning(cfg)
+    try:
+        ops.conv_gemm_split(ops.split(xd), ops.split(wi.to(d)), C=out, M=L, N=Cg, K=k * Cg, Zb=B, G=G, sAb=L * H,
+                            sAg=Cg, ldx=H, stride=1, pad=k // 2, Cg=Cg, Tin=L, sWg=Cg * k * Cg, bias=b.to(d), sBg=Cg,
+                            R=xd, sRb=L * H, sRg=Cg, ldr=H, sCb=L * H, sCg=Cg, ldc=H, epilogue=ops.EPI_GELU)
+    finally:
+        _lib.lib().hfa_gemm_split_tuning(0)
+    _close(out, ref, 2e-5, 2e-5)
+
+
+@pytest.mark.parametrize("outs", [False, True])
+def test_split_single_acc_tiles_bit_identical(outs):
+    """Every automatic tile (7 = 256x256, 9 = 128x128, 10 = 128x64, all single-accumulator) gives the same bits,
+    so a row's result does not depend on the batch (and so the grid) it runs in."""
+    from hubertfa_amd import ops, _lib
+    d = torch.device("cuda")
+    M, N, K = 700, 768, 1536
+    xs, ws = ops.split(_r(M, K, seed=1).to(d)), ops.split(_r(N, K, seed=2, scale=K ** -0.5).to(d))
+    b = _r(N, seed=3).to(d)
+    outs_ = []
+    for cfg in (7, 9, 10, 8):
+        _lib.lib().hfa_gemm_split_tuning(cfg)
+        try:
+            outs_.append(ops.linear_split(xs, ws, b, epilogue=ops.EPI_GELU, out_split=outs))
+        finally:
+            _lib.lib().hfa_gemm_split_tuning(0)
+    for o in outs_[1:]:
+        assert torch.equal(o, outs_[0])
+
+
+@pytest.mark.parametrize("cfg,outs", [(7, False), (8, False), (9, True), (10, False)])
+def test_split_single_acc_weight_range_flag(cfg, outs):
+    """Single-accumulator tiles form 2^11 * hi(w) in f16: a weight with |w| >= 32 overflows there, and the
+    non-finite result raises the split flag (the caller re-runs on the f32 GEMM) instead of passing silently."""
+    from hubertfa_amd import ops, _lib
+    d = torch.device("cuda")
+    M, N, K = 512, 512, 256
+    x, w = _r(M, K, seed=1), _r(N, K, seed=2, scale=K ** -0.5)
+    w[3, 7] = 40.0
+    flag = ops.split_flag(d)
+    flag.zero_()
+    _lib.lib().hfa_gemm_split_tuning(cfg)
+    try:
+        ops.linear_split(ops.split(x.to(d)), ops.split(w.to(d)), None, out_split=outs)
+    finally:
+        _lib.lib().hfa_gemm_split_tuning(0)
+    assert int(flag.item()) == 1
+    flag.zero_()
 
 
 def test_conv0_split_output_matches_f32():
