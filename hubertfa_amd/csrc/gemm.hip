@@ -660,11 +660,16 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const f32x16 (&a
 // output, which the epilogue flags) -- and the result is scaled by 2^-11 at the end.  Half the accumulator
 // registers, so a wave can own a 128 x 64 tile: 0.5 LDS fragment reads per MFMA instead of 0.67 (the LDS, shared
 // by the DMA fills and the fragment reads, is what bounds the 64 x 64-per-wave kernel: scripts/gpu_split_abl.sh).
-template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT, bool GT, bool ONE>
+// BK (halves per row per K-step) 32: [row][4 x 16 B] images, chunk c of row r at c ^ ((r >> 2) & 3); BK 16: [row][2 x
+// 16 B], chunk c at c ^ (((r >> 2) ^ (r >> 3)) & 1).  Both keep the 32x32x16 operand reads (lane: row lane&31, chunk
+// 2 kk + lane/32) conflict-free; BK 16 halves the stage so more stages fit (DMA latency hidden behind more steps).
+template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT, bool GT, bool ONE, int BK>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const GemmP p) {
-    constexpr int BK = 32, CPR = 4, NW = WM * WN;            // halves per row per K-step, 16-B chunks per row
+    static_assert(BK == 16 || BK == 32, "BK 16 or 32");
+    constexpr int CPR = BK / 8, NW = WM * WN;                // 16-B chunks per row per plane
+    constexpr int RPP = 64 / CPR, KK = BK / 16;               // rows per 1-KiB DMA piece, MFMA k-steps per K-step
     constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
-    constexpr int IA = BM / 16, IW = BN / 16;                 // 1-KiB DMA pieces per plane per K-step
+    constexpr int IA = BM / RPP, IW = BN / RPP;               // 1-KiB DMA pieces per plane per K-step
     constexpr int DA = IA / NW, DB = IW / NW;
     static_assert(IA % NW == 0 && IW % NW == 0, "even DMA shares only");
     constexpr int PA = BM * BK, PW = BN * BK;                 // halves per plane image
@@ -688,24 +693,33 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     const __amdgpu_buffer_rsrc_t rW1 = hfa::make_rsrc(Wb, w_bytes);
     const __amdgpu_buffer_rsrc_t rW2 = hfa::make_rsrc(Wb + p.sWp, w_bytes);
 
-    // DMA d of this wave fills rows (wave + d*NW)*16 + lane/4 of each plane, chunk slot lane&3 (swizzled source)
+    // DMA d of this wave fills rows (wave + d*NW)*RPP + lane/CPR of each plane, chunk slot lane%CPR (swizzled source)
+    auto swz = [](int r) { return CPR == 4 ? ((r >> 2) & 3) : (((r >> 2) ^ (r >> 3)) & 1); };
     int a_t0[DA], a_c[DA], a_tap[DA];
     unsigned voffA[DA], voffW[DB];
 #pragma unroll
     for (int d = 0; d < DA; ++d) {
-        const int row = (wave + d * NW) * 16 + (lane >> 2);
+        const int row = (wave + d * NW) * RPP + lane / CPR;
+#ifdef HFA_SABL_SAMETILE
+        int m = row;                                      // ablation: every tile loads tile (0, 0)
+#else
         int m = tm * BM + row;
+#endif
         m = m < p.M ? m : p.M - 1;
         a_t0[d] = m * p.stride - p.pad;
-        a_c[d] = ((lane & 3) ^ ((row >> 2) & 3)) * 8;        // GT: the chunk's channel within its current tap
+        a_c[d] = ((lane % CPR) ^ swz(row)) * 8;             // GT: the chunk's channel within its current tap
         a_tap[d] = 0;
     }
 #pragma unroll
     for (int d = 0; d < DB; ++d) {
-        const int row = (wave + d * NW) * 16 + (lane >> 2);
+        const int row = (wave + d * NW) * RPP + lane / CPR;
+#ifdef HFA_SABL_SAMETILE
+        int n = row;
+#else
         int n = tn * BN + row;
+#endif
         n = n < p.N ? n : p.N - 1;
-        voffW[d] = (unsigned)((n * p.ldw + ((lane & 3) ^ ((row >> 2) & 3)) * 8) * 2);
+        voffW[d] = (unsigned)((n * p.ldw + ((lane % CPR) ^ swz(row)) * 8) * 2);
     }
     auto set_tap = [&](int j) {
 #pragma unroll
@@ -754,12 +768,12 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
 
     const int wm = wave / WN, wn = wave % WN;
     const int r32 = lane & 31, h = lane >> 5;
-    int rdA[2], rdB[2];                                      // f16x8 (16-B) units within a stage
+    int rdA[KK], rdB[KK];                                    // f16x8 (16-B) units within a stage
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
         const int c = kk * 2 + h;
-        rdA[kk] = (wm * (BM / WM) + r32) * CPR + (c ^ ((r32 >> 2) & 3));
-        rdB[kk] = 2 * PA / 8 + (wn * (BN / WN) + r32) * CPR + (c ^ ((r32 >> 2) & 3));
+        rdA[kk] = (wm * (BM / WM) + r32) * CPR + (c ^ swz(r32));
+        rdB[kk] = 2 * PA / 8 + (wn * (BN / WN) + r32) * CPR + (c ^ swz(r32));
     }
     f32x16 accM[TI][TJ], accC[ONE ? 1 : TI][ONE ? 1 : TJ];
 #pragma unroll
@@ -793,7 +807,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
 #endif
         const f16x8* st = s8 + stage * (STAGE / 8);
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
+        for (int kk = 0; kk < KK; ++kk) {
             f16x8 a1[TI], a2[TI], w1[TJ], w2[TJ];
 #pragma unroll
             for (int i = 0; i < TI; ++i) {
@@ -814,8 +828,12 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
 #pragma unroll
                     for (int j = 0; j < TJ; ++j) {
                         accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w1s[j], accM[i][j], 0, 0, 0);
+#if !defined(HFA_SABL_PRODUCTS) || HFA_SABL_PRODUCTS >= 2
                         accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w2[j], accM[i][j], 0, 0, 0);
+#endif
+#if !defined(HFA_SABL_PRODUCTS) || HFA_SABL_PRODUCTS >= 3
                         accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accM[i][j], 0, 0, 0);
+#endif
                     }
             } else {
 #pragma unroll
@@ -998,13 +1016,14 @@ inline int set_grid(GemmP& p, int BM, int BN, dim3& grid, int Z) {
 // ---- split-f16 dispatch --------------------------------------------------------------------------------------
 enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_128x128_NS3 = 4, SCFG_128x128_NS4 = 5,
        SCFG_256x128_NS3 = 6, SCFG_256x256_1 = 7, SCFG_256x128_1 = 8, SCFG_128x128_1 = 9, SCFG_128x64_1 = 10,
-       SCFG_COUNT = 11 };
-struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; };
+       SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_COUNT = 14 };
+struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; };
 constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
-    {128, 128, 2, 2, 2, 2, false}, {128, 128, 2, 2, 2, 2, false}, {128, 64, 2, 2, 2, 2, false},
-    {256, 128, 4, 2, 2, 1, false}, {128, 128, 2, 2, 3, 1, false}, {128, 128, 2, 2, 4, 1, false},
-    {256, 128, 4, 2, 3, 1, false}, {256, 256, 2, 4, 2, 1, true},  {256, 128, 2, 2, 2, 1, true},
-    {128, 128, 2, 2, 2, 2, true},  {128, 64, 2, 2, 2, 2, true}};
+    {128, 128, 2, 2, 2, 2, false, 32}, {128, 128, 2, 2, 2, 2, false, 32}, {128, 64, 2, 2, 2, 2, false, 32},
+    {256, 128, 4, 2, 2, 1, false, 32}, {128, 128, 2, 2, 3, 1, false, 32}, {128, 128, 2, 2, 4, 1, false, 32},
+    {256, 128, 4, 2, 3, 1, false, 32}, {256, 256, 2, 4, 2, 1, true, 32},  {256, 128, 2, 2, 2, 1, true, 32},
+    {128, 128, 2, 2, 2, 2, true, 32},  {128, 64, 2, 2, 2, 2, true, 32},   {256, 256, 2, 4, 4, 1, true, 16},
+    {256, 256, 2, 4, 3, 1, true, 16},  {128, 128, 2, 2, 4, 2, true, 16}};
 int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 
 // Measured on the workload's shapes (scripts/split_gemm_bench.py, profiles/r01/split_gemm_cfgs.txt): the 256 x 256
@@ -1024,8 +1043,8 @@ inline int split_cfg(const GemmP& p, int Z) {
 inline void split_name(int cfg, int epi, bool outs, bool gt, char* buf, int len) {
     if (gt) cfg = kSplitGeom[cfg].BN == 64 ? SCFG_128x64_1 : SCFG_128x128_1;
     const SplitGeom& g = kSplitGeom[cfg];
-    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, %s>", epi, g.BM, g.BN, g.WM, g.WN, g.NS,
-             g.OCC, outs ? "true" : "false", gt ? "true" : "false", g.ONE ? "true" : "false");
+    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, %s, %d>", epi, g.BM, g.BN, g.WM, g.WN,
+             g.NS, g.OCC, outs ? "true" : "false", gt ? "true" : "false", g.ONE ? "true" : "false", g.BK);
 }
 
 template <int EPI, bool OUTS, int CFG, bool GT = false>
@@ -1033,7 +1052,7 @@ int launch_split_cfg(GemmP p, int Z, hipStream_t st) {
     constexpr SplitGeom g = kSplitGeom[CFG];
     dim3 grid;
     if (int rc = set_grid(p, g.BM, g.BN, grid, Z)) return rc;
-    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE>), grid,
+    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE, g.BK>), grid,
                        dim3(64 * g.WM * g.WN), 0, st, p);
     return hfa::check_launch("hfa_conv_gemm_split");
 }
@@ -1059,6 +1078,9 @@ int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
         case SCFG_256x128_1: return launch_split_cfg<EPI, OUTS, SCFG_256x128_1>(p, Z, st);
         case SCFG_128x128_1: return launch_split_cfg<EPI, OUTS, SCFG_128x128_1>(p, Z, st);
         case SCFG_128x64_1: return launch_split_cfg<EPI, OUTS, SCFG_128x64_1>(p, Z, st);
+        case SCFG_256x256_1_K16S4: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1_K16S4>(p, Z, st);
+        case SCFG_256x256_1_K16S3: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1_K16S3>(p, Z, st);
+        case SCFG_128x128_1_K16S4: return launch_split_cfg<EPI, OUTS, SCFG_128x128_1_K16S4>(p, Z, st);
         default: return launch_split_cfg<EPI, OUTS, SCFG_128x128>(p, Z, st);
     }
 }
