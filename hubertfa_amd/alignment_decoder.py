@@ -148,8 +148,9 @@ class AlignmentDecoder:
         if keep_frame_probs:
             src["edge_prob"] = dev_out["lattice"]["edge_prob"]
             src["ph_frame_pred"] = dev_out["lattice"]["ph_frame_pred"]
-        if "split_oflow" in dev_out:             # the split-precision range guard (task._guard)
-            src["split_oflow"] = dev_out["split_oflow"]
+        for k in ("split_oflow", "split_oflow_head"):      # the split-precision range guard (task._guard)
+            if k in dev_out:
+                src[k] = dev_out[k]
         host = {}
         for k, t in src.items():
             h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
@@ -169,7 +170,7 @@ class AlignmentDecoder:
             dev_out = self.fetch(dev_out, keep_frame_probs)
         dev_out["event"].synchronize()
         hd = {k: v.numpy() for k, v in dev_out["host"].items()}
-        if "split_oflow" in hd and int(hd["split_oflow"][0]) and "redo" in dev_out:
+        if "redo" in dev_out and any(int(hd[k][0]) for k in ("split_oflow", "split_oflow_head") if k in hd):
             # a split-f16 operand left f16 range: this batch is recomputed with f32 GEMMs
             return dev_out["redo"]()
         Ts = dev_out["T"]

@@ -271,8 +271,9 @@ def split_flag(device) -> torch.Tensor:
     return _OFLOW[key]
 
 
-def split(x, out=None):
-    """f32 [..., C] (row-strided) -> split planes [2, ..., C]."""
+def split(x, out=None, flag=None):
+    """f32 [..., C] (row-strided) -> split planes [2, ..., C]; out-of-range values raise ``flag`` (default: the
+    device's split_flag)."""
     _need(x, torch.float32, "x", contiguous=False)
     C = x.shape[-1]
     x2 = x.reshape(-1, C) if x.dim() != 2 else x
@@ -283,7 +284,7 @@ def split(x, out=None):
         out = torch.empty((2, *x.shape), dtype=torch.float16, device=x.device)
     o2 = out.view(2, rows, C)
     _lib.call("hfa_split_f16", rows, C, _ptr(x2), x2.stride(0), _ptr(o2), o2.stride(1), o2.stride(0),
-              _ptr(split_flag(x.device)), _stream(x.device))
+              _ptr(split_flag(x.device) if flag is None else flag), _stream(x.device))
     return out
 
 
@@ -293,7 +294,7 @@ def _split_name(M, N, Z, out_split, epilogue, Cg) -> str:
 
 def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None,
                     Tin=None, sWg=0, ldw=None, bias=None, sBg=0, R=None, sRb=0, sRg=0, ldr=0, sCb=0, sCg=0, ldc,
-                    epilogue=EPI_NONE):
+                    epilogue=EPI_NONE, flag=None):
     """conv_gemm on split operands (As, Ws: [2, ...] f16 planes; strides in elements of one plane).  Output to f32
     C (+R) or to split planes Cs [2, ...] (bias/GELU epilogue only)."""
     _need(As, torch.float16, "As", contiguous=False)
@@ -304,7 +305,7 @@ def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0
     args = (M, N, K, Zb, G, _ptr(As), As.stride(0), sAb, sAg, ldx, stride, pad, Cg or K, Tin if Tin is not None else M,
             _ptr(Ws), Ws.stride(0), sWg, ldw if ldw is not None else K, _ptr(bias), sBg, _ptr(R), sRb, sRg, ldr,
             _ptr(C), _ptr(Cs), Cs.stride(0) if Cs is not None else 0, sCb, sCg, ldc, epilogue,
-            _ptr(split_flag(dev)))
+            _ptr(split_flag(dev) if flag is None else flag))
 
     def launch():
         _lib.call("hfa_conv_gemm_split", *args, _stream(dev))
@@ -313,7 +314,7 @@ def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0
     PROBE(_split_name(M, N, Zb * G, Cs is not None, epilogue, Cg or K), 2.0 * M * N * K * Zb * G, launch)
 
 
-def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, out_split=False):
+def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, out_split=False, flag=None):
     """y = epi(x @ W^T + bias) (+ residual) with x, W given as split planes [2, ..., K] / [2, N, K]; y f32, or split
     planes [2, ..., N] when out_split (no residual)."""
     K = xs.shape[-1]
@@ -328,7 +329,7 @@ def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, 
     r2 = residual.reshape(-1, N) if residual is not None else None
     conv_gemm_split(xs, Ws, C=None if out_split else out, Cs=out if out_split else None, M=M, N=N, K=K,
                     ldx=xs.stride(-2) if xs.dim() > 2 else K, bias=bias, R=r2, ldr=r2.stride(0) if r2 is not None else 0,
-                    ldc=N, epilogue=epilogue)
+                    ldc=N, epilogue=epilogue, flag=flag)
     return out
 
 

@@ -134,29 +134,40 @@ class ForcedAlignmentTask:
         else:
             logits = self.head.logits(feats)[:, :n_frames]
         frame, edge = logits[:, :, 2:], logits[:, :, 0]      # LatticeHead.split without the unused ctc logits
-        return self.decoder.decode_batch(frame, edge, wav_lengths, ph_seqs, word_seqs, p2ws, host=False)
+        dev_out = self.decoder.decode_batch(frame, edge, wav_lengths, ph_seqs, word_seqs, p2ws, host=False)
+        if self.head.precision == "split":      # the head's own range flag, snapshot on the stream that ran it
+            dev_out["split_oflow_head"] = self.head.flag.clone()
+            self.head.flag.zero_()
+        return dev_out
 
     def _guard(self, dev_out, redo_args):
         """Split-precision range guard: snapshot (and clear) the split-f16 overflow flag the batch's producers
         raise (ops.split_flag) into the batch's outputs, and attach a re-run of the batch on the f32 GEMMs that
         ``decoder.assemble`` takes instead when the flag is set."""
         enc = getattr(self.unitsEncoder, "model", None)
-        if getattr(enc, "precision", "f32") != "split":
+        enc_split = getattr(enc, "precision", "f32") == "split"
+        if not enc_split and self.head.precision != "split":
             return dev_out
-        flag = ops.split_flag(self.device)
-        dev_out["split_oflow"] = flag.clone()
-        flag.zero_()
+        if enc_split:
+            flag = ops.split_flag(self.device)
+            dev_out["split_oflow"] = flag.clone()
+            flag.zero_()
         dev_out["redo"] = lambda: self._align_f32(*redo_args)
         return dev_out
 
     def _align_f32(self, waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds):
         enc = self.unitsEncoder.model
-        enc.precision = "f32"
+        saved = (getattr(enc, "precision", "f32"), self.head.precision)
+        if hasattr(enc, "precision"):
+            enc.precision = "f32"
+        self.head.precision = "f32"
         try:
             return self.align_batch(waves, ph_seqs, word_seqs, p2ws, wav_sr=wav_sr, lengths=lengths,
                                     chunk_seconds=chunk_seconds)
         finally:
-            enc.precision = "split"
+            if hasattr(enc, "precision"):
+                enc.precision = saved[0]
+            self.head.precision = saved[1]
 
     def align_batch(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
                     host: bool = True, lengths=None, chunk_seconds: float | None = None):

@@ -8,6 +8,10 @@ All tensors stay channels-last [B, T, C]: the k3 convs are implicit GEMMs with p
 the stride-2 down-sampling conv is an implicit GEMM with overlapping-free rows, the transposed up-sampling conv is
 ONE GEMM whose [T, 2*Cout] output is bit-for-bit the [2T, Cout] layout, GroupNorm/LayerNorm fuse their
 Hardswish, and the residual shortcut is the second conv's epilogue.
+
+Precision "split" (default on the GPU): every GEMM runs on the split-f16 MFMA kernel (f32-class accuracy, see
+gemm.hip gemm_split_kernel), each GEMM input converted once to plane pairs; a value outside f16 range raises the
+head's own flag (``LatticeHead.flag``), and the task re-runs the batch on the f32 GEMMs.
 """
 from __future__ import annotations
 
@@ -22,9 +26,43 @@ def _t(x):
     return torch.from_numpy(np.ascontiguousarray(x)) if isinstance(x, np.ndarray) else x.detach().cpu()
 
 
+class _Ctx:
+    """Per-head GEMM dispatch: split-f16 when the head runs split and the weight has planes, else f32."""
+
+    def __init__(self, dev, precision):
+        self.dev = dev
+        self.precision = precision
+        self.flag = torch.zeros(1, dtype=torch.int32, device=dev) if dev.type == "cuda" else None
+
+    def planes(self, w):
+        """One-time split of a weight; |w| >= 16 (none in practice) stays f32 (gemm.hip ONE tiles need |w| < 32)."""
+        if self.precision != "split" or self.dev.type != "cuda" or w.shape[-1] % 32 or not bool(w.abs().max() < 16):
+            return None
+        return ops.split(w, flag=self.flag)
+
+    def use_split(self, ws):
+        return self.precision == "split" and ws is not None
+
+    def split(self, x):
+        return ops.split(x, flag=self.flag)
+
+    def conv(self, x, xs, w, ws, out, **kw):
+        if self.use_split(ws):
+            ops.conv_gemm_split(xs if xs is not None else self.split(x), ws, C=out, flag=self.flag, **kw)
+        else:
+            ops.conv_gemm(x, w, out, **kw)
+        return out
+
+    def linear(self, x, xs, w, ws, bias=None):
+        if self.use_split(ws):
+            return ops.linear_split(xs if xs is not None else self.split(x), ws, bias, flag=self.flag)
+        return ops.linear(x, w, bias)
+
+
 class _Block:
-    def __init__(self, sd, pre, dev):
+    def __init__(self, sd, pre, dev, ctx):
         P = lambda n: _t(sd[pre + n]).float().contiguous().to(dev)  # noqa: E731
+        self.ctx = ctx
         w1 = _t(sd[pre + "block.0.weight"]).float()
         w2 = _t(sd[pre + "block.3.weight"]).float()
         self.cin, self.hid, self.cout = w1.shape[1], w1.shape[0], w2.shape[0]
@@ -34,77 +72,102 @@ class _Block:
         self.n_groups = 16
         self.sc = P("shortcut.0.weight") if pre + "shortcut.0.weight" in sd else None
         self.ln = (P("out.0.weight"), P("out.0.bias"))
+        self.w1s, self.w2s = ctx.planes(self.w1), ctx.planes(self.w2)
+        self.scs = ctx.planes(self.sc) if self.sc is not None else None
 
     def __call__(self, x, lens=None):
         """lens [B] int32 (variable-length batch): rows >= lens[b] are padding — zeroed on the way in (the k3
         convs must read zeros there) and excluded from the GroupNorm statistics, zero on the way out."""
         B, T, _ = x.shape
+        c = self.ctx
         if lens is not None:
             ops.mask_rows(x, lens)
+        xs = c.split(x) if c.use_split(self.w1s) or c.use_split(self.scs) else None
         h = torch.empty((B, T, self.hid), dtype=torch.float32, device=x.device)
-        ops.conv_gemm(x, self.w1, h, M=T, N=self.hid, K=3 * self.cin, Zb=B, sAb=T * self.cin, ldx=self.cin, stride=1,
-                      pad=1, Cg=self.cin, Tin=T, sCb=T * self.hid, ldc=self.hid)
+        c.conv(x, xs, self.w1, self.w1s, h, M=T, N=self.hid, K=3 * self.cin, Zb=B, sAb=T * self.cin, ldx=self.cin,
+               stride=1, pad=1, Cg=self.cin, Tin=T, sCb=T * self.hid, ldc=self.hid)
         h = ops.groupnorm(h, self.n_groups, self.gn[0], self.gn[1], 1e-5, act=ops.ACT_HARDSWISH, out=h, t_len=lens)
-        sc = x if self.sc is None else ops.linear(x, self.sc)
+        sc = x if self.sc is None else c.linear(x, xs, self.sc, self.scs)
         y = torch.empty((B, T, self.cout), dtype=torch.float32, device=x.device)
-        ops.conv_gemm(h, self.w2, y, M=T, N=self.cout, K=3 * self.hid, Zb=B, sAb=T * self.hid, ldx=self.hid, stride=1,
-                      pad=1, Cg=self.hid, Tin=T, R=sc, sRb=T * self.cout, ldr=self.cout, sCb=T * self.cout,
-                      ldc=self.cout)
+        c.conv(h, None, self.w2, self.w2s, y, M=T, N=self.cout, K=3 * self.hid, Zb=B, sAb=T * self.hid, ldx=self.hid,
+               stride=1, pad=1, Cg=self.hid, Tin=T, R=sc, sRb=T * self.cout, ldr=self.cout, sCb=T * self.cout,
+               ldc=self.cout)
         return ops.layernorm(y, self.ln[0], self.ln[1], 1e-5, act=ops.ACT_HARDSWISH, out=y, t_len=lens)
 
 
 class _Down:
-    def __init__(self, sd, pre, dev):
+    def __init__(self, sd, pre, dev, ctx):
         w = _t(sd[pre + "conv.weight"]).float()       # [Cout, Cin, f]
         self.cout, self.cin, self.f = w.shape
         self.w = w.permute(0, 2, 1).reshape(self.cout, -1).contiguous().to(dev)
         self.b = _t(sd[pre + "conv.bias"]).float().contiguous().to(dev)
+        self.ctx = ctx
+        self.ws = ctx.planes(self.w) if self.cin % 32 == 0 else None
 
     def __call__(self, x, lens=None):
         B, T, _ = x.shape
         assert T % self.f == 0, "T is pre-padded to a multiple of factor**times (unet.py:103-106)"
         To = T // self.f
         y = torch.empty((B, To, self.cout), dtype=torch.float32, device=x.device)
-        ops.conv_gemm(x, self.w, y, M=To, N=self.cout, K=self.f * self.cin, Zb=B, sAb=T * self.cin, ldx=self.cin,
-                      stride=self.f, Cg=self.cin, Tin=T, bias=self.b, sCb=To * self.cout, ldc=self.cout)
+        self.ctx.conv(x, None, self.w, self.ws, y, M=To, N=self.cout, K=self.f * self.cin, Zb=B, sAb=T * self.cin,
+                      ldx=self.cin, stride=self.f, Cg=self.cin, Tin=T, bias=self.b, sCb=To * self.cout, ldc=self.cout)
         return y
 
 
 class _Up:
-    def __init__(self, sd, pre, dev):
+    def __init__(self, sd, pre, dev, ctx):
         w = _t(sd[pre + "conv.weight"]).float()       # ConvTranspose1d: [Cin, Cout, f]
         self.cin, self.cout, self.f = w.shape
         # out[f*t + j, o] = sum_c x[t, c] w[c, o, j] + b[o]  ->  W'[(j, o), c]
         self.w = w.permute(2, 1, 0).reshape(self.f * self.cout, self.cin).contiguous().to(dev)
         b = _t(sd[pre + "conv.bias"]).float()
         self.b = b.repeat(self.f).contiguous().to(dev)
+        self.ctx = ctx
+        self.ws = ctx.planes(self.w)
 
     def __call__(self, x, lens=None):
         B, T, _ = x.shape
-        y = ops.linear(x, self.w, self.b)
+        y = self.ctx.linear(x, None, self.w, self.ws, self.b)
         return y.view(B, T * self.f, self.cout)
 
 
 class LatticeHead:
     """UNet backbone + linear head: features [B, T_pad, C_in] -> logits [B, T_pad, V+2]."""
 
-    def __init__(self, arch: UNetArch, state_dict: dict, device="cuda"):
+    def __init__(self, arch: UNetArch, state_dict: dict, device="cuda", precision: str = "split"):
+        if precision not in ("split", "f32"):
+            raise ValueError(f"precision must be 'split' or 'f32', not {precision!r}")
         dev = torch.device(device)
         self.arch = arch
+        self.ctx = c = _Ctx(dev, precision)
         sd = {k[len("backbone."):] if k.startswith("backbone.") else k: v for k, v in state_dict.items()}
         self.divisible = arch.factor ** arch.times
-        self.encoders = [[_Block(sd, "encoders.0.", dev)]]
+        self.encoders = [[_Block(sd, "encoders.0.", dev, c)]]
         for i in range(1, arch.times):
-            self.encoders.append([_Down(sd, f"encoders.{i}.0.", dev), _Block(sd, f"encoders.{i}.1.", dev)])
-        self.bottleneck = [_Down(sd, "bottle_neck.0.", dev), _Block(sd, "bottle_neck.1.", dev),
-                           _Up(sd, "bottle_neck.2.", dev)]
+            self.encoders.append([_Down(sd, f"encoders.{i}.0.", dev, c), _Block(sd, f"encoders.{i}.1.", dev, c)])
+        self.bottleneck = [_Down(sd, "bottle_neck.0.", dev, c), _Block(sd, "bottle_neck.1.", dev, c),
+                           _Up(sd, "bottle_neck.2.", dev, c)]
         self.decoders = []
         for i in range(arch.times - 1):
-            self.decoders.append([_Block(sd, f"decoders.{i}.0.", dev), _Up(sd, f"decoders.{i}.1.", dev)])
-        self.decoders.append([_Block(sd, f"decoders.{arch.times - 1}.", dev)])
+            self.decoders.append([_Block(sd, f"decoders.{i}.0.", dev, c), _Up(sd, f"decoders.{i}.1.", dev, c)])
+        self.decoders.append([_Block(sd, f"decoders.{arch.times - 1}.", dev, c)])
         self.head_w = _t(sd["head.weight"]).float().contiguous().to(dev)
         self.head_b = _t(sd["head.bias"]).float().contiguous().to(dev)
+        self.head_ws = c.planes(self.head_w) if self.head_w.shape[0] % 4 == 0 else None   # f32 C rows: 16-B
         self.vocab_size = self.head_w.shape[0] - 2
+
+    @property
+    def precision(self) -> str:
+        return self.ctx.precision
+
+    @precision.setter
+    def precision(self, value: str):
+        self.ctx.precision = value
+
+    @property
+    def flag(self):
+        """Device int32 [1]: raised when a split operand of this head left f16 range (see task._guard)."""
+        return self.ctx.flag
 
     def padded_len(self, T: int) -> int:
         r = T % self.divisible
@@ -138,7 +201,7 @@ class LatticeHead:
 
     @torch.no_grad()
     def logits(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
-        return ops.linear(self.backbone(x, t_pad), self.head_w, self.head_b)
+        return self.ctx.linear(self.backbone(x, t_pad), None, self.head_w, self.head_ws, self.head_b)
 
     @staticmethod
     def split(logits: torch.Tensor):

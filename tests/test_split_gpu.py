@@ -200,15 +200,43 @@ def test_range_guard_reruns_batch_on_f32():
     task._align_f32 = lambda *a: calls.append(1) or redo(*a)
     got = task.align_batch(w, ph_seqs, word_seqs, p2ws, wav_sr=16000)
     assert calls == [1]
-    assert enc.precision == "split"
-    enc.precision = "f32"
+    assert enc.precision == "split" and task.head.precision == "split"
+    enc.precision = task.head.precision = "f32"
     ref = task.align_batch(w, ph_seqs, word_seqs, p2ws, wav_sr=16000)
-    enc.precision = "split"
+    enc.precision = task.head.precision = "split"
     for a, b in zip(got, ref):
         assert list(a["ph_seq"]) == list(b["ph_seq"])
         assert (a["ph_intervals"] == b["ph_intervals"]).all()
     import hubertfa_amd.ops as ops
     assert int(ops.split_flag(d).item()) == 0
+
+
+def test_range_guard_head_flag_reruns_batch():
+    """A UNet activation outside f16 range raises the head's own flag (snapshot on the stream that ran the head,
+    also through the two-stream submit path); the batch is re-run with f32 GEMMs in the encoder and the head."""
+    import bench
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+    d = torch.device("cuda")
+    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
+    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=d)
+    task.on_predict_start()
+    blk = task.head.encoders[0][0]
+    blk.gn[1][3] = 1.0e5                    # GroupNorm beta of one hidden channel: its conv2 input ~1e5
+    wav, ph_seqs, word_seqs, p2ws = bench.make_inputs(2, 2.0, 6, 5)
+    w = torch.from_numpy(wav).to(d)
+    calls = []
+    redo = task._align_f32
+    task._align_f32 = lambda *a: calls.append(1) or redo(*a)
+    got = task.decoder.assemble(task.submit(w, ph_seqs, word_seqs, p2ws, wav_sr=16000), ph_seqs, word_seqs, p2ws)
+    torch.cuda.synchronize()
+    assert calls == [1]
+    assert task.head.precision == "split" and int(task.head.flag.item()) == 0
+    task.unitsEncoder.model.precision = task.head.precision = "f32"
+    ref = task.align_batch(w, ph_seqs, word_seqs, p2ws, wav_sr=16000)
+    task.unitsEncoder.model.precision = task.head.precision = "split"
+    for a, b in zip(got, ref):
+        assert list(a["ph_seq"]) == list(b["ph_seq"])
+        assert (a["ph_intervals"] == b["ph_intervals"]).all()
 
 
 def _attn_ref(qkv, B, L, H, D, lens=None):
