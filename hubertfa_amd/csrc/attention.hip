@@ -56,7 +56,15 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
     const int bh = wgid / nqb, qb = wgid - bh * nqb;
     const int b = bh / p.H, hd = bh - b * p.H;
     const int L = p.key_len ? p.key_len[b] : p.L;       // this row's length (queries and keys beyond: padding)
-    if (qb * (QW * NW) >= L) return;                     // whole workgroup is padding (uniform exit)
+    if (qb * (QW * NW) >= L) {                           // whole workgroup is padding: zero its O rows, exit
+        for (int i = threadIdx.x; i < QW * NW * (DH / 4); i += NW * 64) {
+            const int qq = qb * (QW * NW) + i / (DH / 4), c4 = (i % (DH / 4)) * 4;
+            if (qq < p.L)
+                *reinterpret_cast<f32x4*>(p.o + b * p.o_bs + (long long)qq * p.o_ld + hd * DH + c4) =
+                    f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r32 = lane & 31, half = lane >> 5;
@@ -202,9 +210,10 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
             const int idx = lane + i * 64;
             const int row = idx >> 3, c4 = (idx & 7) * 4;
             const int qq = q0 + row;
-            if (qq < L) {
+            if (qq < p.L) {                     // rows past this row's length: zeros (padding of a varlen batch)
                 f32x4 v{slab[row * 33 + c4], slab[row * 33 + c4 + 1], slab[row * 33 + c4 + 2],
                         slab[row * 33 + c4 + 3]};
+                if (qq >= L) v = f32x4{0.f, 0.f, 0.f, 0.f};
                 *reinterpret_cast<f32x4*>(p.o + b * p.o_bs + (long long)qq * p.o_ld + hd * DH + dt * 32 + c4) = v;
             }
         }
@@ -263,7 +272,18 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP
     const int bh = wgid / nqb, qb = wgid - bh * nqb;
     const int b = bh / p.H, hd = bh - b * p.H;
     const int L = p.key_len ? p.key_len[b] : p.L;
-    if (qb * (QW * NW) >= L) return;                     // whole workgroup is padding (uniform exit)
+    if (qb * (QW * NW) >= L) {                           // whole workgroup is padding: zero its O rows, exit
+        for (int i = threadIdx.x; i < QW * NW * (DH / 4); i += NW * 64) {
+            const int qq = qb * (QW * NW) + i / (DH / 4), c4 = (i % (DH / 4)) * 4;
+            if (qq < p.L) {
+                _Float16* dst = p.o + b * p.o_bs + (long long)qq * p.o_ld + hd * DH + c4;
+                const f16x4 z{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+                *reinterpret_cast<f16x4*>(dst) = z;
+                *reinterpret_cast<f16x4*>(dst + p.o_sp) = z;
+            }
+        }
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r32 = lane & 31, half = lane >> 5;
@@ -452,11 +472,11 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP
             const int idx = lane + i * 64;
             const int row = idx >> 3, c4 = (idx & 7) * 4;
             const int qq = q0 + row;
-            if (qq < L) {
+            if (qq < p.L) {                     // rows past this row's length: zeros (padding of a varlen batch)
                 f16x4 h1, h2;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    const float x = slab[row * 33 + c4 + t];
+                    const float x = qq < L ? slab[row * 33 + c4 + t] : 0.0f;
                     h1[t] = (_Float16)x;
                     h2[t] = (_Float16)((x - (float)h1[t]) * 2048.0f);
                 }

@@ -9,10 +9,12 @@
 // HBM-bound: one wavefront per row, the row held in registers (C <= 4096), float4 loads, two-pass
 // mean/variance in f32 like ATen's reference path, then y = (x - mean) * rstd * gamma + beta.
 #include "hfa_common.h"
+#include "hfa.h"
 
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_HARDSWISH = 2 };
 
@@ -29,13 +31,24 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps, int act,
                                                         float* __restrict__ y, long long ldy, int T,
-                                                        const int32_t* __restrict__ t_len) {
+                                                        const int32_t* __restrict__ t_len,
+                                                        _Float16* __restrict__ ys, long long ldys, long long sps,
+                                                        int* __restrict__ oflow) {
+    // ys (optional): the output also as split-f16 planes (gemm.hip's split operand: hi, (x - hi) * 2^11), so the
+    // next split GEMM reads it without a separate conversion pass; *oflow raised for |y| >= 65504 / non-finite
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wave >= rows) return;
     if (t_len && wave % T >= t_len[wave / T]) {     // padding row of a variable-length batch: zeros
         float* yr = y + wave * ldy;
-        for (int c = lane * 4; c < C; c += 256) *reinterpret_cast<f32x4*>(yr + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int c = lane * 4; c < C; c += 256) {
+            *reinterpret_cast<f32x4*>(yr + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (ys) {
+                const f16x4 z{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+                *reinterpret_cast<f16x4*>(ys + wave * ldys + c) = z;
+                *reinterpret_cast<f16x4*>(ys + sps + wave * ldys + c) = z;
+            }
+        }
         return;
     }
     const float* xr = x + wave * ldx;
@@ -69,6 +82,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
     const float var = hfa::wave_sum(ss) / (float)C;
     const float rstd = 1.0f / sqrtf(var + eps);
     float* yr = y + wave * ldy;
+    bool bad = false;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
         const int c = (lane + i * 64) * 4;
@@ -79,8 +93,20 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = act_apply((v[i][e] - mean) * rstd * g[e] + bb[e], act);
             *reinterpret_cast<f32x4*>(yr + c) = o;
+            if (ys) {
+                f16x4 h1, h2;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    bad |= !(__builtin_fabsf(o[e]) < 65504.0f);
+                    h1[e] = (_Float16)o[e];
+                    h2[e] = (_Float16)((o[e] - (float)h1[e]) * 2048.0f);
+                }
+                *reinterpret_cast<f16x4*>(ys + wave * ldys + c) = h1;
+                *reinterpret_cast<f16x4*>(ys + sps + wave * ldys + c) = h2;
+            }
         }
     }
+    if (bad && oflow) *oflow = 1;
 }
 
 // GroupNorm over a channels-last [T, C] slab per batch item: group g = channels [g*Cg, (g+1)*Cg) over all T.
@@ -204,6 +230,19 @@ extern "C" {
 int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const float* res, long long ldr,
                       const float* gamma, const float* beta, float eps, int act, float* y, long long ldy, int T,
                       const int32_t* t_len, hipStream_t stream) {
+    return hfa_layernorm_split(rows, C, x, ldx, res, ldr, gamma, beta, eps, act, y, ldy, T, t_len, nullptr, 0, 0,
+                               nullptr, stream);
+}
+
+int hfa_layernorm_split(int rows, int C, const float* x, long long ldx, const float* res, long long ldr,
+                        const float* gamma, const float* beta, float eps, int act, float* y, long long ldy, int T,
+                        const int32_t* t_len, uint16_t* ys_, long long ldys, long long sps, int* oflow,
+                        hipStream_t stream) {
+    _Float16* ys = reinterpret_cast<_Float16*>(ys_);
+    if (ys && ((((uintptr_t)ys) & 7) || ldys % 4 || sps % 4)) {
+        hfa::set_error("hfa_layernorm_split: split planes need 8-byte alignment and strides multiple of 4 halves");
+        return HFA_EINVAL;
+    }
     if (t_len && (T <= 0 || rows % T)) {
         hfa::set_error("hfa_layernorm_f32: t_len needs rows = B * T (T=%d, rows=%d)", T, rows);
         return HFA_EINVAL;
@@ -222,7 +261,7 @@ int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const floa
     const int vpl = (C + 255) / 256;
 #define HFA_LN(V)                                                                                               \
     hipLaunchKernelGGL(layernorm_kernel<V>, dim3(blocks), dim3(256), 0, stream, rows, C, x, ldx, res, ldr, gamma, \
-                       beta, eps, act, y, ldy, T, t_len)
+                       beta, eps, act, y, ldy, T, t_len, ys, ldys, sps, oflow)
     if (vpl <= 1) HFA_LN(1);
     else if (vpl <= 2) HFA_LN(2);
     else if (vpl <= 3) HFA_LN(3);

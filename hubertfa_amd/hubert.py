@@ -215,6 +215,7 @@ class HubertEncoder:
         return h
 
     def _linear(self, x, w, ws, bias=None, residual=None, epilogue=ops.EPI_NONE, out_split=False, xs=None):
+        # (xs: x's split planes when its producer wrote them; only read on the split path)
         """Linear on the split GEMM when this encoder runs split and the weight has planes (x given as f32 and/or
         as planes xs), else on the f32 GEMM."""
         if self.precision == "split" and ws is not None:
@@ -242,7 +243,8 @@ class HubertEncoder:
             ops.conv_gemm(h, self.pos_w, out, **kw)
         return out
 
-    def attention_block(self, h_in: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None) -> torch.Tensor:
+    def attention_block(self, h_in: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None,
+                        hs: torch.Tensor | None = None) -> torch.Tensor:
         """softmax(QK^T/sqrt(dh))V over the fused QKV projection.  Split precision: QKV written as split planes,
         attention on the split kernel, O returned as split planes (the out-projection's A operand)."""
         a = self.arch
@@ -250,7 +252,7 @@ class HubertEncoder:
         nh = a.heads
         dh = H // nh
         if self.precision == "split" and L_.wqkv_s is not None and L_.wo_s is not None and dh == 64:
-            qkv_s = self._linear(h_in, L_.wqkv, L_.wqkv_s, L_.bqkv, out_split=True)
+            qkv_s = self._linear(h_in, L_.wqkv, L_.wqkv_s, L_.bqkv, out_split=True, xs=hs)
             o_s = torch.empty((2, B, L, H), dtype=torch.float16, device=h_in.device)
             return ops.attention_split(qkv_s, o_s, B=B, H=nh, L=L, head_dim=dh, scale=dh ** -0.5, key_len=lens)
         qkv = self._linear(h_in, L_.wqkv, L_.wqkv_s, L_.bqkv)
@@ -265,26 +267,36 @@ class HubertEncoder:
             return self._linear(None, L_.wo, L_.wo_s, L_.bo, residual=residual, xs=o)
         return self._linear(o, L_.wo, L_.wo_s, L_.bo, residual=residual)
 
-    def layer(self, h: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None) -> torch.Tensor:
+    def _ln(self, x, w, b, out=None, split=False):
+        """LayerNorm; with ``split`` (a split GEMM consumes the result) also the split planes, from the same
+        kernel: returns (y, planes) — planes None when not requested."""
         eps = self.arch.layer_norm_eps
+        if split and self.precision == "split":
+            return ops.layernorm(x, w, b, eps, out=out, out_split=True)
+        return ops.layernorm(x, w, b, eps, out=out), None
+
+    def layer(self, h: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None, hs: torch.Tensor | None = None,
+              want_split: bool = False):
+        """One encoder layer: (h, hs) -> (h', hs').  ``hs``: h's split planes if its producer wrote them;
+        ``want_split``: also return the output's planes (the next layer's QKV operand), else None."""
         sp = self.precision == "split" and L_.w1_s is not None and L_.w2_s is not None
         if not self.arch.stable_layer_norm:   # post-LN (HubertEncoderLayer / nn.TransformerEncoderLayer)
-            o = self.attention_block(h, L_, lens)
+            o = self.attention_block(h, L_, lens, hs)
             h1 = self._out_proj(o, L_, h)
-            h1 = ops.layernorm(h1, L_.ln1_w, L_.ln1_b, eps, out=h1)
-            f = self._linear(h1, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp)
+            h1, h1s = self._ln(h1, L_.ln1_w, L_.ln1_b, out=h1, split=sp)
+            f = self._linear(h1, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp, xs=h1s)
             h2 = self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h1, xs=f) if sp else \
                 ops.linear(f, L_.w2, L_.b2, residual=h1)
-            return ops.layernorm(h2, L_.ln2_w, L_.ln2_b, eps, out=h2)
+            return self._ln(h2, L_.ln2_w, L_.ln2_b, out=h2, split=want_split)
         # pre-LN (HubertEncoderLayerStableLayerNorm)
-        a_ = ops.layernorm(h, L_.ln1_w, L_.ln1_b, eps)
-        o = self.attention_block(a_, L_, lens)
+        a_, a_s = self._ln(h, L_.ln1_w, L_.ln1_b, split=L_.wqkv_s is not None)
+        o = self.attention_block(a_, L_, lens, a_s)
         h = self._out_proj(o, L_, h)
-        a_ = ops.layernorm(h, L_.ln2_w, L_.ln2_b, eps)
-        f = self._linear(a_, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp)
+        a_, a_s = self._ln(h, L_.ln2_w, L_.ln2_b, split=sp)
+        f = self._linear(a_, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp, xs=a_s)
         if sp:
-            return self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h, xs=f)
-        return ops.linear(f, L_.w2, L_.b2, residual=h)
+            return self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h, xs=f), None
+        return ops.linear(f, L_.w2, L_.b2, residual=h), None
 
     @torch.no_grad()
     def forward(self, wav: torch.Tensor, n_layers: int | None = None, lengths=None) -> torch.Tensor:
@@ -309,13 +321,15 @@ class HubertEncoder:
         if a.wav_pad:
             x = ops.pad_rows(x, a.wav_pad, x.shape[1] + 2 * a.wav_pad)
         feats = self.feature_extractor(x, lens0)
-        fln = ops.layernorm(feats, self.fp_ln[0], self.fp_ln[1], a.layer_norm_eps)
-        h = self._linear(fln, self.fp_w, self.fp_ws, self.fp_b)
+        fln, flns = self._ln(feats, self.fp_ln[0], self.fp_ln[1], split=self.fp_ws is not None)
+        h = self._linear(fln, self.fp_w, self.fp_ws, self.fp_b, xs=flns)
         h = self.positional(h, lensL)
+        hs = None
+        layers = self.layers[:n_layers]
         if not a.stable_layer_norm:
-            h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
-        for L_ in self.layers[:n_layers]:
-            h = self.layer(h, L_, lensL)
+            h, hs = self._ln(h, self.enc_ln[0], self.enc_ln[1], out=h, split=bool(layers))
+        for i, L_ in enumerate(layers):
+            h, hs = self.layer(h, L_, lensL, hs, want_split=i + 1 < len(layers))
         if a.stable_layer_norm:
             h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
         if self.proj is not None:

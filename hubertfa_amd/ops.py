@@ -143,6 +143,8 @@ _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_
                                     _LL_, _I_, _P_, _P_])
 _lib.register("hfa_attention_split", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _LL_,
                                       _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _P_])
+_lib.register("hfa_layernorm_split", [_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_,
+                                      _LL_, _P_, _P_])
 _lib.register("hfa_layernorm_f32",[_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_])
 _lib.register("hfa_groupnorm_f32", [_I_, _I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_,
                                     _P_, _P_])
@@ -380,8 +382,10 @@ def attention_split(qkv_s, out_s, *, B, H, L, head_dim, scale, key_len=None):
     return out_s
 
 
-def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None, t_len=None):
-    """Row LayerNorm (+act) over the last dim; with ``t_len`` [B] (x is [B, T, C]) rows t >= t_len[b] -> 0."""
+def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None, t_len=None, out_split=None,
+              flag=None):
+    """Row LayerNorm (+act) over the last dim; with ``t_len`` [B] (x is [B, T, C]) rows t >= t_len[b] -> 0.
+    ``out_split`` ([2, ..., C] f16, or True to allocate): the output also as split planes (returned second)."""
     C = x.shape[-1]
     x2 = x.reshape(-1, C)
     if out is None:
@@ -390,10 +394,20 @@ def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None, t
     r2 = residual.reshape(-1, C) if residual is not None else None
     tl = _lens(t_len)
     T = x.shape[-2] if (tl is not None and x.dim() == 3) else 0
-    _lib.call("hfa_layernorm_f32", x2.shape[0], C, _ptr(x2), x2.stride(0), _ptr(r2),
+    if out_split is None or out_split is False:
+        _lib.call("hfa_layernorm_f32", x2.shape[0], C, _ptr(x2), x2.stride(0), _ptr(r2),
+                  r2.stride(0) if r2 is not None else 0, _ptr(gamma), _ptr(beta), float(eps), act, _ptr(o2),
+                  o2.stride(0), T, _ptr(tl), _stream(x.device))
+        return out
+    if out_split is True:
+        out_split = torch.empty((2, *x.shape), dtype=torch.float16, device=x.device)
+    _need(out_split, torch.float16, "out_split")
+    s2 = out_split.view(2, -1, C)
+    _lib.call("hfa_layernorm_split", x2.shape[0], C, _ptr(x2), x2.stride(0), _ptr(r2),
               r2.stride(0) if r2 is not None else 0, _ptr(gamma), _ptr(beta), float(eps), act, _ptr(o2),
-              o2.stride(0), T, _ptr(tl), _stream(x.device))
-    return out
+              o2.stride(0), T, _ptr(tl), _ptr(s2), s2.stride(1), s2.stride(0),
+              _ptr(split_flag(x.device) if flag is None else flag), _stream(x.device))
+    return out, out_split
 
 
 def groupnorm(x, G, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, t_len=None):

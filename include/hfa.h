@@ -127,6 +127,7 @@ int hfa_split_f16(int rows, int cols, const float* x, long long ldx, uint16_t* y
 /* ---- attention (hubertfa_amd/csrc/attention.hip) -----------------------------------------------------------
  * O = softmax(scale * Q K^T) V per (batch, head), head_dim 64, fp32 MFMA flash attention.
  * Q(b,h,i,d) at q + b*q_bs + i*q_ld + h*64 + d (same for k, v, o).
+ * With key_len, O rows i >= key_len[b] (padding queries) are written as zeros.
  * Replaces nn.MultiheadAttention/SDPA in networks/hubert/model.py:27-32 and transformers
  * modeling_hubert.py HubertAttention (eager_attention_forward). */
 int hfa_attention_f32(int B, int H, int L, int head_dim, float scale, const float* q, long long q_bs, int q_ld,
@@ -148,6 +149,13 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
 int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const float* res, long long ldr,
                       const float* gamma, const float* beta, float eps, int act, float* y, long long ldy, int T,
                       const int32_t* t_len, hipStream_t stream);
+/* hfa_layernorm_f32 that also writes its output as split-f16 planes (see hfa_conv_gemm_split): ys row r at
+ * ys + r*ldys, plane 1 at +sps halves (8-B aligned rows), so the consuming split GEMM needs no conversion pass;
+ * *oflow raised for outputs outside f16 range. */
+int hfa_layernorm_split(int rows, int C, const float* x, long long ldx, const float* res, long long ldr,
+                        const float* gamma, const float* beta, float eps, int act, float* y, long long ldy, int T,
+                        const int32_t* t_len, uint16_t* ys, long long ldys, long long sps, int* oflow,
+                        hipStream_t stream);
 /* GroupNorm(G, C) over a channels-last [B, T, C] tensor (+act).  Replaces resnet_block.py:153-154
  * (nn.GroupNorm(16, C) + nn.Hardswish). */
 int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,

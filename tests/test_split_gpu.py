@@ -154,6 +154,31 @@ def test_split_single_acc_weight_range_flag(cfg, outs):
     flag.zero_()
 
 
+@pytest.mark.parametrize("C,act,varlen", [(768, 0, False), (1024, 1, True), (192, 2, True), (512, 0, False)])
+def test_layernorm_split_output(C, act, varlen):
+    """LayerNorm's fused split-plane output equals split(LayerNorm(x)) bit for bit (padding rows zero)."""
+    from hubertfa_amd import ops
+    from hubertfa_amd.hubert import dev_lengths
+    d = torch.device("cuda")
+    B, T = 3, 50
+    x = (_r(B, T, C, seed=20, scale=3.0) + 0.5).to(d)
+    r = _r(B, T, C, seed=21).to(d)
+    g, b = (_r(C, seed=22) * 0.1 + 1).to(d), (_r(C, seed=23) * 0.1).to(d)
+    tl = dev_lengths([50, 17, 3], d) if varlen else None
+    flag = ops.split_flag(d)
+    flag.zero_()
+    y, ys = ops.layernorm(x, g, b, 1e-5, act=act, residual=r, t_len=tl, out_split=True)
+    y_ref = ops.layernorm(x, g, b, 1e-5, act=act, residual=r, t_len=tl)
+    assert torch.equal(y, y_ref)
+    assert torch.equal(ys, ops.split(y_ref))
+    assert int(flag.item()) == 0
+    big = torch.full((4, C), 1.0, device=d)
+    big[:, 0] = 1e9                           # normalised output stays small: no flag
+    ops.layernorm(big, g, b * 0 + 7e4, 1e-5, out_split=True)          # beta 7e4: every output >= 65504
+    assert int(flag.item()) == 1
+    flag.zero_()
+
+
 def test_conv0_split_output_matches_f32():
     from hubertfa_amd import ops
     d = torch.device("cuda")
@@ -275,7 +300,7 @@ def test_attention_split_varlen():
     ref = _attn_ref(qkv, B, L, H, D, lens)
     d = torch.device("cuda")
     qs = ops.split(qkv.to(d))
-    out = torch.zeros(2, B, L, H * D, dtype=torch.float16, device=d)
+    out = torch.full((2, B, L, H * D), float("nan"), dtype=torch.float16, device=d)   # padding rows must be written
     ops.attention_split(qs, out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5, key_len=dev_lengths(lens, d))
     got = (out[0].float() + out[1].float() / 2048.0).cpu()
     for b, n in enumerate(lens):
