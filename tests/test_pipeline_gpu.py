@@ -16,7 +16,10 @@ def _inputs(B, seconds, words, seed0):
     return bench.make_inputs(B, seconds, words, seed0)
 
 
-def test_full_path_logprobs_and_boundaries_vs_oracle():
+@pytest.mark.parametrize("precision", ["split", "f32"])
+def test_full_path_logprobs_and_boundaries_vs_oracle(precision):
+    """Both arithmetic paths meet the bars: the default split-f16 contractions and the f32-MFMA path the range
+    guard falls back to."""
     import yaml
     from hubertfa_amd import synth
     from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
@@ -28,6 +31,7 @@ def test_full_path_logprobs_and_boundaries_vs_oracle():
     B = 3
     wav, ph_seqs, word_seqs, p2ws = _inputs(B, 10.0, 30, 777)
     task.on_predict_start()
+    task.unitsEncoder.model.precision = task.head.precision = precision
     dev_out = task.align_batch(torch.from_numpy(wav).to(dev), ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False)
     res = task.decoder.assemble(dev_out, ph_seqs, word_seqs, p2ws)
     gpu_pl = dev_out["lattice"]["prob_log"].cpu().numpy()
@@ -57,7 +61,7 @@ def test_full_path_logprobs_and_boundaries_vs_oracle():
         assert list(res[b]["ph_seq"]) == list(ph) and list(res[b]["word_seq"]) == list(w)
         np.testing.assert_allclose(res[b]["ph_intervals"], ph_iv, atol=1e-5)
         np.testing.assert_allclose(res[b]["confidence"], conf, rtol=1e-4)
-    print(f"max per-frame log-prob error over {B} x 10 s: {worst:.2e}")
+    print(f"[{precision}] max per-frame log-prob error over {B} x 10 s: {worst:.2e}")
 
 
 def test_smoke_entry():
