@@ -731,7 +731,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     const unsigned lds0 = hfa::lds_addr(smem);
     int cur_j = 0, cur_c0 = 0, cur_k0 = 0;
     if constexpr (!GT) set_tap(0);
-    auto issue = [&](int stage) {
+    auto issueA = [&](int stage) {
         const unsigned base = lds0 + stage * STAGE * 2 + wave * 1024;
 #pragma unroll
         for (int d = 0; d < DA; ++d) {
@@ -750,11 +750,16 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
                 hfa::dma16(voffA[d], rA2, (unsigned)cur_c0 * 2, base + PA * 2 + d * NW * 1024);
             }
         }
+    };
+    auto issueW = [&](int stage) {
+        const unsigned base = lds0 + stage * STAGE * 2 + wave * 1024;
 #pragma unroll
         for (int d = 0; d < DB; ++d) {
             hfa::dma16(voffW[d], rW1, (unsigned)cur_k0 * 2, base + 2 * PA * 2 + d * NW * 1024);
             hfa::dma16(voffW[d], rW2, (unsigned)cur_k0 * 2, base + (2 * PA + PW) * 2 + d * NW * 1024);
         }
+    };
+    auto advance = [&]() {
         cur_k0 += BK;
         if constexpr (!GT) {
             cur_c0 += BK;
@@ -763,6 +768,11 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
                 set_tap(++cur_j);
             }
         }
+    };
+    auto issue = [&](int stage) {
+        issueA(stage);
+        issueW(stage);
+        advance();
     };
     constexpr int DN = 2 * (DA + DB);                       // DMA issues per wave per K-step
 
@@ -802,12 +812,23 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     int stage = 0;
     for (int kt = 0; kt < nk; ++kt) {
         const bool more = kt + NS - 1 < nk;
+        const int nstage = stage == 0 ? NS - 1 : stage - 1;
 #ifndef HFA_SABL_NODMA
-        if (more) issue(stage == 0 ? NS - 1 : stage - 1);
+#ifdef HFA_SPLIT_SPREAD
+        if (more) issueA(nstage);          // W half after the first MFMA sub-step: spreads the LDS-DMA writes
+#else
+        if (more) issue(nstage);
+#endif
 #endif
         const f16x8* st = s8 + stage * (STAGE / 8);
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk) {
+#if defined(HFA_SPLIT_SPREAD) && !defined(HFA_SABL_NODMA)
+            if (kk == KK - 1 && more) {
+                issueW(nstage);
+                advance();
+            }
+#endif
             f16x8 a1[TI], a2[TI], w1[TJ], w2[TJ];
 #pragma unroll
             for (int i = 0; i < TI; ++i) {
@@ -823,6 +844,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
                 f16x8 w1s[TJ];
 #pragma unroll
                 for (int j = 0; j < TJ; ++j) w1s[j] = w1[j] * (_Float16)2048.0f;
+#ifdef HFA_SPLIT_PRIO
+                __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
                 for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -835,6 +859,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
                         accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accM[i][j], 0, 0, 0);
 #endif
                     }
+#ifdef HFA_SPLIT_PRIO
+                __builtin_amdgcn_s_setprio(0);
+#endif
             } else {
 #pragma unroll
                 for (int i = 0; i < TI; ++i)
@@ -1016,14 +1043,15 @@ inline int set_grid(GemmP& p, int BM, int BN, dim3& grid, int Z) {
 // ---- split-f16 dispatch --------------------------------------------------------------------------------------
 enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_128x128_NS3 = 4, SCFG_128x128_NS4 = 5,
        SCFG_256x128_NS3 = 6, SCFG_256x256_1 = 7, SCFG_256x128_1 = 8, SCFG_128x128_1 = 9, SCFG_128x64_1 = 10,
-       SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_COUNT = 14 };
+       SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_256x64_1 = 14,
+       SCFG_COUNT = 15 };
 struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; };
 constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 128, 2, 2, 2, 2, false, 32}, {128, 128, 2, 2, 2, 2, false, 32}, {128, 64, 2, 2, 2, 2, false, 32},
     {256, 128, 4, 2, 2, 1, false, 32}, {128, 128, 2, 2, 3, 1, false, 32}, {128, 128, 2, 2, 4, 1, false, 32},
     {256, 128, 4, 2, 3, 1, false, 32}, {256, 256, 2, 4, 2, 1, true, 32},  {256, 128, 2, 2, 2, 1, true, 32},
     {128, 128, 2, 2, 2, 2, true, 32},  {128, 64, 2, 2, 2, 2, true, 32},   {256, 256, 2, 4, 4, 1, true, 16},
-    {256, 256, 2, 4, 3, 1, true, 16},  {128, 128, 2, 2, 4, 2, true, 16}};
+    {256, 256, 2, 4, 3, 1, true, 16},  {128, 128, 2, 2, 4, 2, true, 16},  {256, 64, 4, 1, 2, 2, true, 32}};
 int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 
 // Measured on the workload's shapes (scripts/split_gemm_bench.py, profiles/r01/split_gemm_cfgs.txt): the 256 x 256
@@ -1036,12 +1064,14 @@ inline int split_cfg(const GemmP& p, int Z) {
     if (g_split_cfg > 0 && g_split_cfg < SCFG_COUNT) return g_split_cfg;
     const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
     const long long blocks256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * Z;
+    if (p.N == 64 && p.Cg % 32 == 0 && (long long)((p.M + 255) / 256) * Z >= 256)
+        return SCFG_256x64_1;              // grouped positional conv at Cg = 64 (Hubert-large): 1.26x the 128x64 tile
     if (p.N <= 64 || blocks128 < 256) return SCFG_128x64_1;
     return (blocks256 >= 128 && p.N >= 512) ? SCFG_256x256_1 : SCFG_128x128_1;
 }
 
 inline void split_name(int cfg, int epi, bool outs, bool gt, char* buf, int len) {
-    if (gt) cfg = kSplitGeom[cfg].BN == 64 ? SCFG_128x64_1 : SCFG_128x128_1;
+    if (gt && cfg != SCFG_256x64_1) cfg = kSplitGeom[cfg].BN == 64 ? SCFG_128x64_1 : SCFG_128x128_1;
     const SplitGeom& g = kSplitGeom[cfg];
     snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, %s, %d>", epi, g.BM, g.BN, g.WM, g.WN,
              g.NS, g.OCC, outs ? "true" : "false", gt ? "true" : "false", g.ONE ? "true" : "false", g.BK);
@@ -1064,6 +1094,7 @@ int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
             hfa::set_error("hfa_conv_gemm_split: Cg %% 32 != 0 takes no split output");
             return HFA_EINVAL;
         } else {
+            if (cfg == SCFG_256x64_1) return launch_split_cfg<EPI, false, SCFG_256x64_1, true>(p, Z, st);
             return kSplitGeom[cfg].BN == 64 ? launch_split_cfg<EPI, false, SCFG_128x64_1, true>(p, Z, st)
                                             : launch_split_cfg<EPI, false, SCFG_128x128_1, true>(p, Z, st);
         }
@@ -1081,6 +1112,7 @@ int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
         case SCFG_256x256_1_K16S4: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1_K16S4>(p, Z, st);
         case SCFG_256x256_1_K16S3: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1_K16S3>(p, Z, st);
         case SCFG_128x128_1_K16S4: return launch_split_cfg<EPI, OUTS, SCFG_128x128_1_K16S4>(p, Z, st);
+        case SCFG_256x64_1: return launch_split_cfg<EPI, OUTS, SCFG_256x64_1>(p, Z, st);
         default: return launch_split_cfg<EPI, OUTS, SCFG_128x128>(p, Z, st);
     }
 }

@@ -116,8 +116,9 @@ const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int e
 /* Tile override for the split GEMM: 0 auto, 1 128x128, 2 128x64, 3 256x128 (8 waves), 4/5 128x128 with 3/4
  * stages (one workgroup per CU), 6 256x128 with 3 stages, 7 256x256 single accumulator (8 waves of 128x64),
  * 8 256x128 single accumulator (4 waves), 9 128x128 single accumulator, 10 128x64 single accumulator, 11/12
- * 256x256 single accumulator with 16-deep K-steps and 4/3 stages, 13 128x128 likewise with 4 stages.  The
- * automatic choice uses single-accumulator tiles only (7, 9, 10): results then do not depend on the tile. */
+ * 256x256 single accumulator with 16-deep K-steps and 4/3 stages, 13 128x128 likewise with 4 stages, 14 256x64
+ * single accumulator (4 waves of 64x64).  The
+ * automatic choice uses single-accumulator tiles only (7, 9, 10, 14): results then do not depend on the tile. */
 int hfa_gemm_split_tuning(int cfg);
 /* x [rows, cols] f32 (row stride ldx) -> split planes y (row stride ldy, plane 1 at +sp); raises *oflow (if
  * non-NULL) for |x| >= 65504 or a non-finite x. */

@@ -1,0 +1,11 @@
+# PMC passes over the attention microbenchmark (split and f32 kernels), one counter group per pass.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS"; do
+  tag=$(echo $C | cut -d' ' -f1)
+  rm -rf gpurun_out/pmc_gemm_$tag
+  timeout -k 10 200 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/pmc_gemm_$tag -o run -- python3 scripts/attn_bench.py --reps 3 > gpurun_out/pmc_gemm_$tag.log 2>&1 || { echo "PMC $tag FAIL"; exit 1; }
+done
+KFILTER=attn_fwd python scripts/pmc_gemm.py gpurun_out > gpurun_out/pmc_attn_summary.txt 2>&1; cat gpurun_out/pmc_attn_summary.txt
+echo ALLOK

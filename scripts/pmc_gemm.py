@@ -13,16 +13,18 @@ import os
 import sys
 from collections import defaultdict
 
+KERNELS = tuple(os.environ.get("KFILTER", "gemm_f32_kernel,gemm_dma_kernel,gemm_split_kernel").split(","))
+
 
 def load(d):
     out = defaultdict(dict)
     for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(fn)):
-            if not any(t in r["Kernel_Name"] for t in ("gemm_f32_kernel", "gemm_dma_kernel", "gemm_split_kernel")):
+            if not any(t in r["Kernel_Name"] for t in KERNELS):
                 continue
             k = int(r["Dispatch_Id"])
             e = out[k]
-            e["name"] = r["Kernel_Name"].split("(anonymous namespace)::")[1].split(">")[0] + ">"
+            e["name"] = r["Kernel_Name"].split("(anonymous namespace)::")[1].split("(")[0]
             e["grid"] = int(r["Grid_Size"])
             e["ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])

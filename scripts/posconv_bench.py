@@ -6,7 +6,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from hubertfa_amd import ops  # noqa: E402
+from hubertfa_amd import ops, _lib  # noqa: E402
 
 
 def timeit(fn, reps=20):
@@ -36,6 +36,11 @@ for H, G in ((768, 16), (1024, 16)):
     ws = ops.split(w)
     fl = 2.0 * B * L * H * Cg * k
     ms32 = timeit(lambda: ops.conv_gemm(x, w, out, **kw))
-    mss = timeit(lambda: ops.conv_gemm_split(ops.split(x), ws, C=out, **kw))
-    print(f"H={H} Cg={Cg}: f32 {ms32:.3f} ms ({fl / ms32 / 1e9:.0f} TF) | split (incl. x split) {mss:.3f} ms "
-          f"({fl / mss / 1e9:.0f} TF)", flush=True)
+    line = f"H={H} Cg={Cg}: f32 {ms32:.3f} ms ({fl / ms32 / 1e9:.0f} TF)"
+    xs = ops.split(x)
+    for cfg in (0, 10, 14, 9):
+        _lib.lib().hfa_gemm_split_tuning(cfg)
+        mss = timeit(lambda: ops.conv_gemm_split(xs, ws, C=out, **kw))
+        line += f" | cfg{cfg} {mss:.3f} ms ({fl / mss / 1e9:.0f} TF)"
+    _lib.lib().hfa_gemm_split_tuning(0)
+    print(line, flush=True)

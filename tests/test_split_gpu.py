@@ -42,7 +42,7 @@ def test_split_planes_and_flag():
     flag.zero_()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13, 14])
 @pytest.mark.parametrize("M,N,K,epi,res,outs", [(300, 200, 128, 0, False, False), (1000, 768, 768, 1, False, False),
                                                 (257, 72, 192, 0, True, False), (4096, 3072, 768, 1, False, True),
                                                 (130, 2304, 768, 0, False, True), (64, 768, 3072, 0, True, False)])
@@ -88,7 +88,8 @@ def test_split_conv_vs_conv1d(Cin, Cout, k, s, pad, T):
 
 
 @pytest.mark.parametrize("H,G,k,L,cfg", [(768, 16, 128, 499, 0), (768, 16, 128, 77, 1), (96, 2, 8, 40, 0),
-                                         (640, 16, 16, 130, 0)])
+                                         (640, 16, 16, 130, 0), (768, 16, 128, 300, 14), (1024, 16, 32, 260, 14),
+                                         (1024, 16, 128, 499, 0)])
 def test_split_grouped_posconv_general_taps(H, G, k, L, cfg):
     """Grouped positional conv with Cg = H/G not a multiple of 32 (48 at Hubert-base: per-lane tap tracking),
     GELU + residual epilogue, pad k/2 and the last frame dropped, against f64 conv1d (model.py:132-147)."""
@@ -124,7 +125,7 @@ def test_split_single_acc_tiles_bit_identical(outs):
     xs, ws = ops.split(_r(M, K, seed=1).to(d)), ops.split(_r(N, K, seed=2, scale=K ** -0.5).to(d))
     b = _r(N, seed=3).to(d)
     outs_ = []
-    for cfg in (7, 9, 10, 8, 11, 12, 13):
+    for cfg in (7, 9, 10, 8, 11, 12, 13, 14):
         _lib.lib().hfa_gemm_split_tuning(cfg)
         try:
             outs_.append(ops.linear_split(xs, ws, b, epilogue=ops.EPI_GELU, out_split=outs))
