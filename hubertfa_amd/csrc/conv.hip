@@ -66,18 +66,28 @@ __global__ __launch_bounds__(NT) void conv0_stats_kernel(int N, int T0, const fl
     pp[0] = sa; pp[1] = qa; pp[2] = sb; pp[3] = qb;
 }
 
+// One block per (64 channels, batch row): 4 partitions of the chunks per channel summed in parallel, then combined
+// in a fixed order (deterministic, independent of the batch it runs in).
 __global__ __launch_bounds__(NT) void conv0_reduce_kernel(int T0, int nchunk, const double* __restrict__ part,
                                                           float eps, float* __restrict__ stats,
                                                           const int32_t* __restrict__ t0_len) {
-    const int b = blockIdx.x;
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), q4 = threadIdx.x >> 6;
     if (t0_len) T0 = t0_len[b];
-    for (int c = threadIdx.x; c < C0; c += NT) {
-        double s = 0.0, q = 0.0;
-        for (int k = 0; k < nchunk; ++k) {
-            const double* pp = part + ((size_t)(b * nchunk + k) * C0 + c) * 2;
-            s += pp[0];
-            q += pp[1];
-        }
+    double s = 0.0, q = 0.0;
+    for (int k = q4; k < nchunk; k += 4) {
+        const double* pp = part + ((size_t)(b * nchunk + k) * C0 + c) * 2;
+        s += pp[0];
+        q += pp[1];
+    }
+    __shared__ double red[2][4][64];
+    red[0][q4][threadIdx.x & 63] = s;
+    red[1][q4][threadIdx.x & 63] = q;
+    __syncthreads();
+    if (q4 == 0) {
+        const int l = threadIdx.x;
+        s = (red[0][0][l] + red[0][1][l]) + (red[0][2][l] + red[0][3][l]);
+        q = (red[1][0][l] + red[1][1][l]) + (red[1][2][l] + red[1][3][l]);
         const double mean = s / T0;
         double var = q / T0 - mean * mean;
         if (var < 0) var = 0;
@@ -149,6 +159,62 @@ __global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const fl
     if (OUTS && bad && oflow) *oflow = 1;
 }
 
+// Split-plane output with 8 channels per lane: a wave stores one frame's 512 channels as 16-B pieces per plane
+// (1 KiB per wave-instruction instead of 256 B); 4 frames in flight per block.  Same arithmetic, same bits as
+// conv0_apply_kernel<MODE, true>.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+template <int MODE>
+__global__ __launch_bounds__(NT) void conv0_apply8_kernel(int N, int T0, const float* __restrict__ x, long long x_bs,
+                                                          const float* __restrict__ w0, const float* __restrict__ stats,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta,
+                                                          const float* __restrict__ bias, _Float16* __restrict__ yh,
+                                                          long long y_bs, long long y_sp, int* __restrict__ oflow) {
+    __shared__ float xs[CH * ST + KW];
+    const int b = blockIdx.y, chunk = blockIdx.x;
+    const int t0 = chunk * CH;
+    const int nt = min(CH, T0 - t0);
+    stage_chunk(xs, x + b * x_bs, t0, nt, N);
+    const int c0 = (threadIdx.x & 63) * 8, fr = threadIdx.x >> 6;
+    float w[8][KW], mul[8], add[8], mu[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < KW; ++j) w[i][j] = w0[(c0 + i) * KW + j];
+        if (MODE == 0) {
+            mu[i] = stats[(b * C0 + c0 + i) * 2];
+            mul[i] = stats[(b * C0 + c0 + i) * 2 + 1];
+            add[i] = beta[c0 + i];
+        } else {
+            mu[i] = 0.f;
+            mul[i] = 1.f;
+            add[i] = bias ? bias[c0 + i] : 0.f;
+        }
+    }
+    float g[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = MODE == 0 ? gamma[c0 + i] : 1.f;
+    __syncthreads();
+    _Float16* yb = yh + b * y_bs + (long long)t0 * C0 + c0;
+    bool bad = false;
+    for (int t = fr; t < nt; t += NT / 64) {
+        f16x8 h1, h2;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float v = conv10(w[i], xs + t * ST);
+            if (MODE == 0) v = hfa::gelu_fast((v - mu[i]) * mul[i] * g[i] + add[i]);
+            else v += add[i];
+            bad |= !(__builtin_fabsf(v) < 65504.0f);
+            h1[i] = (_Float16)v;
+            h2[i] = (_Float16)((v - (float)h1[i]) * 2048.0f);
+        }
+        *reinterpret_cast<f16x8*>(yb + (long long)t * C0) = h1;
+        *reinterpret_cast<f16x8*>(yb + (long long)t * C0 + y_sp) = h2;
+    }
+    if (bad && oflow) *oflow = 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -177,17 +243,25 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
     const int T0 = (N - KW) / ST + 1;
     const int nchunk = (T0 + CH - 1) / CH;
     dim3 grid(nchunk, B);
+    const bool vec8 = ((uintptr_t)y & 15) == 0 && y_bs % 8 == 0 && y_sp % 8 == 0;   // 16-B plane pieces
     if (norm) {
         double* part = reinterpret_cast<double*>(workspace);
         float* stats = reinterpret_cast<float*>(part + (size_t)B * nchunk * C0 * 2);
         hipLaunchKernelGGL(conv0_stats_kernel, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, part, t0_len);
-        hipLaunchKernelGGL(conv0_reduce_kernel, dim3(B), dim3(NT), 0, stream, T0, nchunk, part, eps, stats, t0_len);
-        if (outs)
+        hipLaunchKernelGGL(conv0_reduce_kernel, dim3(C0 / 64, B), dim3(NT), 0, stream, T0, nchunk, part, eps, stats,
+                           t0_len);
+        if (outs && vec8)
+            hipLaunchKernelGGL((conv0_apply8_kernel<0>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats, gamma,
+                               beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
+        else if (outs)
             hipLaunchKernelGGL((conv0_apply_kernel<0, true>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, y, y_bs, y_sp, oflow);
         else
             hipLaunchKernelGGL((conv0_apply_kernel<0, false>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, y, y_bs, y_sp, oflow);
+    } else if (outs && vec8) {
+        hipLaunchKernelGGL((conv0_apply8_kernel<1>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, nullptr, nullptr,
+                           nullptr, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
     } else if (outs) {
         hipLaunchKernelGGL((conv0_apply_kernel<1, true>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, nullptr,
                            nullptr, nullptr, bias, y, y_bs, y_sp, oflow);

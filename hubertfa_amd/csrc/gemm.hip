@@ -708,6 +708,10 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         m = m < p.M ? m : p.M - 1;
         a_t0[d] = m * p.stride - p.pad;
         a_c[d] = ((lane % CPR) ^ swz(row)) * 8;             // GT: the chunk's channel within its current tap
+#ifdef HFA_SABL_WIDEROW     // timing ablation: each DMA covers 8 rows x 128 B (the access pattern of 128-B rows)
+        a_t0[d] = (m - (lane >> 2) + (lane >> 3)) * p.stride - p.pad;
+        a_c[d] = (lane & 7) * 8;
+#endif
         a_tap[d] = 0;
     }
 #pragma unroll
@@ -720,6 +724,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
 #endif
         n = n < p.N ? n : p.N - 1;
         voffW[d] = (unsigned)((n * p.ldw + ((lane % CPR) ^ swz(row)) * 8) * 2);
+#ifdef HFA_SABL_WIDEROW
+        voffW[d] = (unsigned)(((n - (lane >> 2) + (lane >> 3)) * p.ldw + (lane & 7) * 8) * 2);
+#endif
     }
     auto set_tap = [&](int j) {
 #pragma unroll
