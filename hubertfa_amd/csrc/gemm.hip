@@ -1047,18 +1047,154 @@ inline int set_grid(GemmP& p, int BM, int BN, dim3& grid, int Z) {
     return HFA_OK;
 }
 
+// ---- split-f16 GEMM for N = 48 (the grouped positional conv at Hubert-base: 16 groups of Cg = 48) ---------------
+// 48 output columns fit neither the 32x32 MFMA tiles (a 64-wide tile wastes a quarter of its products) nor
+// any 32-multiple, so this kernel uses v_mfma_f32_16x16x32_f16: 48 = 3 x 16.  Tile 128 x 48, 4 waves of 32 x 48
+// (2 x 3 blocks of 16 x 16), the same split-f16 single-accumulator arithmetic, operand planes staged by LDS-DMA
+// into [row][4 x 16 B] images whose chunk swizzle {0, 2, 3, 1}[(row >> 2) & 3] keeps the 16x16x32 operand reads (lane:
+// row lane&15, chunk lane>>4) conflict-free; per-lane tap tracking as GT (Cg % 32 != 0).
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_split48_kernel(const GemmP p) {
+    constexpr int BM = 128, BN = 48, BK = 32, NW = 4, NS = 2, DA = 2;
+    constexpr int PA = BM * BK, PW = BN * BK;                  // halves per plane image
+    constexpr int STAGE = 2 * PA + 2 * PW;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[NS * STAGE];
+
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int tm = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int zb = blockIdx.z / p.G, zg = blockIdx.z - zb * p.G;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    auto swz = [](int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; };   // {0, 2, 3, 1}[(r >> 2) & 3]
+
+    const _Float16* Ab = p.Ah + zb * p.sAb + zg * p.sAg;
+    const _Float16* Wb = p.Wh + zg * p.sWg;
+    const long long a_bytes = ((long long)(p.Tin - 1) * p.ldx + p.Cg) * 2;
+    const long long w_bytes = ((long long)(BN - 1) * p.ldw + p.K) * 2;
+    const __amdgpu_buffer_rsrc_t rA1 = hfa::make_rsrc(Ab, a_bytes), rA2 = hfa::make_rsrc(Ab + p.sAp, a_bytes);
+    const __amdgpu_buffer_rsrc_t rW1 = hfa::make_rsrc(Wb, w_bytes), rW2 = hfa::make_rsrc(Wb + p.sWp, w_bytes);
+
+    // A: pieces wave + 4d (16 rows x 4 chunks each), per-lane (tap, channel) tracking; W: piece = wave (< 3)
+    int a_t0[DA], a_c[DA], a_tap[DA];
+#pragma unroll
+    for (int d = 0; d < DA; ++d) {
+        const int row = (wave + d * NW) * 16 + (lane >> 2);
+        int m = tm * BM + row;
+        m = m < p.M ? m : p.M - 1;
+        a_t0[d] = m * p.stride - p.pad;
+        a_c[d] = ((lane & 3) ^ swz(row)) * 8;
+        a_tap[d] = 0;
+    }
+    const int wrow = wave * 16 + (lane >> 2);
+    const unsigned voffW = (unsigned)(((wrow < BN ? wrow : BN - 1) * p.ldw + ((lane & 3) ^ swz(wrow)) * 8) * 2);
+    const unsigned lds0 = hfa::lds_addr(smem);
+    int cur_k0 = 0;
+    auto issue = [&](int stage) {
+        const unsigned base = lds0 + stage * STAGE * 2 + wave * 1024;
+#pragma unroll
+        for (int d = 0; d < DA; ++d) {
+            const int t = a_t0[d] + a_tap[d];
+            const unsigned vo = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + a_c[d]) * 2) : hfa::DMA_OOB;
+            hfa::dma16(vo, rA1, 0u, base + d * NW * 1024);
+            hfa::dma16(vo, rA2, 0u, base + PA * 2 + d * NW * 1024);
+            a_c[d] += BK;
+            if (a_c[d] >= p.Cg) {                         // Cg >= BK: at most one tap boundary per K-step
+                a_c[d] -= p.Cg;
+                ++a_tap[d];
+            }
+        }
+        if (wave < BN / 16) {
+            hfa::dma16(voffW, rW1, (unsigned)cur_k0 * 2, base + 2 * PA * 2);
+            hfa::dma16(voffW, rW2, (unsigned)cur_k0 * 2, base + (2 * PA + PW) * 2);
+        }
+        cur_k0 += BK;
+    };
+
+    // operand reads (f16x8 units): lane row r16, chunk q = lane >> 4 (k 8q .. 8q + 7 of the 32-deep step)
+    const int r16 = lane & 15, q = lane >> 4;
+    const int sl = q ^ swz(r16);
+    const int rdA = (wave * 32 + r16) * 4 + sl;              // + rb * 64 per 16-row block
+    const int rdW = 2 * PA / 8 + r16 * 4 + sl;              // + cb * 64 per 16-column block
+    f32x4 acc[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = p.K / BK;
+    issue(0);
+    hfa::wait_vm_barrier<0>();
+    const f16x8* s8 = reinterpret_cast<const f16x8*>(smem);
+    int stage = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+        const bool more = kt + 1 < nk;
+        if (more) issue(stage ^ 1);
+        const f16x8* st = s8 + stage * (STAGE / 8);
+        f16x8 a1[2], a2[2], w1[3], w2[3], w1s[3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            a1[i] = st[rdA + i * 64];
+            a2[i] = st[rdA + i * 64 + PA / 8];
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            w1[j] = st[rdW + j * 64];
+            w2[j] = st[rdW + j * 64 + PW / 8];
+            w1s[j] = w1[j] * (_Float16)2048.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], w1s[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], w2[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[i], w1[j], acc[i][j], 0, 0, 0);
+            }
+        if (more) hfa::wait_vm_barrier<0>();
+        stage ^= 1;
+    }
+
+    // epilogue: C/D of the 16x16 MFMA: column lane & 15, rows 4 (lane >> 4) + e
+    float* Cb = p.C + zb * p.sCb + zg * p.sCg;
+    const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
+    const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int col = j * 16 + r16;
+        const float bv = biasb ? biasb[col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = tm * BM + wave * 32 + i * 16 + 4 * q + e;
+                const float a = acc[i][j][e] * (1.0f / 2048.0f);
+                bad |= !__builtin_isfinite(a);
+                if (row < p.M) {
+                    float v = a + bv;
+                    if (EPI == EPI_GELU) v = hfa::gelu_fast(v);
+                    if (Rb) v += Rb[(long long)row * p.ldr + col];
+                    Cb[(long long)row * p.ldc + col] = v;
+                }
+            }
+    }
+    if (bad && p.oflow) *p.oflow = 1;
+}
+
 // ---- split-f16 dispatch --------------------------------------------------------------------------------------
 enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_128x128_NS3 = 4, SCFG_128x128_NS4 = 5,
        SCFG_256x128_NS3 = 6, SCFG_256x256_1 = 7, SCFG_256x128_1 = 8, SCFG_128x128_1 = 9, SCFG_128x64_1 = 10,
        SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_256x64_1 = 14,
-       SCFG_COUNT = 15 };
+       SCFG_N48 = 15, SCFG_COUNT = 16 };
 struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; };
 constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 128, 2, 2, 2, 2, false, 32}, {128, 128, 2, 2, 2, 2, false, 32}, {128, 64, 2, 2, 2, 2, false, 32},
     {256, 128, 4, 2, 2, 1, false, 32}, {128, 128, 2, 2, 3, 1, false, 32}, {128, 128, 2, 2, 4, 1, false, 32},
     {256, 128, 4, 2, 3, 1, false, 32}, {256, 256, 2, 4, 2, 1, true, 32},  {256, 128, 2, 2, 2, 1, true, 32},
     {128, 128, 2, 2, 2, 2, true, 32},  {128, 64, 2, 2, 2, 2, true, 32},   {256, 256, 2, 4, 4, 1, true, 16},
-    {256, 256, 2, 4, 3, 1, true, 16},  {128, 128, 2, 2, 4, 2, true, 16},  {256, 64, 4, 1, 2, 2, true, 32}};
+    {256, 256, 2, 4, 3, 1, true, 16},  {128, 128, 2, 2, 4, 2, true, 16},  {256, 64, 4, 1, 2, 2, true, 32},
+    {128, 48, 4, 1, 2, 2, true, 32}};      // SCFG_N48: gemm_split48_kernel (16x16x32 MFMA), not gemm_split_kernel
 int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 
 // Measured on the workload's shapes (scripts/split_gemm_bench.py, profiles/r01/split_gemm_cfgs.txt): the 256 x 256
@@ -1068,7 +1204,9 @@ int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 // k-blocks, same three products in the same order) whatever the tile, so a row's result does not depend on the
 // batch it is in (variable-length batches stay bit-identical to the reference's B = 1 runs).
 inline int split_cfg(const GemmP& p, int Z) {
-    if (g_split_cfg > 0 && g_split_cfg < SCFG_COUNT) return g_split_cfg;
+    const bool n48 = p.N == 48 && p.Ch == nullptr && p.Cg % 8 == 0 && p.Cg >= 32;
+    if (g_split_cfg > 0 && g_split_cfg < SCFG_COUNT) return (g_split_cfg != SCFG_N48 || n48) ? g_split_cfg : SCFG_128x64_1;
+    if (n48) return SCFG_N48;
     const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
     const long long blocks256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * Z;
     if (p.N == 64 && p.Cg % 32 == 0 && (long long)((p.M + 255) / 256) * Z >= 256)
@@ -1078,6 +1216,10 @@ inline int split_cfg(const GemmP& p, int Z) {
 }
 
 inline void split_name(int cfg, int epi, bool outs, bool gt, char* buf, int len) {
+    if (cfg == SCFG_N48) {
+        snprintf(buf, len, "gemm_split48_kernel<%d>", epi);
+        return;
+    }
     if (gt && cfg != SCFG_256x64_1) cfg = kSplitGeom[cfg].BN == 64 ? SCFG_128x64_1 : SCFG_128x128_1;
     const SplitGeom& g = kSplitGeom[cfg];
     snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, %s, %d>", epi, g.BM, g.BN, g.WM, g.WN,
@@ -1332,6 +1474,12 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
     p.C = C; p.Ch = reinterpret_cast<_Float16*>(Cs); p.sCp = sCp; p.sCb = sCb; p.sCg = sCg; p.ldc = ldc;
     p.oflow = oflow;
     const int Z = Zb * G, cfg = split_cfg(p, Z);
+    if (cfg == SCFG_N48) {                     // N = 48, f32 output: the 16x16x32 kernel
+        dim3 grid((unsigned)((M + 127) / 128), 1, Z);
+        if (epilogue == EPI_GELU) hipLaunchKernelGGL(gemm_split48_kernel<EPI_GELU>, grid, dim3(256), 0, stream, p);
+        else hipLaunchKernelGGL(gemm_split48_kernel<EPI_NONE>, grid, dim3(256), 0, stream, p);
+        return hfa::check_launch("hfa_conv_gemm_split");
+    }
     if (Cs) return epilogue == EPI_GELU ? launch_split<EPI_GELU, true>(p, Z, cfg, stream)
                                         : launch_split<EPI_NONE, true>(p, Z, cfg, stream);
     return epilogue == EPI_GELU ? launch_split<EPI_GELU, false>(p, Z, cfg, stream)
@@ -1339,7 +1487,8 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
 }
 
 const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue, int Cg) {
-    GemmP p = make_params(M, N, 32, 1, nullptr, 0, 0, 0, 1, 0, 32, 1, nullptr, 0, 0);
+    GemmP p = make_params(M, N, 32, 1, nullptr, 0, 0, 0, 1, 0, Cg, 1, nullptr, 0, 0);
+    p.Ch = out_split ? reinterpret_cast<_Float16*>(g_name) : nullptr;    // only its null-ness is read
     split_name(split_cfg(p, Z), epilogue, out_split != 0, Cg % 32 != 0, g_name, sizeof(g_name));
     return g_name;
 }

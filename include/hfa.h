@@ -117,8 +117,9 @@ const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int e
  * stages (one workgroup per CU), 6 256x128 with 3 stages, 7 256x256 single accumulator (8 waves of 128x64),
  * 8 256x128 single accumulator (4 waves), 9 128x128 single accumulator, 10 128x64 single accumulator, 11/12
  * 256x256 single accumulator with 16-deep K-steps and 4/3 stages, 13 128x128 likewise with 4 stages, 14 256x64
- * single accumulator (4 waves of 64x64).  The
- * automatic choice uses single-accumulator tiles only (7, 9, 10, 14): results then do not depend on the tile. */
+ * single accumulator (4 waves of 64x64), 15 the N = 48 kernel (16x16x32 MFMA; chosen automatically for N = 48
+ * with f32 output, e.g. the grouped positional conv at Cg = 48).  The
+ * automatic choice uses single-accumulator tiles only (7, 9, 10, 14, 15): results then do not depend on the tile. */
 int hfa_gemm_split_tuning(int cfg);
 /* x [rows, cols] f32 (row stride ldx) -> split planes y (row stride ldy, plane 1 at +sp); raises *oflow (if
  * non-NULL) for |x| >= 65504 or a non-finite x. */

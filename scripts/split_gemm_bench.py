@@ -17,6 +17,12 @@ SHAPES = [  # name, Tin, Cin, Cout, k, stride, epi
     ("outproj", 499, 768, 768, 1, 1, 0),
     ("ffn1", 499, 768, 3072, 1, 1, 1),
     ("ffn2", 499, 3072, 768, 1, 1, 0),
+    # UNet (T padded to 864 at 86.13 fps, pad 1 for the k3 convs: shapes only, the pad is ignored here)
+    ("unet_k3_768", 866, 768, 192, 3, 1, 0),
+    ("unet_k3_192", 866, 192, 192, 3, 1, 0),
+    ("unet_sc", 864, 768, 192, 1, 1, 0),
+    ("unet_down", 864, 192, 384, 2, 2, 0),
+    ("unet_up", 216, 384, 384, 1, 1, 0),
 ]
 
 

@@ -42,7 +42,7 @@ def test_split_planes_and_flag():
     flag.zero_()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("M,N,K,epi,res,outs", [(300, 200, 128, 0, False, False), (1000, 768, 768, 1, False, False),
                                                 (257, 72, 192, 0, True, False), (4096, 3072, 768, 1, False, True),
                                                 (130, 2304, 768, 0, False, True), (64, 768, 3072, 0, True, False)])
@@ -69,10 +69,13 @@ def test_split_linear(cfg, M, N, K, epi, res, outs):
         _close(got, ref, 2e-5, 2e-5)
 
 
+@pytest.mark.parametrize("cfg", [0, 9])
 @pytest.mark.parametrize("Cin,Cout,k,s,pad,T", [(512, 512, 3, 2, 0, 301), (512, 512, 2, 2, 0, 100),
-                                                (192, 192, 3, 1, 1, 64), (192, 384, 2, 2, 0, 40)])
-def test_split_conv_vs_conv1d(Cin, Cout, k, s, pad, T):
-    from hubertfa_amd import ops
+                                                (192, 192, 3, 1, 1, 64), (192, 384, 2, 2, 0, 40),
+                                                (512, 512, 3, 2, 0, 1301)])
+def test_split_conv_vs_conv1d(Cin, Cout, k, s, pad, T, cfg):
+    from hubertfa_amd import ops, _lib
+    _lib.lib().hfa_gemm_split_tuning(cfg)
     B = 3
     d = torch.device("cuda")
     x = _r(B, T, Cin, seed=5)
@@ -82,17 +85,23 @@ def test_split_conv_vs_conv1d(Cin, Cout, k, s, pad, T):
     Tout = ref.shape[1]
     wi = w.permute(0, 2, 1).reshape(Cout, k * Cin).contiguous()
     y = torch.empty(B, Tout, Cout, device=d)
-    ops.conv_gemm_split(ops.split(x.to(d)), ops.split(wi.to(d)), C=y, M=Tout, N=Cout, K=k * Cin, Zb=B, sAb=T * Cin,
-                        ldx=Cin, stride=s, pad=pad, Cg=Cin, Tin=T, bias=b.to(d), sCb=Tout * Cout, ldc=Cout)
+    try:
+        ops.conv_gemm_split(ops.split(x.to(d)), ops.split(wi.to(d)), C=y, M=Tout, N=Cout, K=k * Cin, Zb=B,
+                            sAb=T * Cin, ldx=Cin, stride=s, pad=pad, Cg=Cin, Tin=T, bias=b.to(d), sCb=Tout * Cout,
+                            ldc=Cout)
+    finally:
+        _lib.lib().hfa_gemm_split_tuning(0)
     _close(y, ref, 2e-5, 2e-5)
 
 
 @pytest.mark.parametrize("H,G,k,L,cfg", [(768, 16, 128, 499, 0), (768, 16, 128, 77, 1), (96, 2, 8, 40, 0),
                                          (640, 16, 16, 130, 0), (768, 16, 128, 300, 14), (1024, 16, 32, 260, 14),
-                                         (1024, 16, 128, 499, 0)])
+                                         (1024, 16, 128, 499, 0), (768, 16, 128, 499, 15), (768, 16, 64, 1000, 15),
+                                         (768, 16, 128, 5, 15), (96, 2, 8, 40, 15), (1024, 16, 32, 100, 15)])
 def test_split_grouped_posconv_general_taps(H, G, k, L, cfg):
-    """Grouped positional conv with Cg = H/G not a multiple of 32 (48 at Hubert-base: per-lane tap tracking),
-    GELU + residual epilogue, pad k/2 and the last frame dropped, against f64 conv1d (model.py:132-147)."""
+    """Grouped positional conv with Cg = H/G not a multiple of 32 (48 at Hubert-base: per-lane tap tracking; the
+    automatic choice and cfg 15 run the 16x16x32 N = 48 kernel), GELU + residual epilogue, pad k/2 and the last
+    frame dropped, against f64 conv1d (model.py:132-147)."""
     from hubertfa_amd import ops, _lib
     B = 2
     Cg = H // G
