@@ -1182,11 +1182,145 @@ __global__ __launch_bounds__(256, 2) void gemm_split48_kernel(const GemmP p) {
     if (bad && p.oflow) *p.oflow = 1;
 }
 
+// ---- grouped positional conv with an LDS-resident input window ------------------------------------------------
+// The implicit GEMM re-fetches the A rows of every tap from L2 (128 taps x 48 channels: ~56 B of DMA per kFLOP for
+// the N = 48 tile), so for the positional conv (stride 1, k = 128, Cg = 48, N = Cg) a workgroup instead stages its
+// whole input window once -- the 256 + k - 1 input rows its 256 output rows read, both planes, zero rows outside
+// [0, Tin) (the conv's padding) -- and streams only W through a 3-stage ring (6 KiB per 32-deep K-step): ~8 B of
+// DMA per kFLOP.  The window is chunk-major ([plane][8-channel chunk][row], 16 B per cell), so a 16x16x32 operand
+// read (16 consecutive rows of one chunk per 16 lanes) covers all 64 banks once; the K index is the flattened
+// (tap, channel) of the im2col weight rows, each lane's 8-wide chunk mapping to its own (tap, chunk) pair.
+// 8 waves x (32 rows x 48 columns) on v_mfma_f32_16x16x32_f16, split-f16 single-accumulator arithmetic.
+constexpr int kWinRows = 384;
+
+template <int EPI, int NB>
+__global__ __launch_bounds__(512, 1) void posconv_split_kernel(const GemmP p) {
+    constexpr int BM = 256, BN = 16 * NB, BK = 32, NW = 8, NS = 3;   // NB = 3 (Cg 48) or 4 (Cg 64)
+    constexpr int PW = BN * BK;                                  // halves per W plane image
+    constexpr int WSTAGE = 2 * PW;
+    const int CC = p.Cg / 8;                                     // 8-channel chunks per row (<= 8)
+    __shared__ __attribute__((aligned(16))) _Float16 dsm[2 * 8 * kWinRows * 8 + NS * WSTAGE];
+    _Float16* win = dsm;                                         // [2][CC][kWinRows] x 8 halves
+    _Float16* wst = dsm + 2 * 8 * kWinRows * 8;                  // NS stages of [2][BN][32]
+
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int tm = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int zb = blockIdx.z / p.G, zg = blockIdx.z - zb * p.G;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    auto swz = [](int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; };   // {0, 2, 3, 1}[(r >> 2) & 3]
+
+    const _Float16* Ab = p.Ah + zb * p.sAb + zg * p.sAg;
+    const _Float16* Wb = p.Wh + zg * p.sWg;
+    const long long a_bytes = ((long long)(p.Tin - 1) * p.ldx + p.Cg) * 2;
+    const long long w_bytes = ((long long)(BN - 1) * p.ldw + p.K) * 2;
+    const __amdgpu_buffer_rsrc_t rA1 = hfa::make_rsrc(Ab, a_bytes), rA2 = hfa::make_rsrc(Ab + p.sAp, a_bytes);
+    const __amdgpu_buffer_rsrc_t rW1 = hfa::make_rsrc(Wb, w_bytes), rW2 = hfa::make_rsrc(Wb + p.sWp, w_bytes);
+    const unsigned lds_win = hfa::lds_addr(win), lds_w = hfa::lds_addr(wst);
+
+    // input window: pieces of 64 rows of one (plane, chunk); window row r <-> input row t0 + r
+    const int t0 = tm * BM - p.pad;
+    const int npieces = 2 * CC * (kWinRows / 64);
+    for (int pc = wave; pc < npieces; pc += NW) {
+        const int plane = pc / (CC * 6), rest = pc - plane * CC * 6, c = rest / 6, g = rest - c * 6;
+        const int t = t0 + g * 64 + lane;
+        const unsigned vo = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + c * 8) * 2) : hfa::DMA_OOB;
+        hfa::dma16(vo, plane ? rA2 : rA1, 0u, lds_win + ((plane * CC + c) * kWinRows + g * 64) * 16);
+    }
+    // W ring: waves 0 .. 2 NB - 1 each own one 1-KiB piece (plane w / NB, rows 16 (w % NB) + lane / 4) of a K-step
+    const int wrow = (wave % NB) * 16 + (lane >> 2);
+    const unsigned voffW = (unsigned)((wrow * p.ldw + ((lane & 3) ^ swz(wrow)) * 8) * 2);
+    const bool wdma = wave < 2 * NB;
+    auto issueW = [&](int stage, int s) {
+        if (wdma)
+            hfa::dma16(voffW, wave < NB ? rW1 : rW2, (unsigned)(s * BK * 2),
+                       lds_w + (stage * WSTAGE + (wave < NB ? 0 : PW)) * 2 + (wave % NB) * 1024);
+    };
+    const int nk = p.K / BK;
+    issueW(0, 0);
+    if (nk > 1) issueW(1, 1);
+    hfa::wait_vm_barrier<0>();                                   // window and steps 0, 1 landed
+
+    // per-lane operand addressing: output row l = 32 wave + 16 b + r16, chunk q = lane >> 4 (k 8q..8q+7 of a step)
+    const int r16 = lane & 15, q = lane >> 4;
+    int tap = 0, ch = q;                                         // (tap, 8-channel chunk) of this lane's k
+    while (ch >= CC) { ch -= CC; ++tap; }
+    const f16x8* w8 = reinterpret_cast<const f16x8*>(wst);
+    const f16x8* a8 = reinterpret_cast<const f16x8*>(win);
+    const int rdW = (r16 * 4) + (q ^ swz(r16));                  // + cb * 64, + plane * PW / 8, + stage * WSTAGE / 8
+    const int lrow = 32 * wave + r16;
+    f32x4 acc[2][NB];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int stage = 0;
+    for (int s = 0; s < nk; ++s) {
+        if (s + 2 < nk) issueW(stage == 0 ? 2 : stage - 1, s + 2);    // into the stage read at step s - 1
+        const f16x8* st = w8 + stage * (WSTAGE / 8);
+        f16x8 a1[2], a2[2], w1[NB], w2[NB], w1s[NB];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int cell = ch * kWinRows + lrow + 16 * b + tap;
+            a1[b] = a8[cell];
+            a2[b] = a8[CC * kWinRows + cell];
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            w1[j] = st[rdW + j * 64];
+            w2[j] = st[rdW + j * 64 + PW / 8];
+            w1s[j] = w1[j] * (_Float16)2048.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], w1s[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], w2[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[i], w1[j], acc[i][j], 0, 0, 0);
+            }
+        ch += 4;                                                 // next step: k + 32 = 4 chunks on
+        if (ch >= CC) { ch -= CC; ++tap; }
+        if (s + 1 < nk) {                                        // step s + 1 landed; every wave done with s - 1
+            if (s + 2 < nk) hfa::wait_vm_barrier<1>();
+            else hfa::wait_vm_barrier<0>();
+        }
+        stage = stage == NS - 1 ? 0 : stage + 1;
+    }
+
+    float* Cb = p.C + zb * p.sCb + zg * p.sCg;
+    const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
+    const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const int col = j * 16 + r16;
+        const float bv = biasb ? biasb[col] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = tm * BM + 32 * wave + i * 16 + 4 * q + e;
+                const float a = acc[i][j][e] * (1.0f / 2048.0f);
+                bad |= !__builtin_isfinite(a);
+                if (row < p.M) {
+                    float v = a + bv;
+                    if (EPI == EPI_GELU) v = hfa::gelu_fast(v);
+                    if (Rb) v += Rb[(long long)row * p.ldr + col];
+                    Cb[(long long)row * p.ldc + col] = v;
+                }
+            }
+    }
+    if (bad && p.oflow) *p.oflow = 1;
+}
+
 // ---- split-f16 dispatch --------------------------------------------------------------------------------------
 enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_128x128_NS3 = 4, SCFG_128x128_NS4 = 5,
        SCFG_256x128_NS3 = 6, SCFG_256x256_1 = 7, SCFG_256x128_1 = 8, SCFG_128x128_1 = 9, SCFG_128x64_1 = 10,
        SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_256x64_1 = 14,
-       SCFG_N48 = 15, SCFG_COUNT = 16 };
+       SCFG_N48 = 15, SCFG_WIN = 16, SCFG_COUNT = 17 };
 struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; };
 constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 128, 2, 2, 2, 2, false, 32}, {128, 128, 2, 2, 2, 2, false, 32}, {128, 64, 2, 2, 2, 2, false, 32},
@@ -1194,8 +1328,10 @@ constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {256, 128, 4, 2, 3, 1, false, 32}, {256, 256, 2, 4, 2, 1, true, 32},  {256, 128, 2, 2, 2, 1, true, 32},
     {128, 128, 2, 2, 2, 2, true, 32},  {128, 64, 2, 2, 2, 2, true, 32},   {256, 256, 2, 4, 4, 1, true, 16},
     {256, 256, 2, 4, 3, 1, true, 16},  {128, 128, 2, 2, 4, 2, true, 16},  {256, 64, 4, 1, 2, 2, true, 32},
-    {128, 48, 4, 1, 2, 2, true, 32}};      // SCFG_N48: gemm_split48_kernel (16x16x32 MFMA), not gemm_split_kernel
+    {128, 48, 4, 1, 2, 2, true, 32},       // SCFG_N48: gemm_split48_kernel (16x16x32 MFMA), not gemm_split_kernel
+    {256, 48, 8, 1, 3, 1, true, 32}};      // SCFG_WIN: posconv_split_kernel (LDS-resident input window)
 int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
+thread_local int g_win_nb = 3;   // column blocks of the window kernel the name query reports (N / 16)
 
 // Measured on the workload's shapes (scripts/split_gemm_bench.py, profiles/r01/split_gemm_cfgs.txt): the 256 x 256
 // single-accumulator tile is 7-15 % faster than 128 x 128 on the extractor convs, FFN and out-projection (even at
@@ -1203,9 +1339,19 @@ int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 // automatic choice is a single-accumulator tile: each output element then sees the same MFMA sequence (same
 // k-blocks, same three products in the same order) whatever the tile, so a row's result does not depend on the
 // batch it is in (variable-length batches stay bit-identical to the reference's B = 1 runs).
+inline bool win_ok(const GemmP& p) {   // posconv_split_kernel: stride 1, N 48 or 64, Cg % 8, Cg <= 64, window fits
+    return (p.N == 48 || p.N == 64) && p.Ch == nullptr && p.stride == 1 && p.Cg % 8 == 0 && p.Cg >= 32 &&
+           p.Cg <= 64 && p.K % p.Cg == 0 && 256 + p.K / p.Cg - 1 <= kWinRows;
+}
+
 inline int split_cfg(const GemmP& p, int Z) {
     const bool n48 = p.N == 48 && p.Ch == nullptr && p.Cg % 8 == 0 && p.Cg >= 32;
-    if (g_split_cfg > 0 && g_split_cfg < SCFG_COUNT) return (g_split_cfg != SCFG_N48 || n48) ? g_split_cfg : SCFG_128x64_1;
+    if (g_split_cfg > 0 && g_split_cfg < SCFG_COUNT) {
+        if (g_split_cfg == SCFG_N48 && !n48) return SCFG_128x64_1;
+        if (g_split_cfg == SCFG_WIN && !win_ok(p)) return SCFG_128x64_1;
+        return g_split_cfg;
+    }
+    if (win_ok(p)) return SCFG_WIN;
     if (n48) return SCFG_N48;
     const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
     const long long blocks256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * Z;
@@ -1218,6 +1364,10 @@ inline int split_cfg(const GemmP& p, int Z) {
 inline void split_name(int cfg, int epi, bool outs, bool gt, char* buf, int len) {
     if (cfg == SCFG_N48) {
         snprintf(buf, len, "gemm_split48_kernel<%d>", epi);
+        return;
+    }
+    if (cfg == SCFG_WIN) {
+        snprintf(buf, len, "posconv_split_kernel<%d, %d>", epi, g_win_nb);
         return;
     }
     if (gt && cfg != SCFG_256x64_1) cfg = kSplitGeom[cfg].BN == 64 ? SCFG_128x64_1 : SCFG_128x128_1;
@@ -1474,6 +1624,18 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
     p.C = C; p.Ch = reinterpret_cast<_Float16*>(Cs); p.sCp = sCp; p.sCb = sCb; p.sCg = sCg; p.ldc = ldc;
     p.oflow = oflow;
     const int Z = Zb * G, cfg = split_cfg(p, Z);
+    if (cfg == SCFG_WIN) {                     // grouped positional conv: LDS-resident input window
+        dim3 grid((unsigned)((M + 255) / 256), 1, Z);
+        if (N == 48 && epilogue == EPI_GELU)
+            hipLaunchKernelGGL((posconv_split_kernel<EPI_GELU, 3>), grid, dim3(512), 0, stream, p);
+        else if (N == 48)
+            hipLaunchKernelGGL((posconv_split_kernel<EPI_NONE, 3>), grid, dim3(512), 0, stream, p);
+        else if (epilogue == EPI_GELU)
+            hipLaunchKernelGGL((posconv_split_kernel<EPI_GELU, 4>), grid, dim3(512), 0, stream, p);
+        else
+            hipLaunchKernelGGL((posconv_split_kernel<EPI_NONE, 4>), grid, dim3(512), 0, stream, p);
+        return hfa::check_launch("hfa_conv_gemm_split");
+    }
     if (cfg == SCFG_N48) {                     // N = 48, f32 output: the 16x16x32 kernel
         dim3 grid((unsigned)((M + 127) / 128), 1, Z);
         if (epilogue == EPI_GELU) hipLaunchKernelGGL(gemm_split48_kernel<EPI_GELU>, grid, dim3(256), 0, stream, p);
@@ -1489,6 +1651,7 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
 const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue, int Cg) {
     GemmP p = make_params(M, N, 32, 1, nullptr, 0, 0, 0, 1, 0, Cg, 1, nullptr, 0, 0);
     p.Ch = out_split ? reinterpret_cast<_Float16*>(g_name) : nullptr;    // only its null-ness is read
+    g_win_nb = N / 16;
     split_name(split_cfg(p, Z), epilogue, out_split != 0, Cg % 32 != 0, g_name, sizeof(g_name));
     return g_name;
 }

@@ -38,7 +38,7 @@ for H, G in ((768, 16), (1024, 16)):
     ms32 = timeit(lambda: ops.conv_gemm(x, w, out, **kw))
     line = f"H={H} Cg={Cg}: f32 {ms32:.3f} ms ({fl / ms32 / 1e9:.0f} TF)"
     xs = ops.split(x)
-    for cfg in (0, 10, 14, 9):
+    for cfg in (0, 10, 14, 15, 16):
         _lib.lib().hfa_gemm_split_tuning(cfg)
         mss = timeit(lambda: ops.conv_gemm_split(xs, ws, C=out, **kw))
         line += f" | cfg{cfg} {mss:.3f} ms ({fl / mss / 1e9:.0f} TF)"

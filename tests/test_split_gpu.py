@@ -97,7 +97,10 @@ def test_split_conv_vs_conv1d(Cin, Cout, k, s, pad, T, cfg):
 @pytest.mark.parametrize("H,G,k,L,cfg", [(768, 16, 128, 499, 0), (768, 16, 128, 77, 1), (96, 2, 8, 40, 0),
                                          (640, 16, 16, 130, 0), (768, 16, 128, 300, 14), (1024, 16, 32, 260, 14),
                                          (1024, 16, 128, 499, 0), (768, 16, 128, 499, 15), (768, 16, 64, 1000, 15),
-                                         (768, 16, 128, 5, 15), (96, 2, 8, 40, 15), (1024, 16, 32, 100, 15)])
+                                         (768, 16, 128, 5, 15), (96, 2, 8, 40, 15), (1024, 16, 32, 100, 15),
+                                         (768, 16, 128, 499, 16), (768, 16, 128, 300, 16), (768, 16, 128, 3, 16),
+                                         (768, 16, 128, 600, 16), (96, 2, 8, 40, 16), (512, 16, 64, 257, 16),
+                                         (1024, 16, 128, 499, 16), (768, 16, 128, 499, 15)])
 def test_split_grouped_posconv_general_taps(H, G, k, L, cfg):
     """Grouped positional conv with Cg = H/G not a multiple of 32 (48 at Hubert-base: per-lane tap tracking; the
     automatic choice and cfg 15 run the 16x16x32 N = 48 kernel), GELU + residual epilogue, pad k/2 and the last
