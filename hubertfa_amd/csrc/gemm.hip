@@ -1320,7 +1320,7 @@ __global__ __launch_bounds__(512, 1) void posconv_split_kernel(const GemmP p) {
 enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_128x128_NS3 = 4, SCFG_128x128_NS4 = 5,
        SCFG_256x128_NS3 = 6, SCFG_256x256_1 = 7, SCFG_256x128_1 = 8, SCFG_128x128_1 = 9, SCFG_128x64_1 = 10,
        SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_256x64_1 = 14,
-       SCFG_N48 = 15, SCFG_WIN = 16, SCFG_256x256_W4 = 17, SCFG_COUNT = 18 };
+       SCFG_N48 = 15, SCFG_WIN = 16, SCFG_COUNT = 17 };
 struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; };
 constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 128, 2, 2, 2, 2, false, 32}, {128, 128, 2, 2, 2, 2, false, 32}, {128, 64, 2, 2, 2, 2, false, 32},
@@ -1329,8 +1329,7 @@ constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 128, 2, 2, 2, 2, true, 32},  {128, 64, 2, 2, 2, 2, true, 32},   {256, 256, 2, 4, 4, 1, true, 16},
     {256, 256, 2, 4, 3, 1, true, 16},  {128, 128, 2, 2, 4, 2, true, 16},  {256, 64, 4, 1, 2, 2, true, 32},
     {128, 48, 4, 1, 2, 2, true, 32},       // SCFG_N48: gemm_split48_kernel (16x16x32 MFMA), not gemm_split_kernel
-    {256, 48, 8, 1, 3, 1, true, 32},       // SCFG_WIN: posconv_split_kernel (LDS-resident input window)
-    {256, 256, 2, 2, 2, 1, true, 32}};     // 4 waves of 128 x 128 (accumulators need AGPRs: experiment)
+    {256, 48, 8, 1, 3, 1, true, 32}};      // SCFG_WIN: posconv_split_kernel (LDS-resident input window)
 int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 thread_local int g_win_nb = 3;   // column blocks of the window kernel the name query reports (N / 16)
 
@@ -1409,9 +1408,6 @@ int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
         case SCFG_256x128_1: return launch_split_cfg<EPI, OUTS, SCFG_256x128_1>(p, Z, st);
         case SCFG_128x128_1: return launch_split_cfg<EPI, OUTS, SCFG_128x128_1>(p, Z, st);
         case SCFG_128x64_1: return launch_split_cfg<EPI, OUTS, SCFG_128x64_1>(p, Z, st);
-#ifdef HFA_SPLIT_W4
-        case SCFG_256x256_W4: return launch_split_cfg<EPI, OUTS, SCFG_256x256_W4>(p, Z, st);
-#endif
         case SCFG_256x256_1_K16S4: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1_K16S4>(p, Z, st);
         case SCFG_256x256_1_K16S3: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1_K16S3>(p, Z, st);
         case SCFG_128x128_1_K16S4: return launch_split_cfg<EPI, OUTS, SCFG_128x128_1_K16S4>(p, Z, st);
