@@ -177,37 +177,44 @@ __global__ __launch_bounds__(NT) void conv0_apply8_kernel(int N, int T0, const f
     const int nt = min(CH, T0 - t0);
     stage_chunk(xs, x + b * x_bs, t0, nt, N);
     const int c0 = (threadIdx.x & 63) * 8, fr = threadIdx.x >> 6;
-    float w[8][KW], mul[8], add[8], mu[8];
+    // channel pairs in packed f32x2 registers: the conv, the affine and the GELU issue as v_pk_* (the kernel is
+    // VALU-bound), with the per-element operation order of conv0_apply_kernel (bit-identical outputs)
+    typedef hfa::hfa_f32x2 f2;
+    f2 w[4][KW], mul[4], add[4], mu[4], g[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
-        for (int j = 0; j < KW; ++j) w[i][j] = w0[(c0 + i) * KW + j];
+        for (int j = 0; j < KW; ++j) w[i][j] = f2{w0[(c0 + 2 * i) * KW + j], w0[(c0 + 2 * i + 1) * KW + j]};
         if (MODE == 0) {
-            mu[i] = stats[(b * C0 + c0 + i) * 2];
-            mul[i] = stats[(b * C0 + c0 + i) * 2 + 1];
-            add[i] = beta[c0 + i];
+            mu[i] = f2{stats[(b * C0 + c0 + 2 * i) * 2], stats[(b * C0 + c0 + 2 * i + 1) * 2]};
+            mul[i] = f2{stats[(b * C0 + c0 + 2 * i) * 2 + 1], stats[(b * C0 + c0 + 2 * i + 1) * 2 + 1]};
+            add[i] = f2{beta[c0 + 2 * i], beta[c0 + 2 * i + 1]};
+            g[i] = f2{gamma[c0 + 2 * i], gamma[c0 + 2 * i + 1]};
         } else {
-            mu[i] = 0.f;
-            mul[i] = 1.f;
-            add[i] = bias ? bias[c0 + i] : 0.f;
+            mu[i] = f2{0.f, 0.f};
+            mul[i] = g[i] = f2{1.f, 1.f};
+            add[i] = bias ? f2{bias[c0 + 2 * i], bias[c0 + 2 * i + 1]} : f2{0.f, 0.f};
         }
     }
-    float g[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) g[i] = MODE == 0 ? gamma[c0 + i] : 1.f;
     __syncthreads();
     _Float16* yb = yh + b * y_bs + (long long)t0 * C0 + c0;
     bool bad = false;
     for (int t = fr; t < nt; t += NT / 64) {
         f16x8 h1, h2;
+        const float* xt = xs + t * ST;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            float v = conv10(w[i], xs + t * ST);
-            if (MODE == 0) v = hfa::gelu_fast((v - mu[i]) * mul[i] * g[i] + add[i]);
+        for (int i = 0; i < 4; ++i) {
+            f2 v = f2{0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < KW; ++j) v = __builtin_elementwise_fma(w[i][j], f2{xt[j], xt[j]}, v);
+            if (MODE == 0) v = hfa::gelu_fast2((v - mu[i]) * mul[i] * g[i] + add[i]);
             else v += add[i];
-            bad |= !(__builtin_fabsf(v) < 65504.0f);
-            h1[i] = (_Float16)v;
-            h2[i] = (_Float16)((v - (float)h1[i]) * 2048.0f);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                bad |= !(__builtin_fabsf(v[e]) < 65504.0f);
+                h1[2 * i + e] = (_Float16)v[e];
+                h2[2 * i + e] = (_Float16)((v[e] - (float)h1[2 * i + e]) * 2048.0f);
+            }
         }
         *reinterpret_cast<f16x8*>(yb + (long long)t * C0) = h1;
         *reinterpret_cast<f16x8*>(yb + (long long)t * C0 + y_sp) = h2;
