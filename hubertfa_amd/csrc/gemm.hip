@@ -670,8 +670,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     constexpr int RPP = 64 / CPR, KK = BK / 16;               // rows per 1-KiB DMA piece, MFMA k-steps per K-step
     constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
     constexpr int IA = BM / RPP, IW = BN / RPP;               // 1-KiB DMA pieces per plane per K-step
-    constexpr int DA = IA / NW, DB = IW / NW;
-    static_assert(IA % NW == 0 && IW % NW == 0, "even DMA shares only");
+    constexpr int DA = (IA + NW - 1) / NW, DB = (IW + NW - 1) / NW;   // uneven shares: wave + d*NW < IA only
+    static_assert(NS == 2 || (IA % NW == 0 && IW % NW == 0), "counted vmcnt waits need even DMA shares");
     constexpr int PA = BM * BK, PW = BN * BK;                 // halves per plane image
     constexpr int STAGE = 2 * PA + 2 * PW;                    // halves per stage: A1, A2, W1, W2
     __shared__ __attribute__((aligned(16))) _Float16 smem[NS * STAGE];
@@ -742,6 +742,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         const unsigned base = lds0 + stage * STAGE * 2 + wave * 1024;
 #pragma unroll
         for (int d = 0; d < DA; ++d) {
+            if (IA % NW != 0 && wave + d * NW >= IA) continue;   // wave-uniform
             if constexpr (GT) {
                 const int t = a_t0[d] + a_tap[d];
                 const unsigned vo = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + a_c[d]) * 2) : hfa::DMA_OOB;
@@ -762,6 +763,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         const unsigned base = lds0 + stage * STAGE * 2 + wave * 1024;
 #pragma unroll
         for (int d = 0; d < DB; ++d) {
+            if (IW % NW != 0 && wave + d * NW >= IW) continue;
             hfa::dma16(voffW[d], rW1, (unsigned)cur_k0 * 2, base + 2 * PA * 2 + d * NW * 1024);
             hfa::dma16(voffW[d], rW2, (unsigned)cur_k0 * 2, base + (2 * PA + PW) * 2 + d * NW * 1024);
         }
