@@ -263,7 +263,13 @@ __device__ __forceinline__ f16x4 lds_tr(const _Float16* base, int byte_off) {
 }
 
 __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP p) {
-    __shared__ __attribute__((aligned(16))) _Float16 smem[SNS * SSTAGE];
+    // Software-pipelined: iteration t issues the score MFMAs of tile t+1, then runs tile t's softmax (VALU) while
+    // those MFMAs execute, then tile t's PV MFMAs.  K runs one tile further ahead than V in separate 2-stage rings
+    // (K(t+1) must have landed when iteration t starts, V(t) only by its PV), so the LDS stays 64 KiB (2 per CU).
+    // The output uses one accumulator at scale 2^11: P is taken relative to m_run + kSlack (p <= 1, so 2^11 p1 is
+    // exact in f16) and O += V1 (2^11 P1) + V1 P2 + V2 P1.
+    constexpr int KST = 2 * SPLANE;                      // halves per K (or V) stage, both planes
+    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * KST];   // K0, K1, V0, V1
 
     const int nwg = gridDim.x, orig = blockIdx.x;
     const int xcd = orig & 7, xq = nwg >> 3, xr = nwg & 7;
@@ -297,7 +303,6 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP
     const __amdgpu_buffer_rsrc_t rK1 = hfa::make_rsrc(Kp, kbytes), rK2 = hfa::make_rsrc(Kp + p.k_sp, kbytes);
     const __amdgpu_buffer_rsrc_t rV1 = hfa::make_rsrc(Vp, vbytes), rV2 = hfa::make_rsrc(Vp + p.v_sp, vbytes);
 
-    // Q fragments (B operand of S^T = K Q^T): lane holds Q[qi][16 kb + 8 half + j], j = 0..7
     f16x8 q1[DH / 16], q2[DH / 16];
 #pragma unroll
     for (int kb = 0; kb < DH / 16; ++kb) {
@@ -311,7 +316,6 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP
         }
     }
 
-    // DMA geometry: per plane 8 x 1 KiB pieces of 8 rows, 2 per wave; lane -> row 8 piece + lane/8, slot lane&7
     int rowd[2], kch[2], vch[2];
 #pragma unroll
     for (int d = 0; d < 2; ++d) {
@@ -320,118 +324,136 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP
         vch[d] = (lane & 7) ^ (((rowd[d] >> 1) & 1) << 2);
     }
     const unsigned lds0 = hfa::lds_addr(smem);
-    auto issue = [&](int stage, int key0) {
-        const unsigned base = lds0 + stage * SSTAGE * 2 + wave * 2 * 1024;
+    auto issueK = [&](int stage, int key0) {
+        const unsigned base = lds0 + stage * KST * 2 + wave * 2 * 1024;
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
             const int key = key0 + rowd[d];
-            const bool ok = key < L;
-            const unsigned ko = ok ? (unsigned)((key * p.k_ld + kch[d] * 8) * 2) : hfa::DMA_OOB;
-            const unsigned vo = ok ? (unsigned)((key * p.v_ld + vch[d] * 8) * 2) : hfa::DMA_OOB;
+            const unsigned ko = key < L ? (unsigned)((key * p.k_ld + kch[d] * 8) * 2) : hfa::DMA_OOB;
             hfa::dma16(ko, rK1, 0u, base + d * 1024);
             hfa::dma16(ko, rK2, 0u, base + SPLANE * 2 + d * 1024);
-            hfa::dma16(vo, rV1, 0u, base + 2 * SPLANE * 2 + d * 1024);
-            hfa::dma16(vo, rV2, 0u, base + 3 * SPLANE * 2 + d * 1024);
+        }
+    };
+    auto issueV = [&](int stage, int key0) {
+        const unsigned base = lds0 + (2 + stage) * KST * 2 + wave * 2 * 1024;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            const int key = key0 + rowd[d];
+            const unsigned vo = key < L ? (unsigned)((key * p.v_ld + vch[d] * 8) * 2) : hfa::DMA_OOB;
+            hfa::dma16(vo, rV1, 0u, base + d * 1024);
+            hfa::dma16(vo, rV2, 0u, base + SPLANE * 2 + d * 1024);
         }
     };
 
-    // K row reads: row 32 kt + r32, chunk 2 kb + half (halves within a plane image)
     int kofs[DH / 16];
 #pragma unroll
     for (int kb = 0; kb < DH / 16; ++kb) kofs[kb] = r32 * DH + (((kb * 2 + half) ^ ((r32 >> 1) & 7)) << 3);
-    // V transposed reads: 16-lane group g supplies rows r0 + (i >> 2), columns c0 + 4 (i & 3) of its block
     const int gi = lane & 15, gq = gi >> 2, gp = gi & 3;
-    const int vrow = 4 * half + gq;                                   // row within the (kt, s, jj) 8-row step
-    const int vch0 = 2 * ((lane >> 4) & 1) + (gp >> 1);               // chunk within the 32-column block
-    const int vfx = (((vrow >> 1) & 1) << 2);                         // the row's swizzle (rows r0 = 0 mod 4)
-    int vofs[2];                                                      // bytes, per d-block db
+    const int vrow = 4 * half + gq;
+    const int vch0 = 2 * ((lane >> 4) & 1) + (gp >> 1);
+    const int vfx = (((vrow >> 1) & 1) << 2);
+    int vofs[2];
 #pragma unroll
     for (int db = 0; db < 2; ++db) vofs[db] = vrow * (DH * 2) + (((4 * db + vch0) ^ vfx) << 4) + 8 * (gp & 1);
 
-    f32x16 oM[2], oC[2];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) oM[0][e] = oM[1][e] = oC[0][e] = oC[1][e] = 0.f;
-    float m_run = -__builtin_inff(), l_run = 0.0f;
     const float qscale = p.scale * 1.44269504088896340736f;
-
-    const int nkb = (L + SKB - 1) / SKB;
-#pragma unroll
-    for (int st = 0; st < SNS - 1; ++st)
-        if (st < nkb) issue(st, st * SKB);
-    if (nkb >= SNS - 1) hfa::wait_vm_barrier<(SNS - 2) * 8>();
-    else hfa::wait_vm_barrier<0>();
-    int stage = 0;
-    for (int kt0 = 0; kt0 < nkb; ++kt0) {
-        const bool more = kt0 + SNS - 1 < nkb;
-        if (more) issue(stage == 0 ? SNS - 1 : stage - 1, (kt0 + SNS - 1) * SKB);
-        const _Float16* sK = smem + stage * SSTAGE;
-        const _Float16* sV = sK + 2 * SPLANE;
-        // S^T[key][query] for two 32-key blocks
-        f32x16 s[2];
+    // scores of a tile (combined, log2 units): s[kt][e] for keys 32 kt + (e & 3) + 8 (e >> 2) + 4 half
+    auto scores = [&](const _Float16* sK, f32x16 (&sM)[2], f32x16 (&sC)[2]) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
-            f32x16 sM, sC;
 #pragma unroll
-            for (int e = 0; e < 16; ++e) sM[e] = sC[e] = 0.f;
+            for (int e = 0; e < 16; ++e) sM[kt][e] = sC[kt][e] = 0.f;
 #pragma unroll
             for (int kb = 0; kb < DH / 16; ++kb) {
                 const f16x8 k1 = *reinterpret_cast<const f16x8*>(sK + kt * 32 * DH + kofs[kb]);
                 const f16x8 k2 = *reinterpret_cast<const f16x8*>(sK + SPLANE + kt * 32 * DH + kofs[kb]);
-                sM = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q1[kb], sM, 0, 0, 0);
-                sC = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q2[kb], sC, 0, 0, 0);
-                sC = __builtin_amdgcn_mfma_f32_32x32x16_f16(k2, q1[kb], sC, 0, 0, 0);
+                sM[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q1[kb], sM[kt], 0, 0, 0);
+                sC[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q2[kb], sC[kt], 0, 0, 0);
+                sC[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k2, q1[kb], sC[kt], 0, 0, 0);
             }
-#pragma unroll
-            for (int e = 0; e < 16; ++e) s[kt][e] = __builtin_fmaf(sC[e], kLo, sM[e]) * qscale;
         }
-        const int key0 = kt0 * SKB;
-        if (key0 + SKB > L) {          // last, partial tile: keys >= L do not exist
+    };
+    // combined raw dot products (qscale is applied inside the exponent); done after the rest of the iteration so
+    // the MFMAs run meanwhile
+    auto combine = [&](const f32x16 (&sM)[2], const f32x16 (&sC)[2], f32x16 (&sc)[2]) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) sc[kt][e] = __builtin_fmaf(sC[kt][e], kLo, sM[kt][e]);
+    };
+
+    f32x16 o[2];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[0][e] = o[1][e] = 0.f;
+    float m_run = -__builtin_inff(), l_run = 0.0f;
+
+    const int nkb = (L + SKB - 1) / SKB;
+    issueK(0, 0);
+    issueV(0, 0);
+    if (nkb > 1) issueK(1, SKB);
+    hfa::wait_vm_barrier<0>();
+    f32x16 s[2], nM[2], nC[2];
+    scores(smem, nM, nC);
+    combine(nM, nC, s);
+    __syncthreads();                                       // every wave's K(0) reads done before K(2) lands there
+    for (int t = 0; t < nkb; ++t) {
+        const int st = t & 1;
+        if (t + 2 < nkb) issueK(st, (t + 2) * SKB);        // K(t) was read by iteration t - 1's scores
+        if (t + 1 < nkb) issueV(st ^ 1, (t + 1) * SKB);    // V(t - 1) was read by iteration t - 1's PV
+        if (t + 1 < nkb) scores(smem + (st ^ 1) * KST, nM, nC);   // tile t + 1, in flight during softmax(t)
+        const int key0 = t * SKB;
+        if (key0 + SKB > L) {
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
                 for (int e = 0; e < 16; ++e)
                     if (key0 + kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * half >= L) s[kt][e] = -__builtin_inff();
         }
-        float bm = fmaxf(s[0][0], s[1][0]);
+        float bq[4];                                       // four independent max3 chains
 #pragma unroll
-        for (int e = 1; e < 16; ++e) bm = fmaxf(bm, fmaxf(s[0][e], s[1][e]));
-        bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+        for (int c = 0; c < 4; ++c) bq[c] = fmaxf(s[0][c], s[1][c]);
+#pragma unroll
+        for (int e = 4; e < 16; ++e) bq[e & 3] = fmaxf(bq[e & 3], fmaxf(s[0][e], s[1][e]));
+        float bm = fmaxf(fmaxf(bq[0], bq[1]), fmaxf(bq[2], bq[3]));
+        bm = fmaxf(bm, __shfl_xor(bm, 32, 64)) * qscale;
         const float m_cand = fmaxf(m_run, bm);
-        const bool move = m_cand > m_run + kSlack;          // first tile: m_run = -inf moves
+        const bool move = m_cand > m_run + kSlack;
         if (__builtin_amdgcn_ballot_w64(move)) {
             const float m_new = move ? m_cand : m_run;
             const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
             l_run *= alpha;
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                oM[0][e] *= alpha; oM[1][e] *= alpha;
-                oC[0][e] *= alpha; oC[1][e] *= alpha;
-            }
+            for (int e = 0; e < 16; ++e) { o[0][e] *= alpha; o[1][e] *= alpha; }
             m_run = m_new;
         }
+        // q = 2^11 p, p = exp2(qscale s - m_run - kSlack) <= 1, so q <= 2048 is an f16 normal down to p = 2^-25
+        const float nref = 11.0f - (m_run + kSlack);
         float ls = 0.0f;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                s[kt][e] = __builtin_amdgcn_exp2f(s[kt][e] - m_run);
+                s[kt][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][e], qscale, nref));
                 ls += s[kt][e];
             }
         ls += __shfl_xor(ls, 32, 64);
         l_run += ls;
-        // O^T[d][q] += sum_key V^T[d][key] P^T[key][q]; k-step (kt, ks) takes P registers 8 ks .. 8 ks + 7 of
-        // block kt, i.e. keys 32 kt + 16 ks + 8 (j >> 2) + 4 half + (j & 3) for element j
+        const _Float16* sV = smem + (2 + st) * KST;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-                f16x8 p1, p2;
+                f16x8 p1, p2, p1s;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float pv = s[kt][8 * ks + j];
-                    p1[j] = (_Float16)pv;
-                    p2[j] = (_Float16)((pv - (float)p1[j]) * 2048.0f);
+                    // 2^11 p1 = q with the low 13 mantissa bits cleared (an f16 value for q >= 2^-14),
+                    // 2^11 (p - p1) = the exact f32 remainder, rounded to f16
+                    const float qv = s[kt][8 * ks + j];
+                    const float qt = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, qv) & 0xFFFFE000u);
+                    p1s[j] = (_Float16)qt;
+                    p2[j] = (_Float16)(qv - qt);
                 }
+                p1 = p1s * (_Float16)kLo;
                 const int rb = (32 * kt + 16 * ks) * (DH * 2);
 #pragma unroll
                 for (int db = 0; db < 2; ++db) {
@@ -441,29 +463,26 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP
                     const f16x4 b1 = lds_tr(sV + SPLANE, rb + 8 * DH * 2 + vofs[db]);
                     const f16x8 v1 = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
                     const f16x8 v2 = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-                    oM[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, p1, oM[db], 0, 0, 0);
-                    oC[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, p2, oC[db], 0, 0, 0);
-                    oC[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v2, p1, oC[db], 0, 0, 0);
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, p1s, o[db], 0, 0, 0);
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, p2, o[db], 0, 0, 0);
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v2, p1, o[db], 0, 0, 0);
                 }
             }
-        if (kt0 + 1 < nkb) {                    // next tile landed; every wave done with this stage
-            if (more) hfa::wait_vm_barrier<(SNS - 2) * 8>();
-            else hfa::wait_vm_barrier<0>();
+        if (t + 1 < nkb) {
+            combine(nM, nC, s);
+            hfa::wait_vm_barrier<0>();                     // K(t+2), V(t+1) landed; K(t+1), V(t) reads done
         }
-        stage = stage + 1 == SNS ? 0 : stage + 1;
     }
 
-    // normalise and stage O[i][d] through LDS (each wave a private 32 x 33 f32 slab), then row-contiguous split
-    // stores (4 d per lane per plane)
     __syncthreads();
-    const float inv = 1.0f / l_run;
+    const float inv = 1.0f / l_run;                        // o and l both carry the 2^11 scale
     float* slab = reinterpret_cast<float*>(smem) + wave * (QW * 33);
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int d = (e & 3) + 8 * (e >> 2) + 4 * half;
-            slab[r32 * 33 + d] = __builtin_fmaf(oC[db][e], kLo, oM[db][e]) * inv;
+            slab[r32 * 33 + d] = o[db][e] * inv;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

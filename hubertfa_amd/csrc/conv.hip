@@ -144,6 +144,7 @@ __global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const fl
             vb += hb;
         }
         if constexpr (OUTS) {
+            asm volatile("" : "+v"(va), "+v"(vb));   // split the rounded f32 values (no multiply-into-cvt fusion)
             bad |= !(__builtin_fabsf(va) < 65504.0f) || !(__builtin_fabsf(vb) < 65504.0f);
             f16x2 v1, v2;
             v1[0] = (_Float16)va;
@@ -160,8 +161,9 @@ __global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const fl
 }
 
 // Split-plane output with 8 channels per lane: a wave stores one frame's 512 channels as 16-B pieces per plane
-// (1 KiB per wave-instruction instead of 256 B); 4 frames in flight per block.  Same arithmetic, same bits as
-// conv0_apply_kernel<MODE, true>.
+// (1 KiB per wave-instruction instead of 256 B); 4 frames in flight per block.  Per element the same scalar
+// operations in the same order as conv0_apply_kernel<MODE, true> (bit-identical outputs).  No packed-f32 math
+// (Makefile NO_PK_F32).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 template <int MODE>
@@ -177,23 +179,20 @@ __global__ __launch_bounds__(NT) void conv0_apply8_kernel(int N, int T0, const f
     const int nt = min(CH, T0 - t0);
     stage_chunk(xs, x + b * x_bs, t0, nt, N);
     const int c0 = (threadIdx.x & 63) * 8, fr = threadIdx.x >> 6;
-    // channel pairs in packed f32x2 registers: the conv, the affine and the GELU issue as v_pk_* (the kernel is
-    // VALU-bound), with the per-element operation order of conv0_apply_kernel (bit-identical outputs)
-    typedef hfa::hfa_f32x2 f2;
-    f2 w[4][KW], mul[4], add[4], mu[4], g[4];
+    float w[8][KW], m[8], r[8], sc[8], sh[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int c = 0; c < 8; ++c) {
 #pragma unroll
-        for (int j = 0; j < KW; ++j) w[i][j] = f2{w0[(c0 + 2 * i) * KW + j], w0[(c0 + 2 * i + 1) * KW + j]};
+        for (int j = 0; j < KW; ++j) w[c][j] = w0[(c0 + c) * KW + j];
         if (MODE == 0) {
-            mu[i] = f2{stats[(b * C0 + c0 + 2 * i) * 2], stats[(b * C0 + c0 + 2 * i + 1) * 2]};
-            mul[i] = f2{stats[(b * C0 + c0 + 2 * i) * 2 + 1], stats[(b * C0 + c0 + 2 * i + 1) * 2 + 1]};
-            add[i] = f2{beta[c0 + 2 * i], beta[c0 + 2 * i + 1]};
-            g[i] = f2{gamma[c0 + 2 * i], gamma[c0 + 2 * i + 1]};
+            m[c] = stats[(b * C0 + c0 + c) * 2];
+            r[c] = stats[(b * C0 + c0 + c) * 2 + 1];
+            sc[c] = gamma[c0 + c];
+            sh[c] = beta[c0 + c];
         } else {
-            mu[i] = f2{0.f, 0.f};
-            mul[i] = g[i] = f2{1.f, 1.f};
-            add[i] = bias ? f2{bias[c0 + 2 * i], bias[c0 + 2 * i + 1]} : f2{0.f, 0.f};
+            m[c] = 0.f;
+            r[c] = sc[c] = 1.f;
+            sh[c] = bias ? bias[c0 + c] : 0.f;
         }
     }
     __syncthreads();
@@ -203,18 +202,14 @@ __global__ __launch_bounds__(NT) void conv0_apply8_kernel(int N, int T0, const f
         f16x8 h1, h2;
         const float* xt = xs + t * ST;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            f2 v = f2{0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < KW; ++j) v = __builtin_elementwise_fma(w[i][j], f2{xt[j], xt[j]}, v);
-            if (MODE == 0) v = hfa::gelu_fast2((v - mu[i]) * mul[i] * g[i] + add[i]);
-            else v += add[i];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                bad |= !(__builtin_fabsf(v[e]) < 65504.0f);
-                h1[2 * i + e] = (_Float16)v[e];
-                h2[2 * i + e] = (_Float16)((v[e] - (float)h1[2 * i + e]) * 2048.0f);
-            }
+        for (int c = 0; c < 8; ++c) {
+            float v = conv10(w[c], xt);
+            if (MODE == 0) v = hfa::gelu_fast((v - m[c]) * r[c] * sc[c] + sh[c]);
+            else v += sh[c];
+            asm volatile("" : "+v"(v));   // split the rounded f32 value: no fusing its last multiply into the f16 cvt
+            bad |= !(__builtin_fabsf(v) < 65504.0f);
+            h1[c] = (_Float16)v;
+            h2[c] = (_Float16)((v - (float)h1[c]) * 2048.0f);
         }
         *reinterpret_cast<f16x8*>(yb + (long long)t * C0) = h1;
         *reinterpret_cast<f16x8*>(yb + (long long)t * C0 + y_sp) = h2;

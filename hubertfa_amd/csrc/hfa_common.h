@@ -127,27 +127,6 @@ __device__ __forceinline__ float gelu_fast(float x) {
     return 0.5f * x * (1.0f + copysignf(e, z));
 }
 
-// gelu_fast on a pair (packed v_pk_fma_f32 / v_pk_mul_f32: half the VALU issue), the same operations in the same
-// order per element, so bit-identical to two gelu_fast calls.
-typedef float hfa_f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ hfa_f32x2 gelu_fast2(hfa_f32x2 x) {
-    const hfa_f32x2 z = x * 0.70710678118654752440f;
-    const hfa_f32x2 a = __builtin_elementwise_min(__builtin_elementwise_abs(z), hfa_f32x2{3.95f, 3.95f});
-    auto c = [](unsigned u) { const float f = __uint_as_float(u); return hfa_f32x2{f, f}; };
-    hfa_f32x2 q = c(0xb6fcc2dfu);
-    q = __builtin_elementwise_fma(q, a, c(0x38d50244u));
-    q = __builtin_elementwise_fma(q, a, c(0xba160ee5u));
-    q = __builtin_elementwise_fma(q, a, c(0x3acb0addu));
-    q = __builtin_elementwise_fma(q, a, c(0xb8060160u));
-    q = __builtin_elementwise_fma(q, a, c(0xbc9d8a4eu));
-    q = __builtin_elementwise_fma(q, a, c(0x3dd28a28u));
-    q = __builtin_elementwise_fma(q, a, c(0x3f22f942u));
-    q = __builtin_elementwise_fma(q, a, c(0x3e0375dfu));
-    q = __builtin_elementwise_fma(a, q, a);
-    const hfa_f32x2 t = q * -1.44269504088896340736f;
-    const hfa_f32x2 e = 1.0f - hfa_f32x2{__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
-    return 0.5f * x * (1.0f + __builtin_elementwise_copysign(e, z));
-}
 
 // torch Hardswish: x * relu6(x + 3) / 6.
 __device__ __forceinline__ float hardswish(float x) {

@@ -37,3 +37,38 @@ def test_ops_refuse_cpu_tensors():
     with pytest.raises(_lib.HFALibraryError):
         ops.viterbi_backtrack(x, x.to(torch.int8), torch.zeros(1, 4, dtype=torch.int32),
                               torch.ones(1, dtype=torch.int32), torch.ones(1, dtype=torch.int32))
+
+
+def test_no_packed_f32_in_device_code():
+    """libhfa carries no packed-f32 VALU (v_pk_fma/mul/add_f32): on MI355X their results came out wrong in groups
+    of lanes, now and then, while MFMA waves of another kernel shared the CU.  The Makefile builds
+    with the packed-fp32-ops target feature off; this checks the shipped code objects."""
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    from hubertfa_amd._lib import LIB_PATH
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(LIB_PATH) or not shutil.which(f"{llvm}/llvm-objcopy"):
+        pytest.skip("library or llvm tools absent")
+    with tempfile.TemporaryDirectory() as td:
+        fat = os.path.join(td, "fat.bin")
+        subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", LIB_PATH, os.path.join(td, "x")],
+                       check=True, capture_output=True)
+        data = open(fat, "rb").read()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        offs = [m.start() for m in re.finditer(re.escape(magic), data)]
+        assert offs, "no offload bundles in libhfa.so"
+        n_mfma = 0
+        for i, o in enumerate(offs):
+            part = os.path.join(td, f"b{i}.bin")
+            co = os.path.join(td, f"b{i}.co")
+            open(part, "wb").write(data[o:offs[i + 1] if i + 1 < len(offs) else len(data)])
+            subprocess.run([f"{llvm}/clang-offload-bundler", "--type=o", f"--input={part}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}", "--unbundle"], check=True)
+            dis = subprocess.run([f"{llvm}/llvm-objdump", "-d", "--mcpu=gfx950", co], capture_output=True,
+                                 text=True, check=True).stdout
+            bad = re.findall(r"v_pk_\w*f32", dis)
+            assert not bad, f"bundle {i}: {len(bad)} packed-f32 instructions, e.g. {bad[0]}"
+            n_mfma += dis.count("v_mfma")
+        assert n_mfma > 0, "disassembly found no MFMA: extraction failed"

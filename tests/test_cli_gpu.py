@@ -43,3 +43,37 @@ def test_infer_cli_end_to_end(tmp_path):
     for i in range(len(SECS)):
         one = next(out1.rglob(f"u{i}.TextGrid")).read_text()
         assert one == batched[i], f"u{i}: batched TextGrid differs from the B=1 run"
+
+
+def test_pipelined_predict_repeatable(tmp_path):
+    """The CLI's two-stream pipeline (encoder of batch i+1 beside head + DP of batch i), one-utterance batches,
+    repeated: every run's intervals and confidences are identical (an intermittent intra-kernel LDS race in the
+    pipelined split attention showed up only here, under the concurrent side stream)."""
+    import infer
+    import hubertfa_amd.g2p as g2p_mod
+    import torch
+    from hubertfa_amd import synth
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+    from hubertfa_amd.wav_io import write_wav
+    d = synth.synth_dictionary(n_words=40)
+    dpath = tmp_path / "dict.txt"
+    dpath.write_text("".join(f"{w}\t{' '.join(p)}\n" for w, p in d.items()))
+    seg = tmp_path / "segments"
+    seg.mkdir()
+    for i, secs in enumerate((2.0, 2.0, 3.5, 2.7, 1.3)):
+        write_wav(seg / f"u{i}.wav", synth.synth_audio(int(secs * 16000), seed=i), 16000)
+        (seg / f"u{i}.lab").write_text(synth.synth_lab(5, d, seed=i))
+    ck = tmp_path / "m.ckpt"
+    synth_checkpoint(str(ck))
+    g = g2p_mod.DictionaryG2P(dictionary=str(dpath))
+    g.set_in_format("lab")
+    rows = list(g.get_dataset(sorted(seg.rglob("*.wav"))))
+    torch.set_grad_enabled(False)
+    task = ForcedAlignmentTask.load_from_checkpoint(str(ck), device=torch.device("cuda"), hubert_model_path="synth:0")
+
+    def key(preds):
+        return {str(p[0]): (np.asarray(p[4]).tobytes(), np.asarray(p[2]).tobytes()) for p in preds}
+    ref = key(infer._predict(task, rows, 32))
+    for rep in range(8):
+        got = key(infer._predict(task, rows, 1))
+        assert got == ref, f"rep {rep}: {[n for n in got if got[n] != ref[n]]} differ"

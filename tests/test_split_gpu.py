@@ -321,6 +321,40 @@ def test_attention_split_varlen():
         assert bool((got[b, n:] == 0).all())
 
 
+def test_attention_split_repeatable():
+    """The pipelined K/V rings: 30 launches over a many-tile, many-workgroup batch are bit-identical, and a
+    varlen batch equals each row run alone (an LDS stage overwritten while another wave still reads it shows
+    up here as run-to-run differences)."""
+    from hubertfa_amd import ops
+    from hubertfa_amd.hubert import dev_lengths
+    B, H, L, D = 16, 12, 499, 64
+    d = torch.device("cuda")
+    qs = ops.split(_r(B, L, 3 * H * D, seed=11, scale=2.0).to(d))
+    lens = [L - 37 * (b % 9) for b in range(B)]
+    kl = dev_lengths(lens, d)
+    first = None
+    side = torch.cuda.Stream(d)                      # a concurrent GEMM stream skews the waves of a workgroup
+    a = torch.randn(4096, 4096, device=d)
+    outs = []
+    for i in range(40):
+        if i % 4 == 0:
+            with torch.cuda.stream(side):
+                for _ in range(4):
+                    a = torch.tanh(a @ a)
+        out = torch.empty(2, B, L, H * D, dtype=torch.float16, device=d)
+        ops.attention_split(qs, out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5, key_len=kl)
+        outs.append(out)
+    torch.cuda.synchronize()
+    first = outs[0]
+    for i, out in enumerate(outs[1:]):
+        assert torch.equal(out, first), f"launch {i + 1} differs from launch 0"
+    for b in (0, 4, 8):
+        n = lens[b]
+        one = torch.empty(2, 1, n, H * D, dtype=torch.float16, device=d)
+        ops.attention_split(qs[:, b:b + 1, :n].contiguous(), one, B=1, H=H, L=n, head_dim=D, scale=D ** -0.5)
+        assert torch.equal(one[:, 0], first[:, b, :n])
+
+
 def test_attention_split_large_scores():
     """Peaked softmax (scores ~ +-60): the score's own f32-level rounding dominates both kernels' error; the split
     kernel stays within 2x the f32 MFMA kernel's error against f64."""
