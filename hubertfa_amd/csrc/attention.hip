@@ -262,13 +262,17 @@ __device__ __forceinline__ f16x4 lds_tr(const _Float16* base, int byte_off) {
         const_cast<__attribute__((address_space(3))) s16x4*>(ptr)));
 }
 
-__global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP p) {
+template <int SNW>
+__global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnSP p) {
     // Software-pipelined: iteration t issues the score MFMAs of tile t+1, then runs tile t's softmax (VALU) while
     // those MFMAs execute, then tile t's PV MFMAs.  K runs one tile further ahead than V in separate 2-stage rings
     // (K(t+1) must have landed when iteration t starts, V(t) only by its PV), so the LDS stays 64 KiB (2 per CU).
     // The output uses one accumulator at scale 2^11: P is taken relative to m_run + kSlack (p <= 1, so 2^11 p1 is
     // exact in f16) and O += V1 (2^11 P1) + V1 P2 + V2 P1.
+    // SNW waves of 32 queries share each K/V tile (8 waves halve the LDS-DMA stream per query at L ~ 500)
     constexpr int KST = 2 * SPLANE;                      // halves per K (or V) stage, both planes
+    constexpr int NW = SNW, PPW = 8 / SNW;               // 1-KiB DMA pieces (8 keys) per plane per wave
+    static_assert(SNW == 4 || SNW == 8, "4 or 8 waves");
     __shared__ __attribute__((aligned(16))) _Float16 smem[4 * KST];   // K0, K1, V0, V1
 
     const int nwg = gridDim.x, orig = blockIdx.x;
@@ -316,18 +320,18 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP
         }
     }
 
-    int rowd[2], kch[2], vch[2];
+    int rowd[PPW], kch[PPW], vch[PPW];
 #pragma unroll
-    for (int d = 0; d < 2; ++d) {
-        rowd[d] = (wave * 2 + d) * 8 + (lane >> 3);
+    for (int d = 0; d < PPW; ++d) {
+        rowd[d] = (wave * PPW + d) * 8 + (lane >> 3);
         kch[d] = (lane & 7) ^ ((rowd[d] >> 1) & 7);
         vch[d] = (lane & 7) ^ (((rowd[d] >> 1) & 1) << 2);
     }
     const unsigned lds0 = hfa::lds_addr(smem);
     auto issueK = [&](int stage, int key0) {
-        const unsigned base = lds0 + stage * KST * 2 + wave * 2 * 1024;
+        const unsigned base = lds0 + stage * KST * 2 + wave * PPW * 1024;
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
+        for (int d = 0; d < PPW; ++d) {
             const int key = key0 + rowd[d];
             const unsigned ko = key < L ? (unsigned)((key * p.k_ld + kch[d] * 8) * 2) : hfa::DMA_OOB;
             hfa::dma16(ko, rK1, 0u, base + d * 1024);
@@ -335,9 +339,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP
         }
     };
     auto issueV = [&](int stage, int key0) {
-        const unsigned base = lds0 + (2 + stage) * KST * 2 + wave * 2 * 1024;
+        const unsigned base = lds0 + (2 + stage) * KST * 2 + wave * PPW * 1024;
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
+        for (int d = 0; d < PPW; ++d) {
             const int key = key0 + rowd[d];
             const unsigned vo = key < L ? (unsigned)((key * p.v_ld + vch[d] * 8) * 2) : hfa::DMA_OOB;
             hfa::dma16(vo, rV1, 0u, base + d * 1024);
@@ -510,6 +514,16 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_split_kernel(const AttnSP
 
 }  // namespace
 
+namespace {
+int g_attn_waves = 0;   // hfa_attention_split_tuning override (0: automatic)
+// Waves (x 32 queries) per workgroup of the split attention: 8 where that still leaves >= 2 workgroups per
+// (batch, head) row of queries, else 4.
+inline int split_attn_waves(int L) {
+    if (g_attn_waves == 4 || g_attn_waves == 8) return g_attn_waves;
+    return L >= 2 * 8 * QW ? 8 : 4;
+}
+}  // namespace
+
 extern "C" {
 
 int hfa_attention_f32(int B, int H, int L, int head_dim, float scale, const float* q, long long q_bs, int q_ld,
@@ -568,13 +582,27 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
     }
     AttnSP p{B, H, L, scale, (const _Float16*)q, q_sp, q_bs, q_ld, (const _Float16*)k, k_sp, k_bs, k_ld,
              (const _Float16*)v, v_sp, v_bs, v_ld, (_Float16*)o, o_sp, o_bs, o_ld, key_len};
-    const long long nblk = (long long)((L + QW * NW - 1) / (QW * NW)) * B * H;
+    const int nw = split_attn_waves(L);
+    const long long nblk = (long long)((L + QW * nw - 1) / (QW * nw)) * B * H;
     if (nblk > 0x7fffffffLL) {
         hfa::set_error("hfa_attention_split: grid too large");
         return HFA_EINVAL;
     }
-    hipLaunchKernelGGL(attn_fwd_split_kernel, dim3((unsigned)nblk), dim3(NW * 64), 0, stream, p);
+    if (nw == 8)
+        hipLaunchKernelGGL(attn_fwd_split_kernel<8>, dim3((unsigned)nblk), dim3(8 * 64), 0, stream, p);
+    else
+        hipLaunchKernelGGL(attn_fwd_split_kernel<4>, dim3((unsigned)nblk), dim3(4 * 64), 0, stream, p);
     return hfa::check_launch("hfa_attention_split");
+}
+
+// Waves per workgroup of hfa_attention_split: 4 or 8, 0 = automatic (benchmarks and the 4/8 parity test).
+int hfa_attention_split_tuning(int waves) {
+    if (waves != 0 && waves != 4 && waves != 8) {
+        hfa::set_error("hfa_attention_split_tuning: waves must be 0, 4 or 8");
+        return HFA_EINVAL;
+    }
+    g_attn_waves = waves;
+    return HFA_OK;
 }
 
 }  // extern "C"

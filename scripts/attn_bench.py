@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-from hubertfa_amd import ops  # noqa: E402
+from hubertfa_amd import ops, _lib  # noqa: E402
 
 SHAPES = [("base B32 L499", 32, 12, 499), ("large B32 L499", 32, 16, 499), ("long B1 L14999", 1, 12, 14999)]
 
@@ -35,7 +35,8 @@ def main():
             ops.attention(qkv, qkv[..., H * D:], qkv[..., 2 * H * D:], out, B=B, H=H, L=L, head_dim=D,
                           scale=D ** -0.5, q_bs=L * 3 * H * D, q_ld=3 * H * D, k_bs=L * 3 * H * D, k_ld=3 * H * D,
                           v_bs=L * 3 * H * D, v_ld=3 * H * D, o_bs=L * H * D, o_ld=H * D)
-        for tag, fn in (("f32", go), ("split", go_split)):
+        for tag, fn, nw in (("f32", go, 0), ("split", go_split, 0), ("spl4w", go_split, 4), ("spl8w", go_split, 8)):
+            _lib.call("hfa_attention_split_tuning", nw)
             for _ in range(3):
                 fn()
             torch.cuda.synchronize()
@@ -46,6 +47,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.reps
+            _lib.call("hfa_attention_split_tuning", 0)
             print(f"{name:16s} {tag:5s} {ms:8.3f} ms  {4.0 * B * H * L * L * D / ms / 1e9:7.1f} TFLOP/s", flush=True)
 
 

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--cfgs", default="0,1,2,3")
     ap.add_argument("--shapes", default="")
+    ap.add_argument("--epi", action="store_true", help="epilogue ablation: GELU vs none, f32 vs planes out")
     args = ap.parse_args()
     keep = set(args.shapes.split(",")) if args.shapes else None
     dev = torch.device("cuda")
@@ -86,6 +87,13 @@ def main():
             ms = timeit(spl, args.reps)
             line += f" | cfg{cfg} {flops / ms / 1e9:6.1f} TF e{ec:.0e}"
         _lib.lib().hfa_gemm_split_tuning(0)
+        if args.epi:
+            ysp = torch.empty(2, B, Tout, Cout, dtype=torch.float16, device=dev)
+            for e_ in (1, 0):
+                kw2 = dict(kw, epilogue=e_)
+                t_c = timeit(lambda: ops.conv_gemm_split(xs, ws, C=ys, **kw2), args.reps)
+                t_p = timeit(lambda: ops.conv_gemm_split(xs, ws, Cs=ysp, **kw2), args.reps)
+                line += f" | epi{e_}: f32-out {t_c:.3f} ms, planes-out {t_p:.3f} ms"
         print(line, flush=True)
 
 

@@ -355,6 +355,28 @@ def test_attention_split_repeatable():
         assert torch.equal(one[:, 0], first[:, b, :n])
 
 
+@pytest.mark.parametrize("L", [499, 700])
+def test_attention_split_waves_bit_identical(L):
+    """4- and 8-wave workgroups give bit-identical planes (each query row sees the same key tiles in the same
+    order), with and without per-row key lengths."""
+    from hubertfa_amd import ops, _lib
+    from hubertfa_amd.hubert import dev_lengths
+    B, H, D = 3, 4, 64
+    d = torch.device("cuda")
+    qs = ops.split(_r(B, L, 3 * H * D, seed=13, scale=2.0).to(d))
+    for kl in (None, dev_lengths([L, L - 200, 65], d)):
+        outs = []
+        for nw in (4, 8):
+            _lib.call("hfa_attention_split_tuning", nw)
+            try:
+                o = torch.full((2, B, L, H * D), float("nan"), dtype=torch.float16, device=d)
+                ops.attention_split(qs, o, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5, key_len=kl)
+                outs.append(o)
+            finally:
+                _lib.call("hfa_attention_split_tuning", 0)
+        assert torch.equal(outs[0], outs[1])
+
+
 def test_attention_split_large_scores():
     """Peaked softmax (scores ~ +-60): the score's own f32-level rounding dominates both kernels' error; the split
     kernel stays within 2x the f32 MFMA kernel's error against f64."""
