@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--serial", action="store_true", help="one stream per step (no head/encoder overlap)")
     ap.add_argument("--chunk-seconds", type=float, default=None,
                     help="long-form: encode overlapping windows of this length (config 5 chunked; B=1 only)")
+    ap.add_argument("--host-input", action="store_true",
+                    help="waves start in pinned host memory and are copied to HBM inside every step (PCIe-inclusive "
+                         "rate; the headline value keeps inputs resident in HBM)")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -202,11 +205,14 @@ def main():
     task.on_predict_start()
     B = args.batch
     wav_np, ph_seqs, word_seqs, p2ws = make_inputs(B, args.seconds, args.words, seed0=1000 * (rank + 1))
-    wav = torch.from_numpy(wav_np).to(dev)
+    wav = wav_dev = torch.from_numpy(wav_np).to(dev)
+    wav_host = torch.from_numpy(wav_np).pin_memory() if args.host_input else None
 
     def launch():
         """GPU half of one step (+ the boundary gather) and the async D2H of its results: the encoder on the main
-        stream, head + DP on a side stream overlapping the next step's encoder (task.submit)."""
+        stream, head + DP on a side stream overlapping the next step's encoder (task.submit).  With --host-input the
+        step starts with the H2D copy of its waves, on the encoder's stream."""
+        wav = wav_host.to(dev, non_blocking=True) if wav_host is not None else wav_dev
         if args.serial:
             dev_out = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False,
                                        chunk_seconds=args.chunk_seconds)
@@ -286,7 +292,7 @@ def main():
                                f"{'' if args.chunk_seconds is None else f', chunked {args.chunk_seconds:g} s windows'}: "
                                f"B={B} x {args.seconds:g} s 16 kHz utterances per GPU, "
                                f"{ {'base': 'Hubert-base (cnhubert arch)', 'large': 'Hubert-large (cnhubert-large arch)', 'soft': 'HubertSoft'}[args.encoder]}"
-                               f" + UNet head + Viterbi; full infer path wave(HBM)->boundaries(host), host assembly "
+                               f" + UNet head + Viterbi; full infer path wave({'host, H2D in the step' if args.host_input else 'HBM'})->boundaries(host), host assembly "
                                f"pipelined one batch behind the GPU",
                    "encoder": encoder,
                    "global_batch": world * B, "seconds_per_utterance": args.seconds, "dp_frames": n_frames,
