@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--chunk-seconds", type=float, default=None,
                     help="long-form: encode overlapping windows of this length (config 5 chunked; B=1 only)")
     ap.add_argument("--host-input", action="store_true",
-                    help="waves start in pinned host memory and are copied to HBM inside every step (PCIe-inclusive "
+                    help="waves start in host memory and are uploaded inside every step (task.upload, as infer.py) (PCIe-inclusive "
                          "rate; the headline value keeps inputs resident in HBM)")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
@@ -211,8 +211,8 @@ def main():
     def launch():
         """GPU half of one step (+ the boundary gather) and the async D2H of its results: the encoder on the main
         stream, head + DP on a side stream overlapping the next step's encoder (task.submit).  With --host-input the
-        step starts with the H2D copy of its waves, on the encoder's stream."""
-        wav = wav_host.to(dev, non_blocking=True) if wav_host is not None else wav_dev
+        step starts with task.upload of its waves (the CLI's pinned non-blocking H2D)."""
+        wav = task.upload(wav_host) if wav_host is not None else wav_dev
         if args.serial:
             dev_out = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False,
                                        chunk_seconds=args.chunk_seconds)

@@ -16,7 +16,6 @@ import click
 
 
 def _predict(task, dataset, batch_size: int):
-    import numpy as np
     import torch
     from hubertfa_amd.batching import plan_batches, resampled_length
     from hubertfa_amd.wav_io import read_wav
@@ -51,10 +50,11 @@ def _predict(task, dataset, batch_size: int):
     pending = None
     for file_sr, chunk in batches():
         lens = [len(c[1]) for c in chunk]
-        wav_np = np.zeros((len(chunk), max(lens)), np.float32)
+        wav_h = torch.zeros((len(chunk), max(lens)), dtype=torch.float32, pin_memory=True)
+        wav_np = wav_h.numpy()           # rows written straight into pinned memory
         for r, c in enumerate(chunk):
             wav_np[r, :lens[r]] = c[1]
-        wav = torch.from_numpy(wav_np).pin_memory().to(task.device, non_blocking=True)   # no host sync
+        wav = task.upload(wav_h)         # pinned non-blocking H2D: no host sync
         handle = task.submit(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
                              wav_sr=file_sr, lengths=lens if len(chunk) > 1 else None)
         n44s = [resampled_length(n, file_sr, sr) for n in lens]
