@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--host-input", action="store_true",
                     help="waves start in host memory and are uploaded inside every step (task.upload, as infer.py) (PCIe-inclusive "
                          "rate; the headline value keeps inputs resident in HBM)")
-    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_r01.json"),
+    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r01", "traffic_r01.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
 
@@ -97,6 +97,18 @@ def make_inputs(B, seconds, words, seed0):
         word_seqs.append(ws)
         p2ws.append(p2w)
     return wav, ph_seqs, word_seqs, p2ws
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
 
 def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s, encoder="cnhubert"):
@@ -131,7 +143,7 @@ def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s, encoder="cnhuber
         done += 1
     el = time.perf_counter() - t0
     secs = done * wav.shape[1] / 16000
-    return {"value": secs / el, "unit": "audio_s/s", "cores": threads, "kind": "port",
+    return {"value": secs / el, "unit": "audio_s/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"{done} x {wav.shape[1] / 16000:.0f} s utterances of the same workload, sequential B=1 "
                       f"(oracle: torch-CPU fp32 resample + {encoder} + UNet, C Viterbi), {el:.1f} s wall"}
 
@@ -217,10 +229,11 @@ def main():
             dev_out = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False,
                                        chunk_seconds=args.chunk_seconds)
             if world > 1:
-                gather_boundaries(dev_out)
+                gather_boundaries(dev_out, uniform=True)
             return task.decoder.fetch(dev_out)
         return task.submit(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000,
-                           on_device=gather_boundaries if world > 1 else None, chunk_seconds=args.chunk_seconds)
+                           on_device=(lambda d: gather_boundaries(d, uniform=True)) if world > 1 else None,
+                           chunk_seconds=args.chunk_seconds)
 
     def finish(handle):
         return task.decoder.assemble(handle, ph_seqs, word_seqs, p2ws)
@@ -285,7 +298,7 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "vs_baseline": None, "dtype": "f32 (split-f16x3)", "data": "synthetic",
         "arithmetic": "f32 operands as split-f16 pairs (x = x1 + 2^-11 x2) on v_mfma_f32_32x32x16_f16, 3 exact products per "
                       "f32 MAC, f32 accumulate; norms/softmax/DP in f32 (DP f32/f64 as the reference)",
         "config": {"workload": f"{config_name(args.encoder, world, B, args.seconds)}"
@@ -294,7 +307,7 @@ def main():
                                f"{ {'base': 'Hubert-base (cnhubert arch)', 'large': 'Hubert-large (cnhubert-large arch)', 'soft': 'HubertSoft'}[args.encoder]}"
                                f" + UNet head + Viterbi; full infer path wave({'host, H2D in the step' if args.host_input else 'HBM'})->boundaries(host), host assembly "
                                f"pipelined one batch behind the GPU",
-                   "encoder": encoder,
+                   "encoder": encoder, "do_normalize": bool(task.unitsEncoder.model.arch.do_normalize),
                    "global_batch": world * B, "seconds_per_utterance": args.seconds, "dp_frames": n_frames,
                    "states": len(ph_seqs[0]), "parallelism": f"utterance-dp{world}"},
         "frames_per_s": frames_ps,

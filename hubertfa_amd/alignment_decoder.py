@@ -51,6 +51,20 @@ def total_confidence(frame_confidence: np.ndarray):
     return np.exp(np.mean(np.log(frame_confidence + 1e-6)) / 3)  # (:97)
 
 
+def utterance_result(rec: dict, ph_seq, word_seq, ph_idx_to_word_idx, frame_length: float) -> dict:
+    """One utterance's decode outputs from its raw boundary record — T, ph_idx_seq [n], ph_time_int [n],
+    frame_confidence [T] and edge_diff [T] (f32 as computed on the GPU; the last frame's entry is replaced by
+    0 as :83) — so every consumer of the raw arrays (the batched decoder, the multi-GPU gather on rank 0) builds
+    bit-identical intervals."""
+    T = rec["T"]
+    ed = np.asarray(rec["edge_diff"])
+    edge_diff = np.concatenate([ed[:T - 1].astype(np.float64), [0.0]]) if T > 0 else np.zeros(0)
+    ph_p, ph_iv, w_p, w_iv = assemble_intervals(rec["ph_idx_seq"], rec["ph_time_int"], edge_diff, T, frame_length,
+                                                ph_seq, word_seq, ph_idx_to_word_idx)
+    return dict(rec, ph_seq=ph_p, ph_intervals=ph_iv, word_seq=w_p, word_intervals=w_iv,
+                confidence=total_confidence(rec["frame_confidence"]))
+
+
 class AlignmentDecoder:
     """GPU alignment decoder with the reference's API (tools/alignment_decoder.py:8-24)."""
 
@@ -184,12 +198,9 @@ class AlignmentDecoder:
             ws = word_seqs[b] if word_seqs is not None and word_seqs[b] is not None else ph_seq
             pw = p2ws[b] if p2ws is not None and p2ws[b] is not None else np.arange(len(ph_seq))
             k = int(n_h[b])
-            pis, pts = idx_h[b, :k].astype(np.int64), tint_h[b, :k].astype(np.int64)
-            fcb = fc_h[b, :T].copy()
-            edge_diff = np.concatenate([ed_h[b, :T - 1].astype(np.float64), [0.0]]) if T > 0 else np.zeros(0)
-            ph_p, ph_iv, w_p, w_iv = assemble_intervals(pis, pts, edge_diff, T, self.frame_length, ph_seq, ws, pw)
-            r = dict(T=T, ph_idx_seq=pis, ph_time_int=pts, frame_confidence=fcb, ph_seq=ph_p, ph_intervals=ph_iv,
-                     word_seq=w_p, word_intervals=w_iv, confidence=total_confidence(fcb))
+            rec = dict(T=T, ph_idx_seq=idx_h[b, :k].astype(np.int64), ph_time_int=tint_h[b, :k].astype(np.int64),
+                       frame_confidence=fc_h[b, :T].copy(), edge_diff=ed_h[b, :T].copy())
+            r = utterance_result(rec, ph_seq, ws, pw, self.frame_length)
             if keep_frame_probs:
                 r["edge_prob"] = ep_h[b, :T].copy()
                 r["ph_frame_pred"] = fp_h[b, :T].copy()

@@ -8,15 +8,12 @@ audio) and are aligned alone.
 """
 from __future__ import annotations
 
-import math
 
 
 def resampled_length(n: int, orig: int, new: int) -> int:
-    """torchaudio Resample output length: ceil(new * n / orig) over the gcd-reduced rates."""
-    if orig == new:
-        return int(n)
-    g = math.gcd(int(orig), int(new))
-    return -(-(int(new) // g) * int(n) // (int(orig) // g))
+    """torchaudio Resample output length (hubertfa_amd.resample.target_length: a float32 ceil)."""
+    from .resample import target_length
+    return target_length(n, orig, new)
 
 
 def encoder_length(n: int, file_sr: int, sr: int = 44100, enc_sr: int = 16000) -> int:

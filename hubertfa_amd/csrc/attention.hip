@@ -515,7 +515,7 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
 }  // namespace
 
 namespace {
-int g_attn_waves = 0;   // hfa_attention_split_tuning override (0: automatic)
+thread_local int g_attn_waves = 0;   // hfa_attention_split_tuning override (0: automatic)
 // Waves (x 32 queries) per workgroup of the split attention: 8 where that still leaves >= 2 workgroups per
 // (batch, head) row of queries, else 4.
 inline int split_attn_waves(int L) {

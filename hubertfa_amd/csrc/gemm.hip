@@ -245,9 +245,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 4 : 2) void gemm_f32
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-#ifndef HFA_ABL_NOGLOBAL
         if (kt + 1 < nk) load_regs((kt + 1) * BK);
-#endif
         const f32x4* sA4 = reinterpret_cast<const f32x4*>(sA[cur]);
         const f32x4* sB4 = reinterpret_cast<const f32x4*>(sB[cur]);
 #pragma unroll
@@ -263,22 +261,10 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 4 : 2) void gemm_f32
                 for (int i = 0; i < TI; ++i)
 #pragma unroll
                     for (int j = 0; j < TJ; ++j)
-#ifdef HFA_GEMM_SETPRIO
-                        {
-                            if (e == 0 && i == 0 && j == 0) __builtin_amdgcn_s_setprio(1);
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
-                            if (e == 3 && i == TI - 1 && j == TJ - 1) __builtin_amdgcn_s_setprio(0);
-                        }
-#else
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
-#endif
         }
-#ifndef HFA_ABL_NOLDSWRITE
         if (kt + 1 < nk) store_lds(cur ^ 1);
-#endif
-#ifndef HFA_ABL_NOBARRIER
         __syncthreads();
-#endif
     }
 
     store_tile<EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane);
@@ -700,33 +686,18 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
 #pragma unroll
     for (int d = 0; d < DA; ++d) {
         const int row = (wave + d * NW) * RPP + lane / CPR;
-#ifdef HFA_SABL_SAMETILE
-        int m = row;                                      // ablation: every tile loads tile (0, 0)
-#else
         int m = tm * BM + row;
-#endif
         m = m < p.M ? m : p.M - 1;
         a_t0[d] = m * p.stride - p.pad;
         a_c[d] = ((lane % CPR) ^ swz(row)) * 8;             // GT: the chunk's channel within its current tap
-#ifdef HFA_SABL_WIDEROW     // timing ablation: each DMA covers 8 rows x 128 B (the access pattern of 128-B rows)
-        a_t0[d] = (m - (lane >> 2) + (lane >> 3)) * p.stride - p.pad;
-        a_c[d] = (lane & 7) * 8;
-#endif
         a_tap[d] = 0;
     }
 #pragma unroll
     for (int d = 0; d < DB; ++d) {
         const int row = (wave + d * NW) * RPP + lane / CPR;
-#ifdef HFA_SABL_SAMETILE
-        int n = row;
-#else
         int n = tn * BN + row;
-#endif
         n = n < p.N ? n : p.N - 1;
         voffW[d] = (unsigned)((n * p.ldw + ((lane % CPR) ^ swz(row)) * 8) * 2);
-#ifdef HFA_SABL_WIDEROW
-        voffW[d] = (unsigned)(((n - (lane >> 2) + (lane >> 3)) * p.ldw + (lane & 7) * 8) * 2);
-#endif
     }
     auto set_tap = [&](int j) {
 #pragma unroll
@@ -822,22 +793,10 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     for (int kt = 0; kt < nk; ++kt) {
         const bool more = kt + NS - 1 < nk;
         const int nstage = stage == 0 ? NS - 1 : stage - 1;
-#ifndef HFA_SABL_NODMA
-#ifdef HFA_SPLIT_SPREAD
-        if (more) issueA(nstage);          // W half after the first MFMA sub-step: spreads the LDS-DMA writes
-#else
         if (more) issue(nstage);
-#endif
-#endif
         const f16x8* st = s8 + stage * (STAGE / 8);
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk) {
-#if defined(HFA_SPLIT_SPREAD) && !defined(HFA_SABL_NODMA)
-            if (kk == KK - 1 && more) {
-                issueW(nstage);
-                advance();
-            }
-#endif
             f16x8 a1[TI], a2[TI], w1[TJ], w2[TJ];
 #pragma unroll
             for (int i = 0; i < TI; ++i) {
@@ -853,36 +812,22 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
                 f16x8 w1s[TJ];
 #pragma unroll
                 for (int j = 0; j < TJ; ++j) w1s[j] = w1[j] * (_Float16)2048.0f;
-#ifdef HFA_SPLIT_PRIO
-                __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
                 for (int i = 0; i < TI; ++i)
 #pragma unroll
                     for (int j = 0; j < TJ; ++j) {
                         accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w1s[j], accM[i][j], 0, 0, 0);
-#if !defined(HFA_SABL_PRODUCTS) || HFA_SABL_PRODUCTS >= 2
                         accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w2[j], accM[i][j], 0, 0, 0);
-#endif
-#if !defined(HFA_SABL_PRODUCTS) || HFA_SABL_PRODUCTS >= 3
                         accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accM[i][j], 0, 0, 0);
-#endif
                     }
-#ifdef HFA_SPLIT_PRIO
-                __builtin_amdgcn_s_setprio(0);
-#endif
             } else {
 #pragma unroll
                 for (int i = 0; i < TI; ++i)
 #pragma unroll
                     for (int j = 0; j < TJ; ++j) {
                         accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w1[j], accM[i][j], 0, 0, 0);
-#if !defined(HFA_SABL_PRODUCTS) || HFA_SABL_PRODUCTS >= 2   // timing-only ablation builds (scripts/gpu_split_abl.sh)
                         accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w2[j], accC[i][j], 0, 0, 0);
-#endif
-#if !defined(HFA_SABL_PRODUCTS) || HFA_SABL_PRODUCTS >= 3
                         accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accC[i][j], 0, 0, 0);
-#endif
                     }
             }
         }
@@ -950,7 +895,7 @@ enum { CFG_AUTO = 0, CFG_128x128 = 1, CFG_128x64 = 2, CFG_256x128 = 3, CFG_128x2
        CFG_128x256_W4 = 6, CFG_256x256 = 7, CFG_128x48 = 8, CFG_128x96 = 9, CFG_COUNT = 10 };
 // Pipelines: register-staged BK 16 / 32, LDS-DMA with 2 or 3 stages.
 enum { PIPE_AUTO = 0, PIPE_REG16 = 16, PIPE_REG32 = 32, PIPE_DMA2 = 102, PIPE_DMA3 = 103 };
-int g_force_pipe = 0, g_force_cfg = 0;   // tuning overrides (hfa_gemm_tuning), 0 = automatic
+thread_local int g_force_pipe = 0, g_force_cfg = 0;   // tuning overrides (hfa_gemm_tuning), 0 = automatic
 
 // workgroups per CU a DMA instantiation is register-capped for: 128x128 3-stage (48 KiB LDS) -> 3, 2-stage and
 // 128x64 -> 4 (a 5th 2-stage workgroup measured no faster), 8-wave 128x256 -> 2 (64 accumulators per lane)
@@ -1332,7 +1277,7 @@ constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {256, 256, 2, 4, 3, 1, true, 16},  {128, 128, 2, 2, 4, 2, true, 16},  {256, 64, 4, 1, 2, 2, true, 32},
     {128, 48, 4, 1, 2, 2, true, 32},       // SCFG_N48: gemm_split48_kernel (16x16x32 MFMA), not gemm_split_kernel
     {256, 48, 8, 1, 3, 1, true, 32}};      // SCFG_WIN: posconv_split_kernel (LDS-resident input window)
-int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
+thread_local int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 thread_local int g_win_nb = 3;   // column blocks of the window kernel the name query reports (N / 16)
 
 // Measured on the workload's shapes (scripts/split_gemm_bench.py, profiles/r01/split_gemm_cfgs.txt): the 256 x 256

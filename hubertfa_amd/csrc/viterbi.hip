@@ -372,7 +372,7 @@ __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
     }
 }
 
-int g_force_k = 0;   // hfa_viterbi_tuning: states per lane of the multi-wave DP (0 = automatic)
+thread_local int g_force_k = 0;   // hfa_viterbi_tuning: states per lane of the multi-wave DP (0 = automatic)
 
 template <int K, int NW, int G>
 int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const int32_t* pad,

@@ -15,7 +15,6 @@ a bshall checkpoint (``torch.load(path)["hubert"]``), or ``synth:<seed>`` for se
 from __future__ import annotations
 
 import json
-import math
 import os
 
 import numpy as np
@@ -24,7 +23,7 @@ import torch
 from . import ops, synth
 from .hubert import HubertEncoder
 from .hubert import dev_lengths
-from .resample import Resampler
+from .resample import Resampler, target_length
 
 
 def _load_tensors(path: str) -> dict:
@@ -117,11 +116,7 @@ class UnitsEncoder:
 
     def resampled_lengths(self, lengths, sample_rate: int):
         """Per-row sample counts after resampling to the encoder rate (torchaudio: ceil(new * n / orig))."""
-        if sample_rate == self.encoder_sample_rate:
-            return [int(n) for n in lengths]
-        g = math.gcd(int(sample_rate), int(self.encoder_sample_rate))
-        orig, new = int(sample_rate) // g, int(self.encoder_sample_rate) // g
-        return [-(-new * int(n) // orig) for n in lengths]
+        return [target_length(int(n), sample_rate, self.encoder_sample_rate) for n in lengths]
 
     @torch.no_grad()
     def units(self, audio: torch.Tensor, sample_rate: int, lengths=None) -> torch.Tensor:
@@ -154,7 +149,7 @@ class UnitsEncoder:
         windows run as ONE variable-length batch (every GEMM and attention launch covers all of them) and the
         core frames [kC, (k+1)C) of each are stitched back in order.  Attention then costs O(L (C + 2O)) instead of
         O(L^2); the price is context: each frame sees its window only, and conv0's GroupNorm statistics are per
-        window.  The reference has no chunking — the unchunked path stays the parity anchor."""
+        window (the wave normalisation keeps whole-utterance statistics).  The reference has no chunking — the unchunked path stays the parity anchor."""
         m = self.model
         hop, rf, pad = 320, 400, m.arch.wav_pad
         x = audio.to(self.device).float().reshape(1, -1)
@@ -163,6 +158,8 @@ class UnitsEncoder:
         C, O = int(chunk_frames), int(overlap_frames)
         if L <= C + O:
             return m(x.contiguous())
+        if m.arch.do_normalize:          # whole-utterance statistics (Wav2Vec2FeatureExtractor), not per window
+            x = ops.wav_normalize(x.contiguous(), 1e-7)
         wins = plan_windows(L, C, O)
         n_win = [window_samples(a, b, hop, rf, pad) for _, _, a, b in wins]
         xs = x[0]
@@ -172,7 +169,7 @@ class UnitsEncoder:
             lo, hi = max(0, s0), min(N, s0 + n_win[i])
             if hi > lo:
                 batch[i, lo - s0:hi - s0] = xs[lo:hi]
-        units = m(batch, lengths=n_win)                   # [K, Wmax, C]
+        units = m(batch, lengths=n_win, normalized=True)  # [K, Wmax, C]
         idx = np.concatenate([i * units.shape[1] + np.arange(c0 - a, c1 - a) for i, (c0, c1, a, _) in
                               enumerate(wins)])
         flat = units.reshape(-1, units.shape[-1])
@@ -205,5 +202,9 @@ class UnitsEncoder:
         return feats, nfs
 
     def encode(self, audio, sample_rate, hop_size):
-        feats, n = self.encode_frames(audio, sample_rate, hop_size)
-        return feats[:, :n].transpose(1, 2)   # [B, C, T] like the reference
+        """[B, N] -> [B, C, T] like the reference; under the split-f16 range guard (a batch whose activations
+        leave f16 range is recomputed on the f32 GEMMs)."""
+        from .task import guarded
+        feats, n = guarded(self.model, ops.split_flag(self.device),
+                           lambda: self.encode_frames(audio, sample_rate, hop_size))
+        return feats[:, :n].transpose(1, 2)

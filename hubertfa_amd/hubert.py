@@ -299,10 +299,12 @@ class HubertEncoder:
         return ops.linear(f, L_.w2, L_.b2, residual=h), None
 
     @torch.no_grad()
-    def forward(self, wav: torch.Tensor, n_layers: int | None = None, lengths=None) -> torch.Tensor:
+    def forward(self, wav: torch.Tensor, n_layers: int | None = None, lengths=None,
+                normalized: bool = False) -> torch.Tensor:
         """wav [B, N] -> units [B, L, C].  ``lengths`` (optional, host ints [B]): samples per row of a
         variable-length batch (rows zero-padded to N); row b's units are valid for frame_lengths(lengths[b])
-        frames and equal what that utterance gives alone."""
+        frames and equal what that utterance gives alone.  ``normalized``: the caller already applied the
+        do_normalize wave statistics (long-form windows of one utterance)."""
         a = self.arch
         x = wav.float().contiguous()
         if x.dim() == 1:
@@ -316,7 +318,7 @@ class HubertEncoder:
             lens0 = dev_lengths([(int(n) + 2 * a.wav_pad - a.conv_kernel[0]) // a.conv_stride[0] + 1
                                  for n in lengths], x.device)
             lensL = dev_lengths([self.frame_lengths(int(n)) for n in lengths], x.device)
-        if a.do_normalize:
+        if a.do_normalize and not normalized:
             x = ops.wav_normalize(x, 1e-7, lens=ns)
         if a.wav_pad:
             x = ops.pad_rows(x, a.wav_pad, x.shape[1] + 2 * a.wav_pad)

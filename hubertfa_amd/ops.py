@@ -508,7 +508,6 @@ def add(a, b, out=None):
 
 def resample(x, orig, new, kernel, width, out=None, workspace=None):
     """Sinc resample rows of x [B, N] (gcd-reduced orig/new rates); returns [B, ceil(new*N/orig)] view."""
-    import math
     B, N = x.shape
     Kpad = kernel.shape[1]
     F = N // orig + 1
@@ -519,4 +518,5 @@ def resample(x, orig, new, kernel, width, out=None, workspace=None):
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
     _lib.call("hfa_resample_f32", B, N, _ptr(x), x.stride(0), orig, new, _ptr(kernel), Kpad, width,
               _ptr(workspace), _ptr(out), out.stride(0), _stream(x.device))
-    return out[:, : int(math.ceil(new * N / orig))]
+    from .resample import target_length
+    return out[:, : target_length(N, orig, new)]

@@ -2,7 +2,7 @@
 
 Replaces ``torchaudio.transforms.Resample`` at tools/load_wav.py:7 (sr -> 44100, lowpass_filter_width 6) and
 tools/encoder.py:46-48 (44100 -> 16000, lowpass_filter_width 128).  Taps follow torchaudio's published
-``sinc_interp_hann`` construction (rolloff 0.99, computed in float64, cast to float32) and are zero-padded to a
+``sinc_interp_hann`` construction (rolloff 0.99, dtype flow of ``dtype=None``, cast to float32) and are zero-padded to a
 multiple of 16 so the MFMA implicit GEMM consumes them directly.  torchaudio is absent from this environment,
 so its parity is unpinned (see oracle/resample.py).
 """
@@ -16,20 +16,37 @@ import torch
 from . import ops
 
 
+def target_length(n: int, orig_freq: int, new_freq: int) -> int:
+    """Output samples of torchaudio's ``_apply_sinc_resample_kernel`` for an n-sample row:
+    ``ceil(torch.as_tensor(new * n / orig))`` over the gcd-reduced rates.  The quotient is a Python float that
+    ``as_tensor`` stores as float32 (the default dtype) before the ceil, so a quotient just above an integer can
+    round down onto it (e.g. 44100 -> 16000 at n = 441 k + 3): the exact-integer ceil would be one sample more."""
+    if int(orig_freq) == int(new_freq):
+        return int(n)
+    g = math.gcd(int(orig_freq), int(new_freq))
+    orig, new = int(orig_freq) // g, int(new_freq) // g
+    return int(np.ceil(np.float32(new * int(n) / orig)))
+
+
 def sinc_taps(orig_freq: int, new_freq: int, lowpass_filter_width: int, rolloff: float = 0.99):
+    """Tap table [new, 2*width + orig] f32 following torchaudio's ``_get_sinc_resample_kernel`` with
+    ``dtype=None`` (what ``transforms.Resample`` passes), operation for operation on torch CPU: positions in
+    float64, the output-phase term ``arange(0, -new, -1) / new`` in float32 (int64 / int -> the default dtype)
+    promoted to float64 by the add, ``kernels *= window * scale``, then the cast to float32."""
     g = math.gcd(int(orig_freq), int(new_freq))
     orig, new = int(orig_freq) // g, int(new_freq) // g
     base = min(orig, new) * rolloff
     width = math.ceil(lowpass_filter_width * orig / base)
-    pos = np.arange(-width, width + orig, dtype=np.float64) / orig          # tap positions (input grid)
-    phase = -np.arange(new, dtype=np.float64)[:, None] / new                 # output phase offsets
-    t = np.clip((phase + pos[None, :]) * base, -lowpass_filter_width, lowpass_filter_width)
-    window = np.cos(t * math.pi / lowpass_filter_width / 2) ** 2
-    arg = t * math.pi
-    with np.errstate(invalid="ignore", divide="ignore"):
-        sinc = np.where(arg == 0, 1.0, np.sin(arg) / arg)
-    taps = (sinc * window * (base / orig)).astype(np.float32)               # [new, 2*width + orig]
-    return taps, width, orig, new
+    with torch.no_grad():
+        pos = torch.arange(-width, width + orig, dtype=torch.float64)[None, :] / orig
+        phase = torch.arange(0, -new, -1)[:, None] / new                    # float32
+        t = (phase + pos) * base
+        t = t.clamp(-lowpass_filter_width, lowpass_filter_width)
+        window = torch.cos(t * math.pi / lowpass_filter_width / 2) ** 2
+        t = t * math.pi
+        sinc = torch.where(t == 0, torch.tensor(1.0, dtype=torch.float64), t.sin() / t)
+        taps = (sinc * (window * (base / orig))).to(torch.float32)
+    return taps.numpy(), width, orig, new
 
 
 class Resampler:

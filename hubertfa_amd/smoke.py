@@ -53,6 +53,6 @@ def run_smoke(seconds: float = 2.0, B: int = 2) -> dict:
         assert list(ref[0]) == list(res[b]["ph_seq"]), "phone sequence differs from the oracle"
         n_match += int(np.array_equal(ref[5]["tint"], res[b]["ph_time_int"]))
         np.testing.assert_allclose(res[b]["ph_intervals"], ref[1], atol=2 * 512 / 44100)
-    assert n_match >= B - 1, f"boundary indices matched the oracle on only {n_match}/{B} utterances"
+    assert n_match == B, f"boundary indices matched the oracle on only {n_match}/{B} utterances"
     print(f"smoke OK: {B} x {seconds:g} s, boundary-exact utterances {n_match}/{B}")
     return {"utterances": B, "boundary_exact": n_match}

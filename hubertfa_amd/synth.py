@@ -59,7 +59,7 @@ class HubertArch:
         return n
 
 
-def arch_cnhubert_base(layers: int = 12, do_normalize: bool = False) -> HubertArch:
+def arch_cnhubert_base(layers: int = 12, do_normalize: bool = True) -> HubertArch:
     return HubertArch(layout="hf", layers=layers, do_normalize=do_normalize)
 
 

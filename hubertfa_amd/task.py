@@ -10,7 +10,6 @@ UNet+head, lattice prologue, DP, backtrack), the path the benchmark and the batc
 """
 from __future__ import annotations
 
-import math
 
 import numpy as np
 import torch
@@ -19,10 +18,29 @@ import yaml
 from . import ops, synth
 from .alignment_decoder import AlignmentDecoder
 from .encoder import UnitsEncoder
-from .resample import Resampler
+from .resample import Resampler, target_length
 from .hubert import dev_lengths
 from .unet import LatticeHead
 from .wav_io import load_wav
+
+
+def guarded(module, flag, fn):
+    """Run ``fn`` (one pass of ``module``'s kernels) under the split-f16 range guard, synchronously: clear
+    ``flag``, run, and if a split producer raised it, clear it and run ``fn`` again with ``module.precision`` =
+    "f32".  Used by the reference-surface entries that return tensors (forward, UnitsEncoder.encode); the
+    pipelined path snapshots the flags on the device instead (ForcedAlignmentTask._guard)."""
+    if getattr(module, "precision", "f32") != "split" or flag is None:
+        return fn()
+    flag.zero_()
+    out = fn()
+    if int(flag.item()):
+        flag.zero_()
+        module.precision = "f32"
+        try:
+            out = fn()
+        finally:
+            module.precision = "split"
+    return out
 
 
 class ForcedAlignmentTask:
@@ -69,13 +87,17 @@ class ForcedAlignmentTask:
 
     @torch.no_grad()
     def forward(self, x):
-        """x [B, T, C] -> (ph_frame_logits [B,T,V], ph_edge_logits [B,T], ctc_logits [B,T,V])."""
+        """x [B, T, C] -> (ph_frame_logits [B,T,V], ph_edge_logits [B,T], ctc_logits [B,T,V]).
+
+        Range guard as on the batched path: if a split-f16 operand of the head left f16 range, the logits are
+        recomputed on the f32 GEMMs (this entry returns tensors, so it checks the head's flag synchronously)."""
         x = x.to(self.device).float()
         T = x.shape[1]
         Tp = self.head.padded_len(T)
         if Tp != T:
             x = torch.nn.functional.pad(x, (0, 0, 0, Tp - T))
-        logits = self.head.logits(x.contiguous())[:, :T]
+        x = x.contiguous()
+        logits = guarded(self.head, self.head.flag, lambda: self.head.logits(x))[:, :T]
         return LatticeHead.split(logits)
 
     __call__ = forward
@@ -115,8 +137,7 @@ class ForcedAlignmentTask:
             up = self.upsampler(wav_sr)
             waves = up(waves)
             if lengths is not None:
-                g = math.gcd(int(wav_sr), int(sr))
-                lengths = [-(-(sr // g) * int(n) // (int(wav_sr) // g)) for n in lengths]
+                lengths = [target_length(int(n), wav_sr, sr) for n in lengths]
                 waves = waves.contiguous()
                 ops.mask_rows(waves, dev_lengths(lengths, waves.device))   # sinc tails past each row's end
         n = waves.shape[-1]
@@ -185,6 +206,8 @@ class ForcedAlignmentTask:
         """Host waves (numpy or CPU tensor [B, N]; pinned f32 avoids a staging copy) -> f32 device tensor: a pinned
         non-blocking H2D on the caller's current stream (no host sync).  A dedicated copy stream, which would let
         the copy run under the previous batch's encoder, measured slower on MI355X."""
+        if isinstance(waves, torch.Tensor) and waves.is_cuda:
+            return waves.to(self.device, torch.float32)
         x = torch.as_tensor(waves, dtype=torch.float32)
         pinned = x if x.is_pinned() else x.contiguous().pin_memory()
         return pinned.to(self.device, non_blocking=True)   # (the pinned block is held until this copy ends)

@@ -55,6 +55,37 @@ def read_wav(path) -> tuple[np.ndarray, int]:
     return x[: n * ch].reshape(n, ch).T.copy(), sr
 
 
+def wav_info(path) -> tuple[int, int, int]:
+    """-> (samples per channel, sample_rate, channels) from the RIFF headers only (the data chunk is skipped,
+    not read): the sharding cost estimate of a multi-GPU run needs every file's length before any is loaded."""
+    with open(path, "rb") as f:
+        head = f.read(12)
+        if head[:4] != b"RIFF" or head[8:12] != b"WAVE":
+            raise ValueError(f"{path}: not a RIFF/WAVE file")
+        fmt, n_bytes = None, None
+        while True:
+            hdr = f.read(8)
+            if len(hdr) < 8:
+                break
+            cid, size = hdr[:4], struct.unpack("<I", hdr[4:])[0]
+            if cid == b"fmt ":
+                body = f.read(size)
+                _, ch, sr, _, block, _ = struct.unpack("<HHIIHH", body[:16])
+                fmt = (ch, sr, block)
+                if size & 1:
+                    f.seek(1, 1)
+            else:
+                if cid == b"data":
+                    n_bytes = size
+                f.seek(size + (size & 1), 1)
+            if fmt is not None and n_bytes is not None:
+                break
+    if fmt is None or n_bytes is None:
+        raise ValueError(f"{path}: missing fmt or data chunk")
+    ch, sr, block = fmt
+    return n_bytes // max(block, 1), sr, ch
+
+
 def write_wav(path, x: np.ndarray, sr: int) -> None:
     """16-bit PCM mono writer (synthetic test/bench inputs)."""
     q = np.clip(np.round(np.asarray(x, np.float64) * 32768.0), -32768, 32767).astype("<i2")

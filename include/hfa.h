@@ -6,7 +6,8 @@
  *   - every pointer is a DEVICE pointer owned by the caller; the library never allocates persistent memory
  *     and never frees caller memory.
  *   - stream-ordered on `stream`, no implicit synchronisation, re-entrant across streams/threads, so every
- *     call can be captured into a hipGraph.
+ *     call can be captured into a hipGraph.  The *_tuning hooks (benchmark overrides) set state of the calling
+ *     thread only (thread-local), so they never change another thread's launches.
  *   - plain pointers and sizes only (no torch types); layouts are row-major with the strides named.
  *
  *   - variable-length batches: the optional `const int32_t*` length arrays ([B], device) give each row's own

@@ -5,50 +5,55 @@
 Same flags and defaults as the reference; extra flags: ``--hubert_path`` (override hubert_config.model_path, e.g.
 ``synth:0``), ``--batch_size`` (utterances per GPU batch: sorted by length, zero-padded, aligned with per-row
 lengths so every result equals the one-utterance run), ``--out_path``.
-Launched under ``torchrun --nproc-per-node N`` it shards the wav files across ranks by estimated cost (LPT);
-rank 0 gathers the per-utterance results and writes the TextGrids / confidence.csv.
+
+Multi-GPU (``torchrun --nproc-per-node N infer.py ...``): every rank reads the folder and runs the
+G2P, the files are sharded by an LPT on a cost estimate from each WAV header, each rank aligns its shard, and the
+per-utterance boundary arrays are gathered to rank 0 (distributed.gather_records: shape all_gather + padded
+all_gather_into_tensor over RCCL), which assembles intervals, post-processes and exports — byte-identical to a
+one-GPU run.  A rank whose shard fails reports it over a gloo control group; its shard is re-run on the healthy
+ranks.  A file that fails alone (a lattice beyond the DP kernel's limits, an unreadable WAV, ...) is recorded in
+the error log and skipped instead of aborting the run.
 """
 from __future__ import annotations
 
+import os
 import pathlib
 
 import click
 
 
-def _predict(task, dataset, batch_size: int):
+def _recoverable():
+    from hubertfa_amd._lib import HFALibraryError
+    return (HFALibraryError, ValueError, AssertionError, KeyError, IndexError)
+
+
+def _predict(task, rows, keys, batch_size: int, errors: list) -> dict:
+    """Align ``rows`` (wav_path, ph_seq, word_seq, ph_idx_to_word_idx); ``keys`` their dataset indices.
+
+    Returns {dataset index: raw boundary record} (alignment_decoder.utterance_result turns a record into the
+    reference's decode outputs).  A batch that raises a recoverable error is re-run file by file; a file that
+    fails alone goes to ``errors`` as [wav_path, exception] (the post-processing log)."""
     import torch
     from hubertfa_amd.batching import plan_batches, resampled_length
     from hubertfa_amd.wav_io import read_wav
 
+    if os.environ.get("HFA_FAULT_INJECT_RANK") == os.environ.get("RANK", "0"):
+        raise RuntimeError("fault injected (HFA_FAULT_INJECT_RANK): this rank's shard fails")
+    recoverable = _recoverable()
     task.on_predict_start()
     sr = task.melspec_config["sample_rate"]
-    items = []
-    for wav_path, ph_seq, word_seq, p2w in dataset:
-        x, file_sr = read_wav(wav_path)
-        items.append((wav_path, x[0], file_sr, ph_seq, word_seq, p2w))
-    # variable-length batches (hubertfa_amd.batching.plan_batches): per sample rate, sorted by length, rows
-    # zero-padded and aligned with per-row lengths, which keeps every utterance's result identical to aligning it
-    # alone (the reference's B=1); files too short for the encoder's 400-sample window are aligned alone
+    items = {}
+    for key, (wav_path, ph_seq, word_seq, p2w) in zip(keys, rows):
+        try:
+            x, file_sr = read_wav(wav_path)
+        except (OSError, ValueError) as e:
+            errors.append([wav_path, e])
+            continue
+        items[key] = (wav_path, x[0], file_sr, ph_seq, word_seq, p2w)
     out = {}
-    by_key = {i: it for i, it in enumerate(items)}
 
-    def finish(job):
-        handle, chunk, n44s = job
-        res = task.decoder.assemble(handle, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk])
-        for c, r, n44 in zip(chunk, res, n44s):
-            out[str(c[0])] = (c[0], n44 / sr, r["confidence"], r["ph_seq"], r["ph_intervals"], r["word_seq"],
-                              r["word_intervals"])
-
-    def batches():
-        plan = plan_batches([(i, len(it[1]), it[2]) for i, it in by_key.items()], batch_size, sr,
-                            task.unitsEncoder.encoder_sample_rate)
-        for file_sr, keys in plan:
-            yield file_sr, [by_key[k] for k in keys]
-
-    # one batch in flight: the host assembles batch i while the GPU runs batch i+1 (task.submit: encoder on the
-    # main stream, head + Viterbi on a side stream)
-    pending = None
-    for file_sr, chunk in batches():
+    def submit(chunk, file_sr):
+        """-> (fetch handle, per-file sample counts at the melspec rate)."""
         lens = [len(c[1]) for c in chunk]
         wav_h = torch.zeros((len(chunk), max(lens)), dtype=torch.float32, pin_memory=True)
         wav_np = wav_h.numpy()           # rows written straight into pinned memory
@@ -57,13 +62,75 @@ def _predict(task, dataset, batch_size: int):
         wav = task.upload(wav_h)         # pinned non-blocking H2D: no host sync
         handle = task.submit(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
                              wav_sr=file_sr, lengths=lens if len(chunk) > 1 else None)
-        n44s = [resampled_length(n, file_sr, sr) for n in lens]
+        return handle, [resampled_length(n, file_sr, sr) for n in lens]
+
+    def finish(job):
+        handle, ks, n44s = job[:3]
+        chunk = [items[k] for k in ks]
+        res = task.decoder.assemble(handle, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk])
+        for k, r, n44 in zip(ks, res, n44s):
+            out[k] = dict(n44=n44, T=r["T"], ph_idx_seq=r["ph_idx_seq"], ph_time_int=r["ph_time_int"],
+                          frame_confidence=r["frame_confidence"], edge_diff=r["edge_diff"])
+
+    def run(ks, file_sr):
+        handle, n44s = submit([items[k] for k in ks], file_sr)
+        return handle, ks, n44s, file_sr
+
+    def alone(k, file_sr):
+        try:
+            finish(run([k], file_sr))
+        except recoverable as e:
+            errors.append([items[k][0], e])
+
+    def settle(job):
+        """Complete a batch; a recoverable failure re-runs its files one by one."""
+        try:
+            finish(job)
+        except recoverable as e:
+            if len(job[1]) == 1:
+                errors.append([items[job[1][0]][0], e])
+            else:
+                for k in job[1]:
+                    alone(k, job[3])
+
+    # variable-length batches (hubertfa_amd.batching.plan_batches): per sample rate, sorted by length, rows
+    # zero-padded and aligned with per-row lengths, which keeps every utterance's result identical to aligning it
+    # alone (the reference's B=1); files too short for the encoder's 400-sample window are aligned alone.
+    # One batch in flight: the host assembles batch i while the GPU runs batch i+1 (task.submit: encoder on the
+    # main stream, head + Viterbi on a side stream).
+    plan = plan_batches([(k, len(it[1]), it[2]) for k, it in items.items()], batch_size, sr,
+                        task.unitsEncoder.encoder_sample_rate)
+    pending = None
+    for file_sr, ks in plan:
+        job, err = None, None
+        try:
+            job = run(ks, file_sr)
+        except recoverable as e:
+            err = e
         if pending is not None:
-            finish(pending)
-        pending = (handle, chunk, n44s)
+            settle(pending)
+            pending = None
+        if job is not None:
+            pending = job
+        elif len(ks) == 1:
+            errors.append([items[ks[0]][0], err])
+        else:
+            for k in ks:
+                alone(k, file_sr)
     if pending is not None:
-        finish(pending)
-    return [out[str(it[0])] for it in items if str(it[0]) in out]
+        settle(pending)
+    return out
+
+
+def _run(task, rows, keys, batch_size, errors):
+    """_predict with the rank-level outcome: (records, ok)."""
+    try:
+        return _predict(task, rows, keys, batch_size, errors), True
+    except Exception as e:  # noqa: BLE001 — reported to the control plane; the shard is re-queued elsewhere
+        import traceback
+        traceback.print_exc()
+        print(f"[rank {os.environ.get('RANK', '0')}] shard failed: {e!r}", flush=True)
+        return {}, False
 
 
 @click.command()
@@ -76,43 +143,88 @@ def _predict(task, dataset, batch_size: int):
 @click.option("--hubert_path", default=None, type=str, help="override hubert_config.model_path")
 @click.option("--batch_size", default=32, type=int, help="max utterances per GPU batch (variable lengths; results equal B=1)")
 @click.option("--out_path", default=None, type=str, help="write TextGrids under this folder instead")
-def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, **kwargs):
-    import os
+@click.option("--dist_backend", default="nccl", type=str, help="multi-GPU data backend: nccl (= RCCL); gloo for rehearsals")
+@click.option("--device", default=None, type=int, help="force every rank onto this GPU (multi-rank rehearsal on one GPU)")
+def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, dist_backend, device, **kwargs):
     import torch
     import hubertfa_amd.g2p as g2p_mod
-    from hubertfa_amd.distributed import env_rank_world, shard_lpt, utterance_cost
+    from hubertfa_amd.alignment_decoder import utterance_result
+    from hubertfa_amd.distributed import env_rank_world, gather_records, shard_lpt, utterance_cost
     from hubertfa_amd.export_tool import Exporter
     from hubertfa_amd.post_processing import post_processing
     from hubertfa_amd.task import ForcedAlignmentTask
+    from hubertfa_amd.wav_io import wav_info
 
     if not g2p.endswith("G2P"):
         g2p += "G2P"
     grapheme_to_phoneme = getattr(g2p_mod, g2p)(**kwargs)
     grapheme_to_phoneme.set_in_format("lab")
-    dataset = grapheme_to_phoneme.get_dataset(sorted(pathlib.Path(folder).rglob("*.wav")))
+    rows = list(grapheme_to_phoneme.get_dataset(sorted(pathlib.Path(folder).rglob("*.wav"))))
 
     rank, world, local = env_rank_world()
+    local = local if device is None else device
     torch.cuda.set_device(local)
-    rows = list(dataset)
+    dist, ctrl, mine, costs, shards = None, None, list(range(len(rows))), None, None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        costs = [utterance_cost(os.path.getsize(r[0]) // 2, len(r[1])) for r in rows]
-        rows = [rows[i] for i in shard_lpt(costs, world)[rank]]
+        if dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(dist_backend)
+        ctrl = dist.new_group(backend="gloo")            # control plane: host memory, survives a lost GPU
+        costs = []
+        for r in rows:
+            try:
+                n, file_sr, _ = wav_info(r[0])
+            except (OSError, ValueError):
+                n, file_sr = 0, 44100
+            costs.append(utterance_cost(n, len(r[1]), file_sr))
+        shards = shard_lpt(costs, world)
+        mine = shards[rank]
 
     torch.set_grad_enabled(False)
     model = ForcedAlignmentTask.load_from_checkpoint(ckpt, device=torch.device("cuda", local),
                                                      hubert_model_path=hubert_path)
-    predictions = _predict(model, rows, batch_size)
+    errors = []
+    records, ok = _run(model, [rows[i] for i in mine], mine, batch_size, errors)
+    if world == 1 and not ok:
+        raise SystemExit(1)
     if world > 1:
-        gathered = [None] * world
-        dist.all_gather_object(gathered, predictions)
-        predictions = [p for part in gathered for p in part]
+        status = [None] * world
+        dist.all_gather_object(status, ok, group=ctrl)
+        failed = [r for r in range(world) if not status[r]]
+        if failed:
+            healthy = [r for r in range(world) if status[r]]
+            if not healthy:
+                raise SystemExit("every rank failed its shard")
+            todo = sorted(i for r in failed for i in shards[r])
+            parts = shard_lpt([costs[i] for i in todo], len(healthy))
+            if rank in healthy:
+                again = [todo[j] for j in parts[healthy.index(rank)]]
+                print(f"[rank {rank}] re-running {len(again)} file(s) of failed rank(s) {failed}", flush=True)
+                more, ok2 = _run(model, [rows[i] for i in again], again, batch_size, errors)
+                if not ok2:
+                    raise SystemExit(f"rank {rank} failed re-running a re-queued shard")
+                records.update(more)
+        # boundary arrays to every rank: RCCL when every GPU is healthy, else the gloo control group
+        records = gather_records(records, group=None if not failed and dist_backend == "nccl" else ctrl)
+        all_errors = [None] * world
+        dist.all_gather_object(all_errors, [[str(p), repr(e)] for p, e in errors], group=ctrl)
+        errors = [e for part in all_errors for e in part]
         if rank != 0:
             dist.destroy_process_group()
             return
+
+    sr = model.melspec_config["sample_rate"]
+    predictions = []
+    for i, (wav_path, ph_seq, word_seq, p2w) in enumerate(rows):
+        if i in records:
+            rec = records[i]
+            r = utterance_result(rec, ph_seq, word_seq, p2w, model.decoder.frame_length)
+            predictions.append((wav_path, rec["n44"] / sr, r["confidence"], r["ph_seq"], r["ph_intervals"],
+                                r["word_seq"], r["word_intervals"]))
     predictions, log = post_processing(predictions)
-    exporter = Exporter(predictions, log, out_path)
+    exporter = Exporter(predictions, errors + log, out_path)
     out_formats = ["textgrid"] + (["confidence"] if save_confidence else [])
     exporter.export(out_formats)
     print("Output files are saved to the same folder as the input wav files.")

@@ -71,9 +71,105 @@ def test_pipelined_predict_repeatable(tmp_path):
     torch.set_grad_enabled(False)
     task = ForcedAlignmentTask.load_from_checkpoint(str(ck), device=torch.device("cuda"), hubert_model_path="synth:0")
 
-    def key(preds):
-        return {str(p[0]): (np.asarray(p[4]).tobytes(), np.asarray(p[2]).tobytes()) for p in preds}
-    ref = key(infer._predict(task, rows, 32))
+    def key(records):
+        return {k: (np.asarray(r["ph_time_int"]).tobytes(), np.asarray(r["frame_confidence"]).tobytes(),
+                    np.asarray(r["edge_diff"]).tobytes()) for k, r in records.items()}
+    keys = list(range(len(rows)))
+    ref = key(infer._predict(task, rows, keys, 32, []))
+    assert len(ref) == len(rows)
     for rep in range(8):
-        got = key(infer._predict(task, rows, 1))
+        got = key(infer._predict(task, rows, keys, 1, []))
         assert got == ref, f"rep {rep}: {[n for n in got if got[n] != ref[n]]} differ"
+
+
+def _mixed_folder(tmp_path):
+    """Mixed lengths and two sample rates (16 kHz / 22.05 kHz) -> (segments dir, dictionary, checkpoint)."""
+    from hubertfa_amd import synth
+    from hubertfa_amd.task import synth_checkpoint
+    from hubertfa_amd.wav_io import write_wav
+    d = synth.synth_dictionary(n_words=40)
+    dpath = tmp_path / "dict.txt"
+    dpath.write_text("".join(f"{w}\t{' '.join(p)}\n" for w, p in d.items()))
+    seg = tmp_path / "segments"
+    seg.mkdir()
+    files = ((2.0, 16000), (3.1, 16000), (1.2, 22050), (4.0, 16000), (2.6, 22050), (0.9, 16000), (5.3, 16000))
+    for i, (secs, sr) in enumerate(files):
+        write_wav(seg / f"m{i}.wav", synth.synth_audio(int(secs * sr), sr, seed=40 + i), sr)
+        (seg / f"m{i}.lab").write_text(synth.synth_lab(4 + i % 3, d, seed=40 + i))
+    ck = tmp_path / "m.ckpt"
+    synth_checkpoint(str(ck))
+    return seg, dpath, ck, len(files)
+
+
+def _torchrun(args, env_extra=None, nproc=2, timeout=420):
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, **(env_extra or {}))
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(repo, "infer.py"), *args]
+    return subprocess.run(cmd, env=env, cwd=repo, capture_output=True, text=True, timeout=timeout)
+
+
+def test_infer_two_ranks_match_one_rank(tmp_path):
+    """torchrun with 2 ranks (both on GPU 0, gloo data backend): LPT shards of mixed-length, mixed-rate files, the
+    boundary-array gather to rank 0, and rank 0's TextGrids byte-identical to the one-rank run; then the same
+    with rank 1's shard failing (fault injection): rank 0 re-runs it and the output is still identical."""
+    from click.testing import CliRunner
+    import infer
+    seg, dpath, ck, n = _mixed_folder(tmp_path)
+    base = ["-c", str(ck), "-f", str(seg), "-d", str(dpath), "--hubert_path", "synth:0", "--batch_size", "3"]
+    out1 = tmp_path / "one"
+    r = CliRunner().invoke(infer.main, base + ["--out_path", str(out1)])
+    assert r.exit_code == 0, r.output + repr(r.exception)
+    one = {p.name: p.read_bytes() for p in out1.rglob("*.TextGrid")}
+    assert len(one) == n
+    for tag, extra in (("two", None), ("requeue", {"HFA_FAULT_INJECT_RANK": "1"})):
+        out = tmp_path / tag
+        p = _torchrun(base + ["--out_path", str(out), "--dist_backend", "gloo", "--device", "0"], extra)
+        assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+        got = {q.name: q.read_bytes() for q in out.rglob("*.TextGrid")}
+        assert got == one, f"{tag}: {[k for k in one if got.get(k) != one[k]]} differ from the one-rank run"
+        if extra:
+            assert "re-running" in p.stdout and "shard failed" in p.stdout
+
+
+def test_predict_isolates_failing_file(tmp_path):
+    """A batch that raises a recoverable error is re-run file by file; the file that fails alone is logged and
+    skipped, every other file gets exactly its normal result."""
+    import infer
+    import hubertfa_amd.g2p as g2p_mod
+    import torch
+    from hubertfa_amd._lib import HFALibraryError
+    from hubertfa_amd.task import ForcedAlignmentTask
+    seg, dpath, ck, n = _mixed_folder(tmp_path)
+    g = g2p_mod.DictionaryG2P(dictionary=str(dpath))
+    g.set_in_format("lab")
+    rows = list(g.get_dataset(sorted(seg.rglob("*.wav"))))
+    torch.set_grad_enabled(False)
+    task = ForcedAlignmentTask.load_from_checkpoint(str(ck), device=torch.device("cuda"), hubert_model_path="synth:0")
+    keys = list(range(len(rows)))
+    ref = infer._predict(task, rows, keys, 4, [])
+    assert sorted(ref) == keys
+    poison = int(round(3.1 * 16000))                  # m1.wav's sample count
+    submit = task.submit
+
+    def bad_submit(waves, *a, lengths=None, **kw):
+        lens = lengths if lengths is not None else [waves.shape[-1]] * waves.shape[0]
+        if poison in lens:
+            raise HFALibraryError("injected: lattice beyond the kernel's limits")
+        return submit(waves, *a, lengths=lengths, **kw)
+    task.submit = bad_submit
+    errors = []
+    got = infer._predict(task, rows, keys, 4, errors)
+    task.submit = submit
+    assert len(errors) == 1 and str(errors[0][0]).endswith("m1.wav")
+    assert sorted(got) == [k for k in keys if not str(rows[k][0]).endswith("m1.wav")]
+    for k in got:
+        for f in ("ph_time_int", "ph_idx_seq", "frame_confidence", "edge_diff"):
+            assert np.array_equal(got[k][f], ref[k][f]), (k, f)

@@ -109,24 +109,43 @@ def test_lpt_sharding_balances():
     assert max(loads) - min(loads) <= 2
 
 
+def _records(rank):
+    """Rank-local raw boundary records of different counts and lengths (rank 1 holds none of rank 0's sizes)."""
+    rng = np.random.default_rng(rank)
+    recs = {}
+    for j in range(3 + 2 * rank):                      # 3 utterances on rank 0, 5 on rank 1
+        T = int(rng.integers(5, 40)) + 17 * rank
+        n = int(rng.integers(1, T))
+        recs[10 * j + rank] = dict(n44=512 * T + j, T=T, ph_idx_seq=np.sort(rng.integers(0, 50, n)),
+                                   ph_time_int=np.sort(rng.choice(T, n, replace=False)),
+                                   frame_confidence=rng.random(T).astype(np.float32),
+                                   edge_diff=rng.standard_normal(T).astype(np.float32))
+    return recs
+
+
 def _gloo_worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
-    from hubertfa_amd.distributed import gather_boundaries
+    from hubertfa_amd.distributed import gather_boundaries, gather_records
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    B, T = 3, 7
+    B, T = 3 + rank, 7 + 4 * rank                         # unequal local batch shapes
     dev_out = {"ph_idx_seq": torch.full((B, T), rank, dtype=torch.int32),
                "ph_time_int": torch.arange(B * T, dtype=torch.int32).view(B, T) + 100 * rank,
                "n": torch.full((B,), rank + 1, dtype=torch.int32),
                "frame_confidence": torch.full((B, T), float(rank))}
     g = gather_boundaries(dev_out)
+    recs = gather_records(_records(rank))
     if rank == 0:
-        q.put({k: v.numpy().tolist() for k, v in g.items()})
+        q.put(({k: [v.numpy().tolist() for v in parts] for k, parts in g.items()},
+               {k: {f: np.asarray(v).tolist() for f, v in r.items()} for k, r in recs.items()}))
     dist.destroy_process_group()
 
 
-def test_boundary_gather_world2_gloo():
+def test_boundary_gather_world2_gloo_unequal_shapes():
+    """all_gather of each rank's (B, Tmax), then a padded all_gather_into_tensor per array; ranks
+    hold different batch sizes and lengths, and rank 0 gets every rank's arrays back unpadded (and the CLI's
+    record tables survive the round trip bit for bit)."""
     import multiprocessing as mp
     import socket
     s = socket.socket()
@@ -138,13 +157,48 @@ def test_boundary_gather_world2_gloo():
     ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = q.get(timeout=120)
+    res, recs = q.get(timeout=120)
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert np.array(res["ph_idx_seq"]).shape == (6, 7)
-    assert np.array(res["n"]).tolist() == [1, 1, 1, 2, 2, 2]
-    assert np.array(res["ph_time_int"])[3, 0] == 100
+    assert np.array(res["ph_idx_seq"][0]).shape == (3, 7) and np.array(res["ph_idx_seq"][1]).shape == (4, 11)
+    assert res["n"][0] == [1, 1, 1] and res["n"][1] == [2, 2, 2, 2]
+    assert np.array(res["ph_time_int"][1])[0, 0] == 100 and np.array(res["ph_time_int"][1])[3, 10] == 143
+    want = {**_records(0), **_records(1)}
+    assert sorted(recs) == sorted(want)
+    for k, r in want.items():
+        for f, v in r.items():
+            assert np.array_equal(np.asarray(recs[k][f]), np.asarray(v)), (k, f)
+
+
+def test_record_table_pack_unpack_world1():
+    from hubertfa_amd.distributed import gather_records
+    want = _records(1)
+    got = gather_records(want)
+    for k, r in want.items():
+        for f, v in r.items():
+            assert np.array_equal(np.asarray(got[k][f]), np.asarray(v)), (k, f)
+    assert gather_records({}) == {}
+
+
+def test_wav_info_header_only(tmp_path):
+    from hubertfa_amd.wav_io import wav_info, write_wav
+    p = tmp_path / "a.wav"
+    write_wav(p, np.zeros(22051, np.float32), 22050)
+    assert wav_info(p) == (22051, 22050, 1)
+
+
+def test_torchaudio_target_length_float32_ceil():
+    """torchaudio's _apply_sinc_resample_kernel takes ceil(as_tensor(new * n / orig)): a float32 quotient, so just
+    above an integer it rounds down (e.g. 44.1 kHz -> 16 kHz at n = 722562: 262154.0045... -> 262154)."""
+    import torch
+    from hubertfa_amd.resample import target_length
+    for n, o, w in ((722562, 44100, 16000), (160000, 16000, 44100), (441000, 44100, 16000), (1, 16000, 44100),
+                    (12345, 48000, 44100), (999999, 22050, 44100)):
+        g = int(np.gcd(o, w))
+        ta = int(torch.ceil(torch.as_tensor((w // g) * n / (o // g))).long())
+        assert target_length(n, o, w) == ta
+    assert target_length(722562, 44100, 16000) == 262154 == -(-160 * 722562 // 441) - 1
 
 
 def test_resampled_and_encoder_lengths():

@@ -3,7 +3,7 @@ batch and stitched.  The reference has no chunking, so the unchunked path is the
   * a window that covers the utterance reproduces the unchunked units exactly;
   * every window yields exactly its frames, and the stitched grid IS the unchunked grid: with the context-free
     part of the encoder (LN-conv extractor, projection, positional conv of receptive field +-64 frames < the
-    100-frame overlap; no attention layers, no whole-utterance wave normalisation) the stitched units equal the
+    100-frame overlap; no attention layers; the wave normalisation uses whole-utterance statistics) the stitched units equal the
     unchunked units bit for bit;
   * with attention the windows see less context, so the alignment only approximates the unchunked one (the
     agreement is printed; with random weights it says little about trained models, so it is not asserted).
@@ -51,7 +51,7 @@ def test_chunked_stitching_exact_without_attention():
     task.on_predict_start()
     enc = task.unitsEncoder
     enc.model.layers = enc.model.layers[:0]          # context-free encoder: LN-conv, projection, pos-conv only
-    enc.model.arch.do_normalize = False              # (the wave normalisation is a whole-utterance statistic)
+    assert enc.model.arch.do_normalize               # whole-utterance wave statistics, applied before windowing
     x = torch.from_numpy(synth.synth_audio(16000 * 30, seed=6)[None]).cuda()
     full = enc.units(x, 16000)
     chunked = enc.units_chunked(x, chunk_frames=400, overlap_frames=100)     # 4 windows over 1499 frames

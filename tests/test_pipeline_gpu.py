@@ -67,4 +67,4 @@ def test_full_path_logprobs_and_boundaries_vs_oracle(precision):
 def test_smoke_entry():
     from hubertfa_amd.smoke import run_smoke
     r = run_smoke()
-    assert r["boundary_exact"] >= 1
+    assert r["boundary_exact"] == r["utterances"]
