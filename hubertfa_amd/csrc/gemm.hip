@@ -580,28 +580,65 @@ __global__ __launch_bounds__(256, 4) void gemm_dma_n48_kernel(const GemmP p) {
 // x 4 chunks), the same XOR-swizzled [row][64 B] image per plane, 4 planes per stage (A1, A2, W1, W2).  A lane's
 // ds_read_b128 brings 8 consecutive k of its row = one MFMA operand (lane l: row l&31, k 8(l>>5)..+7 of a 16-k
 // sub-step; the same mapping on both operands).
-template <int TI, int TJ>
-__device__ __forceinline__ void store_split_lds(const GemmP& p, const f32x16 (&acc)[TI][TJ], int EPI_, int zb, int zg,
-                                                int wrow0, int wcol0, int lane, float* slab) {
+template <int MF> struct AccT;
+template <> struct AccT<32> { typedef f32x16 type; };
+template <> struct AccT<16> { typedef f32x4 type; };
+
+// The 32x32 output block (i, j) of a wave's tile (units of 32 rows / columns) -> the wave's [32][36] LDS slab, with
+// bias and GELU applied, from either accumulator layout: MF 32 = one 32x32x16 accumulator (col lane&31, row (e&3) +
+// 8(e>>2) + 4(lane>>5)), MF 16 = 2 x 2 16x16x32 accumulators (col lane&15, row 4(lane>>4) + e).  Returns true when
+// an accumulator is not finite.
+template <int MF, int NI, int NJ>
+__device__ __forceinline__ bool fill_slab(const typename AccT<MF>::type (&acc)[NI][NJ], int i, int j, int epi,
+                                          const float* biasb, int col0, int N, int lane, float* slab) {
+    bool bad = false;
+    if constexpr (MF == 32) {
+        const int r32 = lane & 31, h = lane >> 5;
+        const float bv = (biasb && col0 + r32 < N) ? biasb[col0 + r32] : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            bad |= !__builtin_isfinite(acc[i][j][e]);
+            float v = acc[i][j][e] + bv;
+            if (epi == EPI_GELU) v = hfa::gelu_fast(v);
+            slab[((e & 3) + 8 * (e >> 2) + 4 * h) * 36 + r32] = v;
+        }
+    } else {
+        const int c16 = lane & 15, g = lane >> 4;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int col = 16 * jj + c16;
+            const float bv = (biasb && col0 + col < N) ? biasb[col0 + col] : 0.0f;
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float a = acc[2 * i + ii][2 * j + jj][e];
+                    bad |= !__builtin_isfinite(a);
+                    float v = a + bv;
+                    if (epi == EPI_GELU) v = hfa::gelu_fast(v);
+                    slab[(16 * ii + 4 * g + e) * 36 + col] = v;
+                }
+        }
+    }
+    return bad;
+}
+
+// Split-plane epilogue: TI x TJ blocks of 32 x 32 per wave, each through the slab (16-B row pieces out).
+template <int MF, int TI, int TJ, int NI, int NJ>
+__device__ __forceinline__ void store_split_lds(const GemmP& p, const typename AccT<MF>::type (&acc)[NI][NJ], int EPI_,
+                                                int zb, int zg, int wrow0, int wcol0, int lane, float* slab) {
     _Float16* Cb = p.Ch + zb * p.sCb + zg * p.sCg;
     const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
-    const int r32 = lane & 31, h = lane >> 5;
     bool bad = false;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
         const int col0 = wcol0 + j * 32;
         if (col0 >= p.N) continue;
-        const float bv = (biasb && col0 + r32 < p.N) ? biasb[col0 + r32] : 0.0f;
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
             const int row0 = wrow0 + i * 32;
             if (row0 >= p.M) continue;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                float v = acc[i][j][e] + bv;
-                if (EPI_ == EPI_GELU) v = hfa::gelu_fast(v);
-                slab[((e & 3) + 8 * (e >> 2) + 4 * h) * 36 + r32] = v;
-            }
+            fill_slab<MF>(acc, i, j, EPI_, biasb, col0, p.N, lane, slab);
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
@@ -638,6 +675,49 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const f32x16 (&a
     if (bad && p.oflow) *p.oflow = 1;
 }
 
+// f32 epilogue of the split kernel (+R), through the slab; raises *oflow on a non-finite accumulator.
+template <int MF, int EPI, int TI, int TJ, int NI, int NJ>
+__device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename AccT<MF>::type (&acc)[NI][NJ], int zb,
+                                              int zg, int wrow0, int wcol0, int lane, float* slab, bool check) {
+    bool bad = false;
+    float* Cb = p.C + zb * p.sCb + zg * p.sCg;
+    const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
+    const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+        const int col0 = wcol0 + j * 32;
+        if (col0 >= p.N) continue;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const int row0 = wrow0 + i * 32;
+            if (row0 >= p.M) continue;
+            bad |= fill_slab<MF>(acc, i, j, EPI, biasb, col0, p.N, lane, slab) && check;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int idx = lane + k * 64;
+                const int r = idx >> 3, c4 = (idx & 7) * 4;
+                const int row = row0 + r, col = col0 + c4;
+                if (row < p.M) {
+                    f32x4 v = *reinterpret_cast<const f32x4*>(slab + r * 36 + c4);
+                    float* dst = Cb + (long long)row * p.ldc + col;
+                    if (col + 3 < p.N) {
+                        if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + (long long)row * p.ldr + col);
+                        *reinterpret_cast<f32x4*>(dst) = v;
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            if (col + t < p.N) dst[t] = v[t] + (Rb ? Rb[(long long)row * p.ldr + col + t] : 0.0f);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (bad && p.oflow) *p.oflow = 1;
+}
+
 // GT (general taps): Cg a multiple of 8 but not of 32 (the grouped positional conv, Cg = 48): a K-step's four
 // 16-B chunks can straddle a tap boundary, so every lane tracks its own chunk's (tap, channel) instead of the
 // workgroup-uniform tap + scalar channel offset.
@@ -649,9 +729,18 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const f32x16 (&a
 // BK (halves per row per K-step) 32: [row][4 x 16 B] images, chunk c of row r at c ^ ((r >> 2) & 3); BK 16: [row][2 x
 // 16 B], chunk c at c ^ (((r >> 2) ^ (r >> 3)) & 1).  Both keep the 32x32x16 operand reads (lane: row lane&31, chunk
 // 2 kk + lane/32) conflict-free; BK 16 halves the stage so more stages fit (DMA latency hidden behind more steps).
-template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT, bool GT, bool ONE, int BK>
+// MF 16 (every automatic tile): v_mfma_f32_16x16x32_f16 instead of 32x32x16 (single accumulator, BK 32 only): the
+// same LDS operand bytes per MFMA FLOP for the same wave tile, one MFMA per 32-deep K-step per 16 x 16 block; the image
+// swizzle is then chunk c of row r at c ^ {0, 2, 3, 1}[(r >> 2) & 3] (conflict-free for the lane map row lane&15,
+// chunk lane>>4).  Measured on the workload's shapes (profiles/r02/split_mf16.txt): 4-9 % faster than the 32x32x16
+// form; the chip holds a higher clock under it (1.96-2.04 vs 1.73-1.85 GHz, same MFMA busy).  The next stage's DMA
+// pieces go out two per A block over the first blocks of a K-step instead of all at its top (+2-6 %), so the
+// two waves of a SIMD do not both stall on DMA issue while the matrix pipe idles.
+template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT, bool GT, bool ONE, int BK,
+          int MF = 32>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const GemmP p) {
     static_assert(BK == 16 || BK == 32, "BK 16 or 32");
+    static_assert(MF == 32 || (MF == 16 && ONE && BK == 32), "16x16x32 tiles: single accumulator, BK 32");
     constexpr int CPR = BK / 8, NW = WM * WN;                // 16-B chunks per row per plane
     constexpr int RPP = 64 / CPR, KK = BK / 16;               // rows per 1-KiB DMA piece, MFMA k-steps per K-step
     constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
@@ -680,7 +769,10 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     const __amdgpu_buffer_rsrc_t rW2 = hfa::make_rsrc(Wb + p.sWp, w_bytes);
 
     // DMA d of this wave fills rows (wave + d*NW)*RPP + lane/CPR of each plane, chunk slot lane%CPR (swizzled source)
-    auto swz = [](int r) { return CPR == 4 ? ((r >> 2) & 3) : (((r >> 2) ^ (r >> 3)) & 1); };
+    auto swz = [](int r) {
+        if constexpr (MF == 16) return (0x78 >> (2 * ((r >> 2) & 3))) & 3;      // {0, 2, 3, 1}[(r >> 2) & 3]
+        return CPR == 4 ? ((r >> 2) & 3) : (((r >> 2) ^ (r >> 3)) & 1);
+    };
     int a_t0[DA], a_c[DA], a_tap[DA];
     unsigned voffA[DA], voffW[DB];
 #pragma unroll
@@ -755,8 +847,104 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         advance();
     };
     constexpr int DN = 2 * (DA + DB);                       // DMA issues per wave per K-step
+    // one DMA piece q of this wave's share (q < 2 DA: A plane q & 1 of piece q >> 1; else W), in issue order;
+    // advance() after the last
+    auto issue_piece = [&](int stage, int q) {
+        const unsigned base = lds0 + stage * STAGE * 2 + wave * 1024;
+        if (q < 2 * DA) {
+            const int d = q >> 1, pl = q & 1;
+            if (IA % NW != 0 && wave + d * NW >= IA) return;
+            if constexpr (GT) {
+                const int t = a_t0[d] + a_tap[d];
+                const unsigned vo = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + a_c[d]) * 2) : hfa::DMA_OOB;
+                hfa::dma16(vo, pl ? rA2 : rA1, 0u, base + pl * PA * 2 + d * NW * 1024);
+                if (pl) {
+                    a_c[d] += BK;
+                    if (a_c[d] >= p.Cg) {
+                        a_c[d] -= p.Cg;
+                        ++a_tap[d];
+                    }
+                }
+            } else {
+                hfa::dma16(voffA[d], pl ? rA2 : rA1, (unsigned)cur_c0 * 2, base + pl * PA * 2 + d * NW * 1024);
+            }
+        } else {
+            const int d = (q - 2 * DA) >> 1, pl = q & 1;
+            if (IW % NW != 0 && wave + d * NW >= IW) return;
+            hfa::dma16(voffW[d], pl ? rW2 : rW1, (unsigned)cur_k0 * 2, base + (2 * PA + pl * PW) * 2 + d * NW * 1024);
+        }
+    };
 
     const int wm = wave / WN, wn = wave % WN;
+    if constexpr (MF == 16) {
+        constexpr int NI = BM / WM / 16, NJ = BN / WN / 16;       // 16 x 16 blocks per wave
+
+        const int r16 = lane & 15, c = lane >> 4;
+        const int rdA = (wm * (BM / WM) + r16) * CPR + (c ^ swz(r16));
+        const int rdB = 2 * PA / 8 + (wn * (BN / WN) + r16) * CPR + (c ^ swz(r16));
+        f32x4 acc[NI][NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const int nk = p.K / BK;
+#pragma unroll
+        for (int s = 0; s < NS - 1; ++s)
+            if (s < nk) issue(s);
+        if (nk >= NS - 1) hfa::wait_vm_barrier<(NS - 2) * DN>();
+        else hfa::wait_vm_barrier<0>();
+        const f16x8* s8 = reinterpret_cast<const f16x8*>(smem);
+        int stage = 0;
+        for (int kt = 0; kt < nk; ++kt) {
+            const bool more = kt + NS - 1 < nk;
+            const int nstage = stage == 0 ? NS - 1 : stage - 1;
+
+            const f16x8* st = s8 + stage * (STAGE / 8);
+            f16x8 w1[NJ], w2[NJ], w1s[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                w1[j] = st[rdB + j * 16 * CPR];
+                w2[j] = st[rdB + PW / 8 + j * 16 * CPR];
+                w1s[j] = w1[j] * (_Float16)2048.0f;
+            }
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                if (more) {                  // the next stage's DMA, two pieces per A block from the first
+#pragma unroll
+                    for (int q = 0; q < DN; ++q)
+                        if ((q / 2 < NI ? q / 2 : NI - 1) == i) issue_piece(nstage, q);
+                }
+                const f16x8 a1 = st[rdA + i * 16 * CPR], a2 = st[rdA + PA / 8 + i * 16 * CPR];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, w1s[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, w2[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, w1[j], acc[i][j], 0, 0, 0);
+                }
+            }
+            if (more) advance();
+            if (kt + 1 < nk) {
+                if (more) hfa::wait_vm_barrier<(NS - 2) * DN>();
+                else hfa::wait_vm_barrier<0>();
+            }
+            stage = stage + 1 == NS ? 0 : stage + 1;
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] *= 1.0f / 2048.0f;
+        static_assert(NW * 32 * 36 * 4 <= NS * STAGE * 2, "epilogue slabs exceed the staging LDS");
+        __syncthreads();
+        float* slab = reinterpret_cast<float*>(smem) + wave * (32 * 36);
+        constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
+        if constexpr (OUT_SPLIT)
+            store_split_lds<16, TI, TJ>(p, acc, EPI, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
+                                        slab);
+        else
+            store_f32_lds<16, EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
+                                           slab, true);
+        return;
+    } else {
     const int r32 = lane & 31, h = lane >> 5;
     int rdA[KK], rdB[KK];                                    // f16x8 (16-B) units within a stage
 #pragma unroll
@@ -850,10 +1038,12 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     __syncthreads();
     float* slab = reinterpret_cast<float*>(smem) + wave * (32 * 36);
     if constexpr (OUT_SPLIT)
-        store_split_lds<TI, TJ>(p, accM, EPI, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane, slab);
+        store_split_lds<32, TI, TJ>(p, accM, EPI, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
+                                    slab);
     else
-        store_tile_lds<EPI, TI, TJ>(p, accM, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane, slab,
-                                    ONE);
+        store_f32_lds<32, EPI, TI, TJ>(p, accM, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane, slab,
+                                       ONE);
+    }
 }
 
 // f32 -> (hi, lo * 2^11) f16 planes, row-wise with 4-element vectors where aligned; raises *oflow for |x| >= 65504
@@ -1267,8 +1457,9 @@ __global__ __launch_bounds__(512, 1) void posconv_split_kernel(const GemmP p) {
 enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_128x128_NS3 = 4, SCFG_128x128_NS4 = 5,
        SCFG_256x128_NS3 = 6, SCFG_256x256_1 = 7, SCFG_256x128_1 = 8, SCFG_128x128_1 = 9, SCFG_128x64_1 = 10,
        SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_256x64_1 = 14,
-       SCFG_N48 = 15, SCFG_WIN = 16, SCFG_COUNT = 17 };
-struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; };
+       SCFG_N48 = 15, SCFG_WIN = 16, SCFG_256x256_M16 = 17, SCFG_128x128_M16 = 18, SCFG_128x64_M16 = 19,
+       SCFG_256x64_M16 = 20, SCFG_COUNT = 21 };
+struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; int MF; };
 constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 128, 2, 2, 2, 2, false, 32}, {128, 128, 2, 2, 2, 2, false, 32}, {128, 64, 2, 2, 2, 2, false, 32},
     {256, 128, 4, 2, 2, 1, false, 32}, {128, 128, 2, 2, 3, 1, false, 32}, {128, 128, 2, 2, 4, 1, false, 32},
@@ -1276,7 +1467,9 @@ constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 128, 2, 2, 2, 2, true, 32},  {128, 64, 2, 2, 2, 2, true, 32},   {256, 256, 2, 4, 4, 1, true, 16},
     {256, 256, 2, 4, 3, 1, true, 16},  {128, 128, 2, 2, 4, 2, true, 16},  {256, 64, 4, 1, 2, 2, true, 32},
     {128, 48, 4, 1, 2, 2, true, 32},       // SCFG_N48: gemm_split48_kernel (16x16x32 MFMA), not gemm_split_kernel
-    {256, 48, 8, 1, 3, 1, true, 32}};      // SCFG_WIN: posconv_split_kernel (LDS-resident input window)
+    {256, 48, 8, 1, 3, 1, true, 32},       // SCFG_WIN: posconv_split_kernel (LDS-resident input window)
+    {256, 256, 2, 4, 2, 1, true, 32, 16}, {128, 128, 2, 2, 2, 2, true, 32, 16}, {128, 64, 2, 2, 2, 2, true, 32, 16},
+    {256, 64, 4, 1, 2, 2, true, 32, 16}};
 thread_local int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 thread_local int g_win_nb = 3;   // column blocks of the window kernel the name query reports (N / 16)
 
@@ -1285,7 +1478,8 @@ thread_local int g_win_nb = 3;   // column blocks of the window kernel the name 
 // 189 tiles for N = 768) and within 3 % on the QKV projection; small grids keep the narrower tiles.  Every
 // automatic choice is a single-accumulator tile: each output element then sees the same MFMA sequence (same
 // k-blocks, same three products in the same order) whatever the tile, so a row's result does not depend on the
-// batch it is in (variable-length batches stay bit-identical to the reference's B = 1 runs).
+// batch it is in (variable-length batches stay bit-identical to the reference's B = 1 runs).  Since round 2 every
+// automatic tile is a 16x16x32 (MF 16) tile; the 32x32x16 tiles stay as tuning choices.
 inline bool win_ok(const GemmP& p) {   // posconv_split_kernel: stride 1, N 48 or 64, Cg % 8, Cg <= 64, window fits
     return (p.N == 48 || p.N == 64) && p.Ch == nullptr && p.stride == 1 && p.Cg % 8 == 0 && p.Cg >= 32 &&
            p.Cg <= 64 && p.K % p.Cg == 0 && 256 + p.K / p.Cg - 1 <= kWinRows;
@@ -1294,8 +1488,8 @@ inline bool win_ok(const GemmP& p) {   // posconv_split_kernel: stride 1, N 48 o
 inline int split_cfg(const GemmP& p, int Z) {
     const bool n48 = p.N == 48 && p.Ch == nullptr && p.Cg % 8 == 0 && p.Cg >= 32;
     if (g_split_cfg > 0 && g_split_cfg < SCFG_COUNT) {
-        if (g_split_cfg == SCFG_N48 && !n48) return SCFG_128x64_1;
-        if (g_split_cfg == SCFG_WIN && !win_ok(p)) return SCFG_128x64_1;
+        if (g_split_cfg == SCFG_N48 && !n48) return SCFG_128x64_M16;
+        if (g_split_cfg == SCFG_WIN && !win_ok(p)) return SCFG_128x64_M16;
         return g_split_cfg;
     }
     if (win_ok(p)) return SCFG_WIN;
@@ -1303,9 +1497,20 @@ inline int split_cfg(const GemmP& p, int Z) {
     const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
     const long long blocks256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * Z;
     if (p.N == 64 && p.Cg % 32 == 0 && (long long)((p.M + 255) / 256) * Z >= 256)
-        return SCFG_256x64_1;              // grouped positional conv at Cg = 64 (Hubert-large): 1.26x the 128x64 tile
-    if (p.N <= 64 || blocks128 < 256) return SCFG_128x64_1;
-    return (blocks256 >= 128 && p.N >= 512) ? SCFG_256x256_1 : SCFG_128x128_1;
+        return SCFG_256x64_M16;            // grouped positional conv at Cg = 64 (Hubert-large): 1.26x the 128x64 tile
+    if (p.N <= 64 || blocks128 < 256) return SCFG_128x64_M16;
+    if (blocks256 < 128 || p.N < 512) return SCFG_128x128_M16;
+    // rounds of resident tiles (256 x 256: one per CU; 128 x 128: two per CU) times the time per round, with the
+    // larger tile's 1.12x per-FLOP speed (profiles/r02/split_mf16.txt): QKV (N = 2304, 567 big tiles = 2.2 rounds)
+    // goes to 128 x 128, the extractor convs, FFN and 768-wide projections stay on 256 x 256
+    const double t256 = (double)((blocks256 + 255) / 256) * 4.0 / 1.12, t128 = (double)((blocks128 + 511) / 512) * 2.0;
+    return t256 <= t128 ? SCFG_256x256_M16 : SCFG_128x128_M16;
+}
+
+// general taps (Cg % 32 != 0, the grouped positional conv off the window kernel): the tiles with a GT instantiation
+inline int gt_cfg(int cfg) {
+    if (cfg == SCFG_256x64_1 || cfg == SCFG_256x64_M16) return SCFG_256x64_M16;
+    return kSplitGeom[cfg].BN == 64 ? SCFG_128x64_M16 : SCFG_128x128_M16;
 }
 
 inline void split_name(int cfg, int epi, bool outs, bool gt, char* buf, int len) {
@@ -1317,10 +1522,11 @@ inline void split_name(int cfg, int epi, bool outs, bool gt, char* buf, int len)
         snprintf(buf, len, "posconv_split_kernel<%d, %d>", epi, g_win_nb);
         return;
     }
-    if (gt && cfg != SCFG_256x64_1) cfg = kSplitGeom[cfg].BN == 64 ? SCFG_128x64_1 : SCFG_128x128_1;
+    if (gt) cfg = gt_cfg(cfg);
     const SplitGeom& g = kSplitGeom[cfg];
-    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, %s, %d>", epi, g.BM, g.BN, g.WM, g.WN,
-             g.NS, g.OCC, outs ? "true" : "false", gt ? "true" : "false", g.ONE ? "true" : "false", g.BK);
+    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, %s, %d, %d>", epi, g.BM, g.BN, g.WM,
+             g.WN, g.NS, g.OCC, outs ? "true" : "false", gt ? "true" : "false", g.ONE ? "true" : "false", g.BK,
+             g.MF ? g.MF : 32);
 }
 
 template <int EPI, bool OUTS, int CFG, bool GT = false>
@@ -1328,8 +1534,9 @@ int launch_split_cfg(GemmP p, int Z, hipStream_t st) {
     constexpr SplitGeom g = kSplitGeom[CFG];
     dim3 grid;
     if (int rc = set_grid(p, g.BM, g.BN, grid, Z)) return rc;
-    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE, g.BK>), grid,
-                       dim3(64 * g.WM * g.WN), 0, st, p);
+    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE, g.BK,
+                                          g.MF ? g.MF : 32>),
+                       grid, dim3(64 * g.WM * g.WN), 0, st, p);
     return hfa::check_launch("hfa_conv_gemm_split");
 }
 
@@ -1340,9 +1547,11 @@ int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
             hfa::set_error("hfa_conv_gemm_split: Cg %% 32 != 0 takes no split output");
             return HFA_EINVAL;
         } else {
-            if (cfg == SCFG_256x64_1) return launch_split_cfg<EPI, false, SCFG_256x64_1, true>(p, Z, st);
-            return kSplitGeom[cfg].BN == 64 ? launch_split_cfg<EPI, false, SCFG_128x64_1, true>(p, Z, st)
-                                            : launch_split_cfg<EPI, false, SCFG_128x128_1, true>(p, Z, st);
+            switch (gt_cfg(cfg)) {
+                case SCFG_256x64_M16: return launch_split_cfg<EPI, false, SCFG_256x64_M16, true>(p, Z, st);
+                case SCFG_128x64_M16: return launch_split_cfg<EPI, false, SCFG_128x64_M16, true>(p, Z, st);
+                default: return launch_split_cfg<EPI, false, SCFG_128x128_M16, true>(p, Z, st);
+            }
         }
     }
     switch (cfg) {
@@ -1359,6 +1568,10 @@ int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
         case SCFG_256x256_1_K16S3: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1_K16S3>(p, Z, st);
         case SCFG_128x128_1_K16S4: return launch_split_cfg<EPI, OUTS, SCFG_128x128_1_K16S4>(p, Z, st);
         case SCFG_256x64_1: return launch_split_cfg<EPI, OUTS, SCFG_256x64_1>(p, Z, st);
+        case SCFG_256x256_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x256_M16>(p, Z, st);
+        case SCFG_128x128_M16: return launch_split_cfg<EPI, OUTS, SCFG_128x128_M16>(p, Z, st);
+        case SCFG_128x64_M16: return launch_split_cfg<EPI, OUTS, SCFG_128x64_M16>(p, Z, st);
+        case SCFG_256x64_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x64_M16>(p, Z, st);
         default: return launch_split_cfg<EPI, OUTS, SCFG_128x128>(p, Z, st);
     }
 }

@@ -42,7 +42,7 @@ def test_split_planes_and_flag():
     flag.zero_()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13, 14, 15, 17, 18, 19, 20])
 @pytest.mark.parametrize("M,N,K,epi,res,outs", [(300, 200, 128, 0, False, False), (1000, 768, 768, 1, False, False),
                                                 (257, 72, 192, 0, True, False), (4096, 3072, 768, 1, False, True),
                                                 (130, 2304, 768, 0, False, True), (64, 768, 3072, 0, True, False)])
@@ -69,7 +69,7 @@ def test_split_linear(cfg, M, N, K, epi, res, outs):
         _close(got, ref, 2e-5, 2e-5)
 
 
-@pytest.mark.parametrize("cfg", [0, 9])
+@pytest.mark.parametrize("cfg", [0, 9, 17, 18, 19])
 @pytest.mark.parametrize("Cin,Cout,k,s,pad,T", [(512, 512, 3, 2, 0, 301), (512, 512, 2, 2, 0, 100),
                                                 (192, 192, 3, 1, 1, 64), (192, 384, 2, 2, 0, 40),
                                                 (512, 512, 3, 2, 0, 1301)])
@@ -128,16 +128,18 @@ def test_split_grouped_posconv_general_taps(H, G, k, L, cfg):
 
 
 @pytest.mark.parametrize("outs", [False, True])
-def test_split_single_acc_tiles_bit_identical(outs):
-    """Every automatic tile (7 = 256x256, 9 = 128x128, 10 = 128x64, all single-accumulator) gives the same bits,
-    so a row's result does not depend on the batch (and so the grid) it runs in."""
+@pytest.mark.parametrize("cfgs", [(0, 17, 18, 19, 20), (7, 9, 10, 8, 11, 12, 13, 14)])
+def test_split_single_acc_tiles_bit_identical(outs, cfgs):
+    """Every automatic tile (17 = 256x256, 18 = 128x128, 19 = 128x64, 20 = 256x64: single-accumulator 16x16x32
+    tiles) gives the same bits, so a row's result does not depend on the batch (and so the grid) it runs in; the
+    32x32x16 tiles (tuning only) agree among themselves the same way."""
     from hubertfa_amd import ops, _lib
     d = torch.device("cuda")
     M, N, K = 700, 768, 1536
     xs, ws = ops.split(_r(M, K, seed=1).to(d)), ops.split(_r(N, K, seed=2, scale=K ** -0.5).to(d))
     b = _r(N, seed=3).to(d)
     outs_ = []
-    for cfg in (7, 9, 10, 8, 11, 12, 13, 14):
+    for cfg in cfgs:
         _lib.lib().hfa_gemm_split_tuning(cfg)
         try:
             outs_.append(ops.linear_split(xs, ws, b, epilogue=ops.EPI_GELU, out_split=outs))
@@ -147,7 +149,8 @@ def test_split_single_acc_tiles_bit_identical(outs):
         assert torch.equal(o, outs_[0])
 
 
-@pytest.mark.parametrize("cfg,outs", [(7, False), (8, False), (9, True), (10, False)])
+@pytest.mark.parametrize("cfg,outs", [(7, False), (8, False), (9, True), (10, False), (17, False), (18, True),
+                                      (19, False), (20, True)])
 def test_split_single_acc_weight_range_flag(cfg, outs):
     """Single-accumulator tiles form 2^11 * hi(w) in f16: a weight with |w| >= 32 overflows there, and the
     non-finite result raises the split flag (the caller re-runs on the f32 GEMM) instead of passing silently."""
