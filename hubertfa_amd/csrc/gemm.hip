@@ -675,12 +675,15 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const typename A
     if (bad && p.oflow) *p.oflow = 1;
 }
 
-// f32 epilogue of the split kernel (+R), through the slab; raises *oflow on a non-finite accumulator.
+// f32 epilogue of the split kernel (+R), through the slab; raises *oflow on a non-finite accumulator.  With p.Ch
+// set as well (dual output) the final values also go out as split planes (the next split GEMM's operand, e.g. the
+// positional conv's input next to its f32 residual copy), with the planes' range check.
 template <int MF, int EPI, int TI, int TJ, int NI, int NJ>
 __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename AccT<MF>::type (&acc)[NI][NJ], int zb,
                                               int zg, int wrow0, int wcol0, int lane, float* slab, bool check) {
     bool bad = false;
     float* Cb = p.C + zb * p.sCb + zg * p.sCg;
+    _Float16* Hb = p.Ch ? p.Ch + zb * p.sCb + zg * p.sCg : nullptr;
     const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
     const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
 #pragma unroll
@@ -708,7 +711,31 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
                     } else {
 #pragma unroll
                         for (int t = 0; t < 4; ++t)
-                            if (col + t < p.N) dst[t] = v[t] + (Rb ? Rb[(long long)row * p.ldr + col + t] : 0.0f);
+                            if (col + t < p.N) {
+                                v[t] += Rb ? Rb[(long long)row * p.ldr + col + t] : 0.0f;
+                                dst[t] = v[t];
+                            }
+                    }
+                    if (Hb) {
+                        f16x4 v1, v2;
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            bad |= !(__builtin_fabsf(v[t]) < 65504.0f) && col + t < p.N;
+                            v1[t] = (_Float16)v[t];
+                            v2[t] = (_Float16)((v[t] - (float)v1[t]) * 2048.0f);
+                        }
+                        _Float16* hd = Hb + (long long)row * p.ldc + col;
+                        if (col + 3 < p.N) {
+                            *reinterpret_cast<f16x4*>(hd) = v1;
+                            *reinterpret_cast<f16x4*>(hd + p.sCp) = v2;
+                        } else {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+                                if (col + t < p.N) {
+                                    hd[t] = v1[t];
+                                    hd[t + p.sCp] = v2[t];
+                                }
+                        }
                     }
                 }
             }
@@ -1743,8 +1770,8 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
         return HFA_EINVAL;
     }
     if (M == 0 || N == 0 || Zb == 0) return HFA_OK;
-    if (!A || !W || (!C == !Cs) || K == 0 || (Cs && R)) {
-        hfa::set_error("hfa_conv_gemm_split: need A, W and exactly one of C / Cs (Cs takes no residual)");
+    if (!A || !W || (!C && !Cs) || K == 0 || (Cs && !C && R)) {
+        hfa::set_error("hfa_conv_gemm_split: need A, W and C and / or Cs (Cs alone takes no residual)");
         return HFA_EINVAL;
     }
     if (K % 32 || Cg % 8 || (Cg % 32 && Cg < 32) || K % Cg) {
@@ -1761,9 +1788,9 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
         hfa::set_error("hfa_conv_gemm_split: operand span past 31-bit buffer offsets");
         return HFA_EINVAL;
     }
-    const bool vc = C ? (al16(C) && ldc % 4 == 0 && sCb % 4 == 0 && sCg % 4 == 0 &&
-                         (!R || (al16(R) && ldr % 4 == 0 && sRb % 4 == 0 && sRg % 4 == 0)))
-                      : (((uintptr_t)Cs & 7) == 0 && ldc % 4 == 0 && (sCp | sCb | sCg) % 4 == 0);
+    const bool vc = (!C || (al16(C) && ldc % 4 == 0 && sCb % 4 == 0 && sCg % 4 == 0 &&
+                            (!R || (al16(R) && ldr % 4 == 0 && sRb % 4 == 0 && sRg % 4 == 0)))) &&
+                    (!Cs || (((uintptr_t)Cs & 7) == 0 && ldc % 4 == 0 && (sCp | sCb | sCg) % 4 == 0));
     if (!vc) {
         hfa::set_error("hfa_conv_gemm_split: C/R (or Cs) rows must be 16-B (8-B) aligned");
         return HFA_EINVAL;
@@ -1802,8 +1829,8 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
         else hipLaunchKernelGGL(gemm_split48_kernel<EPI_NONE>, grid, dim3(256), 0, stream, p);
         return hfa::check_launch("hfa_conv_gemm_split");
     }
-    if (Cs) return epilogue == EPI_GELU ? launch_split<EPI_GELU, true>(p, Z, cfg, stream)
-                                        : launch_split<EPI_NONE, true>(p, Z, cfg, stream);
+    if (Cs && !C) return epilogue == EPI_GELU ? launch_split<EPI_GELU, true>(p, Z, cfg, stream)
+                                              : launch_split<EPI_NONE, true>(p, Z, cfg, stream);
     return epilogue == EPI_GELU ? launch_split<EPI_GELU, false>(p, Z, cfg, stream)
                                 : launch_split<EPI_NONE, false>(p, Z, cfg, stream);
 }

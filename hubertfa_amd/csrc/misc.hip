@@ -53,15 +53,20 @@ __global__ __launch_bounds__(256) void mask_rows_kernel(int T, int C, float* __r
 }
 
 // Wav2Vec2FeatureExtractor zero_mean_unit_var_norm (transformers feature_extraction_wav2vec2.py): per row
-// (x - mean) / sqrt(var + 1e-7), biased variance.  One workgroup per row, f64 statistics.
-__global__ __launch_bounds__(256) void wav_normalize_kernel(int N, const float* __restrict__ x, long long x_bs,
-                                                            float eps, float* __restrict__ y, long long y_bs,
-                                                            const int32_t* __restrict__ lens) {
-    const int b = blockIdx.x;
+// (x - mean) / sqrt(var + 1e-7), biased variance, f64 statistics.  Two launches so a row is spread over the chip:
+// wav_stats_kernel sums fixed chunks of a row into f64 partials (kWavChunks per row, fixed order: deterministic),
+// wav_apply_kernel re-reduces a row's partials in order and normalises its tile (float4 where aligned).
+constexpr int kWavChunks = 64;
+
+__global__ __launch_bounds__(256) void wav_stats_kernel(int N, const float* __restrict__ x, long long x_bs,
+                                                        const int32_t* __restrict__ lens, double* __restrict__ part) {
+    const int b = blockIdx.y, c = blockIdx.x;
     const int Nb = lens ? lens[b] : N;                // statistics over this utterance's samples only
+    const int per = (Nb + kWavChunks - 1) / kWavChunks;
+    const int i0 = c * per, i1 = min(Nb, i0 + per);
     const float* xr = x + b * x_bs;
     double s = 0.0, ss = 0.0;
-    for (int i = threadIdx.x; i < Nb; i += 256) {
+    for (int i = i0 + threadIdx.x; i < i1; i += 256) {
         const double v = xr[i];
         s += v;
         ss += v * v;
@@ -71,15 +76,51 @@ __global__ __launch_bounds__(256) void wav_normalize_kernel(int N, const float* 
     ss = hfa::wave_sum_d(ss);
     if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = s; red[1][threadIdx.x >> 6] = ss; }
     __syncthreads();
-    const double S = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    const double SS = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-    const double mean = Nb > 0 ? S / Nb : 0.0;
-    double var = Nb > 0 ? SS / Nb - mean * mean : 0.0;
-    if (var < 0) var = 0;
-    const float meanf = (float)mean;
-    const float den = (float)sqrt((double)(float)var + (double)eps);
+    if (threadIdx.x == 0) {
+        part[(b * kWavChunks + c) * 2] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        part[(b * kWavChunks + c) * 2 + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    }
+}
+
+__global__ __launch_bounds__(256) void wav_apply_kernel(int N, const float* __restrict__ x, long long x_bs, float eps,
+                                                        float* __restrict__ y, long long y_bs,
+                                                        const int32_t* __restrict__ lens,
+                                                        const double* __restrict__ part, bool vec) {
+    const int b = blockIdx.y;
+    const int Nb = lens ? lens[b] : N;
+    __shared__ float sh[2];
+    if (threadIdx.x == 0) {
+        double S = 0.0, SS = 0.0;
+        for (int c = 0; c < kWavChunks; ++c) {
+            S += part[(b * kWavChunks + c) * 2];
+            SS += part[(b * kWavChunks + c) * 2 + 1];
+        }
+        const double mean = Nb > 0 ? S / Nb : 0.0;
+        double var = Nb > 0 ? SS / Nb - mean * mean : 0.0;
+        if (var < 0) var = 0;
+        sh[0] = (float)mean;
+        sh[1] = (float)sqrt((double)(float)var + (double)eps);
+    }
+    __syncthreads();
+    const float meanf = sh[0], den = sh[1];
+    const float* xr = x + b * x_bs;
     float* yr = y + b * y_bs;
-    for (int i = threadIdx.x; i < N; i += 256) yr[i] = i < Nb ? (xr[i] - meanf) / den : 0.0f;
+    const int i0 = blockIdx.x * 4096;
+    if (vec) {
+        for (int i = i0 + threadIdx.x * 4; i < min(N, i0 + 4096); i += 1024) {
+            if (i + 3 < N) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(xr + i);
+                f32x4 o;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) o[t] = i + t < Nb ? (v[t] - meanf) / den : 0.0f;
+                *reinterpret_cast<f32x4*>(yr + i) = o;
+            } else {
+                for (int t = 0; t < 4 && i + t < N; ++t) yr[i + t] = i + t < Nb ? (xr[i + t] - meanf) / den : 0.0f;
+            }
+        }
+    } else {
+        for (int i = i0 + threadIdx.x; i < min(N, i0 + 4096); i += 256) yr[i] = i < Nb ? (xr[i] - meanf) / den : 0.0f;
+    }
 }
 
 // y[b, i] = x[b, i - left] inside [0, N), else 0, for i < N_out.
@@ -145,14 +186,20 @@ int hfa_mask_rows_f32(int B, int T, int C, float* x, long long x_bs, int ldx, co
     return hfa::check_launch("hfa_mask_rows_f32");
 }
 
+long long hfa_wav_normalize_workspace_bytes(int B) { return B > 0 ? (long long)B * kWavChunks * 2 * 8 : 0; }
+
 int hfa_wav_normalize_f32(int B, int N, const float* x, long long x_bs, float eps, float* y, long long y_bs,
-                          const int32_t* lens, hipStream_t stream) {
-    if (B < 0 || N <= 0 || !x || !y) {
+                          const int32_t* lens, void* workspace, hipStream_t stream) {
+    if (B < 0 || N <= 0 || !x || !y || (B > 0 && !workspace) || B > 65535) {
         hfa::set_error("hfa_wav_normalize_f32: bad arguments");
         return HFA_EINVAL;
     }
     if (B == 0) return HFA_OK;
-    hipLaunchKernelGGL(wav_normalize_kernel, dim3(B), dim3(256), 0, stream, N, x, x_bs, eps, y, y_bs, lens);
+    double* part = static_cast<double*>(workspace);
+    hipLaunchKernelGGL(wav_stats_kernel, dim3(kWavChunks, B), dim3(256), 0, stream, N, x, x_bs, lens, part);
+    const bool vec = ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && x_bs % 4 == 0 && y_bs % 4 == 0;
+    hipLaunchKernelGGL(wav_apply_kernel, dim3((N + 4095) / 4096, B), dim3(256), 0, stream, N, x, x_bs, eps, y, y_bs,
+                       lens, part, vec);
     return hfa::check_launch("hfa_wav_normalize_f32");
 }
 

@@ -223,6 +223,113 @@ __global__ __launch_bounds__(256) void groupnorm_apply_kernel(int T, int C, int 
     }
 }
 
+// Row-parallel GroupNorm for channels-last [T, C] with C % 4 == 0, Cg % 4 == 0, C <= 1024 (the UNet's GN(16) on
+// 192 / 384 channels: a group is 12 / 24 channels, 48 / 96 B of a row, so one workgroup per (batch, group) reads
+// short strided pieces).  Rows are cut into fixed parts of kGnRows rows; pass 1 (grid parts x B) reads whole rows with
+// float4 loads, each thread on one fixed float4 column (one group) and every (256 / (C/4))-th row of the part, and
+// writes f64 partial sums per (batch, part, group), reduced per group in a fixed order; pass 2 re-reduces a row's
+// partials in part order (the parts of a row depend only on its own length: a row gives the same bits in any batch)
+// and applies affine + activation to its part, writing f32 and / or split-f16 planes (the next split GEMM's operand).
+constexpr int kGnRows = 32;
+
+__global__ __launch_bounds__(256) void gn_rows_partial_kernel(int T, int C, int G, const float* __restrict__ x,
+                                                              long long x_bs, int ldx,
+                                                              const int32_t* __restrict__ t_len,
+                                                              double* __restrict__ part) {
+    const int pi = blockIdx.x, b = blockIdx.y, P = gridDim.x;
+    const int C4 = C >> 2, Cg = C / G, rstep = 256 / C4;
+    const int col = threadIdx.x % C4, r0 = threadIdx.x / C4;
+    const int Tb = t_len ? t_len[b] : T;
+    const int t0 = pi * kGnRows, t1 = min(Tb, t0 + kGnRows);
+    double s = 0.0, ss = 0.0;
+    if (r0 < rstep) {
+        const float* xb = x + b * x_bs + col * 4;
+        for (int t = t0 + r0; t < t1; t += rstep) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(xb + (long long)t * ldx);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                s += (double)v[e];
+                ss += (double)v[e] * (double)v[e];
+            }
+        }
+    }
+    __shared__ double red[256][2];
+    red[threadIdx.x][0] = s;
+    red[threadIdx.x][1] = ss;
+    __syncthreads();
+    if (threadIdx.x < G) {                              // group g: columns [g Cg/4, (g+1) Cg/4) of every row lane
+        const int g = threadIdx.x, c0 = g * (Cg >> 2), c1 = c0 + (Cg >> 2);
+        double S = 0.0, SS = 0.0;
+        for (int r = 0; r < rstep; ++r)
+            for (int c = c0; c < c1; ++c) {
+                S += red[r * C4 + c][0];
+                SS += red[r * C4 + c][1];
+            }
+        double* pp = part + (((size_t)b * P + pi) * G + g) * 2;
+        pp[0] = S;
+        pp[1] = SS;
+    }
+}
+
+__global__ __launch_bounds__(256) void gn_rows_apply_kernel(int T, int C, int G, const float* __restrict__ x,
+                                                            long long x_bs, int ldx, const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float eps, int act,
+                                                            float* __restrict__ y, long long y_bs, int ldy,
+                                                            const int32_t* __restrict__ t_len,
+                                                            const double* __restrict__ part,
+                                                            _Float16* __restrict__ ys, long long ys_bs, int ldys,
+                                                            long long sps, int* __restrict__ oflow) {
+    const int pi = blockIdx.x, b = blockIdx.y, P = gridDim.x;
+    const int C4 = C >> 2, Cg = C / G, rstep = 256 / C4;
+    const int Tb = t_len ? t_len[b] : T;
+    __shared__ float stat[64][2];                       // G <= 64: mean, rstd per group
+    if (threadIdx.x < G) {
+        const int g = threadIdx.x, pb = (Tb + kGnRows - 1) / kGnRows;   // this row's own parts, in order
+        double S = 0.0, SS = 0.0;
+        for (int k = 0; k < pb; ++k) {
+            const double* pp = part + (((size_t)b * P + k) * G + g) * 2;
+            S += pp[0];
+            SS += pp[1];
+        }
+        const double n = (double)Tb * Cg;
+        const double mean_d = Tb > 0 ? S / n : 0.0;
+        double var_d = Tb > 0 ? SS / n - mean_d * mean_d : 0.0;
+        if (var_d < 0) var_d = 0;
+        stat[g][0] = (float)mean_d;
+        stat[g][1] = (float)(1.0 / sqrt(var_d + (double)eps));
+    }
+    __syncthreads();
+    const int col = threadIdx.x % C4, r0 = threadIdx.x / C4;
+    if (r0 >= rstep) return;
+    const int c = col * 4, g = c / Cg;
+    const float mean = stat[g][0], rstd = stat[g][1];
+    const f32x4 gm = *reinterpret_cast<const f32x4*>(gamma + c), bt = *reinterpret_cast<const f32x4*>(beta + c);
+    const int t0 = pi * kGnRows, t1 = min(T, t0 + kGnRows);
+    bool bad = false;
+    for (int t = t0 + r0; t < t1; t += rstep) {
+        f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (t < Tb) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(x + b * x_bs + (long long)t * ldx + c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = act_apply((v[e] - mean) * rstd * gm[e] + bt[e], act);
+        }
+        if (y) *reinterpret_cast<f32x4*>(y + b * y_bs + (long long)t * ldy + c) = o;
+        if (ys) {
+            f16x4 h1, h2;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                bad |= !(__builtin_fabsf(o[e]) < 65504.0f);
+                h1[e] = (_Float16)o[e];
+                h2[e] = (_Float16)((o[e] - (float)h1[e]) * 2048.0f);
+            }
+            _Float16* d = ys + b * ys_bs + (long long)t * ldys + c;
+            *reinterpret_cast<f16x4*>(d) = h1;
+            *reinterpret_cast<f16x4*>(d + sps) = h2;
+        }
+    }
+    if (bad && oflow) *oflow = 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -273,8 +380,37 @@ int hfa_layernorm_split(int rows, int C, const float* x, long long ldx, const fl
 }
 
 long long hfa_groupnorm_workspace_bytes(int B, int T, int C, int G) {
-    (void)T; (void)C;
-    return (long long)B * G * 64 * 2 * sizeof(double) + 64;
+    (void)C;
+    const long long a = (long long)B * G * 64 * 2 * sizeof(double) + 64;                      // split-T path
+    const long long r = (long long)B * ((T + kGnRows - 1) / kGnRows) * G * 2 * sizeof(double);   // row-parallel path
+    return a > r ? a : r;
+}
+
+static bool gn_rows_ok(int C, int G) { return C % 4 == 0 && (C / G) % 4 == 0 && C <= 1024 && G <= 64 && C % G == 0; }
+
+int hfa_groupnorm_split(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,
+                        const float* beta, float eps, int act, float* y, long long y_bs, int ldy, const int32_t* t_len,
+                        uint16_t* ys_, long long ys_bs, int ldys, long long sps, int* oflow, void* workspace,
+                        hipStream_t stream) {
+    _Float16* ys = reinterpret_cast<_Float16*>(ys_);
+    if (B < 0 || T < 0 || C <= 0 || G <= 0 || act < 0 || act > 2 || !gn_rows_ok(C, G) || B > 65535) {
+        hfa::set_error("hfa_groupnorm_split: bad sizes (C %% 4, (C/G) %% 4, C <= 1024, G <= 64)");
+        return HFA_EINVAL;
+    }
+    if (B == 0 || T == 0) return HFA_OK;
+    if (!x || !gamma || !beta || (!y && !ys) || !workspace ||
+        (((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)y) & 15) || ldx % 4 || x_bs % 4 ||
+        (y && (ldy % 4 || y_bs % 4)) || (ys && ((((uintptr_t)ys) & 7) || ldys % 4 || ys_bs % 4 || sps % 4))) {
+        hfa::set_error("hfa_groupnorm_split: null or misaligned operand (16-B rows; 8-B plane rows; workspace)");
+        return HFA_EINVAL;
+    }
+    const int P = (T + kGnRows - 1) / kGnRows;
+    double* part = reinterpret_cast<double*>(workspace);
+    hipLaunchKernelGGL(gn_rows_partial_kernel, dim3(P, B), dim3(256), 0, stream, T, C, G, x, x_bs, ldx, t_len, part);
+    // (the apply pass may write y in place of x: every partial of the batch row is complete at this launch boundary)
+    hipLaunchKernelGGL(gn_rows_apply_kernel, dim3(P, B), dim3(256), 0, stream, T, C, G, x, x_bs, ldx, gamma, beta,
+                       eps, act, y, y_bs, ldy, t_len, part, ys, ys_bs, ldys, sps, oflow);
+    return hfa::check_launch("hfa_groupnorm_split");
 }
 
 int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,
@@ -289,7 +425,12 @@ int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs
         hfa::set_error("hfa_groupnorm_f32: null pointer");
         return HFA_EINVAL;
     }
-    // split T when the (group, batch) grid alone cannot fill the chip and the rows are long
+    if (workspace && gn_rows_ok(C, G) && B <= 65535 &&
+        !(((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)y) & 15) && ldx % 4 == 0 &&
+        x_bs % 4 == 0 && ldy % 4 == 0 && y_bs % 4 == 0)
+        return hfa_groupnorm_split(B, T, C, G, x, x_bs, ldx, gamma, beta, eps, act, y, y_bs, ldy, t_len, nullptr, 0,
+                                   0, 0, nullptr, workspace, stream);
+    // general shapes: one workgroup per (batch, group), or T split when that grid cannot fill the chip
     const long long per_pair = (long long)T * (C / G);
     int P = 1;
     if (workspace && (long long)B * G < 512 && per_pair > 65536) {

@@ -224,9 +224,11 @@ class HubertEncoder:
             return ops.linear_split(xs, ws, bias, residual=residual, epilogue=epilogue, out_split=out_split)
         return ops.linear(x, w, bias, residual=residual, epilogue=epilogue)
 
-    def positional(self, h: torch.Tensor, lens: torch.Tensor | None = None) -> torch.Tensor:
+    def positional(self, h: torch.Tensor, lens: torch.Tensor | None = None, hs: torch.Tensor | None = None
+                   ) -> torch.Tensor:
         """h + GELU(grouped conv k128 pad64 (+bias), last frame dropped) — one GEMM launch over (batch, group).
-        With ``lens`` the padding rows are zeroed first: the conv's padding must read zeros past each row's end."""
+        With ``lens`` the padding rows are zeroed first: the conv's padding must read zeros past each row's end.
+        ``hs``: h's split planes when its producer wrote them (uniform batches only)."""
         a = self.arch
         B, L, H = h.shape
         G, k = a.pos_groups, a.pos_kernel
@@ -238,7 +240,7 @@ class HubertEncoder:
                   sWg=Cg * k * Cg, bias=self.pos_b, sBg=Cg, R=h, sRb=L * H, sRg=Cg, ldr=H, sCb=L * H, sCg=Cg, ldc=H,
                   epilogue=ops.EPI_GELU)
         if self.precision == "split" and self.pos_ws is not None:
-            ops.conv_gemm_split(ops.split(h), self.pos_ws, C=out, **kw)
+            ops.conv_gemm_split(hs if (hs is not None and lens is None) else ops.split(h), self.pos_ws, C=out, **kw)
         else:
             ops.conv_gemm(h, self.pos_w, out, **kw)
         return out
@@ -324,8 +326,12 @@ class HubertEncoder:
             x = ops.pad_rows(x, a.wav_pad, x.shape[1] + 2 * a.wav_pad)
         feats = self.feature_extractor(x, lens0)
         fln, flns = self._ln(feats, self.fp_ln[0], self.fp_ln[1], split=self.fp_ws is not None)
-        h = self._linear(fln, self.fp_w, self.fp_ws, self.fp_b, xs=flns)
-        h = self.positional(h, lensL)
+        # uniform batch: the projection also writes its output as planes (the positional conv's operand; the f32
+        # copy is its residual); a variable-length batch masks the padding rows first, so it splits after that
+        dual = lensL is None and self.precision == "split" and self.fp_ws is not None and self.pos_ws is not None
+        h = self._linear(fln, self.fp_w, self.fp_ws, self.fp_b, xs=flns, out_split="dual" if dual else False)
+        h, hps = h if dual else (h, None)
+        h = self.positional(h, lensL, hs=hps)
         hs = None
         layers = self.layers[:n_layers]
         if not a.stable_layer_norm:

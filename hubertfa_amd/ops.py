@@ -150,13 +150,16 @@ _lib.register("hfa_layernorm_f32",[_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_
 _lib.register("hfa_groupnorm_f32", [_I_, _I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_,
                                     _P_, _P_])
 _lib.register("hfa_groupnorm_workspace_bytes", [_I_, _I_, _I_, _I_], ctypes.c_longlong)
+_lib.register("hfa_groupnorm_split", [_I_, _I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_,
+                                      _LL_, _I_, _LL_, _P_, _P_, _P_])
 _lib.register("hfa_conv0_workspace_bytes", [_I_, _I_], ctypes.c_longlong)
 _lib.register("hfa_conv0_f32", [_I_, _I_, _P_, _LL_, _P_, _P_, _I_, _P_, _P_, _F_, _P_, _P_, _LL_, _P_, _P_])
 _lib.register("hfa_conv0_split", [_I_, _I_, _P_, _LL_, _P_, _P_, _I_, _P_, _P_, _F_, _P_, _P_, _LL_, _LL_, _P_, _P_,
                                    _P_])
 _lib.register("hfa_units_gather_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _P_, _P_])
 _lib.register("hfa_mask_rows_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_])
-_lib.register("hfa_wav_normalize_f32", [_I_, _I_, _P_, _LL_, _F_, _P_, _LL_, _P_, _P_])
+_lib.register("hfa_wav_normalize_f32", [_I_, _I_, _P_, _LL_, _F_, _P_, _LL_, _P_, _P_, _P_])
+_lib.register("hfa_wav_normalize_workspace_bytes", [_I_], ctypes.c_longlong)
 _lib.register("hfa_pad_rows_f32", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _LL_, _P_])
 _lib.register("hfa_add_f32", [_LL_, _P_, _P_, _P_, _P_])
 _lib.register("hfa_selftest_erf", [_LL_, _P_, _P_, _P_, _P_])
@@ -299,11 +302,11 @@ def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0
                     Tin=None, sWg=0, ldw=None, bias=None, sBg=0, R=None, sRb=0, sRg=0, ldr=0, sCb=0, sCg=0, ldc,
                     epilogue=EPI_NONE, flag=None):
     """conv_gemm on split operands (As, Ws: [2, ...] f16 planes; strides in elements of one plane).  Output to f32
-    C (+R) or to split planes Cs [2, ...] (bias/GELU epilogue only)."""
+    C (+R), to split planes Cs [2, ...] (bias/GELU epilogue only), or both (dual: the planes of the final C)."""
     _need(As, torch.float16, "As", contiguous=False)
     _need(Ws, torch.float16, "Ws", contiguous=False)
-    if (C is None) == (Cs is None):
-        raise ValueError("conv_gemm_split: exactly one of C / Cs")
+    if C is None and Cs is None:
+        raise ValueError("conv_gemm_split: C and / or Cs")
     dev = (C if C is not None else Cs).device
     args = (M, N, K, Zb, G, _ptr(As), As.stride(0), sAb, sAg, ldx, stride, pad, Cg or K, Tin if Tin is not None else M,
             _ptr(Ws), Ws.stride(0), sWg, ldw if ldw is not None else K, _ptr(bias), sBg, _ptr(R), sRb, sRg, ldr,
@@ -314,26 +317,29 @@ def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0
         _lib.call("hfa_conv_gemm_split", *args, _stream(dev))
     if PROBE is None:
         return launch()
-    PROBE(_split_name(M, N, Zb * G, Cs is not None, epilogue, Cg or K), 2.0 * M * N * K * Zb * G, launch)
+    PROBE(_split_name(M, N, Zb * G, Cs is not None and C is None, epilogue, Cg or K), 2.0 * M * N * K * Zb * G, launch)
 
 
 def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, out_split=False, flag=None):
     """y = epi(x @ W^T + bias) (+ residual) with x, W given as split planes [2, ..., K] / [2, N, K]; y f32, or split
-    planes [2, ..., N] when out_split (no residual)."""
+    planes [2, ..., N] when out_split (no residual), or both as (y, planes) when out_split == "dual"."""
     K = xs.shape[-1]
     N = Ws.shape[1]
     lead = xs.shape[1:-1]
     M = 1
     for d in lead:
         M *= d
+    dual = out_split == "dual"
+    planes = out_split and not dual
     if out is None:
-        out = torch.empty(((2,) if out_split else ()) + (*lead, N), dtype=torch.float16 if out_split else torch.float32,
+        out = torch.empty(((2,) if planes else ()) + (*lead, N), dtype=torch.float16 if planes else torch.float32,
                           device=xs.device)
+    hs = torch.empty((2, *lead, N), dtype=torch.float16, device=xs.device) if dual else None
     r2 = residual.reshape(-1, N) if residual is not None else None
-    conv_gemm_split(xs, Ws, C=None if out_split else out, Cs=out if out_split else None, M=M, N=N, K=K,
+    conv_gemm_split(xs, Ws, C=None if planes else out, Cs=out if planes else hs, M=M, N=N, K=K,
                     ldx=xs.stride(-2) if xs.dim() > 2 else K, bias=bias, R=r2, ldr=r2.stride(0) if r2 is not None else 0,
                     ldc=N, epilogue=epilogue, flag=flag)
-    return out
+    return (out, hs) if dual else out
 
 
 def _lens(lens):
@@ -411,19 +417,31 @@ def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None, t
     return out, out_split
 
 
-def groupnorm(x, G, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, t_len=None):
+def groupnorm(x, G, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, t_len=None, out_split=None, flag=None):
     """GroupNorm over channels-last x [B, T, C] (stats over T x C/G per group; over t_len[b] rows if given,
-    padding rows -> 0)."""
+    padding rows -> 0).  ``out_split`` ([2, B, T, C] f16, or True to allocate): write split planes; with
+    ``out=False`` the planes only (no f32 output).  Returns the f32 output, the planes, or (f32, planes)."""
     B, T, C = x.shape
+    tl = _lens(t_len)
+    ws = torch.empty(max(1, int(_lib.lib().hfa_groupnorm_workspace_bytes(B, T, C, G))), dtype=torch.uint8,
+                     device=x.device)
+    if out_split is None or out_split is False:
+        if out is None:
+            out = torch.empty_like(x)
+        _lib.call("hfa_groupnorm_f32", B, T, C, G, _ptr(x), x.stride(0), x.stride(1), _ptr(gamma), _ptr(beta),
+                  float(eps), act, _ptr(out), out.stride(0), out.stride(1), _ptr(tl), _ptr(ws), _stream(x.device))
+        return out
+    if out_split is True:
+        out_split = torch.empty((2, B, T, C), dtype=torch.float16, device=x.device)
+    _need(out_split, torch.float16, "out_split", contiguous=False)
     if out is None:
         out = torch.empty_like(x)
-    tl = _lens(t_len)
-    ws = None
-    if B * G < 512 and T * (C // G) > 65536:          # long rows: the split-T path needs a small workspace
-        ws = torch.empty(_lib.lib().hfa_groupnorm_workspace_bytes(B, T, C, G), dtype=torch.uint8, device=x.device)
-    _lib.call("hfa_groupnorm_f32", B, T, C, G, _ptr(x), x.stride(0), x.stride(1), _ptr(gamma), _ptr(beta),
-              float(eps), act, _ptr(out), out.stride(0), out.stride(1), _ptr(tl), _ptr(ws), _stream(x.device))
-    return out
+    y = None if out is False else out
+    _lib.call("hfa_groupnorm_split", B, T, C, G, _ptr(x), x.stride(0), x.stride(1), _ptr(gamma), _ptr(beta),
+              float(eps), act, _ptr(y), y.stride(0) if y is not None else 0, y.stride(1) if y is not None else 0,
+              _ptr(tl), _ptr(out_split), out_split.stride(1), out_split.stride(2), out_split.stride(0),
+              _ptr(split_flag(x.device) if flag is None else flag), _ptr(ws), _stream(x.device))
+    return out_split if y is None else (y, out_split)
 
 
 def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, workspace=None, t0_len=None,
@@ -485,8 +503,10 @@ def wav_normalize(x, eps=1e-7, out=None, lens=None):
     if out is None:
         out = torch.empty_like(x)
     ln = _lens(lens)
+    ws = torch.empty(max(1, int(_lib.lib().hfa_wav_normalize_workspace_bytes(B))), dtype=torch.uint8,
+                     device=x.device)
     _lib.call("hfa_wav_normalize_f32", B, N, _ptr(x), x.stride(0), float(eps), _ptr(out), out.stride(0), _ptr(ln),
-              _stream(x.device))
+              _ptr(ws), _stream(x.device))
     return out
 
 

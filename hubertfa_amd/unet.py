@@ -46,17 +46,28 @@ class _Ctx:
     def split(self, x):
         return ops.split(x, flag=self.flag)
 
-    def conv(self, x, xs, w, ws, out, **kw):
+    def conv(self, x, xs, w, ws, out, out_s=None, **kw):
+        """Implicit-GEMM conv into f32 ``out``; on the split path ``out_s`` (optional [2, ...] f16) also receives
+        the output's planes (dual epilogue).  Returns (out, planes or None)."""
         if self.use_split(ws):
-            ops.conv_gemm_split(xs if xs is not None else self.split(x), ws, C=out, flag=self.flag, **kw)
-        else:
-            ops.conv_gemm(x, w, out, **kw)
-        return out
+            ops.conv_gemm_split(xs if xs is not None else self.split(x), ws, C=out, Cs=out_s, flag=self.flag, **kw)
+            return out, out_s
+        ops.conv_gemm(x, w, out, **kw)
+        return out, None
 
-    def linear(self, x, xs, w, ws, bias=None):
+    def linear(self, x, xs, w, ws, bias=None, residual=None, dual=False):
+        """Linear (+residual); ``dual`` on the split path: also the output's planes.  Returns (y, planes or None)."""
         if self.use_split(ws):
-            return ops.linear_split(xs if xs is not None else self.split(x), ws, bias, flag=self.flag)
-        return ops.linear(x, w, bias)
+            r = ops.linear_split(xs if xs is not None else self.split(x), ws, bias, residual=residual, flag=self.flag,
+                                 out_split="dual" if dual else False)
+            return r if dual else (r, None)
+        return ops.linear(x, w, bias, residual=residual), None
+
+    def planes_for(self, t):
+        """[2, *t.shape] f16 planes buffer on the split path, else None."""
+        if self.precision != "split":
+            return None
+        return torch.empty((2, *t.shape), dtype=torch.float16, device=t.device)
 
 
 class _Block:
@@ -75,24 +86,36 @@ class _Block:
         self.w1s, self.w2s = ctx.planes(self.w1), ctx.planes(self.w2)
         self.scs = ctx.planes(self.sc) if self.sc is not None else None
 
-    def __call__(self, x, lens=None):
+    def __call__(self, x, lens=None, xs=None, want_split=False):
         """lens [B] int32 (variable-length batch): rows >= lens[b] are padding — zeroed on the way in (the k3
-        convs must read zeros there) and excluded from the GroupNorm statistics, zero on the way out."""
+        convs must read zeros there) and excluded from the GroupNorm statistics, zero on the way out.  ``xs``: x's
+        split planes when its producer wrote them (only passed when they are valid for ``lens``).  GroupNorm writes
+        the second conv's operand as planes directly, and with ``want_split`` the closing LayerNorm also writes the
+        output's planes for the next split GEMM.  Returns (y, planes or None)."""
         B, T, _ = x.shape
         c = self.ctx
-        if lens is not None:
+        if lens is not None and xs is None:
             ops.mask_rows(x, lens)
-        xs = c.split(x) if c.use_split(self.w1s) or c.use_split(self.scs) else None
+        if xs is None and (c.use_split(self.w1s) or c.use_split(self.scs)):
+            xs = c.split(x)
         h = torch.empty((B, T, self.hid), dtype=torch.float32, device=x.device)
         c.conv(x, xs, self.w1, self.w1s, h, M=T, N=self.hid, K=3 * self.cin, Zb=B, sAb=T * self.cin, ldx=self.cin,
                stride=1, pad=1, Cg=self.cin, Tin=T, sCb=T * self.hid, ldc=self.hid)
-        h = ops.groupnorm(h, self.n_groups, self.gn[0], self.gn[1], 1e-5, act=ops.ACT_HARDSWISH, out=h, t_len=lens)
-        sc = x if self.sc is None else c.linear(x, xs, self.sc, self.scs)
+        hs = None
+        if c.use_split(self.w2s):        # GN(16) + Hardswish straight to the planes of the second conv's operand
+            hs = ops.groupnorm(h, self.n_groups, self.gn[0], self.gn[1], 1e-5, act=ops.ACT_HARDSWISH, out=False,
+                               t_len=lens, out_split=True, flag=c.flag)
+        else:
+            h = ops.groupnorm(h, self.n_groups, self.gn[0], self.gn[1], 1e-5, act=ops.ACT_HARDSWISH, out=h, t_len=lens)
+        sc = x if self.sc is None else c.linear(x, xs, self.sc, self.scs)[0]
         y = torch.empty((B, T, self.cout), dtype=torch.float32, device=x.device)
-        c.conv(h, None, self.w2, self.w2s, y, M=T, N=self.cout, K=3 * self.hid, Zb=B, sAb=T * self.hid, ldx=self.hid,
+        c.conv(h, hs, self.w2, self.w2s, y, M=T, N=self.cout, K=3 * self.hid, Zb=B, sAb=T * self.hid, ldx=self.hid,
                stride=1, pad=1, Cg=self.hid, Tin=T, R=sc, sRb=T * self.cout, ldr=self.cout, sCb=T * self.cout,
                ldc=self.cout)
-        return ops.layernorm(y, self.ln[0], self.ln[1], 1e-5, act=ops.ACT_HARDSWISH, out=y, t_len=lens)
+        if want_split and c.precision == "split":
+            return ops.layernorm(y, self.ln[0], self.ln[1], 1e-5, act=ops.ACT_HARDSWISH, out=y, t_len=lens,
+                                 out_split=True, flag=c.flag)
+        return ops.layernorm(y, self.ln[0], self.ln[1], 1e-5, act=ops.ACT_HARDSWISH, out=y, t_len=lens), None
 
 
 class _Down:
@@ -104,14 +127,17 @@ class _Down:
         self.ctx = ctx
         self.ws = ctx.planes(self.w) if self.cin % 32 == 0 else None
 
-    def __call__(self, x, lens=None):
+    def __call__(self, x, lens=None, xs=None, want_split=False):
+        """Stride-f conv (stride_conv.py:23-47).  Its output rows past a shorter row's length are not zero (the
+        next block masks them), so output planes (dual epilogue) are written only for a uniform batch."""
         B, T, _ = x.shape
         assert T % self.f == 0, "T is pre-padded to a multiple of factor**times (unet.py:103-106)"
         To = T // self.f
         y = torch.empty((B, To, self.cout), dtype=torch.float32, device=x.device)
-        self.ctx.conv(x, None, self.w, self.ws, y, M=To, N=self.cout, K=self.f * self.cin, Zb=B, sAb=T * self.cin,
-                      ldx=self.cin, stride=self.f, Cg=self.cin, Tin=T, bias=self.b, sCb=To * self.cout, ldc=self.cout)
-        return y
+        ys = self.ctx.planes_for(y) if (want_split and lens is None and self.ctx.use_split(self.ws)) else None
+        return self.ctx.conv(x, xs, self.w, self.ws, y, out_s=ys, M=To, N=self.cout, K=self.f * self.cin, Zb=B,
+                             sAb=T * self.cin, ldx=self.cin, stride=self.f, Cg=self.cin, Tin=T, bias=self.b,
+                             sCb=To * self.cout, ldc=self.cout)
 
 
 class _Up:
@@ -125,10 +151,14 @@ class _Up:
         self.ctx = ctx
         self.ws = ctx.planes(self.w)
 
-    def __call__(self, x, lens=None):
+    def __call__(self, x, lens=None, xs=None, want_split=False, skip=None):
+        """Transposed conv as one GEMM; ``skip`` (the UNet's skip connection, [B, f T, Cout]) is added in the
+        epilogue (the same f32 sum as a separate add), and for a uniform batch the sum's planes are written too."""
         B, T, _ = x.shape
-        y = self.ctx.linear(x, None, self.w, self.ws, self.b)
-        return y.view(B, T * self.f, self.cout)
+        dual = want_split and lens is None and self.ctx.use_split(self.ws)
+        r = skip.view(B, T, self.f * self.cout) if skip is not None else None
+        y, ys = self.ctx.linear(x, xs, self.w, self.ws, self.b, residual=r, dual=dual)
+        return y.view(B, T * self.f, self.cout), (ys.view(2, B, T * self.f, self.cout) if ys is not None else None)
 
 
 class LatticeHead:
@@ -173,35 +203,44 @@ class LatticeHead:
         r = T % self.divisible
         return T if r == 0 else T + self.divisible - r
 
-    @staticmethod
-    def _seq(mods, x, lens=None):
-        for m in mods:
-            x = m(x, lens)
-        return x
-
     @torch.no_grad()
-    def backbone(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
+    def backbone(self, x: torch.Tensor, t_pad=None, want_split=False):
         """x [B, T_pad, C_in] with T_pad % factor**times == 0 (zero rows beyond the real T).  ``t_pad`` (optional
         host ints [B]): each row's own padded length (a multiple of factor**times) in a variable-length batch; the
-        reference runs each utterance alone at that length (unet.py:103-106), so every level masks beyond it."""
+        reference runs each utterance alone at that length (unet.py:103-106), so every level masks beyond it.
+        Split path: every producer whose consumer is a split GEMM writes that operand's planes (block GroupNorm and
+        LayerNorm, down / up convs with the skip add in their epilogue), so no separate conversion runs beyond the
+        input's.  Returns y, or (y, planes) with ``want_split``."""
         lv = None
         if t_pad is not None and any(int(t) != x.shape[1] for t in t_pad):
             from .hubert import dev_lengths
             lv = [dev_lengths([int(t) // self.arch.factor ** i for t in t_pad], x.device)
                   for i in range(self.arch.times + 1)]
         L = (lambda i: None) if lv is None else (lambda i: lv[i])
-        h = [x]
+        n_enc = len(self.encoders)
+        h = [(x, None)]
         for i, enc in enumerate(self.encoders):
-            h.append(self._seq(enc, h[-1], L(i)))
-        bott = self.bottleneck
-        y = bott[2](bott[1](bott[0](h[-1]), L(self.arch.times)))
+            t = h[-1]
+            for m in enc:
+                t = m(t[0], L(i), xs=t[1], want_split=True)
+            h.append(t)
+        bd, bb, bu = self.bottleneck
+        t = bd(h[-1][0], L(self.arch.times), xs=h[-1][1], want_split=True)
+        t = bb(t[0], L(self.arch.times), xs=t[1], want_split=True)
+        t = bu(t[0], L(self.arch.times), xs=t[1], want_split=True, skip=h[n_enc][0])
         for i, dec in enumerate(self.decoders):
-            y = self._seq(dec, ops.add(y, h[-1 - i]), L(self.arch.times - 1 - i))
-        return y
+            lev = self.arch.times - 1 - i
+            last = i + 1 == len(self.decoders)
+            t = dec[0](t[0], L(lev), xs=t[1], want_split=want_split if last else True)
+            if len(dec) > 1:
+                t = dec[1](t[0], L(lev), xs=t[1], want_split=True, skip=h[n_enc - 1 - i][0])
+        return t if want_split else t[0]
 
     @torch.no_grad()
     def logits(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
-        return self.ctx.linear(self.backbone(x, t_pad), None, self.head_w, self.head_ws, self.head_b)
+        hs = self.ctx.use_split(self.head_ws)
+        y, ys = self.backbone(x, t_pad, want_split=True) if hs else (self.backbone(x, t_pad), None)
+        return self.ctx.linear(y, ys, self.head_w, self.head_ws, self.head_b)[0]
 
     @staticmethod
     def split(logits: torch.Tensor):

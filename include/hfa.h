@@ -105,8 +105,8 @@ int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, i
  * Requirements: K a multiple of 32, Cg a multiple of 32 (or of 8 and >= 32: per-lane tap tracking, f32 C only); A/W 16-B aligned with 8-half strides; |x| < 65504 for every split value
  * (producers raise *oflow otherwise; the caller recomputes on the f32 path) and |w| < 32 for W (the large
  * single-accumulator tiles form 2^11 * w1 in f16; an overflow there yields a non-finite result, which also raises
- * *oflow).  Output: f32 C (+R, 16-B rows) or,
- * with Cs non-NULL (C NULL), split planes of epi(acc + bias) (no R). */
+ * *oflow).  Output: f32 C (+R, 16-B rows), or with Cs non-NULL and C NULL split planes of epi(acc + bias) (no R),
+ * or with both non-NULL the f32 C and the split planes of that same final value (dual output). */
 int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, long long sAp, long long sAb,
                         long long sAg, int ldx, int stride, int pad, int Cg, int Tin, const uint16_t* W,
                         long long sWp, long long sWg, int ldw, const float* bias, long long sBg, const float* R,
@@ -170,6 +170,14 @@ int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs
 /* Workspace for hfa_groupnorm_f32's split-T path (long rows, few (batch, group) pairs); NULL workspace = one
  * workgroup per pair. */
 long long hfa_groupnorm_workspace_bytes(int B, int T, int C, int G);
+/* GroupNorm (+act) of channels-last [B, T, C] (resnet_block.py:145-162, GroupNorm(16) + Hardswish) writing f32 y
+ * and / or split-f16 planes ys (plane 1 at +sps halves; the next split GEMM's operand: the UNet block's second conv);
+ * C % 4 == 0, (C/G) % 4 == 0, C <= 1024, G <= 64; workspace = hfa_groupnorm_workspace_bytes(B, T, C, G) bytes; rows
+ * t >= t_len[b] are zeros and excluded from the statistics; *oflow raised for a plane value out of f16 range. */
+int hfa_groupnorm_split(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,
+                        const float* beta, float eps, int act, float* y, long long y_bs, int ldy, const int32_t* t_len,
+                        uint16_t* ys, long long ys_bs, int ldys, long long sps, int* oflow, void* workspace,
+                        hipStream_t stream);
 
 /* ---- extractor conv0 (hubertfa_amd/csrc/conv.hip) ------------------------------------------------------------
  * x [B, N] -> y [B, T0, 512] channels-last, T0 = (N-10)/5+1.  norm=1: GroupNorm(512,512) + GELU
@@ -191,9 +199,11 @@ int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w
 int hfa_units_gather_f32(int B, int U, int C, const float* units, long long u_bs, int u_ld, int n_frames, int T_pad,
                          float ratio, float* out, long long o_bs, int o_ld, const int32_t* n_frames_b,
                          const int32_t* U_b, hipStream_t stream);
-/* Wav2Vec2FeatureExtractor zero-mean/unit-variance normalisation (tools/encoder.py:94-95). */
+/* Wav2Vec2FeatureExtractor zero-mean/unit-variance normalisation (tools/encoder.py:94-95), f64 statistics over each
+ * row's own lens[b] samples; workspace: hfa_wav_normalize_workspace_bytes(B) bytes of device memory (row partials). */
+long long hfa_wav_normalize_workspace_bytes(int B);
 int hfa_wav_normalize_f32(int B, int N, const float* x, long long x_bs, float eps, float* y, long long y_bs,
-                          const int32_t* lens, hipStream_t stream);
+                          const int32_t* lens, void* workspace, hipStream_t stream);
 /* Zero rows t >= lens[b] of a [B, T, C] tensor (row t of batch b at x + b*x_bs + t*ldx): the padding rows of a
  * variable-length batch, which padded convs must read as zeros (reference: each utterance runs alone, B=1). */
 int hfa_mask_rows_f32(int B, int T, int C, float* x, long long x_bs, int ldx, const int32_t* lens,

@@ -222,6 +222,43 @@ def test_groupnorm_hardswish(B, T, C):
         assert bool((got[i, n:] == 0).all())
 
 
+@pytest.mark.parametrize("B,T,C", [(3, 864, 192), (2, 216, 384), (1, 30000, 192)])
+def test_groupnorm_split_planes(B, T, C):
+    """GroupNorm's split-plane output (the UNet block's second-conv operand) equals split(GroupNorm f32) bit for bit,
+    planes-only and dual; a row of a variable-length batch gives the same bits as that row alone."""
+    from hubertfa_amd import ops
+    d = torch.device("cuda")
+    x = (_r(B, T, C, seed=15, scale=2.0) + 0.3).to(d)
+    g, b = (_r(C, seed=16) * 0.1 + 1).to(d), (_r(C, seed=17) * 0.1).to(d)
+    y = ops.groupnorm(x, 16, g, b, 1e-5, act=ops.ACT_HARDSWISH)
+    ps = ops.groupnorm(x, 16, g, b, 1e-5, act=ops.ACT_HARDSWISH, out=False, out_split=True)
+    assert torch.equal(ps, ops.split(y))
+    y2, ps2 = ops.groupnorm(x, 16, g, b, 1e-5, act=ops.ACT_HARDSWISH, out_split=True)
+    assert torch.equal(y2, y) and torch.equal(ps2, ps)
+    lens = torch.tensor([T - 5 * i for i in range(B)], dtype=torch.int32, device=d)
+    yl, pl = ops.groupnorm(x, 16, g, b, 1e-5, act=ops.ACT_HARDSWISH, t_len=lens, out_split=True)
+    for i in range(B):
+        n = int(lens[i])
+        alone = ops.groupnorm(x[i:i + 1, :n].contiguous(), 16, g, b, 1e-5, act=ops.ACT_HARDSWISH)
+        assert torch.equal(yl[i, :n], alone[0]), i
+        assert bool((yl[i, n:] == 0).all()) and bool((pl[:, i, n:] == 0).all())
+    assert torch.equal(pl, ops.split(yl))
+
+
+def test_split_gemm_dual_output():
+    """Dual epilogue: the f32 output (+bias, +residual) and the planes of that same value in one launch."""
+    from hubertfa_amd import ops
+    d = torch.device("cuda")
+    M, N, K = 1000, 768, 512
+    x, w = _r(M, K, seed=21).to(d), (_r(N, K, seed=22) * K ** -0.5).to(d)
+    bias, res = _r(N, seed=23).to(d), _r(M, N, seed=24).to(d)
+    xs, ws = ops.split(x), ops.split(w)
+    y = ops.linear_split(xs, ws, bias, residual=res)
+    y2, ys = ops.linear_split(xs, ws, bias, residual=res, out_split="dual")
+    assert torch.equal(y2, y)
+    assert torch.equal(ys, ops.split(y))
+
+
 def test_conv0_groupnorm_gelu():
     from hubertfa_amd import ops
     B, N = 2, 16000
@@ -266,9 +303,18 @@ def test_resample_vs_restated_torchaudio():
         _close(got, ref, 1e-4, 2e-6)
 
 
-def test_wav_normalize():
+@pytest.mark.parametrize("N", [16000, 160000, 4097])
+def test_wav_normalize(N):
     from hubertfa_amd import ops
-    x = _r(3, 16000, seed=20, scale=0.3) + 0.01
+    x = _r(3, N, seed=20, scale=0.3) + 0.01
     ref = (x.double() - x.double().mean(-1, keepdim=True)) / torch.sqrt(x.double().var(-1, unbiased=False, keepdim=True) + 1e-7)
     got = ops.wav_normalize(x.cuda())
     _close(got, ref, 1e-5, 1e-5)
+    # per-row lengths: statistics over each row's own samples, zeros past it, and the same bits as the row alone
+    lens = torch.tensor([N, N - 1000, N // 3], dtype=torch.int32)
+    got = ops.wav_normalize(x.cuda(), lens=lens.cuda())
+    for i in range(3):
+        n = int(lens[i])
+        alone = ops.wav_normalize(x[i:i + 1, :n].contiguous().cuda())
+        assert torch.equal(got[i, :n], alone[0]), i
+        assert bool((got[i, n:] == 0).all())
