@@ -14,6 +14,7 @@ Reference call sites exercised:
   * tools/alignment_decoder.py:232-294  AlignmentDecoder._decode        -> dp_cases.npz (path, confidence)
   * tools/alignment_decoder.py:26-143   AlignmentDecoder.decode         -> decode_cases.npz
   * networks/g2p/*.py                   G2P plugins                     -> g2p.json
+  * networks/g2p/dictionary_g2p.py over dictionary/*.txt (the CLI's default -d)  -> g2p_dicts.json
   * tools/post_processing.py:68-105     post_processing                 -> postproc.json
   * tools/encoder.py:56-59              grid gather index (torch expr)  -> gather_index.npz
   * networks/hubert/model.py            HubertSoft.units                -> hubert_soft.npz
@@ -217,6 +218,39 @@ def gen_g2p():
     print("g2p done")
 
 
+def gen_g2p_dicts():
+    """The reference's own shipped dictionaries (infer.py:37-41 default -d dictionary/opencpop-extension.txt, and the
+    jyutping / japanese ones) through its DictionaryG2P: lyrics-like texts with OOV words, repeated spaces and
+    every entry shape the files hold.  Stored: the texts, the expected outputs, and the dictionary entries the texts
+    touch (so the test also runs where /root/reference is absent)."""
+    from networks.g2p import DictionaryG2P
+    rng = np.random.default_rng(7)
+    res = {}
+    for name in ("opencpop-extension", "jyutping_dict", "japanese_dict_full"):
+        dpath = os.path.join(REF, "dictionary", name + ".txt")
+        g = DictionaryG2P(dictionary=dpath)
+        words = sorted(g.dictionary)
+        texts = []
+        for n in (1, 3, 8, 20, 40):
+            texts.append(" ".join(words[int(i)] for i in rng.integers(0, len(words), n)))
+        texts.append(" ".join([words[0], "not_a_word", words[-1], "  ", words[len(words) // 2]]))
+        multi = [w for w in words if len(g.dictionary[w]) > 2][:5]
+        if multi:
+            texts.append(" ".join(multi))
+        cases, used = [], set()
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            for t in texts:
+                ph, w, m = g(t)
+                cases.append({"text": t, "ph_seq": list(ph), "word_seq": list(w), "map": [int(x) for x in m]})
+                used.update(x for x in t.split(" ") if x in g.dictionary)
+        res[name] = {"cases": cases, "n_entries": len(words),
+                     "entries": {w: g.dictionary[w] for w in sorted(used)}}
+    with open(os.path.join(HERE, "g2p_dicts.json"), "w") as f:
+        json.dump(res, f, indent=1, ensure_ascii=False)
+    print("g2p dictionaries done")
+
+
 def gen_postproc():
     from tools.post_processing import post_processing
 
@@ -370,7 +404,8 @@ def main():
     _import_reference()
     which = sys.argv[1:] or ["dp", "decode", "g2p", "postproc", "gather", "hubert", "unet"]
     for w in which:
-        {"dp": gen_dp_cases, "decode": gen_decode_cases, "g2p": gen_g2p, "postproc": gen_postproc,
+        {"dp": gen_dp_cases, "decode": gen_decode_cases, "g2p": gen_g2p, "g2p_dicts": gen_g2p_dicts,
+         "postproc": gen_postproc,
          "gather": gen_gather_index, "hubert": gen_hubert, "unet": gen_unet}[w]()
 
 

@@ -34,6 +34,29 @@ def test_g2p_plugins_match_reference():
                 assert [int(x) for x in m] == case["map"]
 
 
+@pytest.mark.parametrize("name", ["opencpop-extension", "jyutping_dict", "japanese_dict_full"])
+def test_g2p_reference_dictionaries(name, tmp_path):
+    """DictionaryG2P over the reference's shipped dictionaries (the CLI's default -d opencpop-extension.txt,
+    infer.py:37-41): parsed from the reference's own file when present (entry count must match), else from the
+    entries the golden texts use (tests/golden/g2p_dicts.json, made by the reference's DictionaryG2P)."""
+    from hubertfa_amd.g2p import DictionaryG2P
+    gold = json.load(open(os.path.join(GOLDEN, "g2p_dicts.json"), encoding="utf-8"))[name]
+    path = tmp_path / (name + ".txt")
+    path.write_text("".join(f"{w}\t{' '.join(p)}\n" for w, p in gold["entries"].items()), encoding="utf-8")
+    gs = [DictionaryG2P(dictionary=str(path))]
+    ref_file = os.path.join("/root/reference/dictionary", name + ".txt")
+    if os.path.exists(ref_file):
+        gs.append(DictionaryG2P(dictionary=ref_file))
+        assert len(gs[-1].dictionary) == gold["n_entries"]
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for g in gs:
+            for case in gold["cases"]:
+                ph, w, m = g(case["text"])
+                assert (list(ph), list(w), [int(x) for x in m]) == (case["ph_seq"], case["word_seq"], case["map"]), \
+                    case["text"]
+
+
 def test_post_processing_matches_reference():
     from hubertfa_amd.post_processing import post_processing
     gold = json.load(open(os.path.join(GOLDEN, "postproc.json")))
