@@ -1485,7 +1485,7 @@ enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_
        SCFG_256x128_NS3 = 6, SCFG_256x256_1 = 7, SCFG_256x128_1 = 8, SCFG_128x128_1 = 9, SCFG_128x64_1 = 10,
        SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_256x64_1 = 14,
        SCFG_N48 = 15, SCFG_WIN = 16, SCFG_256x256_M16 = 17, SCFG_128x128_M16 = 18, SCFG_128x64_M16 = 19,
-       SCFG_256x64_M16 = 20, SCFG_COUNT = 21 };
+       SCFG_256x64_M16 = 20, SCFG_256x128_M16_S3 = 21, SCFG_128x256_M16_S3 = 22, SCFG_COUNT = 23 };
 struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; int MF; };
 constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 128, 2, 2, 2, 2, false, 32}, {128, 128, 2, 2, 2, 2, false, 32}, {128, 64, 2, 2, 2, 2, false, 32},
@@ -1496,7 +1496,7 @@ constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 48, 4, 1, 2, 2, true, 32},       // SCFG_N48: gemm_split48_kernel (16x16x32 MFMA), not gemm_split_kernel
     {256, 48, 8, 1, 3, 1, true, 32},       // SCFG_WIN: posconv_split_kernel (LDS-resident input window)
     {256, 256, 2, 4, 2, 1, true, 32, 16}, {128, 128, 2, 2, 2, 2, true, 32, 16}, {128, 64, 2, 2, 2, 2, true, 32, 16},
-    {256, 64, 4, 1, 2, 2, true, 32, 16}};
+    {256, 64, 4, 1, 2, 2, true, 32, 16}, {256, 128, 4, 2, 3, 1, true, 32, 16}, {128, 256, 2, 4, 3, 1, true, 32, 16}};
 thread_local int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 thread_local int g_win_nb = 3;   // column blocks of the window kernel the name query reports (N / 16)
 
@@ -1599,6 +1599,8 @@ int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
         case SCFG_128x128_M16: return launch_split_cfg<EPI, OUTS, SCFG_128x128_M16>(p, Z, st);
         case SCFG_128x64_M16: return launch_split_cfg<EPI, OUTS, SCFG_128x64_M16>(p, Z, st);
         case SCFG_256x64_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x64_M16>(p, Z, st);
+        case SCFG_256x128_M16_S3: return launch_split_cfg<EPI, OUTS, SCFG_256x128_M16_S3>(p, Z, st);
+        case SCFG_128x256_M16_S3: return launch_split_cfg<EPI, OUTS, SCFG_128x256_M16_S3>(p, Z, st);
         default: return launch_split_cfg<EPI, OUTS, SCFG_128x128>(p, Z, st);
     }
 }
