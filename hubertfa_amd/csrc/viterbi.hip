@@ -442,7 +442,11 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
 }
 
 int hfa_viterbi_tuning(int force_k) {
-    g_force_k = (force_k == 2 || force_k == 4 || force_k == 8) ? force_k : 0;
+    if (force_k != 0 && force_k != 2 && force_k != 4 && force_k != 8) {
+        hfa::set_error("hfa_viterbi_tuning: states per lane must be 0 (automatic), 2, 4 or 8 (got %d)", force_k);
+        return HFA_EINVAL;
+    }
+    g_force_k = force_k;
     return HFA_OK;
 }
 
