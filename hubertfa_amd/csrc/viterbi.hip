@@ -202,7 +202,14 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
 //      and an ordered compaction of the emitted (s, t) pairs.
 constexpr int kBtThreads = 256;
 constexpr int kBtChunkBytes = 32768;
+constexpr int kBtLdsFrames = 64000;          // path in LDS up to this many frames (32 KB chunk + 125 KB path)
 
+// GPATH: the chased path (state | emit << 31 per frame) goes to frame_conf's own memory in global memory instead of
+// LDS (Tmax > kBtLdsFrames: a long-form lattice past 160 KB of LDS, reference: any T): the compaction reads it there
+// (non-temporal loads: L2, never a stale L1 line), then the confidence pass overwrites it tile by tile, reading each
+// tile's path entries before any of its stores and carrying the previous tile's last state through LDS.  Outputs are
+// identical to the LDS form.
+template <bool GPATH>
 __global__ __launch_bounds__(kBtThreads) void viterbi_backtrack_kernel(
     int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
     const float* __restrict__ dp, const int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id,
@@ -211,7 +218,8 @@ __global__ __launch_bounds__(kBtThreads) void viterbi_backtrack_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int8_t* chunk = reinterpret_cast<int8_t*>(smem);
     uint16_t* path = reinterpret_cast<uint16_t*>(smem + kBtChunkBytes);
-    __shared__ int s_cur;
+    uint32_t* gpath = reinterpret_cast<uint32_t*>(frame_conf) + (size_t)blockIdx.x * Tmax;
+    __shared__ int s_cur, s_carry;
     __shared__ int warp_cnt[kBtThreads / 64];
 
     const int b = blockIdx.x;
@@ -257,7 +265,8 @@ __global__ __launch_bounds__(kBtThreads) void viterbi_backtrack_kernel(
             for (int t = hi; t >= lo; --t) {
                 const int code = (t == 0) ? -1 : (int)chunk[(t - lo) * W + (s - c0)];
                 const int emit = code != 0;
-                path[t] = (uint16_t)(s | (emit << 15));
+                if constexpr (GPATH) gpath[t] = (uint32_t)s | ((uint32_t)emit << 31);
+                else path[t] = (uint16_t)(s | (emit << 15));
                 if (emit) s -= code;
             }
             s_cur = s;
@@ -270,13 +279,19 @@ __global__ __launch_bounds__(kBtThreads) void viterbi_backtrack_kernel(
         const int t = t0 + tid;
         int emit = 0, s = 0;
         if (t < T) {
-            const uint16_t p = path[t];
-            s = p & 0x7fff;
-            emit = p >> 15;
-            const float v = d[(size_t)t * Smax + s];
-            float vp = 0.0f;
-            if (t > 0) vp = d[(size_t)(t - 1) * Smax + (path[t - 1] & 0x7fff)];
-            frame_conf[(size_t)b * Tmax + t] = expf(v - vp);
+            if constexpr (GPATH) {
+                const uint32_t p = __builtin_nontemporal_load(gpath + t);
+                s = (int)(p & 0x7fffffffu);
+                emit = (int)(p >> 31);
+            } else {
+                const uint16_t p = path[t];
+                s = p & 0x7fff;
+                emit = p >> 15;
+                const float v = d[(size_t)t * Smax + s];
+                float vp = 0.0f;
+                if (t > 0) vp = d[(size_t)(t - 1) * Smax + (path[t - 1] & 0x7fff)];
+                frame_conf[(size_t)b * Tmax + t] = expf(v - vp);
+            }
         }
         const unsigned long long m = __ballot(emit);
         const int lane = tid & 63, w = tid >> 6;
@@ -295,6 +310,25 @@ __global__ __launch_bounds__(kBtThreads) void viterbi_backtrack_kernel(
         __syncthreads();
     }
     if (tid == 0) n_out[b] = base;
+    if constexpr (GPATH) {                      // confidences over the path, in place of it
+        if (tid == 0) s_carry = 0;
+        for (int t0 = 0; t0 < T; t0 += kBtThreads) {
+            const int t = t0 + tid;
+            int s = 0, sp = 0;
+            __syncthreads();                    // s_carry of the previous tile is set
+            if (t < T) {
+                s = (int)(__builtin_nontemporal_load(gpath + t) & 0x7fffffffu);
+                sp = tid > 0 ? (int)(__builtin_nontemporal_load(gpath + t - 1) & 0x7fffffffu) : s_carry;
+            }
+            __syncthreads();                    // every path entry of this tile has been read
+            if (t < T) {
+                if (tid == kBtThreads - 1) s_carry = s;
+                const float v = d[(size_t)t * Smax + s];
+                const float vp = t > 0 ? d[(size_t)(t - 1) * Smax + sp] : 0.0f;
+                frame_conf[(size_t)b * Tmax + t] = expf(v - vp);
+            }
+        }
+    }
 }
 
 // Lattice prologue: one wavefront per DP frame row (alignment_decoder.py:35-84, 239-242).
@@ -453,8 +487,8 @@ int hfa_viterbi_tuning(int force_k) {
 int hfa_viterbi_backtrack(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const float* dp,
                           const int8_t* bt, const int32_t* ph_seq_id, int32_t* ph_idx_seq, int32_t* ph_time_int,
                           int32_t* n_out, float* frame_conf, hipStream_t stream) {
-    if (B < 0 || Tmax < 0 || Smax < 0 || Smax > 32767 || Tmax > 65536) {
-        hfa::set_error("hfa_viterbi_backtrack: bad sizes (Smax<=32767, Tmax<=65536)");
+    if (B < 0 || Tmax < 0 || Smax < 0 || Smax > 32767) {
+        hfa::set_error("hfa_viterbi_backtrack: bad sizes (Smax<=32767)");
         return HFA_EINVAL;
     }
     if (B == 0) return HFA_OK;
@@ -462,17 +496,22 @@ int hfa_viterbi_backtrack(int B, int Tmax, int Smax, const int32_t* T, const int
         hfa::set_error("hfa_viterbi_backtrack: null pointer");
         return HFA_EINVAL;
     }
+    if (Tmax > kBtLdsFrames) {                  // long lattice: the path in global memory (frame_conf's buffer)
+        hipLaunchKernelGGL(viterbi_backtrack_kernel<true>, dim3(B), dim3(kBtThreads), kBtChunkBytes, stream, Tmax,
+                           Smax, T, S, dp, bt, ph_seq_id, ph_idx_seq, ph_time_int, n_out, frame_conf);
+        return hfa::check_launch("hfa_viterbi_backtrack");
+    }
     const size_t lds = kBtChunkBytes + sizeof(uint16_t) * (size_t)(Tmax > 0 ? Tmax : 1);
     if (lds > 65536) {
-        hipError_t e = hipFuncSetAttribute((const void*)viterbi_backtrack_kernel,
+        hipError_t e = hipFuncSetAttribute((const void*)viterbi_backtrack_kernel<false>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) {
             hfa::set_error("hfa_viterbi_backtrack: cannot reserve %zu B of LDS: %s", lds, hipGetErrorString(e));
             return -(int)e;
         }
     }
-    hipLaunchKernelGGL(viterbi_backtrack_kernel, dim3(B), dim3(kBtThreads), lds, stream, Tmax, Smax, T, S, dp, bt,
-                       ph_seq_id, ph_idx_seq, ph_time_int, n_out, frame_conf);
+    hipLaunchKernelGGL(viterbi_backtrack_kernel<false>, dim3(B), dim3(kBtThreads), lds, stream, Tmax, Smax, T, S, dp,
+                       bt, ph_seq_id, ph_idx_seq, ph_time_int, n_out, frame_conf);
     return hfa::check_launch("hfa_viterbi_backtrack");
 }
 

@@ -54,7 +54,7 @@ int hfa_viterbi_tuning(int force_k);
 /* hfa_viterbi_backtrack replaces the backward half of AlignmentDecoder._decode,
  * tools/alignment_decoder.py:263-288: end state, serial backtrack, frame_confidence = exp(diff([0]+dp_path)).
  * Outputs: ph_idx_seq/ph_time_int [B,Tmax] i32 (first n_out[b] valid, ascending t), frame_conf [B,Tmax] f32.
- * Smax <= 32767, Tmax <= 65536. */
+ * Smax <= 32767; any Tmax (past 64000 frames the chased path is kept in frame_conf's buffer instead of LDS). */
 int hfa_viterbi_backtrack(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const float* dp,
                           const int8_t* bt, const int32_t* ph_seq_id, int32_t* ph_idx_seq, int32_t* ph_time_int,
                           int32_t* n_out, float* frame_conf, hipStream_t stream);
