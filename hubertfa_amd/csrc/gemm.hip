@@ -1485,7 +1485,8 @@ enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_
        SCFG_256x128_NS3 = 6, SCFG_256x256_1 = 7, SCFG_256x128_1 = 8, SCFG_128x128_1 = 9, SCFG_128x64_1 = 10,
        SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_256x64_1 = 14,
        SCFG_N48 = 15, SCFG_WIN = 16, SCFG_256x256_M16 = 17, SCFG_128x128_M16 = 18, SCFG_128x64_M16 = 19,
-       SCFG_256x64_M16 = 20, SCFG_256x128_M16_S3 = 21, SCFG_128x256_M16_S3 = 22, SCFG_COUNT = 23 };
+       SCFG_256x64_M16 = 20, SCFG_256x128_M16_S3 = 21, SCFG_128x256_M16_S3 = 22, SCFG_256x192_M16 = 23,
+       SCFG_192x256_M16 = 24, SCFG_COUNT = 25 };
 struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; int MF; };
 constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 128, 2, 2, 2, 2, false, 32}, {128, 128, 2, 2, 2, 2, false, 32}, {128, 64, 2, 2, 2, 2, false, 32},
@@ -1496,7 +1497,8 @@ constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 48, 4, 1, 2, 2, true, 32},       // SCFG_N48: gemm_split48_kernel (16x16x32 MFMA), not gemm_split_kernel
     {256, 48, 8, 1, 3, 1, true, 32},       // SCFG_WIN: posconv_split_kernel (LDS-resident input window)
     {256, 256, 2, 4, 2, 1, true, 32, 16}, {128, 128, 2, 2, 2, 2, true, 32, 16}, {128, 64, 2, 2, 2, 2, true, 32, 16},
-    {256, 64, 4, 1, 2, 2, true, 32, 16}, {256, 128, 4, 2, 3, 1, true, 32, 16}, {128, 256, 2, 4, 3, 1, true, 32, 16}};
+    {256, 64, 4, 1, 2, 2, true, 32, 16}, {256, 128, 4, 2, 3, 1, true, 32, 16}, {128, 256, 2, 4, 3, 1, true, 32, 16},
+    {256, 192, 4, 2, 2, 1, true, 32, 16}, {192, 256, 2, 4, 2, 1, true, 32, 16}};
 thread_local int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 thread_local int g_win_nb = 3;   // column blocks of the window kernel the name query reports (N / 16)
 
@@ -1527,6 +1529,14 @@ inline int split_cfg(const GemmP& p, int Z) {
         return SCFG_256x64_M16;            // grouped positional conv at Cg = 64 (Hubert-large): 1.26x the 128x64 tile
     if (p.N <= 64 || blocks128 < 256) return SCFG_128x64_M16;
     if (blocks256 < 128 || p.N < 512) return SCFG_128x128_M16;
+    // 256 x 192 where the 256 x 256 grid ends in a thin last round and the 192-wide one does not: QKV at N = 2304
+    // (567 tiles = 2.2 rounds -> 756 = 2.95), 12 % faster than 128 x 128 and 256 x 256 (profiles/r02/split_192.txt).
+    // One-round grids (N = 768: 189 vs 252 tiles) gain nothing: the chip is power-limited, and the fewer busy CUs
+    // run a higher clock.
+    const long long blocks192 = (long long)((p.M + 255) / 256) * ((p.N + 191) / 192) * Z;
+    auto fill = [](long long b) { return (double)b / (double)(((b + 255) / 256) * 256); };
+    if (p.N % 192 == 0 && blocks256 > 256 && fill(blocks256) < 0.85 && fill(blocks192) > fill(blocks256) + 0.1)
+        return SCFG_256x192_M16;
     // rounds of resident tiles (256 x 256: one per CU; 128 x 128: two per CU) times the time per round, with the
     // larger tile's 1.12x per-FLOP speed (profiles/r02/split_mf16.txt): QKV (N = 2304, 567 big tiles = 2.2 rounds)
     // goes to 128 x 128, the extractor convs, FFN and 768-wide projections stay on 256 x 256
@@ -1601,6 +1611,8 @@ int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
         case SCFG_256x64_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x64_M16>(p, Z, st);
         case SCFG_256x128_M16_S3: return launch_split_cfg<EPI, OUTS, SCFG_256x128_M16_S3>(p, Z, st);
         case SCFG_128x256_M16_S3: return launch_split_cfg<EPI, OUTS, SCFG_128x256_M16_S3>(p, Z, st);
+        case SCFG_256x192_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x192_M16>(p, Z, st);
+        case SCFG_192x256_M16: return launch_split_cfg<EPI, OUTS, SCFG_192x256_M16>(p, Z, st);
         default: return launch_split_cfg<EPI, OUTS, SCFG_128x128>(p, Z, st);
     }
 }

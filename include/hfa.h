@@ -119,8 +119,11 @@ const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int e
  * 8 256x128 single accumulator (4 waves), 9 128x128 single accumulator, 10 128x64 single accumulator, 11/12
  * 256x256 single accumulator with 16-deep K-steps and 4/3 stages, 13 128x128 likewise with 4 stages, 14 256x64
  * single accumulator (4 waves of 64x64), 15 the N = 48 kernel (16x16x32 MFMA; chosen automatically for N = 48
- * with f32 output, e.g. the grouped positional conv at Cg = 48).  The
- * automatic choice uses single-accumulator tiles only (7, 9, 10, 14, 15): results then do not depend on the tile. */
+ * with f32 output, e.g. the grouped positional conv at Cg = 48), 16 the LDS-window positional conv kernel, 17-20
+ * the 256x256 / 128x128 / 128x64 / 256x64 single-accumulator tiles on v_mfma_f32_16x16x32_f16, 21/22 256x128 /
+ * 128x256 likewise with 3 stages, 23/24 256x192 / 192x256 likewise (one round of 252 tiles for N = 768 at
+ * B*T = 15968 rows).  The automatic choice uses single-accumulator tiles only: results then do not depend on the
+ * tile. */
 int hfa_gemm_split_tuning(int cfg);
 /* x [rows, cols] f32 (row stride ldx) -> split planes y (row stride ldy, plane 1 at +sp); raises *oflow (if
  * non-NULL) for |x| >= 65504 or a non-finite x. */

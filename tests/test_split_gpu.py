@@ -128,10 +128,10 @@ def test_split_grouped_posconv_general_taps(H, G, k, L, cfg):
 
 
 @pytest.mark.parametrize("outs", [False, True])
-@pytest.mark.parametrize("cfgs", [(0, 17, 18, 19, 20), (7, 9, 10, 8, 11, 12, 13, 14)])
+@pytest.mark.parametrize("cfgs", [(0, 17, 18, 19, 20, 23, 24), (7, 9, 10, 8, 11, 12, 13, 14)])
 def test_split_single_acc_tiles_bit_identical(outs, cfgs):
-    """Every automatic tile (17 = 256x256, 18 = 128x128, 19 = 128x64, 20 = 256x64: single-accumulator 16x16x32
-    tiles) gives the same bits, so a row's result does not depend on the batch (and so the grid) it runs in; the
+    """Every automatic tile (17 = 256x256, 18 = 128x128, 19 = 128x64, 20 = 256x64, 23 = 256x192, 24 = 192x256:
+    single-accumulator 16x16x32 tiles) gives the same bits, so a row's result does not depend on the batch (and so the grid) it runs in; the
     32x32x16 tiles (tuning only) agree among themselves the same way."""
     from hubertfa_amd import ops, _lib
     d = torch.device("cuda")
@@ -150,7 +150,7 @@ def test_split_single_acc_tiles_bit_identical(outs, cfgs):
 
 
 @pytest.mark.parametrize("cfg,outs", [(7, False), (8, False), (9, True), (10, False), (17, False), (18, True),
-                                      (19, False), (20, True)])
+                                      (19, False), (20, True), (23, True), (24, False)])
 def test_split_single_acc_weight_range_flag(cfg, outs):
     """Single-accumulator tiles form 2^11 * hi(w) in f16: a weight with |w| >= 32 overflows there, and the
     non-finite result raises the split flag (the caller re-runs on the f32 GEMM) instead of passing silently."""
