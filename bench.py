@@ -36,13 +36,16 @@ sys.path.insert(0, REPO)
 METRIC = "aligned audio sec/sec (RTF^-1) + frames/sec, Hubert-base, 1/2/4/8 MI355X"
 F32_MFMA_PEAK_TFLOPS = 157.3
 # split-f16 GEMM (gemm_split_kernel): 3 exact f16 x f16 partial products per f32-equivalent MAC on
-# v_mfma_f32_32x32x16_f16 (1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz = 2516.6 TFLOP/s dense), so the
-# f32-equivalent ceiling of the scheme is a third of that.
+# v_mfma_f32_16x16x32_f16 (1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz = 2516.6 TFLOP/s dense), so the
+# f32-equivalent ceiling of the scheme is a third of that.  The opt-in f16 mode (--precision f16: instantiations
+# ending in ", true>") runs one product per MAC: its ceiling is the f16 dense peak itself.
 F16_MFMA_PEAK_TFLOPS = 2516.6
 SPLIT_F32EQ_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
 
 
 def mfma_peak(kernel: str) -> float:
+    if kernel.startswith("gemm_split_kernel") and kernel.endswith(", true>"):
+        return F16_MFMA_PEAK_TFLOPS
     split = kernel.startswith("gemm_split_kernel") or kernel.startswith("attn_fwd_split_kernel")
     return SPLIT_F32EQ_PEAK_TFLOPS if split else F32_MFMA_PEAK_TFLOPS
 HBM_PEAK_GBPS = 8000.0             # MI355X HBM3E, MI355X_MICROARCH.md
@@ -65,12 +68,15 @@ def parse():
     ap.add_argument("--probe", default="auto",
                     help="kernel instantiation to time; auto = the one carrying the most FLOPs in a warmup census")
     ap.add_argument("--serial", action="store_true", help="one stream per step (no head/encoder overlap)")
+    ap.add_argument("--precision", default="split", choices=["split", "f16"],
+                    help="split: f32-class split-f16x3 (the headline); f16: opt-in fast mode, one f16 product per MAC "
+                         "in the encoder's split GEMMs (f16-class accuracy, not the reference's f32)")
     ap.add_argument("--chunk-seconds", type=float, default=None,
                     help="long-form: encode overlapping windows of this length (config 5 chunked; B=1 only)")
     ap.add_argument("--host-input", action="store_true",
                     help="waves start in host memory and are uploaded inside every step (task.upload, as infer.py) (PCIe-inclusive "
                          "rate; the headline value keeps inputs resident in HBM)")
-    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r01", "traffic_r01.json"),
+    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r02", "traffic_r02.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
 
@@ -215,6 +221,8 @@ def main():
     ckpt = synth_checkpoint(encoder=encoder, model_path="synth:0", seed=1)
     task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
     task.on_predict_start()
+    if args.precision == "f16":
+        task.unitsEncoder.model.f16 = True
     B = args.batch
     wav_np, ph_seqs, word_seqs, p2ws = make_inputs(B, args.seconds, args.words, seed0=1000 * (rank + 1))
     wav = wav_dev = torch.from_numpy(wav_np).to(dev)
@@ -298,9 +306,13 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "audio_s/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32 (split-f16x3)", "data": "synthetic",
-        "arithmetic": "f32 operands as split-f16 pairs (x = x1 + 2^-11 x2) on v_mfma_f32_32x32x16_f16, 3 exact products per "
-                      "f32 MAC, f32 accumulate; norms/softmax/DP in f32 (DP f32/f64 as the reference)",
+        "vs_baseline": None, "dtype": "f32 (split-f16x3)" if args.precision == "split" else "f16 (opt-in fast mode)",
+        "data": "synthetic",
+        "arithmetic": ("f32 operands as split-f16 pairs (x = x1 + 2^-11 x2) on v_mfma_f32_16x16x32_f16, 3 exact products "
+                       "per f32 MAC, f32 accumulate; norms/softmax/DP in f32 (DP f32/f64 as the reference)"
+                       if args.precision == "split" else
+                       "opt-in fast mode: encoder GEMMs on the f16 high planes alone (one product per MAC, f32 "
+                       "accumulate); attention, grouped positional conv and UNet head split-f16x3; norms/softmax/DP f32"),
         "config": {"workload": f"{config_name(args.encoder, world, B, args.seconds)}"
                                f"{'' if args.chunk_seconds is None else f', chunked {args.chunk_seconds:g} s windows'}: "
                                f"B={B} x {args.seconds:g} s 16 kHz utterances per GPU, "
@@ -309,14 +321,15 @@ def main():
                                f"pipelined one batch behind the GPU",
                    "encoder": encoder, "do_normalize": bool(task.unitsEncoder.model.arch.do_normalize),
                    "global_batch": world * B, "seconds_per_utterance": args.seconds, "dp_frames": n_frames,
-                   "states": len(ph_seqs[0]), "parallelism": f"utterance-dp{world}"},
+                   "states": len(ph_seqs[0]), "parallelism": f"utterance-dp{world}", "precision": args.precision},
         "frames_per_s": frames_ps,
         "realtime_factor": value,
         "encoder_tflops": world * B * (hub_flops + head_flops) * args.steps / el / 1e12,
         "roofline": {"bound": "mfma", "kernel": probe_name, "achieved": achieved, "peak": mfma_peak(probe_name),
                      "unit": "TFLOP/s", "frac": achieved / mfma_peak(probe_name) if achieved else None,
-                     "peak_basis": ("f32-equivalent FLOPs of the split-f16 scheme: 3 f16 MFMA products per f32 MAC, "
-                                    "2516.6 TF f16 dense / 3" if probe_name.startswith("gemm_split_kernel")
+                     "peak_basis": ("f16 MFMA dense peak (one-product f16 mode)" if probe_name.endswith(", true>")
+                                    else "f32-equivalent FLOPs of the split-f16 scheme: 3 f16 MFMA products per f32 "
+                                    "MAC, 2516.6 TF f16 dense / 3" if probe_name.startswith("gemm_split_kernel")
                                     else "f32 MFMA dense peak"),
                      "traffic": traffic, "launches": ps["launches"], "avg_launch_ms": ps["avg_ms"],
                      "flops_per_launch": ps["avg_flops"]},

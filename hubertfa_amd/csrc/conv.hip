@@ -124,7 +124,7 @@ __global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const fl
     if (MODE == 0) {
         ma = stats[(b * C0 + c0) * 2]; ra = stats[(b * C0 + c0) * 2 + 1];
         mb = stats[(b * C0 + c0 + 1) * 2]; rb = stats[(b * C0 + c0 + 1) * 2 + 1];
-        sa = gamma[c0]; ha = beta[c0]; sb = gamma[c0 + 1]; hb = beta[c0 + 1];
+        sa = ra * gamma[c0]; ha = beta[c0]; sb = rb * gamma[c0 + 1]; hb = beta[c0 + 1];   // rstd * gamma folded
     } else {
         ha = bias ? bias[c0] : 0.f;
         hb = bias ? bias[c0 + 1] : 0.f;
@@ -137,8 +137,8 @@ __global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const fl
         float va = conv10(wa, xs + t * ST);
         float vb = conv10(wb, xs + t * ST);
         if (MODE == 0) {
-            va = hfa::gelu_fast((va - ma) * ra * sa + ha);
-            vb = hfa::gelu_fast((vb - mb) * rb * sb + hb);
+            va = hfa::gelu_fast((va - ma) * sa + ha);
+            vb = hfa::gelu_fast((vb - mb) * sb + hb);
         } else {
             va += ha;
             vb += hb;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(NT) void conv0_apply8_kernel(int N, int T0, const f
         if (MODE == 0) {
             m[c] = stats[(b * C0 + c0 + c) * 2];
             r[c] = stats[(b * C0 + c0 + c) * 2 + 1];
-            sc[c] = gamma[c0 + c];
+            sc[c] = r[c] * gamma[c0 + c];   // rstd * gamma folded
             sh[c] = beta[c0 + c];
         } else {
             m[c] = 0.f;
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(NT) void conv0_apply8_kernel(int N, int T0, const f
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             float v = conv10(w[c], xt);
-            if (MODE == 0) v = hfa::gelu_fast((v - m[c]) * r[c] * sc[c] + sh[c]);
+            if (MODE == 0) v = hfa::gelu_fast((v - m[c]) * sc[c] + sh[c]);
             else v += sh[c];
             asm volatile("" : "+v"(v));   // split the rounded f32 value: no fusing its last multiply into the f16 cvt
             bad |= !(__builtin_fabsf(v) < 65504.0f);
@@ -216,6 +216,121 @@ __global__ __launch_bounds__(NT) void conv0_apply8_kernel(int N, int T0, const f
     }
     if (bad && oflow) *oflow = 1;
 }
+
+
+// ---- conv0 on the f32-input MFMA --------------------------------------------------------------------------------
+// v_mfma_f32_16x16x4_f32 is bit for bit a k-ordered fmaf chain, D = fma(a3, b3, fma(a2, b2, fma(a1, b1, fma(a0, b0, C))))
+// (cdna_hip_programming.md §3, "FP32-input MFMA"), so the 10-tap conv as three MFMAs (taps 0-3, 4-7, 8-11 with
+// w10 = w11 = 0, C = 0 first) gives exactly conv10's values: the apply pass below is bit-identical to
+// conv0_apply8_kernel.  Measured (scripts/conv0_bench.py, B = 32 x 10 s): 559 vs 565 us -- the apply pass is bound
+// by VALU issue (~38 VALU ops per output in apply8, ~30 here: GELU ~21 of them; 2.1 GB written would take ~0.35 ms
+// at the 6 TB/s store rate), and the f32 MFMA (32 cycles per 16x16x4 per SIMD) takes most of what it frees.  The
+// same conv in the statistics pass with f64 accumulation was slower (254 vs 176 us: 131 VGPRs), so that pass stays
+// on the VALU.
+// Block: 8 waves over a CH-frame chunk; wave w owns channels 64 w + [0, 64) as four 16-channel MFMA blocks and walks
+// the chunk in groups of 16 frames.  MFMA rows are channels, columns frames.  Block 2p + q, row r -> channel
+// 64 w + 32 p + 8 (r >> 2) + 4 q + (r & 3): lane l (g = l >> 4, frame j = l & 15) then holds, in the D tiles of
+// blocks 2p and 2p + 1, channels 64 w + 32 p + 8 g + [0, 8) of frame j -- one 16-B split-plane piece per pair.
+constexpr int MNT = 512;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void stage_chunk_m(float* xs, const float* xb, int t0, int nt, int N) {
+    const int n = nt * ST + (KW - ST);                  // samples of frames < nt; zeros beyond (taps 10, 11 and
+    for (int i = threadIdx.x; i < CH * ST + 12; i += MNT) {   // frames >= nt read them)
+        const int idx = t0 * ST + i;
+        xs[i] = (i < n && idx < N) ? xb[idx] : 0.0f;
+    }
+}
+
+__device__ __forceinline__ void conv0_wfrag(const float* __restrict__ w0, int wave, int lane, float (&wf)[4][3]) {
+    const int i = lane & 15, k = lane >> 4;
+#pragma unroll
+    for (int blk = 0; blk < 4; ++blk) {
+        const int ch = 64 * wave + 32 * (blk >> 1) + 8 * (i >> 2) + 4 * (blk & 1) + (i & 3);
+#pragma unroll
+        for (int s = 0; s < 3; ++s) wf[blk][s] = 4 * s + k < KW ? w0[ch * KW + 4 * s + k] : 0.0f;
+    }
+}
+
+// conv0 of frames f0 + [0, 16) for the wave's four channel blocks
+__device__ __forceinline__ void conv0_group(const float* xs, int f0, int lane, const float (&wf)[4][3],
+                                            f32x4 (&d)[4]) {
+    const float* xl = xs + ST * (f0 + (lane & 15)) + (lane >> 4);
+    float xb[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) xb[s] = xl[4 * s];
+#pragma unroll
+    for (int blk = 0; blk < 4; ++blk) {
+        d[blk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < 3; ++s) d[blk] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[blk][s], xb[s], d[blk], 0, 0, 0);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(MNT) void conv0_apply_mfma_kernel(int N, int T0, const float* __restrict__ x,
+                                                               long long x_bs, const float* __restrict__ w0,
+                                                               const float* __restrict__ stats,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta,
+                                                               const float* __restrict__ bias,
+                                                               _Float16* __restrict__ yh, long long y_bs,
+                                                               long long y_sp, int* __restrict__ oflow) {
+    __shared__ float xs[CH * ST + 12];
+    const int b = blockIdx.y, chunk = blockIdx.x;
+    const int t0 = chunk * CH;
+    const int nt = min(CH, T0 - t0);
+    stage_chunk_m(xs, x + b * x_bs, t0, nt, N);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+    float wf[4][3];
+    conv0_wfrag(w0, wave, lane, wf);
+    float m[16], r[16], sc[16], sh[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int ch = 64 * wave + 32 * (c >> 3) + 8 * g + (c & 7);
+        if (MODE == 0) {
+            m[c] = stats[(b * C0 + ch) * 2];
+            r[c] = stats[(b * C0 + ch) * 2 + 1];
+            sc[c] = r[c] * gamma[ch];
+            sh[c] = beta[ch];
+        } else {
+            m[c] = 0.f;
+            r[c] = sc[c] = 1.f;
+            sh[c] = bias ? bias[ch] : 0.f;
+        }
+    }
+    __syncthreads();
+    _Float16* yb = yh + b * y_bs + (long long)t0 * C0 + 64 * wave + 8 * g;
+    bool bad = false;
+    for (int f0 = 0; f0 < nt; f0 += 16) {
+        f32x4 d[4];
+        conv0_group(xs, f0, lane, wf, d);
+        const bool live = f0 + j < nt;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            f16x8 h1, h2;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int c = 8 * p + e;
+                float v = d[2 * p + (e >> 2)][e & 3];
+                if (MODE == 0) v = hfa::gelu_fast((v - m[c]) * sc[c] + sh[c]);
+                else v += sh[c];
+                asm volatile("" : "+v"(v));   // split the rounded f32 value: no fusing its last multiply into the cvt
+                bad |= live && !(__builtin_fabsf(v) < 65504.0f);
+                h1[e] = (_Float16)v;
+                h2[e] = (_Float16)((v - (float)h1[e]) * 2048.0f);
+            }
+            if (live) {
+                _Float16* dst = yb + (long long)(f0 + j) * C0 + 32 * p;
+                *reinterpret_cast<f16x8*>(dst) = h1;
+                *reinterpret_cast<f16x8*>(dst + y_sp) = h2;
+            }
+        }
+    }
+    if (bad && oflow) *oflow = 1;
+}
+
+thread_local int g_conv0_mode = 0;   // hfa_conv0_tuning: 0 MFMA conv (default), 1 the VALU kernels
 
 }  // namespace
 
@@ -252,7 +367,10 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
         hipLaunchKernelGGL(conv0_stats_kernel, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, part, t0_len);
         hipLaunchKernelGGL(conv0_reduce_kernel, dim3(C0 / 64, B), dim3(NT), 0, stream, T0, nchunk, part, eps, stats,
                            t0_len);
-        if (outs && vec8)
+        if (outs && vec8 && g_conv0_mode == 0)
+            hipLaunchKernelGGL((conv0_apply_mfma_kernel<0>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, stats,
+                               gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
+        else if (outs && vec8)
             hipLaunchKernelGGL((conv0_apply8_kernel<0>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats, gamma,
                                beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
         else if (outs)
@@ -261,6 +379,9 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
         else
             hipLaunchKernelGGL((conv0_apply_kernel<0, false>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, y, y_bs, y_sp, oflow);
+    } else if (outs && vec8 && g_conv0_mode == 0) {
+        hipLaunchKernelGGL((conv0_apply_mfma_kernel<1>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, nullptr,
+                           nullptr, nullptr, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
     } else if (outs && vec8) {
         hipLaunchKernelGGL((conv0_apply8_kernel<1>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, nullptr, nullptr,
                            nullptr, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
@@ -293,6 +414,17 @@ int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w
                     long long y_sp, int* oflow, const int32_t* t0_len, hipStream_t stream) {
     return conv0_launch(B, N, x, x_bs, w0, bias, norm, gamma, beta, eps, workspace, ys, y_bs, y_sp, true, oflow,
                         t0_len, stream);
+}
+
+// Kernel choice for A/B timing and the bit-identity tests: 0 the MFMA conv (default), 1 the VALU kernels.  Per
+// calling thread.
+int hfa_conv0_tuning(int mode) {
+    if (mode != 0 && mode != 1) {
+        hfa::set_error("hfa_conv0_tuning: mode %d is not 0 or 1", mode);
+        return HFA_EINVAL;
+    }
+    g_conv0_mode = mode;
+    return HFA_OK;
 }
 
 }  // extern "C"

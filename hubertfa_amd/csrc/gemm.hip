@@ -22,6 +22,7 @@
 // summed exactly once.  Block ids are remapped so consecutive logical tiles (same A rows, adjacent W columns)
 // share an XCD's L2.
 #include "hfa_common.h"
+#include "hfa.h"
 
 namespace {
 
@@ -763,11 +764,14 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
 // form; the chip holds a higher clock under it (1.96-2.04 vs 1.73-1.85 GHz, same MFMA busy).  The next stage's DMA
 // pieces go out two per A block over the first blocks of a K-step instead of all at its top (+2-6 %), so the
 // two waves of a SIMD do not both stall on DMA issue while the matrix pipe idles.
+// F16 (opt-in fast mode, MF 16 tiles only): the operands' high planes alone, one product a1 w1 per MAC -- f16-class
+// accuracy (inputs rounded to 11 significand bits, f32 accumulation); the low planes are neither fetched nor read.
 template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT, bool GT, bool ONE, int BK,
-          int MF = 32>
+          int MF = 32, bool F16 = false>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const GemmP p) {
     static_assert(BK == 16 || BK == 32, "BK 16 or 32");
     static_assert(MF == 32 || (MF == 16 && ONE && BK == 32), "16x16x32 tiles: single accumulator, BK 32");
+    static_assert(!F16 || (MF == 16 && NS == 2 && !GT), "the one-product mode runs on the 2-stage 16x16x32 tiles");
     constexpr int CPR = BK / 8, NW = WM * WN;                // 16-B chunks per row per plane
     constexpr int RPP = 64 / CPR, KK = BK / 16;               // rows per 1-KiB DMA piece, MFMA k-steps per K-step
     constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
@@ -837,7 +841,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
                 const int t = a_t0[d] + a_tap[d];
                 const unsigned vo = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + a_c[d]) * 2) : hfa::DMA_OOB;
                 hfa::dma16(vo, rA1, 0u, base + d * NW * 1024);
-                hfa::dma16(vo, rA2, 0u, base + PA * 2 + d * NW * 1024);
+                if constexpr (!F16) hfa::dma16(vo, rA2, 0u, base + PA * 2 + d * NW * 1024);
                 a_c[d] += BK;
                 if (a_c[d] >= p.Cg) {                     // Cg >= BK: at most one tap boundary per K-step
                     a_c[d] -= p.Cg;
@@ -845,7 +849,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
                 }
             } else {
                 hfa::dma16(voffA[d], rA1, (unsigned)cur_c0 * 2, base + d * NW * 1024);
-                hfa::dma16(voffA[d], rA2, (unsigned)cur_c0 * 2, base + PA * 2 + d * NW * 1024);
+                if constexpr (!F16) hfa::dma16(voffA[d], rA2, (unsigned)cur_c0 * 2, base + PA * 2 + d * NW * 1024);
             }
         }
     };
@@ -855,7 +859,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         for (int d = 0; d < DB; ++d) {
             if (IW % NW != 0 && wave + d * NW >= IW) continue;
             hfa::dma16(voffW[d], rW1, (unsigned)cur_k0 * 2, base + 2 * PA * 2 + d * NW * 1024);
-            hfa::dma16(voffW[d], rW2, (unsigned)cur_k0 * 2, base + (2 * PA + PW) * 2 + d * NW * 1024);
+            if constexpr (!F16) hfa::dma16(voffW[d], rW2, (unsigned)cur_k0 * 2, base + (2 * PA + PW) * 2 + d * NW * 1024);
         }
     };
     auto advance = [&]() {
@@ -878,6 +882,17 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     // advance() after the last
     auto issue_piece = [&](int stage, int q) {
         const unsigned base = lds0 + stage * STAGE * 2 + wave * 1024;
+        if (F16 && (q & 1)) {                                     // low planes: not used
+            if (GT && q < 2 * DA) {
+                const int d = q >> 1;
+                a_c[d] += BK;
+                if (a_c[d] >= p.Cg) {
+                    a_c[d] -= p.Cg;
+                    ++a_tap[d];
+                }
+            }
+            return;
+        }
         if (q < 2 * DA) {
             const int d = q >> 1, pl = q & 1;
             if (IA % NW != 0 && wave + d * NW >= IA) return;
@@ -931,8 +946,10 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 w1[j] = st[rdB + j * 16 * CPR];
-                w2[j] = st[rdB + PW / 8 + j * 16 * CPR];
-                w1s[j] = w1[j] * (_Float16)2048.0f;
+                if constexpr (!F16) {
+                    w2[j] = st[rdB + PW / 8 + j * 16 * CPR];
+                    w1s[j] = w1[j] * (_Float16)2048.0f;
+                }
             }
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
@@ -941,12 +958,19 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
                     for (int q = 0; q < DN; ++q)
                         if ((q / 2 < NI ? q / 2 : NI - 1) == i) issue_piece(nstage, q);
                 }
-                const f16x8 a1 = st[rdA + i * 16 * CPR], a2 = st[rdA + PA / 8 + i * 16 * CPR];
+                const f16x8 a1 = st[rdA + i * 16 * CPR];
+                if constexpr (F16) {
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, w1s[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, w2[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, w1[j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, w1[j], acc[i][j], 0, 0, 0);
+                } else {
+                    const f16x8 a2 = st[rdA + PA / 8 + i * 16 * CPR];
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, w1s[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, w2[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, w1[j], acc[i][j], 0, 0, 0);
+                    }
                 }
             }
             if (more) advance();
@@ -956,10 +980,12 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
             }
             stage = stage + 1 == NS ? 0 : stage + 1;
         }
+        if constexpr (!F16) {
 #pragma unroll
-        for (int i = 0; i < NI; ++i)
+            for (int i = 0; i < NI; ++i)
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) acc[i][j] *= 1.0f / 2048.0f;
+                for (int j = 0; j < NJ; ++j) acc[i][j] *= 1.0f / 2048.0f;
+        }
         static_assert(NW * 32 * 36 * 4 <= NS * STAGE * 2, "epilogue slabs exceed the staging LDS");
         __syncthreads();
         float* slab = reinterpret_cast<float*>(smem) + wave * (32 * 36);
@@ -1550,7 +1576,7 @@ inline int gt_cfg(int cfg) {
     return kSplitGeom[cfg].BN == 64 ? SCFG_128x64_M16 : SCFG_128x128_M16;
 }
 
-inline void split_name(int cfg, int epi, bool outs, bool gt, char* buf, int len) {
+inline void split_name(int cfg, int epi, bool outs, bool gt, bool f16, char* buf, int len) {
     if (cfg == SCFG_N48) {
         snprintf(buf, len, "gemm_split48_kernel<%d>", epi);
         return;
@@ -1561,24 +1587,47 @@ inline void split_name(int cfg, int epi, bool outs, bool gt, char* buf, int len)
     }
     if (gt) cfg = gt_cfg(cfg);
     const SplitGeom& g = kSplitGeom[cfg];
-    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, %s, %d, %d>", epi, g.BM, g.BN, g.WM,
-             g.WN, g.NS, g.OCC, outs ? "true" : "false", gt ? "true" : "false", g.ONE ? "true" : "false", g.BK,
-             g.MF ? g.MF : 32);
+    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, %s, %d, %d, %s>", epi, g.BM, g.BN,
+             g.WM, g.WN, g.NS, g.OCC, outs ? "true" : "false", gt ? "true" : "false", g.ONE ? "true" : "false", g.BK,
+             g.MF ? g.MF : 32, f16 ? "true" : "false");
 }
 
-template <int EPI, bool OUTS, int CFG, bool GT = false>
+template <int EPI, bool OUTS, int CFG, bool GT = false, bool F16 = false>
 int launch_split_cfg(GemmP p, int Z, hipStream_t st) {
     constexpr SplitGeom g = kSplitGeom[CFG];
     dim3 grid;
     if (int rc = set_grid(p, g.BM, g.BN, grid, Z)) return rc;
     hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE, g.BK,
-                                          g.MF ? g.MF : 32>),
+                                          g.MF ? g.MF : 32, F16>),
                        grid, dim3(64 * g.WM * g.WN), 0, st, p);
     return hfa::check_launch("hfa_conv_gemm_split");
 }
 
+// the one-product fast mode (HFA_GEMM_F16): the automatic 2-stage 16x16x32 tiles; other choices map to them
+inline int f16_cfg(int cfg) {
+    switch (cfg) {
+        case SCFG_256x256_M16: case SCFG_128x128_M16: case SCFG_128x64_M16: case SCFG_256x64_M16:
+        case SCFG_256x192_M16: return cfg;
+        case SCFG_256x256_1: case SCFG_256x128_M16_S3: case SCFG_128x256_M16_S3: case SCFG_192x256_M16:
+            return SCFG_256x256_M16;
+        default: return kSplitGeom[cfg].BN == 64 ? SCFG_128x64_M16 : SCFG_128x128_M16;
+    }
+}
+
 template <int EPI, bool OUTS>
-int launch_split(GemmP p, int Z, int cfg, hipStream_t st) {
+int launch_split_f16(GemmP p, int Z, int cfg, hipStream_t st) {
+    switch (f16_cfg(cfg)) {
+        case SCFG_256x256_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x256_M16, false, true>(p, Z, st);
+        case SCFG_128x64_M16: return launch_split_cfg<EPI, OUTS, SCFG_128x64_M16, false, true>(p, Z, st);
+        case SCFG_256x64_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x64_M16, false, true>(p, Z, st);
+        case SCFG_256x192_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x192_M16, false, true>(p, Z, st);
+        default: return launch_split_cfg<EPI, OUTS, SCFG_128x128_M16, false, true>(p, Z, st);
+    }
+}
+
+template <int EPI, bool OUTS>
+int launch_split(GemmP p, int Z, int cfg, hipStream_t st, bool f16) {
+    if (f16 && p.Cg % 32 == 0) return launch_split_f16<EPI, OUTS>(p, Z, cfg, st);
     if (p.Cg % 32) {                          // general taps (Cg % 8 == 0): the two common tiles only
         if constexpr (OUTS) {
             hfa::set_error("hfa_conv_gemm_split: Cg %% 32 != 0 takes no split output");
@@ -1809,6 +1858,8 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
         hfa::set_error("hfa_conv_gemm_split: C/R (or Cs) rows must be 16-B (8-B) aligned");
         return HFA_EINVAL;
     }
+    const bool f16 = (epilogue & HFA_GEMM_F16) != 0;
+    epilogue &= ~HFA_GEMM_F16;
     if (epilogue != EPI_NONE && epilogue != EPI_GELU) {
         hfa::set_error("hfa_conv_gemm_split: unknown epilogue %d", epilogue);
         return HFA_EINVAL;
@@ -1843,17 +1894,20 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
         else hipLaunchKernelGGL(gemm_split48_kernel<EPI_NONE>, grid, dim3(256), 0, stream, p);
         return hfa::check_launch("hfa_conv_gemm_split");
     }
-    if (Cs && !C) return epilogue == EPI_GELU ? launch_split<EPI_GELU, true>(p, Z, cfg, stream)
-                                              : launch_split<EPI_NONE, true>(p, Z, cfg, stream);
-    return epilogue == EPI_GELU ? launch_split<EPI_GELU, false>(p, Z, cfg, stream)
-                                : launch_split<EPI_NONE, false>(p, Z, cfg, stream);
+    if (Cs && !C) return epilogue == EPI_GELU ? launch_split<EPI_GELU, true>(p, Z, cfg, stream, f16)
+                                              : launch_split<EPI_NONE, true>(p, Z, cfg, stream, f16);
+    return epilogue == EPI_GELU ? launch_split<EPI_GELU, false>(p, Z, cfg, stream, f16)
+                                : launch_split<EPI_NONE, false>(p, Z, cfg, stream, f16);
 }
 
 const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue, int Cg) {
     GemmP p = make_params(M, N, 32, 1, nullptr, 0, 0, 0, 1, 0, Cg, 1, nullptr, 0, 0);
     p.Ch = out_split ? reinterpret_cast<_Float16*>(g_name) : nullptr;    // only its null-ness is read
     g_win_nb = N / 16;
-    split_name(split_cfg(p, Z), epilogue, out_split != 0, Cg % 32 != 0, g_name, sizeof(g_name));
+    const bool f16 = (epilogue & HFA_GEMM_F16) != 0 && Cg % 32 == 0;
+    int cfg = split_cfg(p, Z);
+    if (f16 && cfg != SCFG_WIN && cfg != SCFG_N48) cfg = f16_cfg(cfg);
+    split_name(cfg, epilogue & ~HFA_GEMM_F16, out_split != 0, Cg % 32 != 0, f16, g_name, sizeof(g_name));
     return g_name;
 }
 

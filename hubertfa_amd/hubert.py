@@ -79,13 +79,17 @@ class HubertEncoder:
     multiples of 32) on the split-f16 MFMA GEMM (gemm.hip gemm_split_kernel: f32-class accuracy, 2-2.5x the f32
     MFMA rate), the operands carried as f16 plane pairs written directly by their producers; "f32" runs every
     GEMM on the f32 MFMA.  A split producer that meets a value outside f16 range raises ops.split_flag(), and
-    the caller re-runs that batch with precision "f32" (task.ForcedAlignmentTask)."""
+    the caller re-runs that batch with precision "f32" (task.ForcedAlignmentTask).  "f16" (opt-in fast mode, not
+    f32-class): the split path with every split GEMM on the operands' high planes alone, one f16 product per MAC
+    (ops.GEMM_F16); attention and the grouped positional conv keep the three products."""
 
     def __init__(self, arch: HubertArch, state_dict: dict, device: str | torch.device = "cuda",
                  precision: str = "split"):
-        if precision not in ("split", "f32"):
-            raise ValueError(f"precision must be 'split' or 'f32', not {precision!r}")
+        if precision not in ("split", "f32", "f16"):
+            raise ValueError(f"precision must be 'split', 'f32' or 'f16', not {precision!r}")
         self.arch = arch
+        self.f16 = precision == "f16"           # a flag beside precision: the f32 re-run of the range guard
+        precision = "split" if self.f16 else precision      # switches precision only
         self.precision = precision
         self.device = torch.device(device)
         sd = _strip(state_dict)
@@ -203,7 +207,7 @@ class HubertEncoder:
                       epilogue=ops.EPI_NONE if layer_norm else ops.EPI_GELU)
             if split_in:
                 ops.conv_gemm_split(h, self.conv_ws[i], C=None if split_out else out, Cs=out if split_out else None,
-                                    **kw)
+                                    f16=self.f16, **kw)
             else:
                 ops.conv_gemm(h, self.conv_w[i], out, **kw)
             if layer_norm:
@@ -221,7 +225,8 @@ class HubertEncoder:
         if self.precision == "split" and ws is not None:
             if xs is None:
                 xs = ops.split(x)
-            return ops.linear_split(xs, ws, bias, residual=residual, epilogue=epilogue, out_split=out_split)
+            return ops.linear_split(xs, ws, bias, residual=residual, epilogue=epilogue, out_split=out_split,
+                                    f16=self.f16)
         return ops.linear(x, w, bias, residual=residual, epilogue=epilogue)
 
     def positional(self, h: torch.Tensor, lens: torch.Tensor | None = None, hs: torch.Tensor | None = None
@@ -240,7 +245,8 @@ class HubertEncoder:
                   sWg=Cg * k * Cg, bias=self.pos_b, sBg=Cg, R=h, sRb=L * H, sRg=Cg, ldr=H, sCb=L * H, sCg=Cg, ldc=H,
                   epilogue=ops.EPI_GELU)
         if self.precision == "split" and self.pos_ws is not None:
-            ops.conv_gemm_split(hs if (hs is not None and lens is None) else ops.split(h), self.pos_ws, C=out, **kw)
+            ops.conv_gemm_split(hs if (hs is not None and lens is None) else ops.split(h), self.pos_ws, C=out,
+                                f16=self.f16, **kw)
         else:
             ops.conv_gemm(h, self.pos_w, out, **kw)
         return out

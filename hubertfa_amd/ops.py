@@ -124,6 +124,7 @@ def lattice_prologue(frame_logits, edge_logits, ph_seq_id, T, S, want_frame_prob
 # Encoder kernels (gemm.hip, attention.hip, norm.hip, conv.hip, misc.hip)
 # ------------------------------------------------------------------------------------------------------------
 EPI_NONE, EPI_GELU = 0, 1
+GEMM_F16 = 0x100          # hfa.h HFA_GEMM_F16: opt-in one-product f16 arithmetic on the split GEMM
 ACT_NONE, ACT_GELU, ACT_HARDSWISH = 0, 1, 2
 
 _P_, _I_, _LL_, _F_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
@@ -144,6 +145,7 @@ _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_
 _lib.register("hfa_attention_split", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _LL_,
                                       _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _P_])
 _lib.register("hfa_attention_split_tuning", [_I_])
+_lib.register("hfa_conv0_tuning", [_I_])
 _lib.register("hfa_layernorm_split", [_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_,
                                       _LL_, _P_, _P_])
 _lib.register("hfa_layernorm_f32",[_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_])
@@ -300,9 +302,12 @@ def _split_name(M, N, Z, out_split, epilogue, Cg) -> str:
 
 def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None,
                     Tin=None, sWg=0, ldw=None, bias=None, sBg=0, R=None, sRb=0, sRg=0, ldr=0, sCb=0, sCg=0, ldc,
-                    epilogue=EPI_NONE, flag=None):
+                    epilogue=EPI_NONE, flag=None, f16=False):
     """conv_gemm on split operands (As, Ws: [2, ...] f16 planes; strides in elements of one plane).  Output to f32
-    C (+R), to split planes Cs [2, ...] (bias/GELU epilogue only), or both (dual: the planes of the final C)."""
+    C (+R), to split planes Cs [2, ...] (bias/GELU epilogue only), or both (dual: the planes of the final C).
+    ``f16``: the opt-in fast mode (high planes only, one f16 product per MAC: f16-class accuracy)."""
+    if f16:
+        epilogue |= GEMM_F16
     _need(As, torch.float16, "As", contiguous=False)
     _need(Ws, torch.float16, "Ws", contiguous=False)
     if C is None and Cs is None:
@@ -320,7 +325,8 @@ def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0
     PROBE(_split_name(M, N, Zb * G, Cs is not None and C is None, epilogue, Cg or K), 2.0 * M * N * K * Zb * G, launch)
 
 
-def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, out_split=False, flag=None):
+def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, out_split=False, flag=None,
+                 f16=False):
     """y = epi(x @ W^T + bias) (+ residual) with x, W given as split planes [2, ..., K] / [2, N, K]; y f32, or split
     planes [2, ..., N] when out_split (no residual), or both as (y, planes) when out_split == "dual"."""
     K = xs.shape[-1]
@@ -338,7 +344,7 @@ def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, 
     r2 = residual.reshape(-1, N) if residual is not None else None
     conv_gemm_split(xs, Ws, C=None if planes else out, Cs=out if planes else hs, M=M, N=N, K=K,
                     ldx=xs.stride(-2) if xs.dim() > 2 else K, bias=bias, R=r2, ldr=r2.stride(0) if r2 is not None else 0,
-                    ldc=N, epilogue=epilogue, flag=flag)
+                    ldc=N, epilogue=epilogue, flag=flag, f16=f16)
     return (out, hs) if dual else out
 
 

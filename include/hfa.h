@@ -106,7 +106,11 @@ int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, i
  * (producers raise *oflow otherwise; the caller recomputes on the f32 path) and |w| < 32 for W (the large
  * single-accumulator tiles form 2^11 * w1 in f16; an overflow there yields a non-finite result, which also raises
  * *oflow).  Output: f32 C (+R, 16-B rows), or with Cs non-NULL and C NULL split planes of epi(acc + bias) (no R),
- * or with both non-NULL the f32 C and the split planes of that same final value (dual output). */
+ * or with both non-NULL the f32 C and the split planes of that same final value (dual output).
+ * epilogue | HFA_GEMM_F16: opt-in fast mode -- the high planes alone, one f16 product per MAC (A1.W1, f32
+ * accumulation: f16-class accuracy, about 2.5x the split rate); ignored by the grouped positional conv kernels
+ * (Cg not a multiple of 32 or N = 48/64 windows), which keep the three products. */
+#define HFA_GEMM_F16 0x100
 int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, long long sAp, long long sAb,
                         long long sAg, int ldx, int stride, int pad, int Cg, int Tin, const uint16_t* W,
                         long long sWp, long long sWg, int ldw, const float* bias, long long sBg, const float* R,
@@ -216,6 +220,9 @@ int hfa_pad_rows_f32(int B, int N, const float* x, long long x_bs, int left, int
                      hipStream_t stream);
 /* Self-test: y_nb = the branch-free erf of every GELU epilogue, y_ref = device erff (must be bit-identical). */
 int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hipStream_t stream);
+/* conv0 kernel choice (per calling thread): 0 = the conv on the f32-input MFMA (default; bit-identical, the MFMA
+ * is an exact k-ordered fmaf chain), 1 = the VALU kernels.  Returns HFA_EINVAL for another value. */
+int hfa_conv0_tuning(int mode);
 /* Self-test: y = the GELU applied by every fused epilogue (GEMM, LayerNorm/GroupNorm act, conv0). */
 int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream);
 /* out = a + b (UNet skip connection, networks/layer/backbone/unet.py:114). */

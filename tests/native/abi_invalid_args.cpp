@@ -91,6 +91,7 @@ int main() {
     CHECK(hfa_attention_split(1, 12, 10, 96, 0.125f, hp, 0, 0, 64, hp, 0, 0, 64, hp, 0, 0, 64, hp, 0, 0, 64,
                                    nullptr, st), "attention_split head_dim");
     CHECK(hfa_attention_split_tuning(3), "attention tuning waves=3");
+    CHECK(hfa_conv0_tuning(2), "conv0 tuning mode=2");
     // norms
     CHECK(hfa_layernorm_f32(10, 6, fp, 8, nullptr, 0, fp, fp, 1e-5f, 0, fp, 8, 0, nullptr, st), "LN C%4");
     CHECK(hfa_layernorm_f32(10, 8, fmis, 8, nullptr, 0, fp, fp, 1e-5f, 0, fp, 8, 0, nullptr, st),
@@ -129,7 +130,7 @@ int main() {
     CHECK(hfa_selftest_gelu(-1, fp, fp, st), "gelu n<0");
     CHECK(hfa_resample_f32(1, 100, fp, 100, 0, 441, fp, 16, 6, ws, fp, 300, st), "resample orig=0");
     // host queries and tuning hooks (thread-local state; name strings stay valid, bounded)
-    for (int cfg = 0; cfg < 23; ++cfg) {
+    for (int cfg = 0; cfg < 25; ++cfg) {
         hfa_gemm_split_tuning(cfg);
         const char* n = hfa_gemm_split_kernel_name(15968, 3072, 1, 1, 1, 768);
         if (!n || std::strlen(n) == 0 || std::strlen(n) >= 128) { std::printf("FAIL split name cfg %d\n", cfg); ++g_fail; }

@@ -210,6 +210,34 @@ def test_conv0_split_output_matches_f32():
     assert float((back - y32.double()).abs().max()) <= 2.0 ** -22 * float(y32.abs().max()) + 1e-9
 
 
+@pytest.mark.parametrize("N,lens", [(16000, None), (12345, None), (16000, [16000, 5003]), (97, None)])
+def test_conv0_mfma_bit_identical_to_valu(N, lens):
+    """conv0's taps on v_mfma_f32_16x16x4_f32 (an exact k-ordered fmaf chain) give the VALU kernels' bits: the
+    GroupNorm+GELU split planes, the raw conv + bias planes (LN-conv variant), and the f32 output (whose stats pass
+    also runs on the MFMA), with ragged chunk tails and per-row frame counts."""
+    from hubertfa_amd import ops, _lib
+    from hubertfa_amd.hubert import dev_lengths
+    d = torch.device("cuda")
+    B = 2
+    x = _r(B, N, seed=31, scale=0.3).to(d)
+    w0 = _r(512, 10, seed=32, scale=0.3).to(d)
+    g, bb = (1 + 0.1 * _r(512, seed=33)).to(d), (0.1 * _r(512, seed=34)).to(d)
+    tl = None if lens is None else dev_lengths([(n - 10) // 5 + 1 for n in lens], d)
+    outs = {}
+    for mode in (0, 1):
+        _lib.call("hfa_conv0_tuning", mode)
+        try:
+            outs[mode] = (ops.conv0(x, w0, gamma=g, beta=bb, out_split=True, t0_len=tl),
+                          ops.conv0(x, w0, bias=bb, out_split=True),
+                          ops.conv0(x, w0, gamma=g, beta=bb, t0_len=tl))
+        finally:
+            _lib.call("hfa_conv0_tuning", 0)
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[0][0][0].float(), outs[0][2].half().float())
+
+
 def test_encoder_split_vs_f32_precision():
     """The whole Hubert-base encoder, split vs f32 GEMMs: units agree to f32-path accuracy."""
     from hubertfa_amd import synth
