@@ -194,6 +194,104 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
         if (valid[k]) cu[s0 + k] = curr[k];
 }
 
+// S > 8192 (up to 32768 states, the backtrack's 15-bit path entries; the reference takes any S): the
+// register-resident form above runs out of lanes (16 waves x 64 x 8), so the state range is walked as up to four
+// segments of 8192 inside every time step, in order.  A lane's dp[t-1] and curr come back from global memory -- its own stores of the previous step, so
+// no value crosses threads through memory -- and the two boundary q values cross waves through the LDS slots as
+// above and segments through the last wave's slot of the previous iteration (read before this iteration's barrier,
+// so the next write of that slot, which follows the barrier, cannot overtake it).  Per-state arithmetic identical to
+// viterbi_forward_kernel (bit-exact with the oracle); slower per step (an HBM/L2 round trip per segment), which only
+// the rare > 8192-phoneme utterance pays.
+constexpr int kWideK = 8, kWideNW = 16, kWideSeg = kWideK * kWideNW * 64;
+
+__global__ __launch_bounds__(64 * kWideNW) void viterbi_forward_wide_kernel(
+    int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
+    const int32_t* __restrict__ padv, const float* __restrict__ prob_log,
+    const float* __restrict__ not_edge_log, const float* __restrict__ edge_log, double* __restrict__ curr_io,
+    float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id) {
+    constexpr int K = kWideK, NW = kWideNW;
+    __shared__ float xq[2][NW][2];
+    const int b = blockIdx.x;
+    const int g = threadIdx.x;
+    const int lane = g & 63, wave = g >> 6;
+    const int T = Tv[b];
+    const int S = Sv[b];
+    if (T <= 1 || S <= 0) return;
+    const int pad = padv ? padv[b] : (S >= 2 ? 2 : 1);
+    const size_t ts = (size_t)b * Tmax * Smax;
+    const float* pl = prob_log + ts;
+    float* d = dp + ts;
+    int8_t* bb = bt + ts;
+    const float* nEp = not_edge_log + (size_t)b * Tmax;
+    const float* Ep = edge_log + (size_t)b * Tmax;
+    const int32_t* ids = ph_seq_id + (size_t)b * Smax;
+    double* cu = curr_io + (size_t)b * Smax;
+    const double ratio = (double)T / (double)S;
+    const int nseg = (S + kWideSeg - 1) / kWideSeg;
+    int it = 0;
+    for (int t = 1; t < T; ++t) {
+        const float E = Ep[t], nE = nEp[t];
+        const size_t row = (size_t)t * Smax, prow = (size_t)(t - 1) * Smax;
+        for (int seg = 0; seg < nseg; ++seg, ++it) {
+            const int s0 = seg * kWideSeg + g * K;
+            float carry1 = neg_inf(), carry2 = neg_inf();   // q of states s0 - 1, s0 - 2 from the previous segment
+            if (seg > 0 && g == 0) {
+                carry1 = xq[(it - 1) & 1][NW - 1][0];
+                carry2 = xq[(it - 1) & 1][NW - 1][1];
+            }
+            float a[K], q[K], dprev[K], L[K];
+            double curr[K];
+            bool valid[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int s = s0 + k;
+                valid[k] = s < S;
+                dprev[k] = valid[k] ? d[prow + s] : neg_inf();
+                curr[k] = valid[k] ? cu[s] : -__builtin_inf();
+                L[k] = valid[k] ? pl[row + s] : 0.0f;
+                a[k] = __fadd_rn(dprev[k], L[k]);
+                const float a2 = __fadd_rn(a[k], E);
+                q[k] = (float)__dadd_rn((double)a2, __dmul_rn(curr[k], ratio));
+            }
+            float qm1 = from_lane_below(q[K - 1]);
+            float qm2 = from_lane_below(q[K - 2]);
+            if (lane == 63) {
+                xq[it & 1][wave][0] = q[K - 1];
+                xq[it & 1][wave][1] = q[K - 2];
+            }
+            __syncthreads();
+            if (lane == 0) {
+                qm1 = wave > 0 ? xq[it & 1][wave - 1][0] : carry1;
+                qm2 = wave > 0 ? xq[it & 1][wave - 1][1] : carry2;
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int s = s0 + k;
+                if (!valid[k]) continue;
+                const int j = s - pad + 1;
+                const bool allow3 = s >= pad && !((j < S - 1) && ids[j] != 0);
+                const float p1 = __fadd_rn(a[k], nE);
+                const float src1 = (k >= 1) ? q[k >= 1 ? k - 1 : 0] : qm1;
+                const float src2 = (k >= 2) ? q[k >= 2 ? k - 2 : 0] : (k == 1 ? qm1 : qm2);
+                const float p2 = (s == 0) ? neg_inf() : src1;
+                const float p3 = allow3 ? (pad == 1 ? src1 : src2) : neg_inf();
+                float best = p1;
+                int idx = 0;
+                if (p2 > best) { best = p2; idx = 1; }
+                if (p3 > best) { best = p3; idx = 2; }
+                d[row + s] = best;
+                bb[row + s] = (int8_t)idx;
+                const double Ld = (double)L[k];
+                double c = curr[k];
+                if (idx == 0) c = (Ld > c) ? Ld : c;
+                else c = Ld;
+                if (ids[s] == 0) c = 0.0;
+                cu[s] = c;
+            }
+        }
+    }
+}
+
 // Backtrack (alignment_decoder.py:263-288): one 256-thread workgroup per utterance.
 //   1. end state: S-2 if S>=2 and dp[T-1,S-2] > dp[T-1,S-1] and ph_seq_id[S-1]==0 else S-1 (:269-272)
 //   2. bt rows staged through LDS in chunks, one lane chases s(t) from T-1 down to 0 (serial by nature),
@@ -471,7 +569,12 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
     if (waves <= 8) HFA_FWD(8, 8, 4);
     if (waves <= 16) HFA_FWD(8, 16, 2);   // 1024 threads cap VGPRs at 128: shorter prefetch ring
 #undef HFA_FWD
-    hfa::set_error("hfa_viterbi_forward: Smax=%d exceeds 8192 states per utterance", Smax);
+    if (Smax <= 4 * kWideSeg) {  // the segmented form, up to 32768 states (the backtrack's 15-bit path entries)
+        hipLaunchKernelGGL(viterbi_forward_wide_kernel, dim3(B), dim3(64 * kWideNW), 0, stream, Tmax, Smax, T, S,
+                           prob3_pad_len, prob_log, not_edge_log, edge_log, curr, dp, bt, ph_seq_id);
+        return hfa::check_launch("hfa_viterbi_forward");
+    }
+    hfa::set_error("hfa_viterbi_forward: Smax=%d exceeds 32768 states per utterance", Smax);
     return HFA_EINVAL;
 }
 
@@ -487,8 +590,8 @@ int hfa_viterbi_tuning(int force_k) {
 int hfa_viterbi_backtrack(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const float* dp,
                           const int8_t* bt, const int32_t* ph_seq_id, int32_t* ph_idx_seq, int32_t* ph_time_int,
                           int32_t* n_out, float* frame_conf, hipStream_t stream) {
-    if (B < 0 || Tmax < 0 || Smax < 0 || Smax > 32767) {
-        hfa::set_error("hfa_viterbi_backtrack: bad sizes (Smax<=32767)");
+    if (B < 0 || Tmax < 0 || Smax < 0 || Smax > 32768) {
+        hfa::set_error("hfa_viterbi_backtrack: bad sizes (Smax<=32768)");
         return HFA_EINVAL;
     }
     if (B == 0) return HFA_OK;

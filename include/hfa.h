@@ -41,7 +41,8 @@ const char* hfa_build_arch(void);
  *   curr [B,Smax] f64 (in/out, = curr_ph_max_prob_log), dp [B,Tmax,Smax] f32 (row 0 in, rows 1.. out),
  *   bt [B,Tmax,Smax] i8 (rows 1.. out; = backtrack_s), prob3_pad_len [B] i32 or NULL (=2 if S>=2 else 1).
  * Bit-exact with the reference (f32 sums, f64 curr*(T/S) term, strict '>' ties stay->advance->skip).
- * Smax <= 8192 (one wave up to 512 states, then 8 states per lane over up to 16 waves). */
+ * Smax <= 32768 (one wave up to 512 states, then 2-8 states per lane over up to 16 waves to 8192 states, then the
+ * state range as segments of 8192 walked in order inside each time step). */
 int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S,
                         const int32_t* prob3_pad_len, const float* prob_log, const float* not_edge_log,
                         const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,
@@ -54,7 +55,7 @@ int hfa_viterbi_tuning(int force_k);
 /* hfa_viterbi_backtrack replaces the backward half of AlignmentDecoder._decode,
  * tools/alignment_decoder.py:263-288: end state, serial backtrack, frame_confidence = exp(diff([0]+dp_path)).
  * Outputs: ph_idx_seq/ph_time_int [B,Tmax] i32 (first n_out[b] valid, ascending t), frame_conf [B,Tmax] f32.
- * Smax <= 32767; any Tmax (past 64000 frames the chased path is kept in frame_conf's buffer instead of LDS). */
+ * Smax <= 32768; any Tmax (past 64000 frames the chased path is kept in frame_conf's buffer instead of LDS). */
 int hfa_viterbi_backtrack(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const float* dp,
                           const int8_t* bt, const int32_t* ph_seq_id, int32_t* ph_idx_seq, int32_t* ph_time_int,
                           int32_t* n_out, float* frame_conf, hipStream_t stream);
