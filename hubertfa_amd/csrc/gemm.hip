@@ -44,6 +44,7 @@ struct GemmP {
     const _Float16* Wh; long long sWp;
     _Float16* Ch; long long sCp;
     int* oflow;
+    int cvec;      // split f32 output: 16-B row pieces (C rows 16-B aligned); 0: scalar stores (no R, no planes)
 };
 
 enum { EPI_NONE = 0, EPI_GELU = 1 };
@@ -119,7 +120,7 @@ __device__ __forceinline__ void store_tile_lds(const GemmP& p, const f32x16 (&ac
                 if (row < p.M) {
                     f32x4 v = *reinterpret_cast<const f32x4*>(slab + r * 36 + c4);
                     float* dst = Cb + (long long)row * p.ldc + col;
-                    if (col + 3 < p.N) {
+                    if (col + 3 < p.N && p.cvec) {
                         if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + (long long)row * p.ldr + col);
                         *reinterpret_cast<f32x4*>(dst) = v;
                     } else {
@@ -706,7 +707,7 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
                 if (row < p.M) {
                     f32x4 v = *reinterpret_cast<const f32x4*>(slab + r * 36 + c4);
                     float* dst = Cb + (long long)row * p.ldc + col;
-                    if (col + 3 < p.N) {
+                    if (col + 3 < p.N && p.cvec) {
                         if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + (long long)row * p.ldr + col);
                         *reinterpret_cast<f32x4*>(dst) = v;
                     } else {
@@ -1768,6 +1769,7 @@ GemmP make_params(int M, int N, int K, int G, const float* A, long long sAb, lon
     p.R = nullptr; p.sRb = p.sRg = 0; p.ldr = 0;
     p.C = nullptr; p.sCb = p.sCg = 0; p.ldc = 0;
     p.Ah = nullptr; p.sAp = 0; p.Wh = nullptr; p.sWp = 0; p.Ch = nullptr; p.sCp = 0; p.oflow = nullptr;
+    p.cvec = 1;
     return p;
 }
 
@@ -1851,11 +1853,13 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
         hfa::set_error("hfa_conv_gemm_split: operand span past 31-bit buffer offsets");
         return HFA_EINVAL;
     }
-    const bool vc = (!C || (al16(C) && ldc % 4 == 0 && sCb % 4 == 0 && sCg % 4 == 0 &&
-                            (!R || (al16(R) && ldr % 4 == 0 && sRb % 4 == 0 && sRg % 4 == 0)))) &&
+    const bool c_al = C && al16(C) && ldc % 4 == 0 && sCb % 4 == 0 && sCg % 4 == 0;
+    const bool vc = (!C || (c_al && (!R || (al16(R) && ldr % 4 == 0 && sRb % 4 == 0 && sRg % 4 == 0))) ||
+                     (!R && !Cs && ((uintptr_t)C & 3) == 0)) &&         // unaligned f32 C alone: scalar stores
                     (!Cs || (((uintptr_t)Cs & 7) == 0 && ldc % 4 == 0 && (sCp | sCb | sCg) % 4 == 0));
     if (!vc) {
-        hfa::set_error("hfa_conv_gemm_split: C/R (or Cs) rows must be 16-B (8-B) aligned");
+        hfa::set_error("hfa_conv_gemm_split: C/R (or Cs) rows must be 16-B (8-B) aligned (an f32 C without R and "
+                       "planes may be unaligned)");
         return HFA_EINVAL;
     }
     const bool f16 = (epilogue & HFA_GEMM_F16) != 0;
@@ -1875,7 +1879,12 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
     p.R = R; p.sRb = sRb; p.sRg = sRg; p.ldr = ldr;
     p.C = C; p.Ch = reinterpret_cast<_Float16*>(Cs); p.sCp = sCp; p.sCb = sCb; p.sCg = sCg; p.ldc = ldc;
     p.oflow = oflow;
+    p.cvec = !C || c_al;
     const int Z = Zb * G, cfg = split_cfg(p, Z);
+    if ((cfg == SCFG_WIN || cfg == SCFG_N48) && !p.cvec) {
+        hfa::set_error("hfa_conv_gemm_split: the grouped positional conv kernels need 16-B aligned C rows");
+        return HFA_EINVAL;
+    }
     if (cfg == SCFG_WIN) {                     // grouped positional conv: LDS-resident input window
         dim3 grid((unsigned)((M + 255) / 256), 1, Z);
         if (N == 48 && epilogue == EPI_GELU)

@@ -1,6 +1,7 @@
 // misc.hip — bandwidth kernels around the encoder: frame-grid gather, wave normalisation, padding,
 // element-wise add, and the sinc resampler entry point (a pad + the MFMA implicit GEMM of gemm.hip).
 #include "hfa_common.h"
+#include "hfa.h"
 
 extern "C" int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg,
                                  int ldx, int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
@@ -131,6 +132,31 @@ __global__ __launch_bounds__(256) void pad_rows_kernel(int N, const float* __res
         const int s = i - left;
         y[b * y_bs + i] = (s >= 0 && s < N) ? x[b * x_bs + s] : 0.0f;
     }
+}
+
+// Split planes of a zero-padded row: y[p][b][i] (i < Lp) of v = x[b, i - front] inside [0, N), else 0 (the resampler's
+// sinc padding): hi = f16(v), lo = f16((v - hi) * 2^11); 8 samples per thread, 16-B plane stores; raises *oflow for
+// |v| >= 65504 or a non-finite v.
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(256) void pad_split_kernel(int N, int Lp, int front, const float* __restrict__ x,
+                                                        long long x_bs, _Float16* __restrict__ y, long long y_bs,
+                                                        long long y_sp, int* __restrict__ oflow) {
+    const int b = blockIdx.y;
+    bool bad = false;
+    for (int i0 = (blockIdx.x * 256 + threadIdx.x) * 8; i0 < Lp; i0 += gridDim.x * 256 * 8) {
+        f16x8_t h1, h2;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int s = i0 + k - front;
+            const float v = (s >= 0 && s < N) ? x[b * x_bs + s] : 0.0f;
+            bad |= !(__builtin_fabsf(v) < 65504.0f);
+            h1[k] = (_Float16)v;
+            h2[k] = (_Float16)((v - (float)h1[k]) * 2048.0f);
+        }
+        *reinterpret_cast<f16x8_t*>(y + b * y_bs + i0) = h1;
+        *reinterpret_cast<f16x8_t*>(y + b * y_bs + i0 + y_sp) = h2;
+    }
+    if (bad && oflow) *oflow = 1;
 }
 
 __global__ __launch_bounds__(256) void add_kernel(long long n4, const f32x4* __restrict__ a,
@@ -277,6 +303,56 @@ int hfa_resample_f32(int B, int N, const float* x, long long x_bs, int orig, int
     if (rc) return rc;
     return hfa_conv_gemm_f32((int)F, newr, Kpad, B, 1, xpad, plen, 0, orig, 1, 0, Kpad, (int)F, kernel, 0, Kpad,
                              nullptr, 0, nullptr, 0, 0, 0, y, y_bs, 0, newr, 0, stream);
+}
+
+// The same resampler on the split-f16 GEMM (f32-class accuracy): the padded rows as split planes in the workspace,
+// then one implicit GEMM whose A rows start 16-B aligned.  G = 1 (orig % 8 == 0): frame f at f * orig.  G = 8
+// (orig % 8 == 1, e.g. 441): frames f = 8 m + g as 8 groups, group g's row m at g (orig - 1) + 8 orig m (8-aligned),
+// i.e. 'g' samples before frame f's true start, so group g's taps are the kernel shifted right by g (Wg [2][G][new][Kg]
+// split planes, built by the caller; Kg % 32 == 0, Kg >= 2 width + orig + G - 1); output frame f row = C + g new +
+// m * 8 new.  y holds F8 * 8 * new floats per row for G = 8 (F8 = ceil(F / 8)), F * new for G = 1.
+static long long resample_split_lp(int N, int orig, int Kg, int G) {
+    const long long F = N / orig + 1;
+    const long long rows = G == 1 ? F : (F + 7) / 8;
+    const long long need = G == 1 ? (F - 1) * orig + Kg : 7LL * (orig - 1) + (rows - 1) * 8 * orig + Kg;
+    return (need + 7) / 8 * 8;
+}
+
+long long hfa_resample_split_workspace_bytes(int B, int N, int orig, int Kg, int G) {
+    if (B < 0 || N <= 0 || orig <= 0 || (G != 1 && G != 8)) return -1;
+    return 2LL * B * resample_split_lp(N, orig, Kg, G) * 2 + 64;
+}
+
+int hfa_resample_split(int B, int N, const float* x, long long x_bs, int orig, int newr, const uint16_t* Wg, int Kg,
+                       int G, int width, void* workspace, float* y, long long y_bs, int* oflow, hipStream_t stream) {
+    if (B < 0 || N <= 0 || orig <= 0 || newr <= 0 || width < 0 || !x || !Wg || !workspace || !y ||
+        !(G == 1 ? orig % 8 == 0 : (G == 8 && orig % 8 == 1)) || Kg % 32 || Kg < 2 * width + orig + G - 1 ||
+        ((uintptr_t)workspace & 15)) {
+        hfa::set_error("hfa_resample_split: bad arguments (G = 1 needs orig %% 8 == 0, G = 8 orig %% 8 == 1; "
+                       "Kg %% 32 == 0 and >= 2 width + orig + G - 1)");
+        return HFA_EINVAL;
+    }
+    if (B == 0) return HFA_OK;
+    const long long F = N / orig + 1;
+    const long long rows = G == 1 ? F : (F + 7) / 8;
+    if (y_bs < rows * (G == 1 ? 1 : 8) * newr) {
+        hfa::set_error("hfa_resample_split: y_bs=%lld too small", y_bs);
+        return HFA_EINVAL;
+    }
+    const long long Lp = resample_split_lp(N, orig, Kg, G);
+    if (Lp >= (1LL << 30) / 2) {
+        hfa::set_error("hfa_resample_split: row too long");
+        return HFA_EINVAL;
+    }
+    _Float16* planes = reinterpret_cast<_Float16*>(workspace);
+    hipLaunchKernelGGL(pad_split_kernel, dim3(grid1d(Lp / 8, 256, 1024), B), dim3(256), 0, stream, N, (int)Lp, width,
+                       x, x_bs, planes, Lp, (long long)B * Lp, oflow);
+    if (int rc = hfa::check_launch("hfa_resample_split")) return rc;
+    const int ldx = G == 1 ? orig : 8 * orig;
+    return hfa_conv_gemm_split((int)rows, newr, Kg, B, G, reinterpret_cast<const uint16_t*>(planes), (long long)B * Lp,
+                               Lp, G == 1 ? 0 : orig - 1, ldx, 1, 0, Kg, (int)rows, Wg, (long long)G * newr * Kg,
+                               (long long)newr * Kg, Kg, nullptr, 0, nullptr, 0, 0, 0, y, nullptr, 0, y_bs,
+                               G == 1 ? 0 : newr, G == 1 ? newr : 8 * newr, 0, oflow, stream);
 }
 
 }  // extern "C"

@@ -107,7 +107,12 @@ class UnitsEncoder:
         key = str(sample_rate)
         if key not in self.resample_kernel:
             self.resample_kernel[key] = Resampler(sample_rate, self.encoder_sample_rate, 128, self.device)
-        return self.resample_kernel[key](audio)
+        return self.resample_kernel[key](audio, split=self.split_resample)
+
+    @property
+    def split_resample(self) -> bool:
+        """Resample on the split-f16 GEMM while the encoder runs split (the range guard's f32 re-run: f32 GEMM)."""
+        return getattr(self.model, "precision", "f32") == "split"
 
     def grid(self, n_samples: int, sample_rate: int, hop_size: int):
         n_frames = n_samples // hop_size + 1
@@ -129,7 +134,7 @@ class UnitsEncoder:
         if lengths is None:
             if audio_res.size(-1) < 400:   # reference pads the ORIGINAL audio here (encoder.py:51-52)
                 audio_res = torch.nn.functional.pad(audio, (0, 400 - audio_res.size(-1)))
-            return self.model(audio_res.contiguous())
+            return self.model(audio_res)          # rows with a pitch are fine (conv0 / normalise take row strides)
         lens16 = self.resampled_lengths(lengths, sample_rate)
         if min(lens16) < 400:
             raise ValueError("utterances shorter than 400 encoder samples take the reference's padding quirk "

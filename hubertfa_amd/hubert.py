@@ -314,9 +314,11 @@ class HubertEncoder:
         frames and equal what that utterance gives alone.  ``normalized``: the caller already applied the
         do_normalize wave statistics (long-form windows of one utterance)."""
         a = self.arch
-        x = wav.float().contiguous()
+        x = wav.float()
         if x.dim() == 1:
             x = x[None]
+        if x.stride(-1) != 1:          # a row pitch is fine (every first consumer takes a row stride), a gap is not
+            x = x.contiguous()
         B, N = x.shape
         if lengths is not None and all(int(n) == N for n in lengths):
             lengths = None

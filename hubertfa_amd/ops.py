@@ -532,6 +532,32 @@ def add(a, b, out=None):
     return out
 
 
+_lib.register("hfa_resample_split_workspace_bytes", [_I_, _I_, _I_, _I_, _I_], ctypes.c_longlong)
+_lib.register("hfa_resample_split", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _I_, _I_, _I_, _P_, _P_, _LL_, _P_, _P_])
+
+
+def resample_split(x, orig, new, w_planes, G, width, out=None, workspace=None, flag=None):
+    """Sinc resample rows of x [B, N] (row stride free, unit element stride) on the split-f16 GEMM; w_planes
+    [2, G, new, Kg] (resample.Resampler builds them).  Returns the [B, ceil(new*N/orig)] view of the output."""
+    _need(x, torch.float32, "x", contiguous=False)
+    if x.stride(-1) != 1:
+        raise ValueError("resample_split: rows must have unit stride")
+    B, N = x.shape
+    Kg = w_planes.shape[-1]
+    F = N // orig + 1
+    cols = F * new if G == 1 else -(-F // 8) * 8 * new
+    if out is None:
+        out = torch.empty((B, cols), dtype=torch.float32, device=x.device)
+    if workspace is None:
+        nbytes = _lib.lib().hfa_resample_split_workspace_bytes(B, N, orig, Kg, G)
+        workspace = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+    _lib.call("hfa_resample_split", B, N, _ptr(x), x.stride(0), orig, new, _ptr(w_planes), Kg, G, width,
+              _ptr(workspace), _ptr(out), out.stride(0), _ptr(split_flag(x.device) if flag is None else flag),
+              _stream(x.device))
+    from .resample import target_length
+    return out[:, : target_length(N, orig, new)]
+
+
 def resample(x, orig, new, kernel, width, out=None, workspace=None):
     """Sinc resample rows of x [B, N] (gcd-reduced orig/new rates); returns [B, ceil(new*N/orig)] view."""
     B, N = x.shape

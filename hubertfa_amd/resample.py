@@ -50,23 +50,43 @@ def sinc_taps(orig_freq: int, new_freq: int, lowpass_filter_width: int, rolloff:
 
 
 class Resampler:
-    """GPU resampler for one (orig, new, width) triple; taps are uploaded once."""
+    """GPU resampler for one (orig, new, width) triple; taps are uploaded once.
+
+    ``split=True`` (the encoder's split precision) runs it on the split-f16 GEMM (ops.resample_split, f32-class)
+    when the gcd-reduced orig is 0 or 1 mod 8 (16 k -> 44.1 k: 160; 44.1 k -> 16 k: 441): 16-B aligned A rows, with
+    frames 8m + g as eight groups whose taps are shifted right by g for orig % 8 == 1; else, and for ``split=False``
+    (the range guard's f32 re-run), the f32-MFMA GEMM (ops.resample)."""
 
     def __init__(self, orig_freq: int, new_freq: int, lowpass_filter_width: int = 6, device=None):
         self.identity = int(orig_freq) == int(new_freq)
         if self.identity:
             return
         taps, self.width, self.orig, self.new = sinc_taps(orig_freq, new_freq, lowpass_filter_width)
+        dev = torch.device(device or "cuda")
         kw = taps.shape[1]
         kpad = (kw + 15) // 16 * 16
         padded = np.zeros((self.new, kpad), np.float32)
         padded[:, :kw] = taps
-        self.kernel = torch.from_numpy(padded).to(device or "cuda")
+        self.kernel = torch.from_numpy(padded).to(dev)
+        self.G = 1 if self.orig % 8 == 0 else (8 if self.orig % 8 == 1 else 0)
+        self.w_planes = None
+        if self.G and dev.type == "cuda":
+            kg = (kw + self.G - 1 + 31) // 32 * 32
+            wg = np.zeros((self.G, self.new, kg), np.float32)
+            for g in range(self.G):
+                wg[g, :, g:g + kw] = taps
+            self.w_planes = ops.split(torch.from_numpy(wg).to(dev))
 
-    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, split: bool = False) -> torch.Tensor:
         if self.identity:
             return x
         squeeze = x.dim() == 1
         x2 = x.reshape(1, -1) if squeeze else x.reshape(-1, x.shape[-1])
-        y = ops.resample(x2.contiguous().float(), self.orig, self.new, self.kernel, self.width)
+        x2 = x2.float()
+        if x2.stride(-1) != 1:
+            x2 = x2.contiguous()
+        if split and self.w_planes is not None:
+            y = ops.resample_split(x2, self.orig, self.new, self.w_planes, self.G, self.width)
+        else:
+            y = ops.resample(x2, self.orig, self.new, self.kernel, self.width)
         return y[0] if squeeze else y.reshape(*x.shape[:-1], y.shape[-1])

@@ -135,7 +135,7 @@ class ForcedAlignmentTask:
             lengths = None
         if wav_sr is not None and wav_sr != sr:
             up = self.upsampler(wav_sr)
-            waves = up(waves)
+            waves = up(waves, split=self.unitsEncoder.split_resample)
             if lengths is not None:
                 lengths = [target_length(int(n), wav_sr, sr) for n in lengths]
                 waves = waves.contiguous()

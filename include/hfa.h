@@ -230,6 +230,14 @@ int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream)
 int hfa_add_f32(long long n, const float* a, const float* b, float* out, hipStream_t stream);
 /* torchaudio.transforms.Resample (sinc_interp_hann) as pad + MFMA GEMM (tools/load_wav.py:7,
  * tools/encoder.py:46-48).  orig/newr gcd-reduced; kernel [newr][Kpad]; y_bs >= (N/orig+1)*newr. */
+/* The resampler on the split-f16 GEMM (f32-class): x padded and split into the workspace, then one split GEMM with
+ * 16-B aligned rows.  G = 1 for orig % 8 == 0 (frame f at f * orig), G = 8 for orig % 8 == 1 (e.g. 44100 -> 16000:
+ * frames 8m+g as 8 groups, group g's taps shifted right by g): Wg is [2][G][new][Kg] split planes of those taps
+ * (Kg % 32 == 0, Kg >= 2 width + orig + G - 1).  y: F*new (G = 1) or ceil(F/8)*8*new (G = 8) floats per row;
+ * the valid length is ceil(new*N/orig).  *oflow as hfa_split_f16. */
+long long hfa_resample_split_workspace_bytes(int B, int N, int orig, int Kg, int G);
+int hfa_resample_split(int B, int N, const float* x, long long x_bs, int orig, int newr, const uint16_t* Wg, int Kg,
+                       int G, int width, void* workspace, float* y, long long y_bs, int* oflow, hipStream_t stream);
 long long hfa_resample_workspace_bytes(int B, int N, int orig, int Kpad);
 int hfa_resample_f32(int B, int N, const float* x, long long x_bs, int orig, int newr, const float* kernel, int Kpad,
                      int width, void* workspace, float* y, long long y_bs, hipStream_t stream);

@@ -303,6 +303,27 @@ def test_resample_vs_restated_torchaudio():
         _close(got, ref, 1e-4, 2e-6)
 
 
+@pytest.mark.parametrize("o,n,w,N", [(16000, 44100, 6, 160000), (44100, 16000, 128, 441000), (44100, 16000, 128, 4413),
+                                     (16000, 44100, 6, 4097), (8000, 44100, 6, 12345), (22050, 44100, 6, 9999),
+                                     (48000, 44100, 6, 48000), (24000, 16000, 128, 24001)])
+def test_resample_split_vs_f32_and_restatement(o, n, w, N):
+    """The resampler on the split-f16 GEMM (G = 1 for orig % 8 == 0, 8 shifted-tap groups for orig % 8 == 1, the
+    f32 GEMM otherwise): same length as the f32 path and the restated torchaudio kernel, within the f32 path's own
+    tolerance of the restatement, from a row-pitched (non-contiguous) input."""
+    from hubertfa_amd.resample import Resampler
+    from oracle.resample import resample as ref_resample
+    x = _r(2, N + 40, seed=21, scale=0.2)[:, 7:N + 7]            # rows with a pitch
+    ref = ref_resample(x.contiguous(), o, n, w)
+    rs = Resampler(o, n, w)
+    xd = x.cuda()
+    got = rs(xd, split=True)
+    f32 = rs(xd, split=False)
+    assert got.shape == ref.shape == f32.shape
+    _close(got, ref, 1e-4, 2e-6)
+    _close(f32, ref, 1e-4, 2e-6)
+    assert float((got.double() - f32.double()).abs().max()) < 2e-6
+
+
 @pytest.mark.parametrize("N", [16000, 160000, 4097])
 def test_wav_normalize(N):
     from hubertfa_amd import ops
