@@ -165,6 +165,41 @@ def config_name(encoder: str, world: int, B: int, seconds: float = 10.0) -> str:
     return "config 3 geometry" + ("" if world * B == 512 else f" (global batch {world * B}, config 3 is 512)")
 
 
+def host_io(wav_np, res, seconds, budget_s=3.0):
+    """file I/O and TextGrid writing, reported beside (not inside) the timed wave->boundaries path:
+    read the batch as 16-bit WAV files (wav_io.read_wav, the CLI's reader) and write its TextGrids + confidence.csv
+    (post_processing + Exporter, the CLI's writer) in a temporary directory, on the host; ms per batch."""
+    import tempfile
+    from hubertfa_amd.export_tool import Exporter
+    from hubertfa_amd.post_processing import post_processing
+    from hubertfa_amd.wav_io import read_wav, write_wav
+    B = wav_np.shape[0]
+    with tempfile.TemporaryDirectory() as td:
+        paths = [os.path.join(td, f"utt{b:04d}.wav") for b in range(B)]
+        for p, x in zip(paths, wav_np):
+            write_wav(p, x, 16000)
+        t_read, n = 0.0, 0
+        while n == 0 or (t_read < budget_s / 2 and n < 20):
+            t0 = time.perf_counter()
+            for p in paths:
+                read_wav(p)
+            t_read += time.perf_counter() - t0
+            n += 1
+        preds = [(p, seconds, r["confidence"], r["ph_seq"], r["ph_intervals"], r["word_seq"], r["word_intervals"])
+                 for p, r in zip(paths, res)]
+        Exporter(*post_processing(list(preds)), os.path.join(td, "warm")).export(["textgrid", "confidence"])
+        t_write, m = 0.0, 0
+        while m == 0 or (t_write < budget_s / 2 and m < 20):
+            pp, log = post_processing(list(preds))
+            t0 = time.perf_counter()
+            Exporter(pp, log, os.path.join(td, "out")).export(["textgrid", "confidence"])
+            t_write += time.perf_counter() - t0
+            m += 1
+    return {"wav_read_ms_per_batch": 1e3 * t_read / n, "textgrid_write_ms_per_batch": 1e3 * t_write / m,
+            "files_per_batch": B, "note": "host only, one thread, outside the timed region (infer.py reads the files "
+                                          "on a thread pool before the GPU pass and writes after it)"}
+
+
 SECONDARY = ("viterbi_forward_kernel", "hfa_conv0_f32", "attn_fwd_split_kernel", "attn_fwd_f32_kernel")
 
 
@@ -323,6 +358,8 @@ def main():
                    "global_batch": world * B, "seconds_per_utterance": args.seconds, "dp_frames": n_frames,
                    "states": len(ph_seqs[0]), "parallelism": f"utterance-dp{world}", "precision": args.precision},
         "frames_per_s": frames_ps,
+        "hubert_frames_per_s": world * B * task.unitsEncoder.model.frame_lengths(int(round(args.seconds * 16000)))
+                               * args.steps / el,
         "realtime_factor": value,
         "encoder_tflops": world * B * (hub_flops + head_flops) * args.steps / el / 1e12,
         "roofline": {"bound": "mfma", "kernel": probe_name, "achieved": achieved, "peak": mfma_peak(probe_name),
@@ -343,6 +380,10 @@ def main():
     torch.cuda.synchronize()
     ops.PROBE = None
     out["secondary"] = secondary_rooflines(iso, probe, n_frames, len(ph_seqs[0]))
+    if rank == 0:
+        import contextlib
+        with contextlib.redirect_stdout(sys.stderr):         # the writers' progress prints stay off the JSON line
+            out["host_io"] = host_io(wav_np, res, args.seconds)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wav_np, ph_seqs, word_seqs, p2ws, ckpt, args.cpu_sample_s, encoder)
     if rank == 0:

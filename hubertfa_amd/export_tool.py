@@ -17,6 +17,9 @@ class _Interval:
     def __init__(self, minTime, maxTime, mark):
         if minTime >= maxTime:   # Praat has no zero/negative-length intervals
             raise ValueError(minTime, maxTime)
+        # numpy float64 -> float: the same value and the same text when formatted, without numpy's slow __format__
+        minTime = float(minTime) if isinstance(minTime, float) else minTime
+        maxTime = float(maxTime) if isinstance(maxTime, float) else maxTime
         self.minTime, self.maxTime, self.mark = minTime, maxTime, mark
 
 
@@ -31,9 +34,13 @@ class IntervalTier:
             raise ValueError(self.minTime)
         if self.maxTime and iv.maxTime > self.maxTime:
             raise ValueError(self.maxTime)
-        pos = 0
-        while pos < len(self.intervals) and self.intervals[pos].minTime < iv.minTime:
-            pos += 1
+        ivs = self.intervals
+        if not ivs or ivs[-1].minTime < iv.minTime:      # in-order adds (the decoder's): O(1), not a linear scan
+            pos = len(ivs)
+        else:
+            pos = 0
+            while pos < len(ivs) and ivs[pos].minTime < iv.minTime:
+                pos += 1
         for nb in self.intervals[max(pos - 1, 0):pos + 1]:
             if nb.minTime < iv.maxTime and iv.minTime < nb.maxTime:
                 raise ValueError("overlapping intervals", nb.minTime, nb.maxTime, minTime, maxTime)
@@ -79,16 +86,15 @@ class TextGrid:
             yield f"\t\txmin = {tier.minTime}"
             yield f"\t\txmax = {maxT}"
             yield f"\t\tintervals: size = {len(ivs)}"
-            for j, iv in enumerate(ivs, 1):
-                yield f"\t\t\tintervals [{j}]:"
-                yield f"\t\t\t\txmin = {iv.minTime}"
-                yield f"\t\t\t\txmax = {iv.maxTime}"
-                yield '\t\t\t\ttext = "{}"'.format(str(iv.mark).replace('"', '""'))
+            for j, iv in enumerate(ivs, 1):      # one chunk of four lines per interval
+                mark = str(iv.mark).replace('"', '""')
+                yield (f'\t\t\tintervals [{j}]:\n\t\t\t\txmin = {iv.minTime}\n\t\t\t\txmax = {iv.maxTime}\n'
+                       f'\t\t\t\ttext = "{mark}"')
 
     def write(self, path, null=""):
+        text = "\n".join(self.lines(null)) + "\n"
         with open(path, "w", encoding="utf-8") as f:
-            for line in self.lines(null):
-                f.write(line + "\n")
+            f.write(text)
 
 
 def read_textgrid(path):
@@ -116,6 +122,7 @@ class Exporter:
 
     def save_textgrids(self):
         print("Saving TextGrids...")
+        made = set()
         for wav_path, wav_length, confidence, ph_seq, ph_intervals, word_seq, word_intervals in self.predictions:
             wav_path = pathlib.Path(wav_path)
             tg = TextGrid()
@@ -129,7 +136,9 @@ class Exporter:
             tg.append(ph_tier)
             base = self.out_path if self.out_path is not None else wav_path.parent
             tg_path = base / "TextGrid" / wav_path.with_suffix(".TextGrid").name
-            tg_path.parent.mkdir(parents=True, exist_ok=True)
+            if tg_path.parent not in made:
+                tg_path.parent.mkdir(parents=True, exist_ok=True)
+                made.add(tg_path.parent)
             tg.write(tg_path)
 
     def save_confidence_fn(self):

@@ -43,12 +43,21 @@ def _predict(task, rows, keys, batch_size: int, errors: list) -> dict:
     task.on_predict_start()
     sr = task.melspec_config["sample_rate"]
     items = {}
-    for key, (wav_path, ph_seq, word_seq, p2w) in zip(keys, rows):
+
+    def _read(path):
         try:
-            x, file_sr = read_wav(wav_path)
+            return read_wav(path), None
         except (OSError, ValueError) as e:
+            return None, e
+    # file reads and the int16 -> f32 conversion release the GIL: a small thread pool overlaps them
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as pool:
+        loaded = list(pool.map(_read, [r[0] for r in rows]))
+    for key, (wav_path, ph_seq, word_seq, p2w), (xs, e) in zip(keys, rows, loaded):
+        if e is not None:
             errors.append([wav_path, e])
             continue
+        x, file_sr = xs
         items[key] = (wav_path, x[0], file_sr, ph_seq, word_seq, p2w)
     out = {}
 
