@@ -96,6 +96,84 @@ __global__ __launch_bounds__(NT) void conv0_reduce_kernel(int T0, int nchunk, co
     }
 }
 
+// ---- GroupNorm(512, 512) statistics from the wave's lag products (the default; conv0_stats_kernel with mode 1) ----
+// conv0 has one input channel and no bias here, so a channel's statistics over the frames are forms in its 10 taps:
+// sum_t v_c(t) = w_c . S and sum_t v_c(t)^2 = w_c^T G w_c with S_j = sum_t x[5t + j], G_jk = sum_t x[5t + j] x[5t + k]
+// -- 10 + 55 numbers per utterance instead of re-running the 512-channel conv.  f64 throughout (the products of two
+// f32 are exact in f64): the statistics of the exact conv outputs, where the conv pass summed them after their f32
+// rounding (relative differences ~1e-16 in the sums; the f32 mean / rstd agree to the last bit or one ulp).
+constexpr int GCH = 4096;      // frames per block of the lag-product pass (8 blocks per 10 s row)
+constexpr int NGR = 65;        // 10 sums + 55 products
+__global__ __launch_bounds__(256) void conv0_gram_kernel(int T0, const float* __restrict__ x, long long x_bs,
+                                                         double* __restrict__ part, const int32_t* __restrict__ t0_len) {
+    const int b = blockIdx.y, chunk = blockIdx.x;
+    const int T0b = t0_len ? t0_len[b] : T0;
+    const float* xb = x + b * x_bs;
+    double acc[NGR];
+#pragma unroll
+    for (int i = 0; i < NGR; ++i) acc[i] = 0.0;
+    for (int k = 0; k < GCH / 256; ++k) {
+        const int t = chunk * GCH + k * 256 + threadIdx.x;
+        if (t < T0b) {                                  // frame t reads x[5t .. 5t + 9], inside the row
+            double xv[KW];
+#pragma unroll
+            for (int j = 0; j < KW; ++j) xv[j] = (double)xb[(long long)t * ST + j];
+            int q = 0;
+#pragma unroll
+            for (int j = 0; j < KW; ++j) acc[q++] += xv[j];
+#pragma unroll
+            for (int j = 0; j < KW; ++j)
+#pragma unroll
+                for (int i = j; i < KW; ++i, ++q) acc[q] = fma(xv[j], xv[i], acc[q]);
+        }
+    }
+    __shared__ double red[4][NGR];                      // fixed order: lane butterfly, then the 4 waves in order
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NGR; ++i) {
+        const double v = hfa::wave_sum_d(acc[i]);
+        if (lane == 0) red[wave][i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NGR) {
+        const int i = threadIdx.x;
+        part[((size_t)b * gridDim.x + chunk) * NGR + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    }
+}
+
+// One block of 512 threads (one per channel) per batch row: the chunk partials summed in order, then each channel's
+// mean and rstd from its taps.
+__global__ __launch_bounds__(C0) void conv0_gram_stats_kernel(int T0, int nchunk, const double* __restrict__ part,
+                                                              const float* __restrict__ w0, float eps,
+                                                              float* __restrict__ stats,
+                                                              const int32_t* __restrict__ t0_len) {
+    const int b = blockIdx.x, c = threadIdx.x;
+    __shared__ double sg[NGR];
+    if (c < NGR) {
+        double s = 0.0;
+        for (int k = 0; k < nchunk; ++k) s += part[((size_t)b * nchunk + k) * NGR + c];
+        sg[c] = s;
+    }
+    __syncthreads();
+    const int T = t0_len ? t0_len[b] : T0;
+    double w[KW];
+#pragma unroll
+    for (int j = 0; j < KW; ++j) w[j] = (double)w0[c * KW + j];
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < KW; ++j) s1 = fma(w[j], sg[j], s1);
+    int q = KW;
+#pragma unroll
+    for (int j = 0; j < KW; ++j)
+#pragma unroll
+        for (int i = j; i < KW; ++i, ++q) s2 += (i == j ? 1.0 : 2.0) * (w[j] * w[i]) * sg[q];
+    const double mean = s1 / T;
+    double var = s2 / T - mean * mean;
+    if (var < 0) var = 0;
+    stats[(b * C0 + c) * 2] = (float)mean;
+    stats[(b * C0 + c) * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
 // mode 0: GroupNorm(stats) + affine + GELU; mode 1: + bias, no norm, no act (LN variant feeds a LayerNorm).
 // OUTS: write the output as split-f16 planes (gemm.hip gemm_split_kernel operand: hi = f16(v), lo = f16((v - hi)
 // * 2^11), plane 1 at +y_sp halves) instead of f32 — the same bytes, and conv1 then runs on the f16 MFMA.
@@ -222,8 +300,8 @@ __global__ __launch_bounds__(NT) void conv0_apply8_kernel(int N, int T0, const f
 // v_mfma_f32_16x16x4_f32 is bit for bit a k-ordered fmaf chain, D = fma(a3, b3, fma(a2, b2, fma(a1, b1, fma(a0, b0, C))))
 // (cdna_hip_programming.md §3, "FP32-input MFMA"), so the 10-tap conv as three MFMAs (taps 0-3, 4-7, 8-11 with
 // w10 = w11 = 0, C = 0 first) gives exactly conv10's values: the apply pass below is bit-identical to
-// conv0_apply8_kernel.  Measured (scripts/conv0_bench.py, B = 32 x 10 s): 559 vs 565 us -- the apply pass is bound
-// by VALU issue (~38 VALU ops per output in apply8, ~30 here: GELU ~21 of them; 2.1 GB written would take ~0.35 ms
+// conv0_apply8_kernel.  Measured (scripts/conv0_bench.py, B = 32 x 10 s): no faster (559-576 vs 531-565 us), so it
+// is hfa_conv0_tuning mode 2, not the default -- the apply pass is bound by VALU issue (~38 VALU ops per output in apply8, ~30 here: GELU ~21 of them; 2.1 GB written would take ~0.35 ms
 // at the 6 TB/s store rate), and the f32 MFMA (32 cycles per 16x16x4 per SIMD) takes most of what it frees.  The
 // same conv in the statistics pass with f64 accumulation was slower (254 vs 176 us: 131 VGPRs), so that pass stays
 // on the VALU.
@@ -330,7 +408,7 @@ __global__ __launch_bounds__(MNT) void conv0_apply_mfma_kernel(int N, int T0, co
     if (bad && oflow) *oflow = 1;
 }
 
-thread_local int g_conv0_mode = 0;   // hfa_conv0_tuning: 0 MFMA conv (default), 1 the VALU kernels
+thread_local int g_conv0_mode = 0;   // hfa_conv0_tuning: 0 lag-product stats (default), 1 round 1, 2 MFMA apply
 
 }  // namespace
 
@@ -364,10 +442,17 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
     if (norm) {
         double* part = reinterpret_cast<double*>(workspace);
         float* stats = reinterpret_cast<float*>(part + (size_t)B * nchunk * C0 * 2);
-        hipLaunchKernelGGL(conv0_stats_kernel, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, part, t0_len);
-        hipLaunchKernelGGL(conv0_reduce_kernel, dim3(C0 / 64, B), dim3(NT), 0, stream, T0, nchunk, part, eps, stats,
-                           t0_len);
-        if (outs && vec8 && g_conv0_mode == 0)
+        if (g_conv0_mode != 1) {
+            const int ng = (T0 + GCH - 1) / GCH;                      // <= nchunk: fits the partials region
+            hipLaunchKernelGGL(conv0_gram_kernel, dim3(ng, B), dim3(256), 0, stream, T0, x, x_bs, part, t0_len);
+            hipLaunchKernelGGL(conv0_gram_stats_kernel, dim3(B), dim3(C0), 0, stream, T0, ng, part, w0, eps, stats,
+                               t0_len);
+        } else {
+            hipLaunchKernelGGL(conv0_stats_kernel, grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, part, t0_len);
+            hipLaunchKernelGGL(conv0_reduce_kernel, dim3(C0 / 64, B), dim3(NT), 0, stream, T0, nchunk, part, eps,
+                               stats, t0_len);
+        }
+        if (outs && vec8 && g_conv0_mode == 2)
             hipLaunchKernelGGL((conv0_apply_mfma_kernel<0>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
         else if (outs && vec8)
@@ -379,7 +464,7 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
         else
             hipLaunchKernelGGL((conv0_apply_kernel<0, false>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, y, y_bs, y_sp, oflow);
-    } else if (outs && vec8 && g_conv0_mode == 0) {
+    } else if (outs && vec8 && g_conv0_mode == 2) {
         hipLaunchKernelGGL((conv0_apply_mfma_kernel<1>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, nullptr,
                            nullptr, nullptr, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
     } else if (outs && vec8) {
@@ -416,11 +501,13 @@ int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w
                         t0_len, stream);
 }
 
-// Kernel choice for A/B timing and the bit-identity tests: 0 the MFMA conv (default), 1 the VALU kernels.  Per
+// Kernel choice for A/B timing and the parity tests: 0 (default) the lag-product statistics and conv0_apply8_kernel,
+// 1 the round-1 passes (the conv re-run on the VALU for the statistics), 2 the lag-product statistics with the MFMA
+// apply pass (bit-identical to 0; measured 0.575-0.620 vs 0.566-0.571 ms per batch, scripts/conv0_bench.py).  Per
 // calling thread.
 int hfa_conv0_tuning(int mode) {
-    if (mode != 0 && mode != 1) {
-        hfa::set_error("hfa_conv0_tuning: mode %d is not 0 or 1", mode);
+    if (mode < 0 || mode > 2) {
+        hfa::set_error("hfa_conv0_tuning: mode %d is not 0, 1 or 2", mode);
         return HFA_EINVAL;
     }
     g_conv0_mode = mode;

@@ -221,8 +221,10 @@ int hfa_pad_rows_f32(int B, int N, const float* x, long long x_bs, int left, int
                      hipStream_t stream);
 /* Self-test: y_nb = the branch-free erf of every GELU epilogue, y_ref = device erff (must be bit-identical). */
 int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hipStream_t stream);
-/* conv0 kernel choice (per calling thread): 0 = the conv on the f32-input MFMA (default; bit-identical, the MFMA
- * is an exact k-ordered fmaf chain), 1 = the VALU kernels.  Returns HFA_EINVAL for another value. */
+/* conv0 kernel choice (per calling thread): 0 = default: GroupNorm statistics from the wave's lag products
+ * (S_j, G_jk over the frames: 65 numbers per utterance, f64) and the VALU apply pass; 1 = the round-1 passes (the
+ * conv re-run for f64 sums of its outputs); 2 = lag-product statistics with the taps of the apply pass on the
+ * f32-input MFMA (an exact k-ordered fmaf chain: mode 0's bits).  HFA_EINVAL otherwise. */
 int hfa_conv0_tuning(int mode);
 /* Self-test: y = the GELU applied by every fused epilogue (GEMM, LayerNorm/GroupNorm act, conv0). */
 int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream);

@@ -26,7 +26,7 @@ def main():
     out = torch.empty(2, args.B, T0, 512, dtype=torch.float16, device=d)
     ws = torch.empty(_lib.lib().hfa_conv0_workspace_bytes(args.B, N), dtype=torch.uint8, device=d)
     nbytes = args.B * (4.0 * N + 4.0 * 512 * T0)
-    for mode in (0, 1, 0, 1):
+    for mode in (0, 2, 1, 0, 2, 1):
         _lib.call("hfa_conv0_tuning", mode)
         fn = lambda: ops.conv0(x, w0, gamma=gam, beta=bet, out=out, workspace=ws, out_split=True)  # noqa: E731
         for _ in range(3):
@@ -39,7 +39,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.reps
-        print(f"mode {mode} ({'mfma' if mode == 0 else 'valu'}): {ms:.3f} ms per batch (stats + reduce + apply), "
+        print(f"mode {mode} ({['lag-product stats + VALU apply', 'round-1: VALU stats + VALU apply', 'lag-product stats + MFMA apply'][mode]}): {ms:.3f} ms per batch (stats + reduce + apply), "
               f"{nbytes / ms / 1e6:.0f} GB/s of algorithmic bytes", flush=True)
     _lib.call("hfa_conv0_tuning", 0)
 

@@ -212,9 +212,11 @@ def test_conv0_split_output_matches_f32():
 
 @pytest.mark.parametrize("N,lens", [(16000, None), (12345, None), (16000, [16000, 5003]), (97, None)])
 def test_conv0_mfma_bit_identical_to_valu(N, lens):
-    """conv0's taps on v_mfma_f32_16x16x4_f32 (an exact k-ordered fmaf chain) give the VALU kernels' bits: the
-    GroupNorm+GELU split planes, the raw conv + bias planes (LN-conv variant), and the f32 output (whose stats pass
-    also runs on the MFMA), with ragged chunk tails and per-row frame counts."""
+    """conv0's taps on v_mfma_f32_16x16x4_f32 (an exact k-ordered fmaf chain, mode 2) give the VALU kernel's bits
+    (mode 0; also the raw conv + bias planes of the LN-conv variant); with GroupNorm, the lag-product statistics
+    (modes 0, 2) and the conv-pass f64 sums (mode 1) agree to f32 rounding, so the normalised outputs agree to a few
+    ulps; the f32 and split outputs of one mode share the statistics and agree bitwise.  Ragged chunk tails and
+    per-row frame counts included."""
     from hubertfa_amd import ops, _lib
     from hubertfa_amd.hubert import dev_lengths
     d = torch.device("cuda")
@@ -224,7 +226,7 @@ def test_conv0_mfma_bit_identical_to_valu(N, lens):
     g, bb = (1 + 0.1 * _r(512, seed=33)).to(d), (0.1 * _r(512, seed=34)).to(d)
     tl = None if lens is None else dev_lengths([(n - 10) // 5 + 1 for n in lens], d)
     outs = {}
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         _lib.call("hfa_conv0_tuning", mode)
         try:
             outs[mode] = (ops.conv0(x, w0, gamma=g, beta=bb, out_split=True, t0_len=tl),
@@ -233,9 +235,34 @@ def test_conv0_mfma_bit_identical_to_valu(N, lens):
         finally:
             _lib.call("hfa_conv0_tuning", 0)
     torch.cuda.synchronize()
-    for a, b in zip(outs[0], outs[1]):
+    for a, b in zip(outs[0], outs[2]):                             # MFMA taps = VALU fmaf chain, same statistics
         assert torch.equal(a, b)
-    assert torch.equal(outs[0][0][0].float(), outs[0][2].half().float())
+    assert torch.equal(outs[0][1], outs[1][1])                     # no statistics: bit-identical
+    for i in (0, 2):
+        a = outs[0][i].double() if i == 2 else outs[0][i][0].double() + outs[0][i][1].double() / 2048
+        b = outs[1][i].double() if i == 2 else outs[1][i][0].double() + outs[1][i][1].double() / 2048
+        if tl is not None:                                         # rows past a row's frames are don't-care
+            a, b = a[:1], b[:1]
+        assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
+    for m in (0, 1, 2):
+        assert torch.equal(outs[m][0][0].float(), outs[m][2].half().float())
+
+
+def test_conv0_lag_product_stats_dc_heavy():
+    """GroupNorm statistics from lag products on a wave with a large DC offset (mean >> std per channel: the
+    variance is a small difference of large sums) against an f64 evaluation of conv -> GroupNorm -> GELU."""
+    import torch.nn.functional as F
+    from hubertfa_amd import ops
+    d = torch.device("cuda")
+    B, N = 2, 48000
+    x = 0.8 + 0.01 * _r(B, N, seed=35)
+    w0 = _r(512, 10, seed=36, scale=0.3)
+    g, bb = 1 + 0.1 * _r(512, seed=37), 0.1 * _r(512, seed=38)
+    c = F.conv1d(x.double()[:, None], w0.double()[:, None], stride=5)
+    ref = F.gelu(F.group_norm(c, 512, g.double(), bb.double(), 1e-5)).transpose(1, 2)
+    got = ops.conv0(x.to(d), w0.to(d), gamma=g.to(d), beta=bb.to(d))
+    err = float((got.double().cpu() - ref).abs().max())
+    assert err < 2e-4, err
 
 
 def test_encoder_split_vs_f32_precision():
