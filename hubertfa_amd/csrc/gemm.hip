@@ -45,6 +45,7 @@ struct GemmP {
     _Float16* Ch; long long sCp;
     int* oflow;
     int cvec;      // split f32 output: 16-B row pieces (C rows 16-B aligned); 0: scalar stores (no R, no planes)
+    const _Float16* Rh; long long sRp;   // split f32 output: the residual as split planes (strides of R, in halves)
 };
 
 enum { EPI_NONE = 0, EPI_GELU = 1 };
@@ -687,6 +688,7 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
     float* Cb = p.C + zb * p.sCb + zg * p.sCg;
     _Float16* Hb = p.Ch ? p.Ch + zb * p.sCb + zg * p.sCg : nullptr;
     const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
+    const _Float16* Rhb = p.Rh ? p.Rh + zb * p.sRb + zg * p.sRg : nullptr;
     const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
@@ -709,12 +711,23 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
                     float* dst = Cb + (long long)row * p.ldc + col;
                     if (col + 3 < p.N && p.cvec) {
                         if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + (long long)row * p.ldr + col);
+                        if (Rhb) {          // residual planes: hi + 2^-11 lo (exact in f32), one rounding in the add
+                            const _Float16* rh = Rhb + (long long)row * p.ldr + col;
+                            const f16x4 r1 = *reinterpret_cast<const f16x4*>(rh);
+                            const f16x4 r2 = *reinterpret_cast<const f16x4*>(rh + p.sRp);
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) v[t] += __builtin_fmaf((float)r2[t], 1.0f / 2048.0f, (float)r1[t]);
+                        }
                         *reinterpret_cast<f32x4*>(dst) = v;
                     } else {
 #pragma unroll
                         for (int t = 0; t < 4; ++t)
                             if (col + t < p.N) {
                                 v[t] += Rb ? Rb[(long long)row * p.ldr + col + t] : 0.0f;
+                                if (Rhb) {
+                                    const _Float16* rh = Rhb + (long long)row * p.ldr + col + t;
+                                    v[t] += __builtin_fmaf((float)rh[p.sRp], 1.0f / 2048.0f, (float)rh[0]);
+                                }
                                 dst[t] = v[t];
                             }
                     }
@@ -1770,6 +1783,7 @@ GemmP make_params(int M, int N, int K, int G, const float* A, long long sAb, lon
     p.C = nullptr; p.sCb = p.sCg = 0; p.ldc = 0;
     p.Ah = nullptr; p.sAp = 0; p.Wh = nullptr; p.sWp = 0; p.Ch = nullptr; p.sCp = 0; p.oflow = nullptr;
     p.cvec = 1;
+    p.Rh = nullptr; p.sRp = 0;
     return p;
 }
 
@@ -1828,8 +1842,9 @@ int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, i
 int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, long long sAp, long long sAb,
                         long long sAg, int ldx, int stride, int pad, int Cg, int Tin, const uint16_t* W,
                         long long sWp, long long sWg, int ldw, const float* bias, long long sBg, const float* R,
-                        long long sRb, long long sRg, int ldr, float* C, uint16_t* Cs, long long sCp, long long sCb,
-                        long long sCg, int ldc, int epilogue, int* oflow, hipStream_t stream) {
+                        long long sRb, long long sRg, int ldr, const uint16_t* Rs, long long sRp, float* C,
+                        uint16_t* Cs, long long sCp, long long sCb, long long sCg, int ldc, int epilogue, int* oflow,
+                        hipStream_t stream) {
     if (M < 0 || N < 0 || K < 0 || Zb < 0 || G < 1 || stride < 1 || Cg < 1 || Tin < 1) {
         hfa::set_error("hfa_conv_gemm_split: bad sizes M=%d N=%d K=%d Zb=%d G=%d", M, N, K, Zb, G);
         return HFA_EINVAL;
@@ -1851,6 +1866,11 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
     const long long a_span = ((long long)(Tin - 1) * ldx + Cg) * 2, w_span = ((long long)(N - 1) * ldw + K) * 2;
     if (a_span >= 0x7fffffffLL || w_span >= 0x7fffffffLL) {
         hfa::set_error("hfa_conv_gemm_split: operand span past 31-bit buffer offsets");
+        return HFA_EINVAL;
+    }
+    if (Rs && (R || !C || Cs || ((uintptr_t)Rs & 7) || (ldr | sRb | sRg | sRp) % 4)) {
+        hfa::set_error("hfa_conv_gemm_split: a split-plane residual Rs goes with an f32 C alone (no R, no Cs), 8-B "
+                       "aligned with strides multiple of 4 halves");
         return HFA_EINVAL;
     }
     const bool c_al = C && al16(C) && ldc % 4 == 0 && sCb % 4 == 0 && sCg % 4 == 0;
@@ -1880,9 +1900,15 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
     p.C = C; p.Ch = reinterpret_cast<_Float16*>(Cs); p.sCp = sCp; p.sCb = sCb; p.sCg = sCg; p.ldc = ldc;
     p.oflow = oflow;
     p.cvec = !C || c_al;
+    p.Rh = reinterpret_cast<const _Float16*>(Rs); p.sRp = sRp;
+    if (Rs && !p.cvec) {
+        hfa::set_error("hfa_conv_gemm_split: a split-plane residual needs 16-B aligned C rows");
+        return HFA_EINVAL;
+    }
     const int Z = Zb * G, cfg = split_cfg(p, Z);
-    if ((cfg == SCFG_WIN || cfg == SCFG_N48) && !p.cvec) {
-        hfa::set_error("hfa_conv_gemm_split: the grouped positional conv kernels need 16-B aligned C rows");
+    if ((cfg == SCFG_WIN || cfg == SCFG_N48) && (!p.cvec || Rs)) {
+        hfa::set_error("hfa_conv_gemm_split: the grouped positional conv kernels need 16-B aligned C rows and an f32 "
+                       "residual");
         return HFA_EINVAL;
     }
     if (cfg == SCFG_WIN) {                     // grouped positional conv: LDS-resident input window

@@ -351,7 +351,7 @@ int hfa_resample_split(int B, int N, const float* x, long long x_bs, int orig, i
     const int ldx = G == 1 ? orig : 8 * orig;
     return hfa_conv_gemm_split((int)rows, newr, Kg, B, G, reinterpret_cast<const uint16_t*>(planes), (long long)B * Lp,
                                Lp, G == 1 ? 0 : orig - 1, ldx, 1, 0, Kg, (int)rows, Wg, (long long)G * newr * Kg,
-                               (long long)newr * Kg, Kg, nullptr, 0, nullptr, 0, 0, 0, y, nullptr, 0, y_bs,
+                               (long long)newr * Kg, Kg, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, y, nullptr, 0, y_bs,
                                G == 1 ? 0 : newr, G == 1 ? newr : 8 * newr, 0, oflow, stream);
 }
 

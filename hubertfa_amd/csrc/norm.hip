@@ -40,9 +40,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
     const int lane = threadIdx.x & 63;
     if (wave >= rows) return;
     if (t_len && wave % T >= t_len[wave / T]) {     // padding row of a variable-length batch: zeros
-        float* yr = y + wave * ldy;
+        float* yr = y ? y + wave * ldy : nullptr;
         for (int c = lane * 4; c < C; c += 256) {
-            *reinterpret_cast<f32x4*>(yr + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (yr) *reinterpret_cast<f32x4*>(yr + c) = f32x4{0.f, 0.f, 0.f, 0.f};
             if (ys) {
                 const f16x4 z{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
                 *reinterpret_cast<f16x4*>(ys + wave * ldys + c) = z;
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
     }
     const float var = hfa::wave_sum(ss) / (float)C;
     const float rstd = 1.0f / sqrtf(var + eps);
-    float* yr = y + wave * ldy;
+    float* yr = y ? y + wave * ldy : nullptr;      // y NULL: split planes only (the residual is read from them)
     bool bad = false;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
             f32x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = act_apply((v[i][e] - mean) * rstd * g[e] + bb[e], act);
-            *reinterpret_cast<f32x4*>(yr + c) = o;
+            if (yr) *reinterpret_cast<f32x4*>(yr + c) = o;
             if (ys) {
                 f16x4 h1, h2;
 #pragma unroll
@@ -359,9 +359,11 @@ int hfa_layernorm_split(int rows, int C, const float* x, long long ldx, const fl
         return HFA_EINVAL;
     }
     if (rows == 0) return HFA_OK;
-    if (!x || !gamma || !beta || !y || (((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) & 15) ||
-        ldx % 4 || ldy % 4 || (res && (((uintptr_t)res & 15) || ldr % 4))) {
-        hfa::set_error("hfa_layernorm_f32: operands must be non-null, 16-byte aligned, strides multiple of 4");
+    if (!x || !gamma || !beta || (!y && !ys) ||
+        (((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) & 15) || ldx % 4 || ldy % 4 ||
+        (res && (((uintptr_t)res & 15) || ldr % 4))) {
+        hfa::set_error("hfa_layernorm_split: operands must be non-null (y may be NULL with planes), 16-byte aligned, "
+                       "strides multiple of 4");
         return HFA_EINVAL;
     }
     const int blocks = (rows + 3) / 4;

@@ -256,12 +256,12 @@ class HubertEncoder:
         """softmax(QK^T/sqrt(dh))V over the fused QKV projection.  Split precision: QKV written as split planes,
         attention on the split kernel, O returned as split planes (the out-projection's A operand)."""
         a = self.arch
-        B, L, H = h_in.shape
+        B, L, H = (h_in if h_in is not None else hs[0]).shape      # h_in None: the input lives in its planes
         nh = a.heads
         dh = H // nh
         if self.precision == "split" and L_.wqkv_s is not None and L_.wo_s is not None and dh == 64:
             qkv_s = self._linear(h_in, L_.wqkv, L_.wqkv_s, L_.bqkv, out_split=True, xs=hs)
-            o_s = torch.empty((2, B, L, H), dtype=torch.float16, device=h_in.device)
+            o_s = torch.empty((2, B, L, H), dtype=torch.float16, device=qkv_s.device)
             return ops.attention_split(qkv_s, o_s, B=B, H=nh, L=L, head_dim=dh, scale=dh ** -0.5, key_len=lens)
         qkv = self._linear(h_in, L_.wqkv, L_.wqkv_s, L_.bqkv)
         o = torch.empty((B, L, H), dtype=torch.float32, device=h_in.device)
@@ -275,12 +275,13 @@ class HubertEncoder:
             return self._linear(None, L_.wo, L_.wo_s, L_.bo, residual=residual, xs=o)
         return self._linear(o, L_.wo, L_.wo_s, L_.bo, residual=residual)
 
-    def _ln(self, x, w, b, out=None, split=False):
+    def _ln(self, x, w, b, out=None, split=False, planes_only=False):
         """LayerNorm; with ``split`` (a split GEMM consumes the result) also the split planes, from the same
-        kernel: returns (y, planes) — planes None when not requested."""
+        kernel: returns (y, planes) — planes None when not requested.  ``planes_only`` (split path): no f32 output
+        (y None) — every consumer, residual adds included, reads the planes."""
         eps = self.arch.layer_norm_eps
         if split and self.precision == "split":
-            return ops.layernorm(x, w, b, eps, out=out, out_split=True)
+            return ops.layernorm(x, w, b, eps, out=False if planes_only else out, out_split=True)
         return ops.layernorm(x, w, b, eps, out=out), None
 
     def layer(self, h: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None, hs: torch.Tensor | None = None,
@@ -289,13 +290,16 @@ class HubertEncoder:
         ``want_split``: also return the output's planes (the next layer's QKV operand), else None."""
         sp = self.precision == "split" and L_.w1_s is not None and L_.w2_s is not None
         if not self.arch.stable_layer_norm:   # post-LN (HubertEncoderLayer / nn.TransformerEncoderLayer)
+            # split path: the residual stream rides in the LayerNorms' split planes (hi + 2^-11 lo, 22 significand
+            # bits, the precision every split GEMM operand has): no f32 LayerNorm output is written or read back
             o = self.attention_block(h, L_, lens, hs)
-            h1 = self._out_proj(o, L_, h)
-            h1, h1s = self._ln(h1, L_.ln1_w, L_.ln1_b, out=h1, split=sp)
+            res = hs if (hs is not None and L_.wo_s is not None and self.precision == "split") else h
+            h1 = self._out_proj(o, L_, res)
+            h1, h1s = self._ln(h1, L_.ln1_w, L_.ln1_b, out=h1, split=sp, planes_only=sp)
             f = self._linear(h1, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp, xs=h1s)
-            h2 = self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h1, xs=f) if sp else \
+            h2 = self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h1s, xs=f) if sp else \
                 ops.linear(f, L_.w2, L_.b2, residual=h1)
-            return self._ln(h2, L_.ln2_w, L_.ln2_b, out=h2, split=want_split)
+            return self._ln(h2, L_.ln2_w, L_.ln2_b, out=h2, split=want_split, planes_only=want_split)
         # pre-LN (HubertEncoderLayerStableLayerNorm)
         a_, a_s = self._ln(h, L_.ln1_w, L_.ln1_b, split=L_.wqkv_s is not None)
         o = self.attention_block(a_, L_, lens, a_s)
@@ -342,10 +346,15 @@ class HubertEncoder:
         h = self.positional(h, lensL, hs=hps)
         hs = None
         layers = self.layers[:n_layers]
+        def planes_in(L_):       # a layer that reads its input (QKV operand, out-projection residual) from planes
+            return (self.precision == "split" and L_.wqkv_s is not None and L_.wo_s is not None and
+                    a.hidden // a.heads == 64)
         if not a.stable_layer_norm:
-            h, hs = self._ln(h, self.enc_ln[0], self.enc_ln[1], out=h, split=bool(layers))
+            first = bool(layers) and planes_in(layers[0])
+            h, hs = self._ln(h, self.enc_ln[0], self.enc_ln[1], out=h, split=bool(layers), planes_only=first)
         for i, L_ in enumerate(layers):
-            h, hs = self.layer(h, L_, lensL, hs, want_split=i + 1 < len(layers))
+            nxt = i + 1 < len(layers)
+            h, hs = self.layer(h, L_, lensL, hs, want_split=nxt and (a.stable_layer_norm or planes_in(layers[i + 1])))
         if a.stable_layer_norm:
             h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
         if self.proj is not None:

@@ -134,8 +134,8 @@ _lib.register("hfa_gemm_tuning", [_I_, _I_])
 _lib.register("hfa_gemm_kernel_name", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_, _LL_,
                                        _I_, _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _I_], ctypes.c_char_p)
 _lib.register("hfa_conv_gemm_split", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_,
-                                       _LL_, _LL_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _P_, _LL_, _LL_, _LL_,
-                                       _I_, _I_, _P_, _P_])
+                                       _LL_, _LL_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _P_, _P_, _LL_,
+                                       _LL_, _LL_, _I_, _I_, _P_, _P_])
 _lib.register("hfa_gemm_split_kernel_name", [_I_, _I_, _I_, _I_, _I_, _I_], ctypes.c_char_p)
 _lib.register("hfa_gemm_split_tuning", [_I_])
 _lib.register("hfa_split_f16", [_I_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _P_, _P_])
@@ -305,7 +305,11 @@ def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0
                     epilogue=EPI_NONE, flag=None, f16=False):
     """conv_gemm on split operands (As, Ws: [2, ...] f16 planes; strides in elements of one plane).  Output to f32
     C (+R), to split planes Cs [2, ...] (bias/GELU epilogue only), or both (dual: the planes of the final C).
+    R may be f32 or split planes [2, ...] f16 (f32 C alone; its strides in halves of one plane).
     ``f16``: the opt-in fast mode (high planes only, one f16 product per MAC: f16-class accuracy)."""
+    Rs = None
+    if R is not None and R.dtype == torch.float16:
+        R, Rs = None, R
     if f16:
         epilogue |= GEMM_F16
     _need(As, torch.float16, "As", contiguous=False)
@@ -315,6 +319,7 @@ def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0
     dev = (C if C is not None else Cs).device
     args = (M, N, K, Zb, G, _ptr(As), As.stride(0), sAb, sAg, ldx, stride, pad, Cg or K, Tin if Tin is not None else M,
             _ptr(Ws), Ws.stride(0), sWg, ldw if ldw is not None else K, _ptr(bias), sBg, _ptr(R), sRb, sRg, ldr,
+            _ptr(Rs), Rs.stride(0) if Rs is not None else 0,
             _ptr(C), _ptr(Cs), Cs.stride(0) if Cs is not None else 0, sCb, sCg, ldc, epilogue,
             _ptr(split_flag(dev) if flag is None else flag))
 
@@ -341,9 +346,14 @@ def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, 
         out = torch.empty(((2,) if planes else ()) + (*lead, N), dtype=torch.float16 if planes else torch.float32,
                           device=xs.device)
     hs = torch.empty((2, *lead, N), dtype=torch.float16, device=xs.device) if dual else None
-    r2 = residual.reshape(-1, N) if residual is not None else None
+    if residual is None:
+        r2 = None
+    elif residual.dtype == torch.float16:                  # split planes [2, ..., N] (a LayerNorm's plane output)
+        r2 = residual.reshape(2, -1, N)
+    else:
+        r2 = residual.reshape(-1, N)
     conv_gemm_split(xs, Ws, C=None if planes else out, Cs=out if planes else hs, M=M, N=N, K=K,
-                    ldx=xs.stride(-2) if xs.dim() > 2 else K, bias=bias, R=r2, ldr=r2.stride(0) if r2 is not None else 0,
+                    ldx=xs.stride(-2) if xs.dim() > 2 else K, bias=bias, R=r2, ldr=r2.stride(-2) if r2 is not None else 0,
                     ldc=N, epilogue=epilogue, flag=flag, f16=f16)
     return (out, hs) if dual else out
 
@@ -401,9 +411,14 @@ def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None, t
     ``out_split`` ([2, ..., C] f16, or True to allocate): the output also as split planes (returned second)."""
     C = x.shape[-1]
     x2 = x.reshape(-1, C)
-    if out is None:
-        out = torch.empty_like(x)
-    o2 = out.view(-1, C)
+    if out is False:                                      # split planes only (out_split required)
+        if out_split is None or out_split is False:
+            raise ValueError("layernorm: out=False needs out_split")
+        o2 = None
+    else:
+        if out is None:
+            out = torch.empty_like(x)
+        o2 = out.view(-1, C)
     r2 = residual.reshape(-1, C) if residual is not None else None
     tl = _lens(t_len)
     T = x.shape[-2] if (tl is not None and x.dim() == 3) else 0
@@ -418,9 +433,9 @@ def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None, t
     s2 = out_split.view(2, -1, C)
     _lib.call("hfa_layernorm_split", x2.shape[0], C, _ptr(x2), x2.stride(0), _ptr(r2),
               r2.stride(0) if r2 is not None else 0, _ptr(gamma), _ptr(beta), float(eps), act, _ptr(o2),
-              o2.stride(0), T, _ptr(tl), _ptr(s2), s2.stride(1), s2.stride(0),
+              o2.stride(0) if o2 is not None else 0, T, _ptr(tl), _ptr(s2), s2.stride(1), s2.stride(0),
               _ptr(split_flag(x.device) if flag is None else flag), _stream(x.device))
-    return out, out_split
+    return (None if o2 is None else out), out_split
 
 
 def groupnorm(x, G, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, t_len=None, out_split=None, flag=None):

@@ -107,7 +107,9 @@ int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, i
  * (producers raise *oflow otherwise; the caller recomputes on the f32 path) and |w| < 32 for W (the large
  * single-accumulator tiles form 2^11 * w1 in f16; an overflow there yields a non-finite result, which also raises
  * *oflow).  Output: f32 C (+R, 16-B rows), or with Cs non-NULL and C NULL split planes of epi(acc + bias) (no R),
- * or with both non-NULL the f32 C and the split planes of that same final value (dual output).
+ * or with both non-NULL the f32 C and the split planes of that same final value (dual output).  Rs (instead of
+ * R, f32 C alone): the residual as split planes (plane 1 at +sRp; strides sRb, sRg, ldr in halves), added as
+ * hi + 2^-11 lo -- the residual stream carried by the planes a LayerNorm already wrote for the next GEMM.
  * epilogue | HFA_GEMM_F16: opt-in fast mode -- the high planes alone, one f16 product per MAC (A1.W1, f32
  * accumulation: f16-class accuracy, about 2.5x the split rate); ignored by the grouped positional conv kernels
  * (Cg not a multiple of 32 or N = 48/64 windows), which keep the three products. */
@@ -115,8 +117,9 @@ int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, i
 int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, long long sAp, long long sAb,
                         long long sAg, int ldx, int stride, int pad, int Cg, int Tin, const uint16_t* W,
                         long long sWp, long long sWg, int ldw, const float* bias, long long sBg, const float* R,
-                        long long sRb, long long sRg, int ldr, float* C, uint16_t* Cs, long long sCp, long long sCb,
-                        long long sCg, int ldc, int epilogue, int* oflow, hipStream_t stream);
+                        long long sRb, long long sRg, int ldr, const uint16_t* Rs, long long sRp, float* C,
+                        uint16_t* Cs, long long sCp, long long sCb, long long sCg, int ldc, int epilogue, int* oflow,
+                        hipStream_t stream);
 /* rocprof symbol stem of the split instantiation for an M x N output over Z = Zb*G (out_split: planes out). */
 const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue, int Cg);
 /* Tile override for the split GEMM: 0 auto, 1 128x128, 2 128x64, 3 256x128 (8 waves), 4/5 128x128 with 3/4
@@ -165,7 +168,8 @@ int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const floa
                       const int32_t* t_len, hipStream_t stream);
 /* hfa_layernorm_f32 that also writes its output as split-f16 planes (see hfa_conv_gemm_split): ys row r at
  * ys + r*ldys, plane 1 at +sps halves (8-B aligned rows), so the consuming split GEMM needs no conversion pass;
- * *oflow raised for outputs outside f16 range. */
+ * *oflow raised for outputs outside f16 range.  y may be NULL: planes only (the consumers read the residual from
+ * them, hfa_conv_gemm_split Rs). */
 int hfa_layernorm_split(int rows, int C, const float* x, long long ldx, const float* res, long long ldr,
                         const float* gamma, const float* beta, float eps, int act, float* y, long long ldy, int T,
                         const int32_t* t_len, uint16_t* ys, long long ldys, long long sps, int* oflow,

@@ -69,18 +69,12 @@ int main() {
     CHECK(hfa_conv_gemm_f32(64, 64, 64, 1, 1, fp, 0, 0, 64, 1, 0, 64, 64, fp, 0, 64, nullptr, 0, nullptr, 0,
                                  0, 0, fp, 0, 0, 64, 7, st), "conv_gemm_f32 epilogue");
     CHECK(hfa_gemm_f32(64, 64, 64, nullptr, 64, fp, 64, nullptr, nullptr, 0, fp, 64, 0, st), "gemm_f32 NULL A");
-    CHECK(hfa_conv_gemm_split(-1, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0,
-                                   nullptr, 0, 0, 0, fp, nullptr, 0, 0, 0, 64, 0, op, st), "split M<0");
-    CHECK(hfa_conv_gemm_split(64, 64, 48, 1, 1, hp, 0, 0, 0, 48, 1, 0, 48, 64, hp, 0, 0, 48, nullptr, 0,
-                                   nullptr, 0, 0, 0, fp, nullptr, 0, 0, 0, 64, 0, op, st), "split K%32");
-    CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hmis, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0,
-                                   nullptr, 0, 0, 0, fp, nullptr, 0, 0, 0, 64, 0, op, st), "split A misaligned");
-    CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0,
-                                   nullptr, 0, 0, 0, nullptr, nullptr, 0, 0, 0, 64, 0, op, st), "split no output");
-    CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0, fp, 0,
-                                   0, 64, nullptr, hp, 0, 0, 0, 64, 0, op, st), "split planes-only + residual");
-    CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0,
-                                   nullptr, 0, 0, 0, fmis, nullptr, 0, 0, 0, 64, 0, op, st), "split C misaligned");
+    CHECK(hfa_conv_gemm_split(-1, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, fp, nullptr, 0, 0, 0, 64, 0, op, st), "split M<0");
+    CHECK(hfa_conv_gemm_split(64, 64, 48, 1, 1, hp, 0, 0, 0, 48, 1, 0, 48, 64, hp, 0, 0, 48, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, fp, nullptr, 0, 0, 0, 64, 0, op, st), "split K%32");
+    CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hmis, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, fp, nullptr, 0, 0, 0, 64, 0, op, st), "split A misaligned");
+    CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, nullptr, nullptr, 0, 0, 0, 64, 0, op, st), "split no output");
+    CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0, fp, 0, 0, 64, nullptr, 0, nullptr, hp, 0, 0, 0, 64, 0, op, st), "split planes-only + residual");
+    CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, fmis, nullptr, 0, 0, 0, 64, 0, op, st), "split C misaligned");
     CHECK(hfa_split_f16(-1, 4, fp, 4, hp, 4, 16, op, st), "split_f16 rows<0");
     CHECK(hfa_split_f16(4, 4, nullptr, 4, hp, 4, 16, op, st), "split_f16 NULL x");
     // attention
