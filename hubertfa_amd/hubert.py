@@ -300,11 +300,14 @@ class HubertEncoder:
             h2 = self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h1s, xs=f) if sp else \
                 ops.linear(f, L_.w2, L_.b2, residual=h1)
             return self._ln(h2, L_.ln2_w, L_.ln2_b, out=h2, split=want_split, planes_only=want_split)
-        # pre-LN (HubertEncoderLayerStableLayerNorm)
-        a_, a_s = self._ln(h, L_.ln1_w, L_.ln1_b, split=L_.wqkv_s is not None)
+        # pre-LN (HubertEncoderLayerStableLayerNorm): the LayerNorm outputs feed only split GEMMs (planes only);
+        # the residual stream is the raw f32 sum
+        q_planes = (self.precision == "split" and L_.wqkv_s is not None and L_.wo_s is not None and
+                    self.arch.hidden // self.arch.heads == 64)
+        a_, a_s = self._ln(h, L_.ln1_w, L_.ln1_b, split=L_.wqkv_s is not None, planes_only=q_planes)
         o = self.attention_block(a_, L_, lens, a_s)
         h = self._out_proj(o, L_, h)
-        a_, a_s = self._ln(h, L_.ln2_w, L_.ln2_b, split=sp)
+        a_, a_s = self._ln(h, L_.ln2_w, L_.ln2_b, split=sp, planes_only=sp)
         f = self._linear(a_, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp, xs=a_s)
         if sp:
             return self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h, xs=f), None
