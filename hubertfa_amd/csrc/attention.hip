@@ -25,10 +25,7 @@ constexpr int DH = 64;
 constexpr int KB = 32;          // keys per tile
 constexpr int QW = 32;          // queries per wave
 constexpr int NW = 4;           // waves per workgroup
-#ifndef HFA_ATTN_NS
-#define HFA_ATTN_NS 2
-#endif
-constexpr int NS = HFA_ATTN_NS; // LDS stages (NS-1 key tiles in flight)
+constexpr int NS = 2;           // LDS stages (NS-1 key tiles in flight)
 constexpr int TILE = KB * DH;   // floats per K (or V) tile image
 constexpr float kSlack = 8.0f;  // stale-max slack of the online softmax (log2 units)
 
