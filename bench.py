@@ -41,6 +41,7 @@ F32_MFMA_PEAK_TFLOPS = 157.3
 # ending in ", true>") runs one product per MAC: its ceiling is the f16 dense peak itself.
 F16_MFMA_PEAK_TFLOPS = 2516.6
 SPLIT_F32EQ_PEAK_TFLOPS = F16_MFMA_PEAK_TFLOPS / 3
+RANDOM_DATA_F16_TFLOPS = 1247.0    # MI355X_MICROARCH.md 'DVFS give-back' (1): bf16 GEMM on random data, measured
 
 
 def mfma_peak(kernel: str) -> float:
@@ -371,6 +372,13 @@ def main():
                      "traffic": traffic, "launches": ps["launches"], "avg_launch_ms": ps["avg_ms"],
                      "flops_per_launch": ps["avg_flops"]},
     }
+    if probe_name.startswith("gemm_split_kernel") and achieved:
+        # context, not the contract's peak: MI355X_MICROARCH.md 'DVFS give-back' item 1 measures a plain bf16 GEMM
+        # on random data at 1247 TF/s (the chip holds ~1.9 GHz under dense MFMA load), the rate a random-data f16
+        # MFMA loop can sustain; the split scheme's f32-equivalent share of it is a third (one product: all of it)
+        rd = RANDOM_DATA_F16_TFLOPS / (1 if probe_name.endswith(", true>") else 3)
+        out["roofline"]["random_data_mfma_rate"] = rd
+        out["roofline"]["frac_of_random_data_rate"] = achieved / rd
     iso = ops.KernelProbe("-", extra=SECONDARY)       # isolated serial steps for the secondary rooflines
     ops.PROBE = iso
     for _ in range(2):
