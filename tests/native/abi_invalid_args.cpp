@@ -75,6 +75,8 @@ int main() {
     CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, nullptr, nullptr, 0, 0, 0, 64, 0, op, st), "split no output");
     CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0, fp, 0, 0, 64, nullptr, 0, nullptr, hp, 0, 0, 0, 64, 0, op, st), "split planes-only + residual");
     CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, fmis, nullptr, 0, 0, 0, 64, 0, op, st), "split C misaligned");
+    CHECK(hfa_conv_gemm_split(64, 64, 64, 1, 1, hp, 0, 0, 0, 64, 1, 0, 64, 64, hp, 0, 0, 64, nullptr, 0, fp, 0,
+                              0, 64, hp, 4096, fp, nullptr, 0, 0, 0, 64, 0, op, st), "split R and Rs together");
     CHECK(hfa_split_f16(-1, 4, fp, 4, hp, 4, 16, op, st), "split_f16 rows<0");
     CHECK(hfa_split_f16(4, 4, nullptr, 4, hp, 4, 16, op, st), "split_f16 NULL x");
     // attention

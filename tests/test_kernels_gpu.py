@@ -259,6 +259,27 @@ def test_split_gemm_dual_output():
     assert torch.equal(ys, ops.split(y))
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(1000, 768, 512, 0), (997, 764, 768, 1), (15968 // 4, 768, 3072, 0)])
+def test_split_gemm_residual_planes(M, N, K, epi):
+    """Residual given as split planes (the post-LN residual stream): the same result as adding the f32 value the
+    planes encode (hi + 2^-11 lo, exact in f32), within one f32 rounding of adding the original f32 residual; N not a
+    multiple of the tile takes the column tail.  A plane residual with planes output is rejected."""
+    from hubertfa_amd import ops, _lib
+    d = torch.device("cuda")
+    x, w = _r(M, K, seed=41).to(d), (_r(N, K, seed=42) * K ** -0.5).to(d)
+    bias, res = _r(N, seed=43).to(d), (3 * _r(M, N, seed=44)).to(d)
+    xs, ws, rs = ops.split(x), ops.split(w), ops.split(res)
+    r22 = rs[0].float() + rs[1].float() / 2048.0               # the value the planes carry
+    y_pl = ops.linear_split(xs, ws, bias, residual=rs, epilogue=epi)
+    y_f22 = ops.linear_split(xs, ws, bias, residual=r22.contiguous(), epilogue=epi)
+    y_f32 = ops.linear_split(xs, ws, bias, residual=res, epilogue=epi)
+    assert torch.equal(y_pl, y_f22)
+    assert float((y_pl - y_f32).abs().max()) <= 2.0 ** -21 * float(res.abs().max()) + 1e-6
+    with pytest.raises(_lib.HFALibraryError):
+        ops.conv_gemm_split(xs, ws, Cs=torch.empty(2, M, N, dtype=torch.float16, device=d), M=M, N=N, K=K, ldx=K,
+                            R=rs, ldr=N, ldc=N)
+
+
 def test_conv0_groupnorm_gelu():
     from hubertfa_amd import ops
     B, N = 2, 16000
