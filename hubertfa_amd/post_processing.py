@@ -16,7 +16,9 @@ def add_SP(word_seq, word_intervals, wav_length, add_phone="SP"):
     if len(word_seq) == 0:
         return [add_phone], [[0, wav_length]]
     seq, ivs = [add_phone], [[0, word_intervals[0, 0]]]
-    for word, (start, end) in zip(word_seq, word_intervals):
+    # rows as Python floats (the same f64 values): iterating numpy rows costs ~2 us per interval
+    rows = word_intervals.tolist() if hasattr(word_intervals, "tolist") else word_intervals
+    for word, (start, end) in zip(word_seq, rows):
         if ivs[-1][1] < start:
             seq.append(add_phone)
             ivs.append([ivs[-1][1], start])

@@ -164,11 +164,14 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
     from hubertfa_amd.task import ForcedAlignmentTask
     from hubertfa_amd.wav_io import wav_info
 
+    import time
+    t_start = time.perf_counter()
     if not g2p.endswith("G2P"):
         g2p += "G2P"
     grapheme_to_phoneme = getattr(g2p_mod, g2p)(**kwargs)
     grapheme_to_phoneme.set_in_format("lab")
     rows = list(grapheme_to_phoneme.get_dataset(sorted(pathlib.Path(folder).rglob("*.wav"))))
+    t_g2p = time.perf_counter()
 
     rank, world, local = env_rank_world()
     local = local if device is None else device
@@ -194,8 +197,11 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
     torch.set_grad_enabled(False)
     model = ForcedAlignmentTask.load_from_checkpoint(ckpt, device=torch.device("cuda", local),
                                                      hubert_model_path=hubert_path)
+    model.on_predict_start()                             # the units encoder's weights (reference: predict start)
     errors = []
+    t_load = time.perf_counter()
     records, ok = _run(model, [rows[i] for i in mine], mine, batch_size, errors)
+    t_align = time.perf_counter()
     if world == 1 and not ok:
         raise SystemExit(1)
     if world > 1:
@@ -236,7 +242,10 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
     exporter = Exporter(predictions, errors + log, out_path)
     out_formats = ["textgrid"] + (["confidence"] if save_confidence else [])
     exporter.export(out_formats)
+    t_end = time.perf_counter()
     print("Output files are saved to the same folder as the input wav files.")
+    print(f"[timing] g2p {t_g2p - t_start:.2f} s, model load {t_load - t_g2p:.2f} s, wav read + align "
+          f"{t_align - t_load:.2f} s ({len(records)} files), gather + post-processing + export {t_end - t_align:.2f} s")
     if world > 1:
         dist.destroy_process_group()
 
