@@ -120,26 +120,32 @@ class Exporter:
         self.log = log
         self.out_path = pathlib.Path(out_path) if out_path else None
 
+    def write_textgrid(self, prediction, made=None):
+        """One prediction's ``TextGrid/<stem>.TextGrid``; ``made`` caches the folders already created."""
+        wav_path, wav_length, confidence, ph_seq, ph_intervals, word_seq, word_intervals = prediction
+        wav_path = pathlib.Path(wav_path)
+        tg = TextGrid()
+        word_tier = IntervalTier(name="words")
+        ph_tier = IntervalTier(name="phones")
+        for word, (start, end) in zip(word_seq, word_intervals):
+            word_tier.add(start, end, word)
+        for ph, (start, end) in zip(ph_seq, ph_intervals):
+            ph_tier.add(minTime=float(start), maxTime=end, mark=ph)
+        tg.append(word_tier)
+        tg.append(ph_tier)
+        base = self.out_path if self.out_path is not None else wav_path.parent
+        tg_path = base / "TextGrid" / wav_path.with_suffix(".TextGrid").name
+        if made is None or tg_path.parent not in made:
+            tg_path.parent.mkdir(parents=True, exist_ok=True)
+            if made is not None:
+                made.add(tg_path.parent)
+        tg.write(tg_path)
+
     def save_textgrids(self):
         print("Saving TextGrids...")
         made = set()
-        for wav_path, wav_length, confidence, ph_seq, ph_intervals, word_seq, word_intervals in self.predictions:
-            wav_path = pathlib.Path(wav_path)
-            tg = TextGrid()
-            word_tier = IntervalTier(name="words")
-            ph_tier = IntervalTier(name="phones")
-            for word, (start, end) in zip(word_seq, word_intervals):
-                word_tier.add(start, end, word)
-            for ph, (start, end) in zip(ph_seq, ph_intervals):
-                ph_tier.add(minTime=float(start), maxTime=end, mark=ph)
-            tg.append(word_tier)
-            tg.append(ph_tier)
-            base = self.out_path if self.out_path is not None else wav_path.parent
-            tg_path = base / "TextGrid" / wav_path.with_suffix(".TextGrid").name
-            if tg_path.parent not in made:
-                tg_path.parent.mkdir(parents=True, exist_ok=True)
-                made.add(tg_path.parent)
-            tg.write(tg_path)
+        for prediction in self.predictions:
+            self.write_textgrid(prediction, made)
 
     def save_confidence_fn(self):
         import pandas as pd
@@ -155,8 +161,10 @@ class Exporter:
             path.mkdir(parents=True, exist_ok=True)
             pd.DataFrame(data).to_csv(path / "confidence.csv", index=False)
 
-    def export(self, out_formats):
-        self.save_textgrids()
+    def export(self, out_formats, textgrids=True):
+        """``textgrids=False``: the TextGrids were already written (infer.py's streaming export)."""
+        if textgrids:
+            self.save_textgrids()
         if "confidence" in out_formats:
             self.save_confidence_fn()
         if self.log:

@@ -61,16 +61,26 @@ def fill_small_gaps(word_seq, word_intervals, wav_length):
     return word_seq, iv
 
 
+def post_process_one(prediction, add_phone="SP"):
+    """One utterance -> (processed prediction, None), or (None, [wav_path, exception]) for the error log."""
+    wav_path, wav_length, confidence, ph_seq, ph_intervals, word_seq, word_intervals = prediction
+    try:
+        word_seq, word_intervals = fill_small_gaps(word_seq, word_intervals, wav_length)
+        ph_seq, ph_intervals = fill_small_gaps(ph_seq, ph_intervals, wav_length)
+        word_seq, word_intervals = add_SP(word_seq, word_intervals, wav_length, add_phone)
+        ph_seq, ph_intervals = add_SP(ph_seq, ph_intervals, wav_length, add_phone)
+        return [wav_path, wav_length, confidence, ph_seq, ph_intervals, word_seq, word_intervals], None
+    except Exception as e:  # noqa: BLE001 — collected, never aborts the batch
+        return None, [wav_path, e]
+
+
 def post_processing(predictions, add_phone="SP"):
     print("Post-processing...")
     res, error_log = [], []
-    for wav_path, wav_length, confidence, ph_seq, ph_intervals, word_seq, word_intervals in predictions:
-        try:
-            word_seq, word_intervals = fill_small_gaps(word_seq, word_intervals, wav_length)
-            ph_seq, ph_intervals = fill_small_gaps(ph_seq, ph_intervals, wav_length)
-            word_seq, word_intervals = add_SP(word_seq, word_intervals, wav_length, add_phone)
-            ph_seq, ph_intervals = add_SP(ph_seq, ph_intervals, wav_length, add_phone)
-            res.append([wav_path, wav_length, confidence, ph_seq, ph_intervals, word_seq, word_intervals])
-        except Exception as e:  # noqa: BLE001 — collected, never aborts the batch
-            error_log.append([wav_path, e])
+    for pred in predictions:
+        r, err = post_process_one(pred, add_phone)
+        if err is None:
+            res.append(r)
+        else:
+            error_log.append(err)
     return res, error_log

@@ -27,12 +27,46 @@ def _recoverable():
     return (HFALibraryError, ValueError, AssertionError, KeyError, IndexError)
 
 
-def _predict(task, rows, keys, batch_size: int, errors: list) -> dict:
+class _StreamingExport:
+    """One-GPU runs: post-process and write each batch's TextGrids as soon as the batch is back, on the host while
+    the GPU runs the next batch, instead of after the whole folder.  The files written are the same; the
+    confidence table and the error log are assembled at the end in dataset order, as the batch path does."""
+
+    def __init__(self, rows, sr, frame_length, out_path):
+        from hubertfa_amd.export_tool import Exporter
+        self.rows, self.sr, self.frame_length = rows, sr, frame_length
+        self.writer = Exporter([], [], out_path)
+        self.done, self.log, self.made = {}, {}, set()
+        print("Post-processing...")
+        print("Saving TextGrids...")
+
+    def __call__(self, records: dict, keys):
+        from hubertfa_amd.alignment_decoder import utterance_result
+        from hubertfa_amd.post_processing import post_process_one
+        for i in keys:
+            wav_path, ph_seq, word_seq, p2w = self.rows[i]
+            rec = records[i]
+            r = utterance_result(rec, ph_seq, word_seq, p2w, self.frame_length)
+            pred, err = post_process_one((wav_path, rec["n44"] / self.sr, r["confidence"], r["ph_seq"],
+                                          r["ph_intervals"], r["word_seq"], r["word_intervals"]))
+            if err is not None:
+                self.log[i] = err
+                continue
+            self.writer.write_textgrid(pred, self.made)
+            self.done[i] = pred
+
+    def results(self):
+        """-> (predictions, post-processing log), both in dataset order."""
+        return [self.done[i] for i in sorted(self.done)], [self.log[i] for i in sorted(self.log)]
+
+
+def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> dict:
     """Align ``rows`` (wav_path, ph_seq, word_seq, ph_idx_to_word_idx); ``keys`` their dataset indices.
 
     Returns {dataset index: raw boundary record} (alignment_decoder.utterance_result turns a record into the
     reference's decode outputs).  A batch that raises a recoverable error is re-run file by file; a file that
-    fails alone goes to ``errors`` as [wav_path, exception] (the post-processing log)."""
+    fails alone goes to ``errors`` as [wav_path, exception] (the post-processing log).  ``on_batch(out, keys)``
+    is called with each completed batch's dataset indices (the one-GPU streaming export)."""
     import torch
     from hubertfa_amd.batching import plan_batches, resampled_length
     from hubertfa_amd.wav_io import read_wav
@@ -80,6 +114,8 @@ def _predict(task, rows, keys, batch_size: int, errors: list) -> dict:
         for k, r, n44 in zip(ks, res, n44s):
             out[k] = dict(n44=n44, T=r["T"], ph_idx_seq=r["ph_idx_seq"], ph_time_int=r["ph_time_int"],
                           frame_confidence=r["frame_confidence"], edge_diff=r["edge_diff"])
+        if on_batch is not None:
+            on_batch(out, ks)
 
     def run(ks, file_sr):
         handle, n44s = submit([items[k] for k in ks], file_sr)
@@ -131,10 +167,10 @@ def _predict(task, rows, keys, batch_size: int, errors: list) -> dict:
     return out
 
 
-def _run(task, rows, keys, batch_size, errors):
+def _run(task, rows, keys, batch_size, errors, on_batch=None):
     """_predict with the rank-level outcome: (records, ok)."""
     try:
-        return _predict(task, rows, keys, batch_size, errors), True
+        return _predict(task, rows, keys, batch_size, errors, on_batch), True
     except Exception as e:  # noqa: BLE001 — reported to the control plane; the shard is re-queued elsewhere
         import traceback
         traceback.print_exc()
@@ -200,7 +236,10 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
     model.on_predict_start()                             # the units encoder's weights (reference: predict start)
     errors = []
     t_load = time.perf_counter()
-    records, ok = _run(model, [rows[i] for i in mine], mine, batch_size, errors)
+    sr = model.melspec_config["sample_rate"]
+    # one GPU: each batch is post-processed and its TextGrids written while the GPU runs the next batch
+    stream = _StreamingExport(rows, sr, model.decoder.frame_length, out_path) if world == 1 else None
+    records, ok = _run(model, [rows[i] for i in mine], mine, batch_size, errors, stream)
     t_align = time.perf_counter()
     if world == 1 and not ok:
         raise SystemExit(1)
@@ -230,21 +269,24 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
             dist.destroy_process_group()
             return
 
-    sr = model.melspec_config["sample_rate"]
-    predictions = []
-    for i, (wav_path, ph_seq, word_seq, p2w) in enumerate(rows):
-        if i in records:
-            rec = records[i]
-            r = utterance_result(rec, ph_seq, word_seq, p2w, model.decoder.frame_length)
-            predictions.append((wav_path, rec["n44"] / sr, r["confidence"], r["ph_seq"], r["ph_intervals"],
-                                r["word_seq"], r["word_intervals"]))
-    predictions, log = post_processing(predictions)
+    if stream is not None:
+        predictions, log = stream.results()
+    else:
+        predictions = []
+        for i, (wav_path, ph_seq, word_seq, p2w) in enumerate(rows):
+            if i in records:
+                rec = records[i]
+                r = utterance_result(rec, ph_seq, word_seq, p2w, model.decoder.frame_length)
+                predictions.append((wav_path, rec["n44"] / sr, r["confidence"], r["ph_seq"], r["ph_intervals"],
+                                    r["word_seq"], r["word_intervals"]))
+        predictions, log = post_processing(predictions)
     exporter = Exporter(predictions, errors + log, out_path)
     out_formats = ["textgrid"] + (["confidence"] if save_confidence else [])
-    exporter.export(out_formats)
+    exporter.export(out_formats, textgrids=stream is None)
     t_end = time.perf_counter()
     print("Output files are saved to the same folder as the input wav files.")
-    print(f"[timing] g2p {t_g2p - t_start:.2f} s, model load {t_load - t_g2p:.2f} s, wav read + align "
+    what = "align + post-processing + TextGrids (streamed)" if stream is not None else "align"
+    print(f"[timing] g2p {t_g2p - t_start:.2f} s, model load {t_load - t_g2p:.2f} s, wav read + {what} "
           f"{t_align - t_load:.2f} s ({len(records)} files), gather + post-processing + export {t_end - t_align:.2f} s")
     if world > 1:
         dist.destroy_process_group()

@@ -123,18 +123,22 @@ def test_infer_two_ranks_match_one_rank(tmp_path):
     from click.testing import CliRunner
     import infer
     seg, dpath, ck, n = _mixed_folder(tmp_path)
-    base = ["-c", str(ck), "-f", str(seg), "-d", str(dpath), "--hubert_path", "synth:0", "--batch_size", "3"]
+    base = ["-c", str(ck), "-f", str(seg), "-d", str(dpath), "--hubert_path", "synth:0", "--batch_size", "3", "-sc"]
     out1 = tmp_path / "one"
-    r = CliRunner().invoke(infer.main, base + ["--out_path", str(out1)])
+    r = CliRunner().invoke(infer.main, base + ["--out_path", str(out1)])   # one GPU: the streaming export
     assert r.exit_code == 0, r.output + repr(r.exception)
     one = {p.name: p.read_bytes() for p in out1.rglob("*.TextGrid")}
     assert len(one) == n
+    conf = sorted(seg.rglob("confidence.csv"))
+    conf1 = [c.read_bytes() for c in conf]
+    assert conf1
     for tag, extra in (("two", None), ("requeue", {"HFA_FAULT_INJECT_RANK": "1"})):
         out = tmp_path / tag
         p = _torchrun(base + ["--out_path", str(out), "--dist_backend", "gloo", "--device", "0"], extra)
         assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
         got = {q.name: q.read_bytes() for q in out.rglob("*.TextGrid")}
         assert got == one, f"{tag}: {[k for k in one if got.get(k) != one[k]]} differ from the one-rank run"
+        assert [c.read_bytes() for c in conf] == conf1, f"{tag}: confidence.csv differs from the one-rank run"
         if extra:
             assert "re-running" in p.stdout and "shard failed" in p.stdout
 

@@ -102,6 +102,52 @@ def test_textgrid_and_confidence_export(tmp_path):
     assert list(df.columns) == ["name", "confidence"] and df["name"][0] == "utt"
 
 
+def test_streaming_export_matches_batch_export(tmp_path):
+    """infer.py's one-GPU streaming export (post-process + TextGrid per completed batch, batches out of dataset
+    order) writes the same TextGrids, confidence table and error log as post-processing the whole folder."""
+    import infer
+    from hubertfa_amd.alignment_decoder import utterance_result
+    from hubertfa_amd.export_tool import Exporter
+    from hubertfa_amd.post_processing import post_processing
+    rng = np.random.default_rng(3)
+    rows, records = [], {}
+    for i in range(7):
+        wav = tmp_path / "seg" / f"u{i}.wav"
+        wav.parent.mkdir(exist_ok=True)
+        wav.write_bytes(b"")
+        n_ph = 5 + i
+        ph_seq = ["SP"] + [f"p{j}" for j in range(n_ph - 2)] + ["SP"]
+        p2w = [-1] + [j // 2 for j in range(n_ph - 2)] + [-1]
+        words = [f"w{j}" for j in range((n_ph - 2 + 1) // 2)]
+        T = 200 + 30 * i
+        cuts = np.sort(rng.choice(np.arange(1, T - 1), n_ph - 1, replace=False))
+        rec = dict(n44=T * 512 + 100, T=T, ph_idx_seq=np.arange(n_ph), ph_time_int=np.concatenate([[0], cuts]),
+                   frame_confidence=rng.uniform(0.2, 1.0, T).astype(np.float32),
+                   edge_diff=rng.uniform(-1, 1, T).astype(np.float32))
+        if i == 4:                                   # all SP: no intervals, post-processing fails -> error log
+            ph_seq = ["SP"] * n_ph
+        rows.append((str(wav), ph_seq, words, p2w))
+        records[i] = rec
+    sr, fl = 44100, 512 / 44100
+    sink = infer._StreamingExport(rows, sr, fl, tmp_path / "stream")
+    for ks in ([5, 6], [0, 3, 1], [2, 4]):
+        sink(records, ks)
+    s_preds, s_log = sink.results()
+    preds = []
+    for i, (wav, ph_seq, words, p2w) in enumerate(rows):
+        r = utterance_result(records[i], ph_seq, words, p2w, fl)
+        preds.append((wav, records[i]["n44"] / sr, r["confidence"], r["ph_seq"], r["ph_intervals"], r["word_seq"],
+                      r["word_intervals"]))
+    b_preds, b_log = post_processing(preds)
+    Exporter(b_preds, b_log, tmp_path / "batch").export(["textgrid"])
+    assert [p[0] for p in s_preds] == [p[0] for p in b_preds]
+    assert [p[2] for p in s_preds] == [p[2] for p in b_preds]
+    assert len(b_log) == 1 and [(e[0], repr(e[1])) for e in s_log] == [(e[0], repr(e[1])) for e in b_log]
+    streamed = {p.name: p.read_bytes() for p in (tmp_path / "stream").rglob("*.TextGrid")}
+    batch = {p.name: p.read_bytes() for p in (tmp_path / "batch").rglob("*.TextGrid")}
+    assert streamed == batch and len(batch) == len(b_preds)
+
+
 def test_wav_roundtrip(tmp_path):
     from hubertfa_amd import synth
     from hubertfa_amd.wav_io import read_wav, write_wav
