@@ -220,8 +220,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_f32_kernel(const AttnP p) {
 
 // ---- split-f16 flash attention ---------------------------------------------------------------------------------
 // Q, K, V and O as split-f16 plane pairs (x = x1 + 2^-11 x2, gemm.hip's split scheme): every product is three exact
-// f16 x f16 MFMA products (x1 y1 into a main accumulator, x1 y2 + x2 y1 into a correction accumulator scaled by
-// 2^-11 at the end), so the contractions keep f32-class accuracy while running on v_mfma_f32_32x32x16_f16.
+// f16 x f16 MFMA products (scores: x1 y1 + x1 (2^-11 y2) + x2 (2^-11 y1) on one accumulator; output: one
+// accumulator at scale 2^11), so the contractions keep f32-class accuracy while running on
+// v_mfma_f32_32x32x16_f16.
 // Same structure as attn_fwd_f32_kernel (S^T = K Q^T with one query per lane, stale-max online softmax in the
 // exp2 domain, the P accumulator as the B operand of O^T += V^T P^T), with 64-key tiles and:
 //   * K image [64 keys][8 chunks of 16 B] per plane, chunk c of row r at slot c ^ ((r >> 1) & 7): the
@@ -358,29 +359,35 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
     for (int db = 0; db < 2; ++db) vofs[db] = vrow * (DH * 2) + (((4 * db + vch0) ^ vfx) << 4) + 8 * (gp & 1);
 
     const float qscale = p.scale * 1.44269504088896340736f;
-    // scores of a tile (combined, log2 units): s[kt][e] for keys 32 kt + (e & 3) + 8 (e >> 2) + 4 half
-    auto scores = [&](const _Float16* sK, f32x16 (&sM)[2], f32x16 (&sC)[2]) {
+    // One score accumulator: k1 q1 + k1 (2^-11 q2) + k2 (2^-11 q1), the two small products on Q planes pre-scaled
+    // once per wave (2^-11 q2 is the exact residual q - q1; an f16 subnormal below 2^-14, i.e. an absolute error
+    // <= 2^-25 |k| per product, under the f32 score's own rounding) -- no second accumulator, no combine pass.
+    // Against the two-accumulator form (main + correction, combined by one FMA per score): 0.092 -> 0.087 ms per
+    // layer (base), 0.118 -> 0.112 (large), 215 -> 204 VGPRs (profiles/r02/attn_single_acc_ab.txt).
+    f16x8 q1s[DH / 16], q2s[DH / 16];
+#pragma unroll
+    for (int kb = 0; kb < DH / 16; ++kb) {
+        q1s[kb] = q1[kb] * (_Float16)kLo;
+        q2s[kb] = q2[kb] * (_Float16)kLo;
+    }
+    auto scores = [&](const _Float16* sK, f32x16 (&sM)[2], f32x16 (&)[2]) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-            for (int e = 0; e < 16; ++e) sM[kt][e] = sC[kt][e] = 0.f;
+            for (int e = 0; e < 16; ++e) sM[kt][e] = 0.f;
 #pragma unroll
             for (int kb = 0; kb < DH / 16; ++kb) {
                 const f16x8 k1 = *reinterpret_cast<const f16x8*>(sK + kt * 32 * DH + kofs[kb]);
                 const f16x8 k2 = *reinterpret_cast<const f16x8*>(sK + SPLANE + kt * 32 * DH + kofs[kb]);
                 sM[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q1[kb], sM[kt], 0, 0, 0);
-                sC[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q2[kb], sC[kt], 0, 0, 0);
-                sC[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k2, q1[kb], sC[kt], 0, 0, 0);
+                sM[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q2s[kb], sM[kt], 0, 0, 0);
+                sM[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k2, q1s[kb], sM[kt], 0, 0, 0);
             }
         }
     };
-    // combined raw dot products (qscale is applied inside the exponent); done after the rest of the iteration so
-    // the MFMAs run meanwhile
-    auto combine = [&](const f32x16 (&sM)[2], const f32x16 (&sC)[2], f32x16 (&sc)[2]) {
+    auto combine = [&](const f32x16 (&sM)[2], const f32x16 (&)[2], f32x16 (&sc)[2]) {
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) sc[kt][e] = __builtin_fmaf(sC[kt][e], kLo, sM[kt][e]);
+        for (int kt = 0; kt < 2; ++kt) sc[kt] = sM[kt];
     };
 
     f32x16 o[2];
