@@ -27,6 +27,11 @@ _SIGS = {
     "hfa_viterbi_backtrack": [I, I, I, P, P, P, P, P, P, P, P, P, P],
     "hfa_lattice_prologue": [I, I, I, I, P, P, P, LL, LL, P, LL, LL, P, P, P, P, P, P, P, P, P],
     "hfa_viterbi_tuning": [I],
+    # WAV front end (wav.cpp, host memory)
+    "hfa_wav_info": [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32),
+                     ctypes.POINTER(ctypes.c_int32)],
+    "hfa_wav_read": [ctypes.c_char_p, ctypes.c_int32, P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                     ctypes.POINTER(ctypes.c_int32)],
 }
 _RESTYPE = {"hfa_last_error": ctypes.c_char_p, "hfa_build_arch": ctypes.c_char_p}
 

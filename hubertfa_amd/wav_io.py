@@ -1,89 +1,63 @@
 """WAV reading (torchaudio.load replacement) + ``load_wav`` (reference: tools/load_wav.py:4-8).
 
-RIFF/WAVE parser for PCM 8/16/24/32-bit integer and IEEE float 32/64 (incl. WAVE_FORMAT_EXTENSIBLE), scaled
-like torchaudio's default ``normalize=True`` (int16 / 2^15, int32 / 2^31, 24-bit / 2^23, uint8 (x-128)/128).
-``load_wav`` then resamples sr -> sample_rate with the width-6 sinc on the GPU and returns channel 0.
+The RIFF/WAVE decoder is native (libhfa ``hfa_wav_info`` / ``hfa_wav_read``, hubertfa_amd/csrc/wav.cpp): PCM
+8/16/24/32-bit integer and IEEE float 32/64 (incl. WAVE_FORMAT_EXTENSIBLE), scaled like torchaudio's default
+``normalize=True`` (int16 / 2^15, int32 / 2^31, 24-bit / 2^23, uint8 (x-128)/128), decoded straight into the
+caller's array (``read_wav_into``: a row of infer.py's pinned batch buffer).  ``load_wav`` then resamples
+sr -> sample_rate with the width-6 sinc on the GPU and returns channel 0.
 """
 from __future__ import annotations
 
+import ctypes
+import os
 import struct
 
 import numpy as np
 import torch
 
+from . import _lib
 
-def read_wav(path) -> tuple[np.ndarray, int]:
-    """-> (float32 [channels, N], sample_rate)."""
-    with open(path, "rb") as f:
-        data = f.read()
-    if data[:4] != b"RIFF" or data[8:12] != b"WAVE":
-        raise ValueError(f"{path}: not a RIFF/WAVE file")
-    pos, fmt, pcm = 12, None, None
-    while pos + 8 <= len(data):
-        cid, size = data[pos:pos + 4], struct.unpack("<I", data[pos + 4:pos + 8])[0]
-        body = data[pos + 8:pos + 8 + size]
-        if cid == b"fmt ":
-            tag, ch, sr, _, _, bits = struct.unpack("<HHIIHH", body[:16])
-            if tag == 0xFFFE and len(body) >= 26:
-                tag = struct.unpack("<H", body[24:26])[0]
-            fmt = (tag, ch, sr, bits)
-        elif cid == b"data":
-            pcm = body
-        pos += 8 + size + (size & 1)
-    if fmt is None or pcm is None:
-        raise ValueError(f"{path}: missing fmt or data chunk")
-    tag, ch, sr, bits = fmt
-    if tag == 3:
-        x = np.frombuffer(pcm, dtype="<f4" if bits == 32 else "<f8").astype(np.float32)
-    elif tag == 1:
-        if bits == 8:
-            x = (np.frombuffer(pcm, np.uint8).astype(np.float32) - 128.0) / 128.0
-        elif bits == 16:
-            x = np.frombuffer(pcm, "<i2").astype(np.float32) / 32768.0
-        elif bits == 24:
-            b = np.frombuffer(pcm[: len(pcm) // 3 * 3], np.uint8).reshape(-1, 3).astype(np.int32)
-            v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
-            v = np.where(v >= 1 << 23, v - (1 << 24), v)
-            x = v.astype(np.float32) / float(1 << 23)
-        elif bits == 32:
-            x = (np.frombuffer(pcm, "<i4").astype(np.float64) / 2147483648.0).astype(np.float32)
-        else:
-            raise ValueError(f"{path}: unsupported PCM width {bits}")
-    else:
-        raise ValueError(f"{path}: unsupported WAVE format tag {tag}")
-    n = len(x) // ch
-    return x[: n * ch].reshape(n, ch).T.copy(), sr
+def _path(path) -> bytes:
+    return os.fsencode(os.fspath(path))
+
+
+def _err(path, e: Exception) -> ValueError:
+    return ValueError(f"{path}: {e}")
 
 
 def wav_info(path) -> tuple[int, int, int]:
-    """-> (samples per channel, sample_rate, channels) from the RIFF headers only (the data chunk is skipped,
-    not read): the sharding cost estimate of a multi-GPU run needs every file's length before any is loaded."""
-    with open(path, "rb") as f:
-        head = f.read(12)
-        if head[:4] != b"RIFF" or head[8:12] != b"WAVE":
-            raise ValueError(f"{path}: not a RIFF/WAVE file")
-        fmt, n_bytes = None, None
-        while True:
-            hdr = f.read(8)
-            if len(hdr) < 8:
-                break
-            cid, size = hdr[:4], struct.unpack("<I", hdr[4:])[0]
-            if cid == b"fmt ":
-                body = f.read(size)
-                _, ch, sr, _, block, _ = struct.unpack("<HHIIHH", body[:16])
-                fmt = (ch, sr, block)
-                if size & 1:
-                    f.seek(1, 1)
-            else:
-                if cid == b"data":
-                    n_bytes = size
-                f.seek(size + (size & 1), 1)
-            if fmt is not None and n_bytes is not None:
-                break
-    if fmt is None or n_bytes is None:
-        raise ValueError(f"{path}: missing fmt or data chunk")
-    ch, sr, block = fmt
-    return n_bytes // max(block, 1), sr, ch
+    """-> (samples per channel, sample_rate, channels) from the RIFF headers only (the data chunk is not read):
+    the batch plan and the multi-GPU shard costs need every file's length before any is decoded."""
+    n, ch, sr = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32()
+    try:
+        _lib.call("hfa_wav_info", _path(path), ctypes.byref(n), ctypes.byref(ch), ctypes.byref(sr))
+    except _lib.HFALibraryError as e:
+        raise _err(path, e) from None
+    return n.value, sr.value, ch.value
+
+
+def read_wav_into(path, dst: np.ndarray, channel: int = 0) -> tuple[int, int]:
+    """Decode ``channel`` of ``path`` into the front of the contiguous float32 array ``dst`` -> (frames,
+    sample_rate).  ValueError if the file is unreadable or does not fit."""
+    if dst.dtype != np.float32 or not dst.flags.c_contiguous:
+        raise ValueError("read_wav_into: dst must be a contiguous float32 array")
+    n, sr = ctypes.c_int64(), ctypes.c_int32()
+    try:
+        _lib.call("hfa_wav_read", _path(path), channel, dst.ctypes.data, dst.size, ctypes.byref(n),
+                  ctypes.byref(sr))
+    except _lib.HFALibraryError as e:
+        raise _err(path, e) from None
+    return n.value, sr.value
+
+
+def read_wav(path) -> tuple[np.ndarray, int]:
+    """-> (float32 [channels, N], sample_rate)."""
+    n, _, ch = wav_info(path)
+    x = np.empty((ch, n), np.float32)
+    m, sr = read_wav_into(path, x.reshape(-1), channel=-1)
+    if m != n:
+        raise ValueError(f"{path}: changed while being read")
+    return x, sr
 
 
 def write_wav(path, x: np.ndarray, sr: int) -> None:

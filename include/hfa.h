@@ -3,8 +3,8 @@
  * Conventions (all entry points):
  *   - return 0 on success, HFA_EINVAL (-1000) on a bad argument, -(hipError_t) on a HIP launch error;
  *     hfa_last_error() gives the calling thread's last message.
- *   - every pointer is a DEVICE pointer owned by the caller; the library never allocates persistent memory
- *     and never frees caller memory.
+ *   - every pointer is a DEVICE pointer owned by the caller (except the host-side WAV reader's), the library
+ *     never allocates persistent memory and never frees caller memory.
  *   - stream-ordered on `stream`, no implicit synchronisation, re-entrant across streams/threads, so every
  *     call can be captured into a hipGraph.  The *_tuning hooks (benchmark overrides) set state of the calling
  *     thread only (thread-local), so they never change another thread's launches.
@@ -33,6 +33,19 @@ extern "C" {
 const char* hfa_last_error(void);
 int hfa_abi_version(void);
 const char* hfa_build_arch(void);
+
+/* ---- WAV front end (hubertfa_amd/csrc/wav.cpp; HOST memory, no stream, never touches the GPU) ----------------
+ * Replace torchaudio.load in tools/load_wav.py:5 (default normalize=True): RIFF/WAVE, PCM 8/16/24/32-bit or IEEE
+ * float 32/64, plain or WAVE_FORMAT_EXTENSIBLE; samples scaled as torchaudio (uint8 (x-128)/128, int16 / 2^15,
+ * 24-bit / 2^23, int32 / 2^31, f64 rounded to f32).  A data chunk longer than the file ends at end of file.
+ * hfa_wav_info reads the headers only (frames per channel, channels, sample rate): the length-sorted batch plan
+ * and the multi-GPU shard costs need every file's length before any is decoded.
+ * hfa_wav_read decodes channel `channel` (0-based; the reference keeps waveform[0]) into dst[frames], or every
+ * channel planar into dst[channels][frames] with channel = -1; `capacity` is dst's size in floats (HFA_EINVAL
+ * if the samples do not fit).  `path` is a NUL-terminated file name; both are re-entrant. */
+int hfa_wav_info(const char* path, int64_t* frames, int32_t* channels, int32_t* sample_rate);
+int hfa_wav_read(const char* path, int32_t channel, float* dst, int64_t capacity, int64_t* frames,
+                 int32_t* sample_rate);
 
 /* ---- alignment decoder (hubertfa_amd/csrc/viterbi.hip) ------------------------------------------------------
  * hfa_viterbi_forward replaces AlignmentDecoder.forward_pass, tools/alignment_decoder.py:170-230 (numba JIT),

@@ -69,7 +69,7 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
     is called with each completed batch's dataset indices (the one-GPU streaming export)."""
     import torch
     from hubertfa_amd.batching import plan_batches, resampled_length
-    from hubertfa_amd.wav_io import read_wav
+    from hubertfa_amd.wav_io import read_wav_into, wav_info
 
     if os.environ.get("HFA_FAULT_INJECT_RANK") == os.environ.get("RANK", "0"):
         raise RuntimeError("fault injected (HFA_FAULT_INJECT_RANK): this rank's shard fails")
@@ -78,30 +78,36 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
     sr = task.melspec_config["sample_rate"]
     items = {}
 
-    def _read(path):
+    def _info(path):
         try:
-            return read_wav(path), None
+            return wav_info(path), None
         except (OSError, ValueError) as e:
             return None, e
-    # file reads and the int16 -> f32 conversion release the GIL: a small thread pool overlaps them
+    # Only the RIFF headers are read up front (lengths for the batch plan); each batch's files are decoded when the
+    # batch is submitted, by libhfa's native reader straight into the batch's pinned buffer, on a thread pool
+    # (ctypes drops the GIL), so host memory holds the batches in flight, not the folder.
     from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as pool:
-        loaded = list(pool.map(_read, [r[0] for r in rows]))
-    for key, (wav_path, ph_seq, word_seq, p2w), (xs, e) in zip(keys, rows, loaded):
+    pool = ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1))
+    for key, (wav_path, ph_seq, word_seq, p2w), (info, e) in zip(keys, rows, pool.map(_info, [r[0] for r in rows])):
         if e is not None:
             errors.append([wav_path, e])
             continue
-        x, file_sr = xs
-        items[key] = (wav_path, x[0], file_sr, ph_seq, word_seq, p2w)
+        n, file_sr, _ = info
+        items[key] = (wav_path, n, file_sr, ph_seq, word_seq, p2w)
     out = {}
+
+    def _decode(job):
+        path, row, n = job
+        got, _ = read_wav_into(path, row, channel=0)     # channel 0, as the reference's waveform[0]
+        if got != n:
+            raise ValueError(f"{path}: {got} samples read, the header said {n}")
 
     def submit(chunk, file_sr):
         """-> (fetch handle, per-file sample counts at the melspec rate)."""
-        lens = [len(c[1]) for c in chunk]
+        lens = [c[1] for c in chunk]
         wav_h = torch.zeros((len(chunk), max(lens)), dtype=torch.float32, pin_memory=True)
-        wav_np = wav_h.numpy()           # rows written straight into pinned memory
-        for r, c in enumerate(chunk):
-            wav_np[r, :lens[r]] = c[1]
+        wav_np = wav_h.numpy()           # rows decoded straight into pinned memory
+        list(pool.map(_decode, [(c[0], wav_np[r], lens[r]) for r, c in enumerate(chunk)]))
         wav = task.upload(wav_h)         # pinned non-blocking H2D: no host sync
         handle = task.submit(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
                              wav_sr=file_sr, lengths=lens if len(chunk) > 1 else None)
@@ -143,27 +149,30 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
     # alone (the reference's B=1); files too short for the encoder's 400-sample window are aligned alone.
     # One batch in flight: the host assembles batch i while the GPU runs batch i+1 (task.submit: encoder on the
     # main stream, head + Viterbi on a side stream).
-    plan = plan_batches([(k, len(it[1]), it[2]) for k, it in items.items()], batch_size, sr,
-                        task.unitsEncoder.encoder_sample_rate)
-    pending = None
-    for file_sr, ks in plan:
-        job, err = None, None
-        try:
-            job = run(ks, file_sr)
-        except recoverable as e:
-            err = e
+    try:
+        plan = plan_batches([(k, it[1], it[2]) for k, it in items.items()], batch_size, sr,
+                            task.unitsEncoder.encoder_sample_rate)
+        pending = None
+        for file_sr, ks in plan:
+            job, err = None, None
+            try:
+                job = run(ks, file_sr)
+            except recoverable as e:
+                err = e
+            if pending is not None:
+                settle(pending)
+                pending = None
+            if job is not None:
+                pending = job
+            elif len(ks) == 1:
+                errors.append([items[ks[0]][0], err])
+            else:
+                for k in ks:
+                    alone(k, file_sr)
         if pending is not None:
             settle(pending)
-            pending = None
-        if job is not None:
-            pending = job
-        elif len(ks) == 1:
-            errors.append([items[ks[0]][0], err])
-        else:
-            for k in ks:
-                alone(k, file_sr)
-    if pending is not None:
-        settle(pending)
+    finally:
+        pool.shutdown()
     return out
 
 

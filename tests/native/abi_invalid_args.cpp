@@ -125,6 +125,37 @@ int main() {
     CHECK(hfa_selftest_erf(-1, fp, fp, fp, st), "erf n<0");
     CHECK(hfa_selftest_gelu(-1, fp, fp, st), "gelu n<0");
     CHECK(hfa_resample_f32(1, 100, fp, 100, 0, 441, fp, 16, 6, ws, fp, 300, st), "resample orig=0");
+    // WAV front end (host memory): null arguments, a missing file, a non-RIFF file, a short buffer, a bad channel
+    {
+        int64_t nf = 0;
+        int32_t ch = 0, sr = 0;
+        float buf[64];
+        CHECK(hfa_wav_info(nullptr, &nf, &ch, &sr), "wav_info NULL path");
+        CHECK(hfa_wav_info("/nonexistent/x.wav", &nf, &ch, &sr), "wav_info missing file");
+        CHECK(hfa_wav_read("/nonexistent/x.wav", 0, buf, 64, &nf, &sr), "wav_read missing file");
+        CHECK(hfa_wav_read("/proc/self/cmdline", 0, buf, 64, &nf, &sr), "wav_read not RIFF");
+        CHECK(hfa_wav_read(nullptr, 0, buf, 64, &nf, &sr), "wav_read NULL path");
+        CHECK(hfa_wav_read("/proc/self/cmdline", 0, nullptr, 64, &nf, &sr), "wav_read NULL dst");
+        CHECK(hfa_wav_read("/proc/self/cmdline", 0, buf, -1, &nf, &sr), "wav_read capacity<0");
+        const char* tmp = "/tmp/hfa_abi_invalid.wav";   // 16-bit mono, 100 frames
+        if (FILE* f = std::fopen(tmp, "wb")) {
+            const unsigned char hdr[44] = {'R', 'I', 'F', 'F', 236, 0, 0, 0, 'W', 'A', 'V', 'E', 'f', 'm', 't', ' ',
+                                           16, 0, 0, 0, 1, 0, 1, 0, 0x80, 0x3e, 0, 0, 0, 0x7d, 0, 0, 2, 0, 16, 0,
+                                           'd', 'a', 't', 'a', 200, 0, 0, 0};
+            std::fwrite(hdr, 1, 44, f);
+            const short z[100] = {0};
+            std::fwrite(z, 2, 100, f);
+            std::fclose(f);
+            CHECK(hfa_wav_read(tmp, 0, buf, 64, &nf, &sr), "wav_read short buffer");
+            CHECK(hfa_wav_read(tmp, 1, buf, 64, &nf, &sr), "wav_read channel 1 of 1");
+            CHECK(hfa_wav_read(tmp, -2, buf, 64, &nf, &sr), "wav_read channel -2");
+            if (hfa_wav_info(tmp, &nf, &ch, &sr) != 0 || nf != 100 || ch != 1 || sr != 16000) {
+                std::printf("FAIL wav_info on a valid file\n");
+                ++g_fail;
+            }
+            std::remove(tmp);
+        }
+    }
     // host queries and tuning hooks (thread-local state; name strings stay valid, bounded)
     for (int cfg = 0; cfg < 25; ++cfg) {
         hfa_gemm_split_tuning(cfg);

@@ -177,3 +177,32 @@ def test_predict_isolates_failing_file(tmp_path):
     for k in got:
         for f in ("ph_time_int", "ph_idx_seq", "frame_confidence", "edge_diff"):
             assert np.array_equal(got[k][f], ref[k][f]), (k, f)
+
+
+def test_infer_cli_skips_unreadable_and_multichannel(tmp_path):
+    """A file that is not a WAV is logged and skipped (the rest of the folder is aligned); a stereo 24-bit file
+    is aligned on its channel 0 (the reference's waveform[0]) exactly like the mono 16-bit file holding the same
+    samples."""
+    import struct
+    from click.testing import CliRunner
+    import infer
+    from hubertfa_amd.wav_io import read_wav
+    seg, dpath, ck, n = _mixed_folder(tmp_path)
+    (seg / "zz_bad.wav").write_bytes(b"not a wav file at all")
+    (seg / "zz_bad.lab").write_text((seg / "m0.lab").read_text())
+    x, sr = read_wav(seg / "m3.wav")                                # 16-bit samples: exact in 24 bits
+    v = np.round(x[0].astype(np.float64) * (1 << 23)).astype(np.int64)
+    frames = np.stack([v, -v], axis=1).reshape(-1)                 # channel 1 differs
+    pcm = b"".join(int(s & 0xFFFFFF).to_bytes(3, "little") for s in frames)
+    fmt = struct.pack("<HHIIHH", 1, 2, sr, sr * 6, 6, 24)
+    body = b"fmt " + struct.pack("<I", 16) + fmt + b"data" + struct.pack("<I", len(pcm)) + pcm
+    (seg / "zz_st.wav").write_bytes(b"RIFF" + struct.pack("<I", 4 + len(body)) + b"WAVE" + body)
+    (seg / "zz_st.lab").write_text((seg / "m3.lab").read_text())
+    out = tmp_path / "out"
+    r = CliRunner().invoke(infer.main, ["-c", str(ck), "-f", str(seg), "-d", str(dpath), "--hubert_path", "synth:0",
+                                        "--batch_size", "4", "--out_path", str(out)])
+    assert r.exit_code == 0, r.output + repr(r.exception)
+    assert "zz_bad.wav" in r.output and "not a RIFF/WAVE file" in r.output
+    got = {p.name for p in out.rglob("*.TextGrid")}
+    assert "zz_bad.TextGrid" not in got and len(got) == n + 1
+    assert (out / "TextGrid" / "zz_st.TextGrid").read_text() == (out / "TextGrid" / "m3.TextGrid").read_text()

@@ -159,6 +159,79 @@ def test_wav_roundtrip(tmp_path):
     np.testing.assert_array_equal(y[0], x)   # synth audio is already s16-quantised
 
 
+def _wav_bytes(tag, bits, ch, payload, extensible=False, extra=False, data_size=None):
+    import struct
+    block = ch * bits // 8
+    if extensible:
+        fmt = struct.pack("<HHIIHHHHIH14s", 0xFFFE, ch, 22050, 22050 * block, block, bits, 22, bits, 0, tag,
+                          b"\x00\x00\x00\x00\x10\x00\x80\x00\x00\xaa\x00\x38\x9b\x71")
+    else:
+        fmt = struct.pack("<HHIIHH", tag, ch, 22050, 22050 * block, block, bits)
+    body = b"fmt " + struct.pack("<I", len(fmt)) + fmt
+    if extra:                                    # an odd-sized chunk (padded to even) before the data
+        body += b"LIST" + struct.pack("<I", 5) + b"abcde" + b"\x00"
+    body += b"data" + struct.pack("<I", len(payload) if data_size is None else data_size) + payload
+    return b"RIFF" + struct.pack("<I", 4 + len(body)) + b"WAVE" + body
+
+
+@pytest.mark.parametrize("tag,bits,dtype", [(1, 8, "u1"), (1, 16, "<i2"), (1, 24, None), (1, 32, "<i4"),
+                                            (3, 32, "<f4"), (3, 64, "<f8")])
+@pytest.mark.parametrize("ch,extensible,extra", [(1, False, False), (2, True, True), (3, False, True)])
+def test_native_wav_reader_matches_restatement(tmp_path, tag, bits, dtype, ch, extensible, extra):
+    """libhfa's hfa_wav_read / hfa_wav_info (csrc/wav.cpp) against the numpy restatement of torchaudio.load's
+    normalisation (oracle/wav_read.py), bit for bit, every format and channel layout the reader accepts."""
+    from hubertfa_amd.wav_io import read_wav, read_wav_into, wav_info
+    from oracle.wav_read import read_wav_np, wav_info_np
+    rng = np.random.default_rng(bits * 10 + ch)
+    n = 70001                                    # > one 65 536-frame decode block
+    if dtype is None:
+        payload = rng.integers(0, 256, n * ch * 3, dtype=np.uint8).tobytes()
+    elif dtype[-2] == "f":
+        payload = (rng.standard_normal(n * ch) * 0.5).astype(dtype).tobytes()
+    else:
+        info = np.iinfo(np.dtype(dtype))
+        v = rng.integers(info.min, info.max, n * ch, dtype=np.int64, endpoint=True)
+        v[:4] = [info.min, info.max, 0, -1 if info.min < 0 else 128]
+        payload = v.astype(dtype).tobytes()
+    p = tmp_path / "x.wav"
+    p.write_bytes(_wav_bytes(tag, bits, ch, payload, extensible, extra))
+    x, sr = read_wav(p)
+    y, sr2 = read_wav_np(p)
+    assert sr == sr2 == 22050 and x.shape == y.shape == (ch, n)
+    np.testing.assert_array_equal(x, y)
+    assert wav_info(p) == wav_info_np(p) == (n, 22050, ch)
+    row = np.full(n + 5, 7.0, np.float32)      # one channel into a longer row: the tail is left alone
+    assert read_wav_into(p, row, channel=ch - 1) == (n, 22050)
+    np.testing.assert_array_equal(row[:n], y[ch - 1])
+    assert (row[n:] == 7.0).all()
+
+
+def test_native_wav_reader_edges(tmp_path):
+    from hubertfa_amd.wav_io import read_wav, read_wav_into, wav_info
+    from oracle.wav_read import read_wav_np
+    v = np.arange(-500, 501, dtype="<i2")
+    p = tmp_path / "s.wav"
+    p.write_bytes(_wav_bytes(1, 16, 1, v.tobytes(), data_size=0xFFFFFFFF))   # streaming writer's size
+    x, _ = read_wav(p)
+    np.testing.assert_array_equal(x, read_wav_np(p)[0])
+    assert wav_info(p)[0] == 1001
+    p.write_bytes(_wav_bytes(1, 16, 2, v.tobytes()[:-2]))                   # a trailing partial frame is dropped
+    assert read_wav(p)[0].shape == (2, 500)
+    bad = [(b"RIFX" + b"\0" * 40, "not a RIFF"), (_wav_bytes(1, 12, 1, b"\0" * 8), "unsupported"),
+           (_wav_bytes(1, 16, 1, b"")[:36], "missing fmt or data")]
+    for raw, msg in bad:
+        p.write_bytes(raw)
+        with pytest.raises(ValueError, match=msg):
+            read_wav(p)
+    with pytest.raises(ValueError, match="cannot open"):
+        wav_info(tmp_path / "nope.wav")
+    p.write_bytes(_wav_bytes(1, 16, 1, v.tobytes()))
+    with pytest.raises(ValueError, match="do not fit"):
+        read_wav_into(p, np.zeros(1000, np.float32))
+    with pytest.raises(ValueError, match="channel 1 of 1"):
+        read_wav_into(p, np.zeros(2000, np.float32), channel=1)
+
+
 def test_checkpoint_roundtrip(tmp_path):
     import torch
     from hubertfa_amd.task import synth_checkpoint
