@@ -168,7 +168,7 @@ def config_name(encoder: str, world: int, B: int, seconds: float = 10.0) -> str:
 
 def host_io(wav_np, res, seconds, budget_s=3.0):
     """file I/O and TextGrid writing, reported beside (not inside) the timed wave->boundaries path:
-    read the batch as 16-bit WAV files (wav_io.read_wav, the CLI's reader) and write its TextGrids + confidence.csv
+    read the batch as 16-bit WAV files (wav_io.read_wav, the CLI's native reader) and write its TextGrids + confidence.csv
     (post_processing + Exporter, the CLI's writer) in a temporary directory, on the host; ms per batch."""
     import tempfile
     from hubertfa_amd.export_tool import Exporter
@@ -197,8 +197,9 @@ def host_io(wav_np, res, seconds, budget_s=3.0):
             t_write += time.perf_counter() - t0
             m += 1
     return {"wav_read_ms_per_batch": 1e3 * t_read / n, "textgrid_write_ms_per_batch": 1e3 * t_write / m,
-            "files_per_batch": B, "note": "host only, one thread, outside the timed region (infer.py reads the files "
-                                          "on a thread pool before the GPU pass and writes after it)"}
+            "files_per_batch": B, "note": "host only, one thread, outside the timed region (infer.py decodes a batch's "
+                                          "files on a thread pool into its pinned upload buffer, and on one GPU "
+                                          "writes each batch's TextGrids, while the GPU runs the neighbouring batch)"}
 
 
 SECONDARY = ("viterbi_forward_kernel", "hfa_conv0_f32", "attn_fwd_split_kernel", "attn_fwd_f32_kernel")
