@@ -92,6 +92,8 @@ int parse(File& fh, const char* path, WavFmt& w) {
     return 0;
 }
 
+static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "RIFF samples are little-endian; so is the host");
+
 // one sample, scaled as torchaudio.load(normalize=True)
 template <int TAG, int BITS>
 inline float sample(const unsigned char* p) {
@@ -106,13 +108,17 @@ inline float sample(const unsigned char* p) {
     } else if constexpr (BITS == 8) {
         return ((float)p[0] - 128.0f) / 128.0f;
     } else if constexpr (BITS == 16) {
-        return (float)(int16_t)rd16(p) * (1.0f / 32768.0f);
+        int16_t v;                                   // little-endian host (static_assert above): a plain load
+        memcpy(&v, p, 2);
+        return (float)v * (1.0f / 32768.0f);
     } else if constexpr (BITS == 24) {
         int32_t v = (int32_t)(p[0] | (p[1] << 8) | (p[2] << 16));
         if (v >= (1 << 23)) v -= (1 << 24);
         return (float)v * (1.0f / 8388608.0f);
     } else {
-        return (float)(int32_t)rd32(p) * (1.0f / 2147483648.0f);   // round to f32, then exact scaling
+        int32_t v;
+        memcpy(&v, p, 4);
+        return (float)v * (1.0f / 2147483648.0f);    // round to f32, then exact scaling
     }
 }
 
@@ -120,11 +126,16 @@ inline float sample(const unsigned char* p) {
 template <int TAG, int BITS>
 void decode(const unsigned char* b, long long m, int ch, int channel, long long f0, long long n, float* dst) {
     constexpr int bps = BITS / 8;
-    if (channel >= 0) {
-        for (long long i = 0; i < m; ++i) dst[f0 + i] = sample<TAG, BITS>(b + (i * ch + channel) * bps);
-    } else {
-        for (long long i = 0; i < m; ++i)
-            for (int c = 0; c < ch; ++c) dst[c * n + f0 + i] = sample<TAG, BITS>(b + (i * ch + c) * bps);
+    if (ch == 1) {                                   // mono: contiguous, vectorised
+        float* __restrict__ d = dst + f0;
+        for (long long i = 0; i < m; ++i) d[i] = sample<TAG, BITS>(b + i * bps);
+        return;
+    }
+    const int c0 = channel >= 0 ? channel : 0, c1 = channel >= 0 ? channel + 1 : ch;
+    for (int c = c0; c < c1; ++c) {                  // one channel at a time: a strided gather per channel
+        float* __restrict__ d = dst + (channel >= 0 ? 0 : (long long)c * n) + f0;
+        const unsigned char* s = b + (long long)c * bps;
+        for (long long i = 0; i < m; ++i) d[i] = sample<TAG, BITS>(s + i * ch * bps);
     }
 }
 
