@@ -114,6 +114,46 @@ def read_textgrid(path):
     return tiers
 
 
+def _tier_rows(seq, intervals, start_as_float, null=""):
+    """(start, end, mark) of one tier with its gaps filled by ``null``, the values exactly as IntervalTier.add
+    stores them (``start_as_float``: the phones tier's float(start)), for in-order, non-overlapping intervals
+    starting at >= 0; None when the tier needs IntervalTier's general path (out of order, overlapping, empty or
+    negative-length intervals, which it sorts or rejects, or float32 arrays, whose scalars it keeps as numpy)."""
+    if hasattr(intervals, "dtype"):
+        if intervals.dtype != "float64":
+            return None
+        intervals = intervals.tolist()           # numpy f64 -> float: the conversion _Interval applies
+    rows, prev = [], 0.0
+    for mark, (a, b) in zip(seq, intervals):
+        a = float(a) if start_as_float or isinstance(a, float) else a
+        b = float(b) if isinstance(b, float) else b
+        if not (a < b) or a < prev:
+            return None
+        if prev < a:
+            rows.append((prev, a, null))
+        rows.append((a, b, mark))
+        prev = b
+    return rows
+
+
+def textgrid_text(word_seq, word_intervals, ph_seq, ph_intervals, null=""):
+    """The file ``Exporter`` writes for one prediction (TextGrid with tiers ``words`` and ``phones``), built
+    straight from the interval arrays; None when a tier needs the general IntervalTier path."""
+    tiers = [("words", _tier_rows(word_seq, word_intervals, False, null)),
+             ("phones", _tier_rows(ph_seq, ph_intervals, True, null))]
+    if any(r is None or not r for _, r in tiers):
+        return None
+    maxT = max(r[-1][1] for _, r in tiers)
+    out = ['File type = "ooTextFile"', 'Object class = "TextGrid"', "", "xmin = 0.0", f"xmax = {maxT}",
+           "tiers? <exists>", f"size = {len(tiers)}", "item []:"]
+    for i, (name, rows) in enumerate(tiers, 1):
+        out += [f"\titem [{i}]:", '\t\tclass = "IntervalTier"', f'\t\tname = "{name}"', "\t\txmin = 0.0",
+                f"\t\txmax = {maxT}", f"\t\tintervals: size = {len(rows)}"]
+        out += [f'\t\t\tintervals [{j}]:\n\t\t\t\txmin = {a}\n\t\t\t\txmax = {b}\n\t\t\t\ttext = "'
+                + str(m).replace('"', '""') + '"' for j, (a, b, m) in enumerate(rows, 1)]
+    return "\n".join(out) + "\n"
+
+
 class Exporter:
     def __init__(self, predictions, log, out_path=None):
         self.predictions = predictions
@@ -124,6 +164,17 @@ class Exporter:
         """One prediction's ``TextGrid/<stem>.TextGrid``; ``made`` caches the folders already created."""
         wav_path, wav_length, confidence, ph_seq, ph_intervals, word_seq, word_intervals = prediction
         wav_path = pathlib.Path(wav_path)
+        base = self.out_path if self.out_path is not None else wav_path.parent
+        tg_path = base / "TextGrid" / wav_path.with_suffix(".TextGrid").name
+        if made is None or tg_path.parent not in made:
+            tg_path.parent.mkdir(parents=True, exist_ok=True)
+            if made is not None:
+                made.add(tg_path.parent)
+        text = textgrid_text(word_seq, word_intervals, ph_seq, ph_intervals)
+        if text is not None:                 # in-order intervals (post-processing's output): one formatting pass
+            with open(tg_path, "w", encoding="utf-8") as f:
+                f.write(text)
+            return
         tg = TextGrid()
         word_tier = IntervalTier(name="words")
         ph_tier = IntervalTier(name="phones")
@@ -133,12 +184,6 @@ class Exporter:
             ph_tier.add(minTime=float(start), maxTime=end, mark=ph)
         tg.append(word_tier)
         tg.append(ph_tier)
-        base = self.out_path if self.out_path is not None else wav_path.parent
-        tg_path = base / "TextGrid" / wav_path.with_suffix(".TextGrid").name
-        if made is None or tg_path.parent not in made:
-            tg_path.parent.mkdir(parents=True, exist_ok=True)
-            if made is not None:
-                made.add(tg_path.parent)
         tg.write(tg_path)
 
     def save_textgrids(self):

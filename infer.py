@@ -84,11 +84,10 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
         except (OSError, ValueError) as e:
             return None, e
     # Only the RIFF headers are read up front (lengths for the batch plan); each batch's files are decoded when the
-    # batch is submitted, by libhfa's native reader straight into the batch's pinned buffer, on a thread pool
-    # (ctypes drops the GIL), so host memory holds the batches in flight, not the folder.
-    from concurrent.futures import ThreadPoolExecutor
-    pool = ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1))
-    for key, (wav_path, ph_seq, word_seq, p2w), (info, e) in zip(keys, rows, pool.map(_info, [r[0] for r in rows])):
+    # batch is submitted, by libhfa's native reader straight into the batch's pinned buffer, so host memory holds
+    # the batches in flight, not the folder.  In the calling thread: ~70 us per 10 s file, less than a thread
+    # pool's hand-offs cost here (measured: scripts/cli_bench.py --profile).
+    for key, (wav_path, ph_seq, word_seq, p2w), (info, e) in zip(keys, rows, map(_info, [r[0] for r in rows])):
         if e is not None:
             errors.append([wav_path, e])
             continue
@@ -96,18 +95,19 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
         items[key] = (wav_path, n, file_sr, ph_seq, word_seq, p2w)
     out = {}
 
-    def _decode(job):
-        path, row, n = job
+    def _decode(path, row, n):
         got, _ = read_wav_into(path, row, channel=0)     # channel 0, as the reference's waveform[0]
         if got != n:
             raise ValueError(f"{path}: {got} samples read, the header said {n}")
+        row[n:] = 0.0                                    # the zero padding past this row's length
 
     def submit(chunk, file_sr):
         """-> (fetch handle, per-file sample counts at the melspec rate)."""
         lens = [c[1] for c in chunk]
-        wav_h = torch.zeros((len(chunk), max(lens)), dtype=torch.float32, pin_memory=True)
+        wav_h = torch.empty((len(chunk), max(lens)), dtype=torch.float32, pin_memory=True)
         wav_np = wav_h.numpy()           # rows decoded straight into pinned memory
-        list(pool.map(_decode, [(c[0], wav_np[r], lens[r]) for r, c in enumerate(chunk)]))
+        for r, c in enumerate(chunk):
+            _decode(c[0], wav_np[r], lens[r])
         wav = task.upload(wav_h)         # pinned non-blocking H2D: no host sync
         handle = task.submit(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
                              wav_sr=file_sr, lengths=lens if len(chunk) > 1 else None)
@@ -149,30 +149,27 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
     # alone (the reference's B=1); files too short for the encoder's 400-sample window are aligned alone.
     # One batch in flight: the host assembles batch i while the GPU runs batch i+1 (task.submit: encoder on the
     # main stream, head + Viterbi on a side stream).
-    try:
-        plan = plan_batches([(k, it[1], it[2]) for k, it in items.items()], batch_size, sr,
-                            task.unitsEncoder.encoder_sample_rate)
-        pending = None
-        for file_sr, ks in plan:
-            job, err = None, None
-            try:
-                job = run(ks, file_sr)
-            except recoverable as e:
-                err = e
-            if pending is not None:
-                settle(pending)
-                pending = None
-            if job is not None:
-                pending = job
-            elif len(ks) == 1:
-                errors.append([items[ks[0]][0], err])
-            else:
-                for k in ks:
-                    alone(k, file_sr)
+    plan = plan_batches([(k, it[1], it[2]) for k, it in items.items()], batch_size, sr,
+                        task.unitsEncoder.encoder_sample_rate)
+    pending = None
+    for file_sr, ks in plan:
+        job, err = None, None
+        try:
+            job = run(ks, file_sr)
+        except recoverable as e:
+            err = e
         if pending is not None:
             settle(pending)
-    finally:
-        pool.shutdown()
+            pending = None
+        if job is not None:
+            pending = job
+        elif len(ks) == 1:
+            errors.append([items[ks[0]][0], err])
+        else:
+            for k in ks:
+                alone(k, file_sr)
+    if pending is not None:
+        settle(pending)
     return out
 
 

@@ -148,6 +148,44 @@ def test_streaming_export_matches_batch_export(tmp_path):
     assert streamed == batch and len(batch) == len(b_preds)
 
 
+def test_textgrid_text_matches_tier_objects():
+    """Exporter's direct formatter (textgrid_text) writes exactly what the IntervalTier/TextGrid objects write,
+    for post-processed predictions (gaps, touching intervals, an int end from add_SP, quotes in marks), and
+    declines (None) whatever the objects must sort or reject."""
+    from hubertfa_amd.export_tool import IntervalTier, TextGrid, textgrid_text
+    from hubertfa_amd.post_processing import post_processing
+
+    def objects(ws, wiv, ps, piv):
+        tg, wt, pt = TextGrid(), IntervalTier(name="words"), IntervalTier(name="phones")
+        for w, (a, b) in zip(ws, wiv):
+            wt.add(a, b, w)
+        for ph, (a, b) in zip(ps, piv):
+            pt.add(minTime=float(a), maxTime=b, mark=ph)
+        tg.append(wt)
+        tg.append(pt)
+        return "\n".join(tg.lines()) + "\n"
+    rng = np.random.default_rng(5)
+    preds = []
+    for i in range(40):
+        n = int(rng.integers(1, 12))
+        cuts = np.sort(rng.uniform(0.05, 9.5, 2 * n))
+        ph_iv = cuts.reshape(n, 2).copy()
+        if i % 3 == 0:
+            ph_iv[1:, 0] = ph_iv[:-1, 1]                     # touching intervals
+        marks = np.array([f'p{j}' if j % 5 else 'q"x' for j in range(n)])
+        w_iv = ph_iv[::2].copy()
+        w_iv[:, 1] = ph_iv[1::2, 1] if n > 1 and len(ph_iv[1::2]) == len(w_iv) else w_iv[:, 1]
+        preds.append((f"u{i}.wav", 10 if i % 4 == 0 else 10.0, 0.5, marks, ph_iv, marks[::2], w_iv))
+    res, log = post_processing(preds)
+    assert len(res) > 30
+    for _, _, _, ps, piv, ws, wiv in res:
+        assert textgrid_text(ws, wiv, ps, piv) == objects(ws, wiv, ps, piv)
+    iv = np.array([[0.5, 1.0], [0.2, 0.4]])                     # out of order: the objects sort it
+    assert textgrid_text(["a", "b"], iv, ["a", "b"], iv) is None
+    assert textgrid_text(["a"], np.array([[1.0, 1.0]]), ["a"], np.array([[0.0, 1.0]])) is None   # empty interval
+    assert textgrid_text(["a"], np.array([[0.0, 1.0]], np.float32), ["a"], np.array([[0.0, 1.0]])) is None
+
+
 def test_wav_roundtrip(tmp_path):
     from hubertfa_amd import synth
     from hubertfa_amd.wav_io import read_wav, write_wav
