@@ -101,7 +101,7 @@ def _mixed_folder(tmp_path):
     return seg, dpath, ck, len(files)
 
 
-def _torchrun(args, env_extra=None, nproc=2, timeout=420):
+def _torchrun(args, env_extra=None, nproc=2, timeout=420, script="infer.py"):
     import socket
     import subprocess
     import sys
@@ -112,7 +112,7 @@ def _torchrun(args, env_extra=None, nproc=2, timeout=420):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, **(env_extra or {}))
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(repo, "infer.py"), *args]
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(repo, script), *args]
     return subprocess.run(cmd, env=env, cwd=repo, capture_output=True, text=True, timeout=timeout)
 
 
@@ -141,6 +141,26 @@ def test_infer_two_ranks_match_one_rank(tmp_path):
         assert [c.read_bytes() for c in conf] == conf1, f"{tag}: confidence.csv differs from the one-rank run"
         if extra:
             assert "re-running" in p.stdout and "shard failed" in p.stdout
+
+
+def test_bench_contract_two_ranks():
+    """The driver's N > 1 bench launch (torchrun, one process per rank, barrier + synchronize around the timed
+    steps, max over ranks), rehearsed with 2 ranks on GPU 0 over gloo: rank 0 alone prints one JSON line whose
+    value is the whole-job rate (global batch = world x per-rank batch) and whose metric is BASELINE.json's."""
+    import json
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = _torchrun(["--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "4", "--seconds", "2",
+                   "--no-cpu-baseline", "--dist-backend", "gloo", "--device", "0"], script="bench.py", timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    base = json.load(open(os.path.join(repo, "BASELINE.json")))
+    assert d["metric"] == base["metric"]
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["config"]["global_batch"] == 8 and d["higher_is_better"] is True
+    assert d["value"] > 0 and abs(d["value"] - 2 * 4 * 2.0 * 2 / (2 * d["ms_per_step"] * 1e-3)) < 1e-6 * d["value"]
+    assert d["roofline"]["bound"] == "mfma" and 0 < d["roofline"]["frac"] < 1
 
 
 def test_predict_isolates_failing_file(tmp_path):
