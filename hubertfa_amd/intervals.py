@@ -1,0 +1,51 @@
+"""Host-side interval/word assembly of the alignment decoder (reference: tools/alignment_decoder.py:97-138).
+
+numpy only (no torch), so the CLI's export worker processes (host_workers.py) can import it; alignment_decoder
+re-exports these names.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def assemble_intervals(ph_idx_seq, ph_time_int, edge_diff, T, frame_length, ph_seq, word_seq, ph_idx_to_word_idx):
+    """Fractional boundaries and word grouping (alignment_decoder.py:103-138), numpy f64 as the reference."""
+    ph_time_int = np.asarray(ph_time_int)
+    edge_diff = np.asarray(edge_diff, dtype=np.float64)
+    ph_time_fractional = (edge_diff[ph_time_int] / 2).clip(-0.5, 0.5)
+    ph_time_pred = frame_length * np.concatenate([ph_time_int.astype("float32") + ph_time_fractional, [T]])
+    ph_intervals = np.stack([ph_time_pred[:-1], ph_time_pred[1:]], axis=1)
+    ph_seq_pred, ph_intervals_pred, word_seq_pred, word_intervals_pred = [], [], [], []
+    word_idx_last = -1
+    for i, ph_idx in enumerate(ph_idx_seq):
+        if ph_seq[ph_idx] == "SP":
+            continue
+        ph_seq_pred.append(ph_seq[ph_idx])
+        ph_intervals_pred.append(ph_intervals[i, :])
+        word_idx = ph_idx_to_word_idx[ph_idx]
+        if word_idx == word_idx_last:
+            word_intervals_pred[-1][1] = ph_intervals[i, 1]
+        else:
+            word_seq_pred.append(word_seq[word_idx])
+            word_intervals_pred.append([ph_intervals[i, 0], ph_intervals[i, 1]])
+            word_idx_last = word_idx
+    return (np.array(ph_seq_pred), np.array(ph_intervals_pred).clip(min=0, max=None), np.array(word_seq_pred),
+            np.array(word_intervals_pred).clip(min=0, max=None))
+
+
+def total_confidence(frame_confidence: np.ndarray):
+    return np.exp(np.mean(np.log(frame_confidence + 1e-6)) / 3)  # (:97)
+
+
+def utterance_result(rec: dict, ph_seq, word_seq, ph_idx_to_word_idx, frame_length: float) -> dict:
+    """One utterance's decode outputs from its raw boundary record — T, ph_idx_seq [n], ph_time_int [n],
+    frame_confidence [T] and edge_diff [T] (f32 as computed on the GPU; the last frame's entry is replaced by
+    0 as :83) — so every consumer of the raw arrays (the batched decoder, the multi-GPU gather on rank 0) builds
+    bit-identical intervals."""
+    T = rec["T"]
+    ed = np.asarray(rec["edge_diff"])
+    edge_diff = np.concatenate([ed[:T - 1].astype(np.float64), [0.0]]) if T > 0 else np.zeros(0)
+    ph_p, ph_iv, w_p, w_iv = assemble_intervals(rec["ph_idx_seq"], rec["ph_time_int"], edge_diff, T, frame_length,
+                                                ph_seq, word_seq, ph_idx_to_word_idx)
+    return dict(rec, ph_seq=ph_p, ph_intervals=ph_iv, word_seq=w_p, word_intervals=w_iv,
+                confidence=total_confidence(rec["frame_confidence"]))
