@@ -1,7 +1,8 @@
 """Host-side interval/word assembly of the alignment decoder (reference: tools/alignment_decoder.py:97-138).
 
-numpy only (no torch), so the CLI's export worker processes (host_workers.py) can import it; alignment_decoder
-re-exports these names.
+numpy only (no torch): the host half of decoding, used by AlignmentDecoder.assemble, by the CLI's streamed export
+(infer.py, from the raw boundary records) and by rank 0 after the multi-GPU gather; alignment_decoder re-exports
+these names.
 """
 from __future__ import annotations
 

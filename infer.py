@@ -30,52 +30,33 @@ def _recoverable():
 class _StreamingExport:
     """One-GPU runs: post-process and write each batch's TextGrids as soon as the batch is back, on the host while
     the GPU runs the next batch, instead of after the whole folder.  The files written are the same; the
-    confidence table and the error log are assembled at the end in dataset order, as the batch path does.
-    With ``pool`` (hubertfa_amd.host_workers.start_pool) the post-processing and TextGrid writing run in worker
-    processes, so the main thread only assembles intervals and keeps the GPU fed."""
+    confidence table and the error log are assembled at the end in dataset order, as the batch path does."""
 
-    def __init__(self, rows, sr, frame_length, out_path, pool=None):
+    def __init__(self, rows, sr, frame_length, out_path):
         from hubertfa_amd.export_tool import Exporter
-        self.rows, self.sr, self.frame_length, self.out_path = rows, sr, frame_length, out_path
+        self.rows, self.sr, self.frame_length = rows, sr, frame_length
         self.writer = Exporter([], [], out_path)
         self.done, self.log, self.made = {}, {}, set()
-        self.pool, self.futures = pool, []
         print("Post-processing...")
         print("Saving TextGrids...")
 
     def __call__(self, records: dict, keys):
-        from hubertfa_amd.alignment_decoder import utterance_result
+        from hubertfa_amd.intervals import utterance_result
         from hubertfa_amd.post_processing import post_process_one
-        if self.pool is not None:
-            from hubertfa_amd.host_workers import assemble_post_write
-            items = [(i, records[i], self.rows[i]) for i in keys]
-            n = max(1, -(-len(items) // self.pool._max_workers))
-            for j in range(0, len(items), n):
-                self.futures.append(self.pool.submit(assemble_post_write, self.out_path, self.sr, self.frame_length,
-                                                     items[j:j + n]))
-            return
         for i in keys:
             wav_path, ph_seq, word_seq, p2w = self.rows[i]
             rec = records[i]
             r = utterance_result(rec, ph_seq, word_seq, p2w, self.frame_length)
-            pred = (wav_path, rec["n44"] / self.sr, r["confidence"], r["ph_seq"], r["ph_intervals"], r["word_seq"],
-                    r["word_intervals"])
-            p, err = post_process_one(pred)
+            pred, err = post_process_one((wav_path, rec["n44"] / self.sr, r["confidence"], r["ph_seq"],
+                                          r["ph_intervals"], r["word_seq"], r["word_intervals"]))
             if err is not None:
                 self.log[i] = err
                 continue
-            self.writer.write_textgrid(p, self.made)
-            self.done[i] = p
+            self.writer.write_textgrid(pred, self.made)
+            self.done[i] = pred
 
     def results(self):
         """-> (predictions, post-processing log), both in dataset order."""
-        for f in self.futures:
-            for i, p, err in f.result():
-                if err is not None:
-                    self.log[i] = err
-                else:
-                    self.done[i] = p
-        self.futures = []
         return [self.done[i] for i in sorted(self.done)], [self.log[i] for i in sorted(self.log)]
 
 
@@ -216,10 +197,7 @@ def _run(task, rows, keys, batch_size, errors, on_batch=None):
 @click.option("--out_path", default=None, type=str, help="write TextGrids under this folder instead")
 @click.option("--dist_backend", default="nccl", type=str, help="multi-GPU data backend: nccl (= RCCL); gloo for rehearsals")
 @click.option("--device", default=None, type=int, help="force every rank onto this GPU (multi-rank rehearsal on one GPU)")
-@click.option("--export_workers", default=3, type=int,
-              help="one GPU: host processes for interval assembly, post-processing and TextGrid writing (0: inline)")
-def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, dist_backend, device, export_workers,
-         **kwargs):
+def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, dist_backend, device, **kwargs):
     import torch
     import hubertfa_amd.g2p as g2p_mod
     from hubertfa_amd.alignment_decoder import utterance_result
@@ -240,12 +218,6 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
 
     rank, world, local = env_rank_world()
     local = local if device is None else device
-    # one GPU, more than one batch: post-processing + TextGrid writing in worker processes, started before this
-    # process touches the GPU
-    pool = None
-    if world == 1 and export_workers > 0 and len(rows) > batch_size:
-        from hubertfa_amd.host_workers import start_pool
-        pool = start_pool(export_workers)
     torch.cuda.set_device(local)
     dist, ctrl, mine, costs, shards = None, None, list(range(len(rows))), None, None
     if world > 1:
@@ -273,7 +245,7 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
     t_load = time.perf_counter()
     sr = model.melspec_config["sample_rate"]
     # one GPU: each batch is post-processed and its TextGrids written while the GPU runs the next batch
-    stream = _StreamingExport(rows, sr, model.decoder.frame_length, out_path, pool) if world == 1 else None
+    stream = _StreamingExport(rows, sr, model.decoder.frame_length, out_path) if world == 1 else None
     records, ok = _run(model, [rows[i] for i in mine], mine, batch_size, errors, stream)
     t_align = time.perf_counter()
     if world == 1 and not ok:
@@ -306,8 +278,6 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
 
     if stream is not None:
         predictions, log = stream.results()
-        if pool is not None:
-            pool.shutdown()
     else:
         predictions = []
         for i, (wav_path, ph_seq, word_seq, p2w) in enumerate(rows):

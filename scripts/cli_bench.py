@@ -15,7 +15,6 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--profile", action="store_true", help="cProfile the second run (host time by function)")
-    ap.add_argument("--export_workers", default="3", help="comma list: infer.py --export_workers values, interleaved")
     ap.add_argument("--reps", type=int, default=2)
     args = ap.parse_args()
     import numpy as np
@@ -41,9 +40,8 @@ def main():
         ck = os.path.join(td, "m.ckpt")
         synth_checkpoint(ck)
         argv0 = ["-c", ck, "-f", seg, "-d", dpath, "-sc", "--hubert_path", "synth:0", "--batch_size", str(args.batch)]
-        runs = [(rep, w) for rep in range(args.reps) for w in args.export_workers.split(",")]
-        for rep, w in runs:                       # the first run also pays kernel loading and warm-up
-            argv = argv0 + ["--export_workers", w]
+        for rep in range(args.reps):              # the first run also pays kernel loading and warm-up
+            argv = argv0
             prof = None
             if args.profile and rep == 1:
                 import cProfile
@@ -61,7 +59,7 @@ def main():
                 print(r.output[-2000:], repr(r.exception))
                 raise SystemExit(1)
             timing = [ln for ln in r.output.splitlines() if ln.startswith("[timing]")]
-            print(f"run {rep} export_workers {w}: {args.n} files, {secs.sum():.0f} s of audio in {el:.2f} s wall -> "
+            print(f"run {rep}: {args.n} files, {secs.sum():.0f} s of audio in {el:.2f} s wall -> "
                   f"{secs.sum() / el:.0f} x realtime; " + "; ".join(timing), flush=True)
 
 
