@@ -185,6 +185,25 @@ def _run(task, rows, keys, batch_size, errors, on_batch=None):
         return {}, False
 
 
+def _write_metrics(path, records, sr, world, n_files, n_errors, phases):
+    """One JSON line per run (SURVEY §5 'Metrics / logging'): aligned audio seconds per wall second of the
+    alignment phase (WAV reads + GPU + boundaries; the streamed export too on one GPU) and of the whole run, DP and
+    Hubert frames per second, phase times."""
+    import json
+    import time
+    audio_s = sum(r["n44"] for r in records.values()) / sr
+    dp_frames = sum(int(r["T"]) for r in records.values())
+    total = sum(phases.values())
+    line = dict(time=time.time(), files=n_files, aligned=len(records), errors=n_errors, world=world,
+                audio_s=audio_s, dp_frames=dp_frames, hubert_frames=int(round(audio_s * 50)),
+                rtf_inv_align=audio_s / phases["align"] if phases["align"] > 0 else None,
+                rtf_inv_total=audio_s / total if total > 0 else None,
+                dp_frames_per_s=dp_frames / phases["align"] if phases["align"] > 0 else None,
+                phases_s=phases)
+    with open(path, "a", encoding="utf-8") as f:
+        f.write(json.dumps(line) + "\n")
+
+
 @click.command()
 @click.option("--ckpt", "-c", default=None, required=True, type=str, help="path to the checkpoint")
 @click.option("--folder", "-f", default="segments", type=str, help="path to the input folder")
@@ -197,7 +216,9 @@ def _run(task, rows, keys, batch_size, errors, on_batch=None):
 @click.option("--out_path", default=None, type=str, help="write TextGrids under this folder instead")
 @click.option("--dist_backend", default="nccl", type=str, help="multi-GPU data backend: nccl (= RCCL); gloo for rehearsals")
 @click.option("--device", default=None, type=int, help="force every rank onto this GPU (multi-rank rehearsal on one GPU)")
-def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, dist_backend, device, **kwargs):
+@click.option("--metrics", default=None, type=str, help="append one JSON line of run metrics to this file (SURVEY §5)")
+def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, dist_backend, device, metrics,
+         **kwargs):
     import torch
     import hubertfa_amd.g2p as g2p_mod
     from hubertfa_amd.alignment_decoder import utterance_result
@@ -295,6 +316,9 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
     what = "align + post-processing + TextGrids (streamed)" if stream is not None else "align"
     print(f"[timing] g2p {t_g2p - t_start:.2f} s, model load {t_load - t_g2p:.2f} s, wav read + {what} "
           f"{t_align - t_load:.2f} s ({len(records)} files), gather + post-processing + export {t_end - t_align:.2f} s")
+    if metrics:
+        _write_metrics(metrics, records, sr, world, len(rows), len(errors) + len(log),
+                       dict(g2p=t_g2p - t_start, load=t_load - t_g2p, align=t_align - t_load, export=t_end - t_align))
     if world > 1:
         dist.destroy_process_group()
 

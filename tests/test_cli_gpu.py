@@ -25,9 +25,14 @@ def test_infer_cli_end_to_end(tmp_path):
         (seg / f"u{i}.lab").write_text(synth.synth_lab(5, d, seed=i))
     ck = tmp_path / "m.ckpt"
     synth_checkpoint(str(ck))
+    mpath = tmp_path / "metrics.jsonl"
     r = CliRunner().invoke(infer.main, ["-c", str(ck), "-f", str(seg), "-d", str(dpath), "-sc",
-                                        "--hubert_path", "synth:0"])
+                                        "--hubert_path", "synth:0", "--metrics", str(mpath)])
     assert r.exit_code == 0, r.output + repr(r.exception)
+    import json
+    m = json.loads(mpath.read_text().strip().splitlines()[-1])
+    assert m["files"] == m["aligned"] == len(SECS) and m["errors"] == 0 and m["world"] == 1
+    assert abs(m["audio_s"] - sum(SECS)) < 1e-3 and m["rtf_inv_align"] > 0 and m["dp_frames"] > 0
     for i, secs in enumerate(SECS):
         tg = read_textgrid(seg / "TextGrid" / f"u{i}.TextGrid")
         words = [t for t in tg["words"] if t[2] != "SP"]
