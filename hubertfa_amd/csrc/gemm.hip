@@ -1,11 +1,11 @@
 // gemm.hip — f32 MFMA implicit-GEMM (v_mfma_f32_32x32x2_f32) with fused epilogues, for every dense
 // contraction on the path:
 //   * nn.Linear / addmm: feature projection, QKV, out-proj, FFN (networks/hubert/model.py:27-33,122;
-//     transformers HubertAttention/HubertFeedForward), UNet shortcut + head (resnet_block.py:164-168,
+//     transformers HubertAttention/HubertFeedForward), UNet shortcut + head (resnet_block.py:36-40,
 //     forced_alignment.py:53-55)
 //   * conv1d as implicit GEMM over a [T, C] (channels-last) activation: extractor conv1..6 (model.py:100-114),
 //     grouped positional conv k128/pad64/g16 (model.py:135-147), UNet k3 convs / k2 stride-2 down-sampling /
-//     k2 stride-2 transposed up-sampling (resnet_block.py:145-162, stride_conv.py:23-47)
+//     k2 stride-2 transposed up-sampling (resnet_block.py:18-24,27-33, stride_conv.py:23-47)
 //   * the polyphase sinc resampler (torchaudio Resample: tools/load_wav.py:7, tools/encoder.py:46-48) as a
 //     GEMM over overlapping frames of the padded wave.
 //

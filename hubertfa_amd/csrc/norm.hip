@@ -5,7 +5,7 @@
 //     (model.py:25,52; HF HubertEncoder.layer_norm), per-layer norm1/norm2 (post-LN) or pre-LN + final LN
 //     (HF HubertEncoderLayerStableLayerNorm), LN-conv feature extractor of the large variant
 //     (HF HubertLayerNormConvLayer: conv -> LN over channels -> GELU).
-//   * UNet ResidualBasicBlock: GroupNorm(16) + Hardswish and LN + Hardswish (resnet_block.py:145-173).
+//   * UNet ResidualBasicBlock: GroupNorm(16) + Hardswish and LN + Hardswish (resnet_block.py:25-26, :42-45).
 // HBM-bound: one wavefront per row, the row held in registers (C <= 4096), float4 loads, two-pass
 // mean/variance in f32 like ATen's reference path, then y = (x - mean) * rstd * gamma + beta.
 #include "hfa_common.h"

@@ -177,7 +177,7 @@ def synth_hubert_state_dict(arch: HubertArch, seed: int = 0) -> dict[str, np.nda
 
 
 def synth_unet_state_dict(arch: UNetArch, seed: int = 1) -> dict[str, np.ndarray]:
-    """Seeded ``backbone.*`` + ``head.*`` weights (unet.py:43-98, resnet_block.py:145-173, stride_conv.py)."""
+    """Seeded ``backbone.*`` + ``head.*`` weights (unet.py:43-98, resnet_block.py:17-50, stride_conv.py)."""
     g = _Gen(seed)
 
     def block(prefix, c_in, c_out):

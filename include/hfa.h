@@ -93,7 +93,7 @@ int hfa_lattice_prologue(int B, int Tmax, int V, int Smax, const int32_t* T, con
  * Replaces ATen addmm (nn.Linear) and conv1d on the path:
  *   networks/hubert/model.py:100-114 (conv1-6), :122 (projection), :135-147 (grouped positional conv),
  *   :27-33 (nn.TransformerEncoderLayer in/out proj, linear1/2), transformers HubertAttention/HubertFeedForward,
- *   networks/layer/block/resnet_block.py:145-168 (k3 convs, shortcut), networks/layer/scaling/stride_conv.py:23-47
+ *   networks/layer/block/resnet_block.py:17-40 (k3 convs :18-24,27-33, shortcut :36-40), networks/layer/scaling/stride_conv.py:23-47
  *   (k2 s2 conv, ConvTranspose), networks/task/forced_alignment.py:53-55 (head). */
 int hfa_conv_gemm_f32(int M, int N, int K, int Zb, int G, const float* A, long long sAb, long long sAg, int ldx,
                       int stride, int pad, int Cg, int Tin, const float* W, long long sWg, int ldw,
@@ -175,7 +175,7 @@ int hfa_attention_split_tuning(int waves);
  * y = act(LayerNorm(x (+ res)) * gamma + beta) over rows of C <= 4096 (C % 4 == 0).
  * Replaces LayerNorm in networks/hubert/model.py:25,121 and nn.TransformerEncoderLayer norm1/2,
  * transformers HubertFeatureProjection/HubertEncoder(*StableLayerNorm)/HubertLayerNormConvLayer,
- * networks/layer/block/resnet_block.py:170-173 (LN + Hardswish). */
+ * networks/layer/block/resnet_block.py:42-45 (LN + Hardswish). */
 int hfa_layernorm_f32(int rows, int C, const float* x, long long ldx, const float* res, long long ldr,
                       const float* gamma, const float* beta, float eps, int act, float* y, long long ldy, int T,
                       const int32_t* t_len, hipStream_t stream);
@@ -187,7 +187,7 @@ int hfa_layernorm_split(int rows, int C, const float* x, long long ldx, const fl
                         const float* gamma, const float* beta, float eps, int act, float* y, long long ldy, int T,
                         const int32_t* t_len, uint16_t* ys, long long ldys, long long sps, int* oflow,
                         hipStream_t stream);
-/* GroupNorm(G, C) over a channels-last [B, T, C] tensor (+act).  Replaces resnet_block.py:153-154
+/* GroupNorm(G, C) over a channels-last [B, T, C] tensor (+act).  Replaces resnet_block.py:25-26
  * (nn.GroupNorm(16, C) + nn.Hardswish). */
 int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs, int ldx, const float* gamma,
                       const float* beta, float eps, int act, float* y, long long y_bs, int ldy, const int32_t* t_len,
@@ -195,7 +195,7 @@ int hfa_groupnorm_f32(int B, int T, int C, int G, const float* x, long long x_bs
 /* Workspace for hfa_groupnorm_f32's split-T path (long rows, few (batch, group) pairs); NULL workspace = one
  * workgroup per pair. */
 long long hfa_groupnorm_workspace_bytes(int B, int T, int C, int G);
-/* GroupNorm (+act) of channels-last [B, T, C] (resnet_block.py:145-162, GroupNorm(16) + Hardswish) writing f32 y
+/* GroupNorm (+act) of channels-last [B, T, C] (resnet_block.py:17-26, GroupNorm(16) + Hardswish) writing f32 y
  * and / or split-f16 planes ys (plane 1 at +sps halves; the next split GEMM's operand: the UNet block's second conv);
  * C % 4 == 0, (C/G) % 4 == 0, C <= 1024, G <= 64; workspace = hfa_groupnorm_workspace_bytes(B, T, C, G) bytes; rows
  * t >= t_len[b] are zeros and excluded from the statistics; *oflow raised for a plane value out of f16 range. */

@@ -1,0 +1,111 @@
+"""Every `file.py:N-M` citation of the reference in the ABI header (and the product sources) points at lines that
+exist: N <= M <= the cited file's line count under /root/reference (or in the installed transformers package for
+its modeling files).  Skipped where the reference is absent (the GPU box)."""
+from __future__ import annotations
+
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+
+# a file token (optionally) followed by :spec, or a bare :spec continuing the previous file token
+_CITE = re.compile(r"(?P<file>[A-Za-z_][\w/.\-]*\.py)?:(?P<spec>\d+(?:-\d+)?(?:,\s?\d+(?:-\d+)?)*)")
+_THIRD_PARTY = ("modeling_hubert.py", "configuration_hubert.py", "feature_extraction_wav2vec2.py")
+
+
+def _index_reference():
+    by_name = {}
+    for root, _dirs, files in os.walk(REF):
+        if "/.git" in root:
+            continue
+        for f in files:
+            if f.endswith(".py"):
+                p = os.path.join(root, f)
+                by_name.setdefault(f, []).append(p)
+    return by_name
+
+
+def _resolve(name: str, by_name):
+    if name.endswith(_THIRD_PARTY):
+        try:
+            import transformers
+        except ImportError:
+            return None
+        base = os.path.dirname(transformers.__file__)
+        sub = "wav2vec2" if "wav2vec2" in name else "hubert"
+        return os.path.join(base, "models", sub, os.path.basename(name))
+    if "/" in name:
+        p = os.path.join(REF, name)
+        if os.path.isfile(p):
+            return p
+        # a path relative to a package dir that the text shortened (e.g. "hubert/model.py")
+        cands = [q for q in by_name.get(os.path.basename(name), []) if q.endswith("/" + name)]
+    else:
+        cands = by_name.get(name, [])
+    return cands[0] if len(cands) == 1 else None
+
+
+def _citations(text: str):
+    """Yield (file, first, last) for every citation; bare ':N' binds to the last file named on the same or an
+    earlier line of the same comment block."""
+    cur = None
+    for m in _CITE.finditer(text):
+        f = m.group("file")
+        if f is None:
+            # bare continuation: only after a file token, and only when the colon follows whitespace/'(' or ', '
+            pre = text[max(0, m.start() - 1):m.start()]
+            if cur is None or pre not in (" ", "(", "\t"):
+                continue
+            f = cur
+        else:
+            cur = f
+        for part in re.split(r",\s?", m.group("spec")):
+            a, _, b = part.partition("-")
+            yield f, int(a), int(b or a), m.start()
+
+
+def _line_count(path: str) -> int:
+    with open(path, "rb") as fh:
+        return len(fh.read().splitlines())
+
+
+def _check_file(rel: str, by_name):
+    bad = []
+    text = open(os.path.join(REPO, rel), encoding="utf-8").read()
+    for f, a, b, pos in _citations(text):
+        if f.startswith(("hubertfa_amd/", "tests/", "oracle/", "scripts/", "bench.py", "infer.py")) or \
+                os.path.basename(f) in {"bench.py", "__graft_entry__.py", "gen_golden.py"}:
+            continue  # the build's own files
+        p = _resolve(f, by_name)
+        if p is None:
+            continue  # not a reference file (or an ambiguous bare name)
+        n = _line_count(p)
+        line = text.count("\n", 0, pos) + 1
+        if not (1 <= a <= b <= n):
+            bad.append(f"{rel}:{line}: {f}:{a}-{b} (file has {n} lines)")
+    return bad
+
+
+needs_ref = pytest.mark.skipif(not os.path.isdir(REF), reason="reference absent (GPU box)")
+
+
+@needs_ref
+def test_abi_header_citations_exist():
+    by_name = _index_reference()
+    assert not _check_file("include/hfa.h", by_name)
+
+
+@needs_ref
+def test_product_source_citations_exist():
+    by_name = _index_reference()
+    bad = []
+    for sub in ("hubertfa_amd", "hubertfa_amd/csrc", "hubertfa_amd/g2p", "oracle"):
+        for f in sorted(os.listdir(os.path.join(REPO, sub))):
+            if f.endswith((".py", ".hip", ".cpp", ".h", ".c")):
+                bad += _check_file(os.path.join(sub, f), by_name)
+    for f in ("infer.py", "bench.py", "include/hfa.h", "INTEGRATION.md", "DESIGN.md"):
+        bad += _check_file(f, by_name)
+    assert not bad, "\n".join(bad)
