@@ -36,8 +36,21 @@ _SIGS = {
 _RESTYPE = {"hfa_last_error": ctypes.c_char_p, "hfa_build_arch": ctypes.c_char_p}
 
 
+HFA_EINVAL = -1000
+
+
 class HFALibraryError(RuntimeError):
-    pass
+    """A libhfa failure; ``rc`` is the status (HFA_EINVAL for a bad argument, -(hipError_t) for a HIP error, None
+    when the library itself is missing)."""
+
+    def __init__(self, msg: str, rc: int | None = None):
+        super().__init__(msg)
+        self.rc = rc
+
+
+class HFAArgumentError(HFALibraryError, ValueError):
+    """rc == HFA_EINVAL: the call's arguments (one input's shape, a file's contents) were rejected before anything
+    ran on the device, so the device is still healthy and the caller may go on with other inputs."""
 
 
 _lib = None
@@ -87,7 +100,8 @@ def lib():
 def check(rc: int, what: str = "") -> None:
     if rc != 0:
         msg = lib().hfa_last_error()
-        raise HFALibraryError(f"{what or 'libhfa'} failed (rc={rc}): {msg.decode() if msg else ''}")
+        cls = HFAArgumentError if rc == HFA_EINVAL else HFALibraryError
+        raise cls(f"{what or 'libhfa'} failed (rc={rc}): {msg.decode() if msg else ''}", rc)
 
 
 def call(name: str, *args) -> None:

@@ -11,6 +11,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <exception>
 #include <vector>
 
 namespace {
@@ -85,8 +86,8 @@ int parse(File& fh, const char* path, WavFmt& w) {
         hfa::set_error("hfa_wav: %s: unsupported format tag %d / %d bits", path, w.tag, w.bits);
         return HFA_EINVAL;
     }
-    if (w.channels < 1) {
-        hfa::set_error("hfa_wav: %s: %d channels", path, w.channels);
+    if (w.channels < 1 || w.rate < 1) {
+        hfa::set_error("hfa_wav: %s: %d channels at %d Hz", path, w.channels, w.rate);
         return HFA_EINVAL;
     }
     return 0;
@@ -158,8 +159,8 @@ int hfa_wav_info(const char* path, int64_t* frames, int32_t* channels, int32_t* 
     return 0;
 }
 
-int hfa_wav_read(const char* path, int32_t channel, float* dst, int64_t capacity, int64_t* frames,
-                 int32_t* sample_rate) {
+static int wav_read(const char* path, int32_t channel, float* dst, int64_t capacity, int64_t* frames,
+                    int32_t* sample_rate) {
     if (!path || !dst || !frames || capacity < 0) {
         hfa::set_error("hfa_wav_read: null argument or negative capacity");
         return HFA_EINVAL;
@@ -178,9 +179,14 @@ int hfa_wav_read(const char* path, int32_t channel, float* dst, int64_t capacity
         hfa::set_error("hfa_wav_read: %s: %lld samples do not fit a buffer of %lld", path, need, (long long)capacity);
         return HFA_EINVAL;
     }
-    // decode in blocks of whole frames through a small staging buffer (no copy of the whole data chunk)
-    constexpr long long kBlock = 1 << 16;                   // frames per block
-    std::vector<unsigned char> buf((size_t)(kBlock * bps * ch));
+    // decode in blocks of whole frames through a small staging buffer (no copy of the whole data chunk), at most
+    // 64 Ki frames and 4 MiB whatever the header's channel count and sample width claim
+    constexpr long long kBudget = 4ll << 20;
+    const long long frame_bytes = (long long)bps * ch;
+    long long kBlock = kBudget / frame_bytes < (1 << 16) ? kBudget / frame_bytes : (1 << 16);
+    if (kBlock > n) kBlock = n;
+    if (kBlock < 1) kBlock = 1;
+    std::vector<unsigned char> buf((size_t)(kBlock * frame_bytes));
     if (fseeko(fh.f, w.data_off, SEEK_SET) != 0) {
         hfa::set_error("hfa_wav_read: %s: seek failed", path);
         return HFA_EINVAL;
@@ -202,6 +208,16 @@ int hfa_wav_read(const char* path, int32_t channel, float* dst, int64_t capacity
     *frames = n;
     if (sample_rate) *sample_rate = w.rate;
     return 0;
+}
+
+int hfa_wav_read(const char* path, int32_t channel, float* dst, int64_t capacity, int64_t* frames,
+                 int32_t* sample_rate) {
+    try {                                            // nothing may unwind through the C ABI (ctypes callers)
+        return wav_read(path, channel, dst, capacity, frames, sample_rate);
+    } catch (const std::exception& e) {
+        hfa::set_error("hfa_wav_read: %s: %s", path ? path : "(null)", e.what());
+        return HFA_EINVAL;
+    }
 }
 
 }  // extern "C"

@@ -31,7 +31,7 @@ def wav_info(path) -> tuple[int, int, int]:
     n, ch, sr = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32()
     try:
         _lib.call("hfa_wav_info", _path(path), ctypes.byref(n), ctypes.byref(ch), ctypes.byref(sr))
-    except _lib.HFALibraryError as e:
+    except _lib.HFAArgumentError as e:      # an unreadable file (a missing library or a HIP error propagates)
         raise _err(path, e) from None
     return n.value, sr.value, ch.value
 
@@ -45,7 +45,7 @@ def read_wav_into(path, dst: np.ndarray, channel: int = 0) -> tuple[int, int]:
     try:
         _lib.call("hfa_wav_read", _path(path), channel, dst.ctypes.data, dst.size, ctypes.byref(n),
                   ctypes.byref(sr))
-    except _lib.HFALibraryError as e:
+    except _lib.HFAArgumentError as e:      # an unreadable file (a missing library or a HIP error propagates)
         raise _err(path, e) from None
     return n.value, sr.value
 

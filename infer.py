@@ -23,8 +23,17 @@ import click
 
 
 def _recoverable():
-    from hubertfa_amd._lib import HFALibraryError
-    return (HFALibraryError, ValueError, AssertionError, KeyError, IndexError)
+    """Errors that concern one input and leave the GPU healthy: a rejected argument (HFA_EINVAL: a lattice beyond
+    the DP kernel's limits, an unreadable WAV), the reference's own per-utterance assertions and lookups.  A HIP
+    error (libhfa rc = -(hipError_t)), a missing library or anything else fails the rank, so its shard is re-queued
+    on a healthy rank instead of being logged file by file."""
+    from hubertfa_amd._lib import HFAArgumentError
+    return (HFAArgumentError, ValueError, AssertionError, KeyError, IndexError)
+
+
+def _export_errors():
+    """Errors of one file's post-processing / TextGrid write (e.g. IntervalTier's overlap check)."""
+    return (ValueError, AssertionError, KeyError, IndexError, OSError)
 
 
 class _StreamingExport:
@@ -46,13 +55,17 @@ class _StreamingExport:
         for i in keys:
             wav_path, ph_seq, word_seq, p2w = self.rows[i]
             rec = records[i]
-            r = utterance_result(rec, ph_seq, word_seq, p2w, self.frame_length)
-            pred, err = post_process_one((wav_path, rec["n44"] / self.sr, r["confidence"], r["ph_seq"],
-                                          r["ph_intervals"], r["word_seq"], r["word_intervals"]))
+            try:
+                r = utterance_result(rec, ph_seq, word_seq, p2w, self.frame_length)
+                pred, err = post_process_one((wav_path, rec["n44"] / self.sr, r["confidence"], r["ph_seq"],
+                                              r["ph_intervals"], r["word_seq"], r["word_intervals"]))
+                if err is None:
+                    self.writer.write_textgrid(pred, self.made)
+            except _export_errors() as e:            # this file's export failed: logged as an export error
+                pred, err = None, [wav_path, e]
             if err is not None:
                 self.log[i] = err
                 continue
-            self.writer.write_textgrid(pred, self.made)
             self.done[i] = pred
 
     def results(self):
@@ -114,6 +127,7 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
         return handle, [resampled_length(n, file_sr, sr) for n in lens]
 
     def finish(job):
+        """Complete a batch's alignment (the export of its files is not part of it: see emit)."""
         handle, ks, n44s = job[:3]
         chunk = [items[k] for k in ks]
         res = task.decoder.assemble(handle, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
@@ -121,6 +135,10 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
         for k, r, n44 in zip(ks, res, n44s):
             out[k] = dict(n44=n44, T=r["T"], ph_idx_seq=r["ph_idx_seq"], ph_time_int=r["ph_time_int"],
                           frame_confidence=r["frame_confidence"], edge_diff=r["edge_diff"])
+        return ks
+
+    def emit(ks):
+        # outside the alignment guards: an export error is logged by on_batch, never taken for a GPU failure
         if on_batch is not None:
             on_batch(out, ks)
 
@@ -130,20 +148,24 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
 
     def alone(k, file_sr):
         try:
-            finish(run([k], file_sr))
+            ks = finish(run([k], file_sr))
         except recoverable as e:
             errors.append([items[k][0], e])
+            return
+        emit(ks)
 
     def settle(job):
         """Complete a batch; a recoverable failure re-runs its files one by one."""
         try:
-            finish(job)
+            ks = finish(job)
         except recoverable as e:
             if len(job[1]) == 1:
                 errors.append([items[job[1][0]][0], e])
             else:
                 for k in job[1]:
                     alone(k, job[3])
+            return
+        emit(ks)
 
     # variable-length batches (hubertfa_amd.batching.plan_batches): per sample rate, sorted by length, rows
     # zero-padded and aligned with per-row lengths, which keeps every utterance's result identical to aligning it
@@ -175,11 +197,14 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
 
 
 def _run(task, rows, keys, batch_size, errors, on_batch=None):
-    """_predict with the rank-level outcome: (records, ok)."""
+    """_predict with the rank-level outcome: (records, ok).  A failed shard leaves ``errors`` as it found it: its
+    files are re-run elsewhere, so the entries it logged would be duplicates (or wrong, for files aligned there)."""
+    n_err = len(errors)
     try:
         return _predict(task, rows, keys, batch_size, errors, on_batch), True
     except Exception as e:  # noqa: BLE001 — reported to the control plane; the shard is re-queued elsewhere
         import traceback
+        del errors[n_err:]
         traceback.print_exc()
         print(f"[rank {os.environ.get('RANK', '0')}] shard failed: {e!r}", flush=True)
         return {}, False

@@ -174,7 +174,7 @@ def test_predict_isolates_failing_file(tmp_path):
     import infer
     import hubertfa_amd.g2p as g2p_mod
     import torch
-    from hubertfa_amd._lib import HFALibraryError
+    from hubertfa_amd._lib import HFA_EINVAL, HFAArgumentError
     from hubertfa_amd.task import ForcedAlignmentTask
     seg, dpath, ck, n = _mixed_folder(tmp_path)
     g = g2p_mod.DictionaryG2P(dictionary=str(dpath))
@@ -191,7 +191,7 @@ def test_predict_isolates_failing_file(tmp_path):
     def bad_submit(waves, *a, lengths=None, **kw):
         lens = lengths if lengths is not None else [waves.shape[-1]] * waves.shape[0]
         if poison in lens:
-            raise HFALibraryError("injected: lattice beyond the kernel's limits")
+            raise HFAArgumentError("injected: lattice beyond the kernel's limits", HFA_EINVAL)
         return submit(waves, *a, lengths=lengths, **kw)
     task.submit = bad_submit
     errors = []
@@ -231,3 +231,55 @@ def test_infer_cli_skips_unreadable_and_multichannel(tmp_path):
     got = {p.name for p in out.rglob("*.TextGrid")}
     assert "zz_bad.TextGrid" not in got and len(got) == n + 1
     assert (out / "TextGrid" / "zz_st.TextGrid").read_text() == (out / "TextGrid" / "m3.TextGrid").read_text()
+
+
+def test_hip_error_fails_the_shard(tmp_path):
+    """A HIP-level libhfa error (rc = -(hipError_t)) in the middle of a shard is not a per-file error: the rank
+    reports its shard as failed (so it is re-queued on a healthy rank) instead of re-running and logging every
+    file, and the errors the shard had logged before are dropped (its files are re-run elsewhere); an export error
+    of one file in the streaming export is logged for that file and the rest are written."""
+    import infer
+    import hubertfa_amd.g2p as g2p_mod
+    import torch
+    from hubertfa_amd._lib import HFALibraryError
+    from hubertfa_amd.task import ForcedAlignmentTask
+    seg, dpath, ck, n = _mixed_folder(tmp_path)
+    (seg / "zz_bad.wav").write_bytes(b"not a wav file at all")      # logged by the shard before the failure
+    (seg / "zz_bad.lab").write_text((seg / "m0.lab").read_text())
+    g = g2p_mod.DictionaryG2P(dictionary=str(dpath))
+    g.set_in_format("lab")
+    rows = list(g.get_dataset(sorted(seg.rglob("*.wav"))))
+    torch.set_grad_enabled(False)
+    task = ForcedAlignmentTask.load_from_checkpoint(str(ck), device=torch.device("cuda"), hubert_model_path="synth:0")
+    keys = list(range(len(rows)))
+    submit, calls = task.submit, []
+
+    def hip_fail_submit(*a, **kw):
+        calls.append(1)
+        if len(calls) == 2:
+            raise HFALibraryError("injected: hfa_conv_gemm_split failed (rc=-719): unspecified launch failure", -719)
+        return submit(*a, **kw)
+    task.submit = hip_fail_submit
+    errors = [["earlier.wav", ValueError("logged before this shard")]]
+    got, ok = infer._run(task, rows, keys, 2, errors)
+    task.submit = submit
+    assert not ok and got == {} and len(calls) == 2, (ok, len(calls))
+    assert [e[0] for e in errors] == ["earlier.wav"]
+    # streaming export: one file's TextGrid write fails -> that file is in the log, every other file is written
+    stream = infer._StreamingExport(rows, task.melspec_config["sample_rate"], task.decoder.frame_length,
+                                    str(tmp_path / "out"))
+    write = stream.writer.write_textgrid
+
+    def bad_write(pred, made=None):
+        if str(pred[0]).endswith("m2.wav"):
+            raise ValueError("overlapping intervals (injected)")
+        return write(pred, made)
+    stream.writer.write_textgrid = bad_write
+    errors = []
+    got, ok = infer._run(task, rows, keys, 2, errors, stream)
+    preds, log = stream.results()
+    assert ok and len(got) == n
+    assert [str(e[0]).endswith("zz_bad.wav") for e in errors] == [True]
+    assert len(log) == 1 and str(log[0][0]).endswith("m2.wav")
+    assert sorted(p.name for p in (tmp_path / "out").rglob("*.TextGrid")) == \
+        sorted(f"m{i}.TextGrid" for i in range(n) if i != 2)

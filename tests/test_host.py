@@ -270,6 +270,34 @@ def test_native_wav_reader_edges(tmp_path):
         read_wav_into(p, np.zeros(2000, np.float32), channel=1)
 
 
+def test_native_wav_reader_hostile_headers(tmp_path):
+    """Headers that claim 65535 channels of 64-bit floats (0.5 MB per frame): the staging buffer stays within its
+    fixed budget whatever the header says, so an empty or short data chunk reads as such instead of asking for
+    ~34 GB; a zero sample rate is rejected.  Every failure is a ValueError for that file, never an abort."""
+    import struct
+    from hubertfa_amd.wav_io import read_wav, read_wav_into, wav_info
+    def hostile(payload):                                       # block align does not fit its 16 bits either
+        fmt = struct.pack("<HHIIHH", 3, 65535, 22050, 0xFFFFFFFF, 0xFFFF, 64)
+        body = b"fmt " + struct.pack("<I", len(fmt)) + fmt + b"data" + struct.pack("<I", len(payload)) + payload
+        return b"RIFF" + struct.pack("<I", 4 + len(body)) + b"WAVE" + body
+    p = tmp_path / "h.wav"
+    p.write_bytes(hostile(b""))
+    assert wav_info(p) == (0, 22050, 65535)
+    assert read_wav_into(p, np.zeros(4, np.float32), channel=3) == (0, 22050)
+    frames = np.arange(3 * 65535, dtype="<f8") / 1e6            # three whole frames
+    p.write_bytes(hostile(frames.tobytes()))
+    row = np.zeros(3, np.float32)
+    assert read_wav_into(p, row, channel=65534) == (3, 22050)
+    np.testing.assert_array_equal(row, frames.reshape(3, 65535)[:, 65534].astype(np.float32))
+    with pytest.raises(ValueError, match="do not fit"):
+        read_wav_into(p, np.zeros(10, np.float32), channel=-1)
+    raw = bytearray(_wav_bytes(1, 16, 1, b"\0\0" * 8))
+    raw[24:28] = struct.pack("<I", 0)                            # sample rate 0
+    p.write_bytes(bytes(raw))
+    with pytest.raises(ValueError, match="0 Hz"):
+        wav_info(p)
+
+
 def test_checkpoint_roundtrip(tmp_path):
     import torch
     from hubertfa_amd.task import synth_checkpoint
