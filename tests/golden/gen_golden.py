@@ -35,6 +35,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.dirname(HERE))          # tests/ (ckpt_files)
 
 from hubertfa_amd import synth  # noqa: E402
 
@@ -397,16 +398,232 @@ def gen_unet():
     np.savez_compressed(os.path.join(HERE, "unet_head.npz"), **out)
 
 
+def _reference_encoder_module():
+    """tools/encoder.py imports ``torchaudio.transforms.Resample`` at module level and torchaudio is absent here.
+    A stub is installed for that one import and removed again (transformers probes torchaudio's presence later);
+    the stub's Resample refuses to run.  The fixtures hand the reference's UnitsEncoder its 16 kHz wave through its
+    own ``resample_kernel`` cache (encoder.py:44-48), so no resampling is ever executed and the resampler stays
+    unpinned."""
+    import transformers  # noqa: F401  (imported before the stub exists)
+    if "tools.encoder" in sys.modules:
+        return sys.modules["tools.encoder"]
+    ta = types.ModuleType("torchaudio")
+    tr = types.ModuleType("torchaudio.transforms")
+
+    class Resample:
+        def __init__(self, *a, **k):
+            raise RuntimeError("torchaudio is absent: the fixtures never resample")
+    tr.Resample = Resample
+    ta.transforms = tr
+    sys.modules["torchaudio"], sys.modules["torchaudio.transforms"] = ta, tr
+    try:
+        import tools.encoder as enc
+    finally:
+        del sys.modules["torchaudio"], sys.modules["torchaudio.transforms"]
+    return enc
+
+
+def _reference_lattice(units_encoder, wav16, n44, ua, usd, vocab, ph_seq, word_seq, p2w):
+    """The reference's predict_step arithmetic after load_wav (forced_alignment.py:157-176), resampling excepted:
+    UnitsEncoder.encode at the 44.1 kHz grid with the 16 kHz wave injected as its resampler's output, then
+    UNetBackbone + head, the forward split (:284-292) and AlignmentDecoder.decode.  _decode's inputs are captured
+    (ph_prob_log: the north star's per-frame log-probs)."""
+    import torch
+    from networks.layer.backbone.unet import UNetBackbone
+    from networks.layer.block.resnet_block import ResidualBasicBlock
+    from networks.layer.scaling.stride_conv import DownSampling, UpSampling
+    from tools.alignment_decoder import AlignmentDecoder
+
+    wav_t = torch.from_numpy(wav16)[None]
+    units_encoder.resample_kernel["44100"] = lambda audio: wav_t       # the resampler's output, injected
+    with torch.inference_mode():
+        feat = units_encoder.encode(torch.zeros(1, n44), 44100, 512)    # [1, C, T] (encoder.py:36-60)
+    bb = UNetBackbone(ua.input_dims, ua.output_dims, ua.hidden_dims, ResidualBasicBlock, DownSampling, UpSampling,
+                      ua.factor, ua.times, ua.scaleup).eval()
+    head = torch.nn.Linear(ua.output_dims, ua.vocab_size + 2).eval()
+    bb.load_state_dict({k[len("backbone."):]: torch.from_numpy(v) for k, v in usd.items() if k.startswith("backbone.")})
+    head.load_state_dict({k[len("head."):]: torch.from_numpy(v) for k, v in usd.items() if k.startswith("head.")})
+    with torch.no_grad():
+        logits = head(bb(feat.transpose(1, 2)))
+    frame, edge = logits[:, :, 2:], logits[:, :, 0]
+    ctc = torch.cat([logits[:, :, [1]], logits[:, :, 3:]], dim=-1)
+    dec = AlignmentDecoder(vocab, {"hop_length": 512, "sample_rate": 44100})
+    seen = {}
+    inner = dec._decode
+
+    def capture(ph_seq_id, ph_prob_log, edge_prob):
+        seen.update(ph_prob_log=ph_prob_log.copy(), edge_prob=edge_prob.copy())
+        return inner(ph_seq_id, ph_prob_log, edge_prob)
+    dec._decode = capture
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        ph_pred, ph_int, w_pred, w_int, conf = dec.decode(frame, edge, ctc, n44 / 44100, ph_seq, word_seq, p2w)
+    return dict(units=feat, ph_prob_log=seen["ph_prob_log"].astype(np.float32),
+                edge_prob=seen["edge_prob"].astype(np.float32), ph_idx_seq=dec.ph_idx_seq.astype(np.int32),
+                ph_time_int=dec.ph_time_int_pred.astype(np.int32),
+                frame_confidence=dec.frame_confidence.astype(np.float32),
+                ph_intervals=np.asarray(ph_int, np.float64), word_intervals=np.asarray(w_int, np.float64),
+                ph_seq_pred=[str(x) for x in ph_pred], word_seq_pred=[str(x) for x in w_pred],
+                confidence=float(conf))
+
+
+def gen_e2e10s():
+    """BASELINE config-2 geometry from the reference itself (VERDICT r02 'next' 1): one 10 s utterance (160 000
+    samples at 16 kHz = the encoder's input; N44 = 441 000 -> 862 grid frames, T = 861) through the reference's
+    UnitsEncoder (HF HubertModel base 12L, HF Hubert-large 24L stable-LN, bshall HubertSoft) -> reference UNet +
+    head -> AlignmentDecoder.decode, with the product's default synthetic weights (synth:0 encoders, the
+    synth_checkpoint(seed=1) UNet/head, V = 63) so the GPU box rebuilds them bit-identically.  Text: 30 words of
+    the synthetic dictionary through the reference's DictionaryG2P (S = 91)."""
+    import shutil
+    import tempfile
+    import torch
+    from networks.g2p import DictionaryG2P
+    import ckpt_files
+    UnitsEncoder = _reference_encoder_module().UnitsEncoder
+
+    wav16 = synth.synth_audio(160000, seed=2024)
+    n44 = 441000
+    vocab = synth.synth_vocab(62)
+    g2p = DictionaryG2P(dictionary=os.path.join(HERE, "synth_dict.txt"))
+    dic = synth.synth_dictionary(n_words=40)
+    text = synth.synth_lab(30, dic, seed=2024)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        ph_seq, word_seq, p2w = g2p(text)
+    p2w = [int(x) for x in p2w]
+    meta = {"text": text, "ph_seq": list(ph_seq), "word_seq": list(word_seq), "ph_idx_to_word_idx": p2w,
+            "n44": n44, "wav_seed": 2024, "encoders": {}}
+    arrays = {"wav16_s16": np.round(wav16 * 32768).astype(np.int16)}
+    tmp = tempfile.mkdtemp(prefix="hfa_gold_")
+    try:
+        for name, arch, enc in (("base", synth.arch_cnhubert_base(), "cnhubert"),
+                                ("large", synth.arch_cnhubert_large(), "cnhubert"),
+                                ("soft", synth.arch_hubertsoft(), "hubertsoft")):
+            sd = synth.synth_hubert_state_dict(arch, seed=0)
+            path = os.path.join(tmp, name)
+            if enc == "cnhubert":
+                ckpt_files.save_hf_folder(path, arch, sd, do_normalize=True)
+            else:
+                path += ".pt"
+                torch.save({"hubert": {"module." + k: torch.from_numpy(v) for k, v in sd.items()}}, path)
+            del sd
+            ue = UnitsEncoder(enc, path, 16000, 320, device="cpu")
+            ua = synth.UNetArch(input_dims=arch.out_channels, vocab_size=vocab["vocab_size"])
+            usd = synth.synth_unet_state_dict(ua, seed=1)
+            r = _reference_lattice(ue, wav16, n44, ua, usd, vocab, ph_seq, word_seq, p2w)
+            del ue
+            if name == "base":          # Hubert units at the grid, [C, 862] -> the [L, C] frames they gather
+                arrays["base_units"] = r["units"][0].transpose(0, 1).numpy().astype(np.float32)
+            for k in ("ph_prob_log", "edge_prob", "ph_idx_seq", "ph_time_int", "frame_confidence", "ph_intervals",
+                      "word_intervals"):
+                arrays[f"{name}_{k}"] = r[k]
+            meta["encoders"][name] = {"encoder": enc, "channel": arch.out_channels,
+                                      "ph_seq_pred": r["ph_seq_pred"], "word_seq_pred": r["word_seq_pred"],
+                                      "confidence": r["confidence"], "n_ph": int(len(r["ph_idx_seq"]))}
+            print(f"e2e 10 s {name}: T={r['ph_prob_log'].shape[0]} S={len(ph_seq)} n_ph={len(r['ph_idx_seq'])} "
+                  f"conf={r['confidence']:.4f}")
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    np.savez_compressed(os.path.join(HERE, "e2e_10s.npz"), **arrays)
+    with open(os.path.join(HERE, "e2e_10s.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+LOADER_SAMPLES = 16000      # loader fixtures: 1 s of audio through 2-layer encoders (tests/ckpt_files.py)
+
+
+def gen_loaders():
+    """Checkpoint-loader goldens (VERDICT r02 'next' 3).  The weight files themselves are rebuilt at test time by
+    tests/ckpt_files.py from the same seeds (base-size conv stacks are ~17 MB of f32: too big to commit); what is
+    stored is what the reference / transformers computed from each file:
+      * HF folder written by HubertModel.save_pretrained (parametrized weight norm), preprocessor do_normalize
+        true / false, and the legacy layout (pytorch_model.bin, weight_g/weight_v, "hubert." prefix), each loaded
+        by the reference's Audio2CNHubert (HubertModel / Wav2Vec2FeatureExtractor.from_pretrained,
+        encoder.py:86-96) -> units [1, 49, 768];
+      * bshall {"hubert": {"module." + key: tensor}} loaded by the reference's Audio2HubertSoft (encoder.py:63-78,
+        consume_prefix_in_state_dict_if_present) -> units [1, 50, 256];
+      * a Lightning-layout .ckpt: state_dict = the reference modules' own keys (backbone / head, and every loss
+        module's registered buffers, GHMLoss.py:18,64,123,126,225,227, under forced_alignment.py:82-108's
+        attribute names) + hyper_parameters from configs/train_config.yaml; the reference UNet + head on a fixed
+        input -> logits.  The buffer names/shapes are stored (the .ckpt is rebuilt at test time)."""
+    import shutil
+    import tempfile
+    import torch
+    import yaml
+    import ckpt_files
+    from networks.loss.BinaryEMDLoss import BinaryEMDLoss
+    from networks.loss.GHMLoss import CTCGHMLoss, GHMLoss, MultiLabelGHMLoss
+    UnitsEncoder = _reference_encoder_module().UnitsEncoder
+
+    wav = synth.synth_audio(LOADER_SAMPLES, seed=5)
+    out = {"wav": wav}
+    tmp = tempfile.mkdtemp(prefix="hfa_gold_")
+    try:
+        units = {}
+        for kind in ckpt_files.HF_KINDS:
+            path = os.path.join(tmp, kind)
+            ckpt_files.write_hf_folder(path, kind)
+            ue = UnitsEncoder("cnhubert", path, 16000, 320, device="cpu")
+            with torch.inference_mode():
+                units[kind] = ue.model(torch.from_numpy(wav)[None])[0].numpy()
+        assert np.array_equal(units["hf"], units["hf_legacy"]), "transformers loads both layouts to one model"
+        out["hf_units"] = units["hf"]
+        out["hf_nonorm_units"] = units["hf_nonorm"]
+        path = os.path.join(tmp, "soft.pt")
+        ckpt_files.write_bshall(path)
+        ue = UnitsEncoder("hubertsoft", path, 16000, 320, device="cpu")
+        with torch.inference_mode():
+            out["soft_units"] = ue.model(torch.from_numpy(wav)[None])[0].numpy()
+        print("loader units:", {k: v.shape for k, v in out.items()})
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    # the loss modules' buffers, as LitForcedAlignmentTask.__init__ builds them (forced_alignment.py:82-108)
+    cfg = yaml.safe_load(open(os.path.join(REF, "configs", "train_config.yaml")))
+    lf = cfg["loss_config"]["function"]
+    vocab = synth.synth_vocab(62)
+    V = vocab["vocab_size"]
+    losses = {"ph_frame_GHM_loss_fn": GHMLoss(V, lf["num_bins"], lf["alpha"], lf["label_smoothing"]),
+              "pseudo_label_GHM_loss_fn": MultiLabelGHMLoss(V, lf["num_bins"], lf["alpha"], lf["label_smoothing"]),
+              "ph_edge_GHM_loss_fn": MultiLabelGHMLoss(1, lf["num_bins"], lf["alpha"], label_smoothing=0.0),
+              "EMD_loss_fn": BinaryEMDLoss(),
+              "ph_edge_diff_GHM_loss_fn": MultiLabelGHMLoss(1, lf["num_bins"], lf["alpha"], label_smoothing=0.0),
+              "CTC_GHM_loss_fn": CTCGHMLoss(alpha=1 - 1e-3)}
+    buffers = {f"{n}.{k}": list(v.shape) for n, m in losses.items() for k, v in m.state_dict().items()}
+    # the reference UNet + head on a fixed input through the checkpoint's weights
+    ua = synth.UNetArch(vocab_size=V)
+    usd = synth.synth_unet_state_dict(ua, seed=ckpt_files.CKPT_SEED)
+    from networks.layer.backbone.unet import UNetBackbone
+    from networks.layer.block.resnet_block import ResidualBasicBlock
+    from networks.layer.scaling.stride_conv import DownSampling, UpSampling
+    bb = UNetBackbone(ua.input_dims, ua.output_dims, ua.hidden_dims, ResidualBasicBlock, DownSampling, UpSampling,
+                      ua.factor, ua.times, ua.scaleup).eval()
+    head = torch.nn.Linear(ua.output_dims, V + 2).eval()
+    bb.load_state_dict({k[len("backbone."):]: torch.from_numpy(v) for k, v in usd.items() if k.startswith("backbone.")})
+    head.load_state_dict({k[len("head."):]: torch.from_numpy(v) for k, v in usd.items() if k.startswith("head.")})
+    x = synth.rng(77).standard_normal((1, 301, ua.input_dims)).astype(np.float32)
+    with torch.no_grad():
+        out["ckpt_logits"] = head(bb(torch.from_numpy(x))).numpy()[0]
+    meta = {"loss_buffers": buffers, "model_config": cfg["model"], "hubert_config": cfg["hubert_config"],
+            "melspec_config": cfg["melspec_config"], "optimizer_config": cfg["optimizer_config"],
+            "loss_config": cfg["loss_config"], "unet_input_seed": 77, "unet_input_T": 301,
+            "layers": ckpt_files.LOADER_LAYERS, "wav_seed": 5}
+    np.savez_compressed(os.path.join(HERE, "loaders.npz"), **out)
+    with open(os.path.join(HERE, "loaders.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print("loaders done:", len(buffers), "loss buffers")
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference absent: fixtures are generated only in the survey/build container; skipping")
         return
     _import_reference()
-    which = sys.argv[1:] or ["dp", "decode", "g2p", "postproc", "gather", "hubert", "unet"]
+    which = sys.argv[1:] or ["dp", "decode", "g2p", "postproc", "gather", "hubert", "unet", "e2e10s", "loaders"]
     for w in which:
         {"dp": gen_dp_cases, "decode": gen_decode_cases, "g2p": gen_g2p, "g2p_dicts": gen_g2p_dicts,
          "postproc": gen_postproc,
-         "gather": gen_gather_index, "hubert": gen_hubert, "unet": gen_unet}[w]()
+         "gather": gen_gather_index, "hubert": gen_hubert, "unet": gen_unet, "e2e10s": gen_e2e10s,
+         "loaders": gen_loaders}[w]()
 
 
 if __name__ == "__main__":
