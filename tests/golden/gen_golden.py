@@ -452,14 +452,14 @@ def _reference_lattice(units_encoder, wav16, n44, ua, usd, vocab, ph_seq, word_s
     inner = dec._decode
 
     def capture(ph_seq_id, ph_prob_log, edge_prob):
-        seen.update(ph_prob_log=ph_prob_log.copy(), edge_prob=edge_prob.copy())
+        seen.update(ph_prob_log=ph_prob_log.copy(), edge_prob=edge_prob.copy())   # edge_prob is f64 (:84)
         return inner(ph_seq_id, ph_prob_log, edge_prob)
     dec._decode = capture
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
         ph_pred, ph_int, w_pred, w_int, conf = dec.decode(frame, edge, ctc, n44 / 44100, ph_seq, word_seq, p2w)
     return dict(units=feat, ph_prob_log=seen["ph_prob_log"].astype(np.float32),
-                edge_prob=seen["edge_prob"].astype(np.float32), ph_idx_seq=dec.ph_idx_seq.astype(np.int32),
+                edge_prob=seen["edge_prob"], ph_idx_seq=dec.ph_idx_seq.astype(np.int32),
                 ph_time_int=dec.ph_time_int_pred.astype(np.int32),
                 frame_confidence=dec.frame_confidence.astype(np.float32),
                 ph_intervals=np.asarray(ph_int, np.float64), word_intervals=np.asarray(w_int, np.float64),
