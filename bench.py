@@ -74,6 +74,8 @@ def parse():
                          "in the encoder's split GEMMs (f16-class accuracy, not the reference's f32)")
     ap.add_argument("--chunk-seconds", type=float, default=None,
                     help="long-form: encode overlapping windows of this length (config 5 chunked; B=1 only)")
+    ap.add_argument("--no-config3", action="store_true",
+                    help="N > 1: skip the extra BASELINE config-3 measurement (global batch 512) after the timed steps")
     ap.add_argument("--host-input", action="store_true",
                     help="waves start in host memory and are uploaded inside every step (task.upload, as infer.py) (PCIe-inclusive "
                          "rate; the headline value keeps inputs resident in HBM)")
@@ -164,6 +166,16 @@ def config_name(encoder: str, world: int, B: int, seconds: float = 10.0) -> str:
     if world == 1:
         return "config 2" if B == 32 else f"config 2 geometry (B={B}, config 2 is 32)"
     return "config 3 geometry" + ("" if world * B == 512 else f" (global batch {world * B}, config 3 is 512)")
+
+
+def config3_batch(args, world: int) -> int:
+    """Per-GPU batch of BASELINE config 3 (512 x 10 s over the node) when this multi-GPU run's own global batch is
+    not already 512; 0 when there is nothing extra to measure."""
+    if world <= 1 or args.encoder != "base" or args.seconds != 10.0 or args.chunk_seconds is not None:
+        return 0
+    if world * args.batch == 512 or 512 % world or args.no_config3:
+        return 0
+    return 512 // world
 
 
 def host_io(wav_np, res, seconds, budget_s=3.0):
@@ -264,37 +276,55 @@ def main():
     wav_np, ph_seqs, word_seqs, p2ws = make_inputs(B, args.seconds, args.words, seed0=1000 * (rank + 1))
     wav = wav_dev = torch.from_numpy(wav_np).to(dev)
     wav_host = torch.from_numpy(wav_np).pin_memory() if args.host_input else None
+    inputs = (wav_dev, wav_host, ph_seqs, word_seqs, p2ws)
 
-    def launch():
+    def launch(inp):
         """GPU half of one step (+ the boundary gather) and the async D2H of its results: the encoder on the main
         stream, head + DP on a side stream overlapping the next step's encoder (task.submit).  With --host-input the
         step starts with task.upload of its waves (the CLI's pinned non-blocking H2D)."""
-        wav = task.upload(wav_host) if wav_host is not None else wav_dev
+        wav_d, wav_h, ph, ws, pw = inp
+        wav = task.upload(wav_h) if wav_h is not None else wav_d
         if args.serial:
-            dev_out = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False,
-                                       chunk_seconds=args.chunk_seconds)
+            dev_out = task.align_batch(wav, ph, ws, pw, wav_sr=16000, host=False, chunk_seconds=args.chunk_seconds)
             if world > 1:
                 gather_boundaries(dev_out, uniform=True)
             return task.decoder.fetch(dev_out)
-        return task.submit(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000,
+        return task.submit(wav, ph, ws, pw, wav_sr=16000,
                            on_device=(lambda d: gather_boundaries(d, uniform=True)) if world > 1 else None,
                            chunk_seconds=args.chunk_seconds)
 
-    def finish(handle):
-        return task.decoder.assemble(handle, ph_seqs, word_seqs, p2ws)
+    def finish(handle, inp):
+        return task.decoder.assemble(handle, *inp[2:])
 
-    def run(k):
+    def run(k, inp=inputs):
         """k steps, software-pipelined: the host assembles batch i while the GPU runs batch i+1."""
         pending, res = None, None
         for _ in range(k):
             t0 = time.perf_counter()
-            h = launch()
+            h = launch(inp)
             t1 = time.perf_counter()
             if pending is not None:
-                res = finish(pending)
+                res = finish(pending, inp)
             host_t.append((t1 - t0, time.perf_counter() - t1))
             pending = h
-        return finish(pending) if pending is not None else res
+        return finish(pending, inp) if pending is not None else res
+
+    def timed(k, inp=inputs):
+        """exactly k steps between barrier + synchronize pairs -> (results, max seconds over ranks)."""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = run(k, inp)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([e], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            e = float(tt.item())
+        return r, e
 
     host_t = []   # (enqueue, wait + assemble) seconds per step, reported on stderr
 
@@ -306,20 +336,8 @@ def main():
     probe_name = census.dominant() if args.probe == "auto" else args.probe
     probe = ops.KernelProbe(probe_name, extra=SECONDARY)
     ops.PROBE = probe
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    res = run(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+    res, el = timed(args.steps)
     ops.PROBE = None
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
 
     n_frames = res[0]["T"]
     audio_s = world * B * args.seconds * args.steps
@@ -380,11 +398,24 @@ def main():
         rd = RANDOM_DATA_F16_TFLOPS / (1 if probe_name.endswith(", true>") else 3)
         out["roofline"]["random_data_mfma_rate"] = rd
         out["roofline"]["frac_of_random_data_rate"] = achieved / rd
+    c3 = config3_batch(args, world)
+    if c3:
+        # BASELINE config 3 (512 x 10 s over the node) measured after the weak-scaling region, whose per-GPU batch
+        # stays at config 2's 32 so the driver's N = 1..8 curve compares equal per-GPU work
+        inp3 = make_inputs(c3, args.seconds, args.words, seed0=7000 * (rank + 1))
+        inp3 = (torch.from_numpy(inp3[0]).to(dev), None) + inp3[1:]
+        run(1, inp3)
+        _, el3 = timed(args.steps, inp3)
+        out["config3"] = {"workload": f"config 3: global batch {world * c3} x {args.seconds:g} s ({c3} per GPU, "
+                                      f"{world} GPUs), same path and timing protocol", "per_gpu_batch": c3,
+                          "global_batch": world * c3, "steps": args.steps, "ms_per_step": el3 / args.steps * 1e3,
+                          "value": world * c3 * args.seconds * args.steps / el3, "unit": "audio_s/s",
+                          "frames_per_s": world * c3 * n_frames * args.steps / el3}
     iso = ops.KernelProbe("-", extra=SECONDARY)       # isolated serial steps for the secondary rooflines
     ops.PROBE = iso
     for _ in range(2):
         torch.cuda.synchronize()
-        task.decoder.assemble(task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False,
+        task.decoder.assemble(task.align_batch(wav_dev, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False,
                                                chunk_seconds=args.chunk_seconds), ph_seqs, word_seqs, p2ws)
     torch.cuda.synchronize()
     ops.PROBE = None

@@ -55,7 +55,7 @@ def _comm_device(group=None) -> torch.device:
     return torch.device("cuda", torch.cuda.current_device())
 
 
-def gather_boundaries(dev_out: dict, keys=BOUNDARY_KEYS, uniform: bool = False, group=None):
+def gather_boundaries(dev_out: dict, keys=BOUNDARY_KEYS, uniform: bool = False, group=None, shortcut: bool = True):
     """All-gather per-utterance arrays of every rank; the local shapes may differ between ranks.
 
     ``dev_out[k]`` is [B] or [B, Tmax, ...] (one B per rank, one Tmax per rank over the 2-D keys).  Step 1
@@ -63,9 +63,10 @@ def gather_boundaries(dev_out: dict, keys=BOUNDARY_KEYS, uniform: bool = False, 
     ``all_gather_into_tensor`` per key.  ``uniform=True`` skips step 1 (every rank is known to hold the same
     shapes, e.g. the benchmark's equal batches: no host synchronisation then).
 
-    Returns ``{k: [tensor of rank r, unpadded to its own (B_r, Tmax_r)] for r in ranks}``."""
+    Returns ``{k: [tensor of rank r, unpadded to its own (B_r, Tmax_r)] for r in ranks}``.  ``shortcut=False``
+    runs the collectives even in a one-rank group (exercises the RCCL path on a one-GPU box)."""
     world = _world(group)
-    if world == 1:
+    if world == 1 and (shortcut or not dist.is_initialized()):
         return {k: [dev_out[k]] for k in keys}
     cdev = _comm_device(group)
     first2d = next((k for k in keys if dev_out[k].dim() >= 2), None)

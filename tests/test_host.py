@@ -444,3 +444,16 @@ def test_longform_window_plan_and_spans():
     for arch in (synth.arch_cnhubert_base(), synth.arch_cnhubert_large(), synth.arch_hubertsoft()):
         for a, b in ((0, 1), (0, 400), (300, 1601), (5, 6)):
             assert frame_count(arch, window_samples(a, b, pad=arch.wav_pad)) == b - a
+
+
+def test_bench_config3_batch():
+    """bench.py's N > 1 runs keep config 2's per-GPU batch for the weak-scaling line and add a BASELINE config-3
+    measurement (global batch 512) after it: 256 / 128 / 64 per GPU at N = 2 / 4 / 8."""
+    import argparse
+    import bench
+    a = argparse.Namespace(encoder="base", seconds=10.0, chunk_seconds=None, batch=32, no_config3=False)
+    assert [bench.config3_batch(a, n) for n in (1, 2, 4, 8)] == [0, 256, 128, 64]
+    assert bench.config3_batch(argparse.Namespace(**{**vars(a), "batch": 64}), 8) == 0     # already config 3
+    assert bench.config3_batch(argparse.Namespace(**{**vars(a), "encoder": "large"}), 8) == 0
+    assert bench.config3_batch(argparse.Namespace(**{**vars(a), "no_config3": True}), 8) == 0
+    assert bench.config_name("base", 8, 64) == "config 3 geometry"
