@@ -168,6 +168,30 @@ def config_name(encoder: str, world: int, B: int, seconds: float = 10.0) -> str:
     return "config 3 geometry" + ("" if world * B == 512 else f" (global batch {world * B}, config 3 is 512)")
 
 
+def step_breakdown(task, wav, ph_seqs, word_seqs, p2ws, k, step_s):
+    """What the side stream (UNet head + lattice + Viterbi + D2H, overlapped with the next batch's encoder) costs
+    the pipelined step: the same k steps with the encoder alone (main stream, nothing beside it), and the head + DP
+    alone on the encoder's output (serial).  Outside the timed region."""
+    import torch
+    feats, n_frames, wl = task.encode_batch(wav, 16000)
+    torch.cuda.synchronize()
+
+    def clock(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / k * 1e3
+    enc_ms = clock(lambda: task.encode_batch(wav, 16000))
+    head_ms = clock(lambda: task.decoder.fetch(task.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)))
+    return {"pipelined_step_ms": step_s * 1e3, "encoder_only_ms": enc_ms, "head_dp_only_ms": head_ms,
+            "side_stream_cost_ms": step_s * 1e3 - enc_ms,
+            "note": "encoder_only / head_dp_only: the step's two halves run alone, serially, k steps each; "
+                    "side_stream_cost = pipelined step - encoder alone (what overlapping the head costs the encoder)"}
+
+
 def config3_batch(args, world: int) -> int:
     """Per-GPU batch of BASELINE config 3 (512 x 10 s over the node) when this multi-GPU run's own global batch is
     not already 512; 0 when there is nothing extra to measure."""
@@ -411,6 +435,8 @@ def main():
                           "global_batch": world * c3, "steps": args.steps, "ms_per_step": el3 / args.steps * 1e3,
                           "value": world * c3 * args.seconds * args.steps / el3, "unit": "audio_s/s",
                           "frames_per_s": world * c3 * n_frames * args.steps / el3}
+    if world == 1 and args.chunk_seconds is None and not args.serial:
+        out["step_breakdown"] = step_breakdown(task, wav_dev, ph_seqs, word_seqs, p2ws, args.steps, el / args.steps)
     iso = ops.KernelProbe("-", extra=SECONDARY)       # isolated serial steps for the secondary rooflines
     ops.PROBE = iso
     for _ in range(2):
