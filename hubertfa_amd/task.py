@@ -21,7 +21,7 @@ from .encoder import UnitsEncoder
 from .resample import Resampler, target_length
 from .hubert import dev_lengths
 from .unet import LatticeHead
-from .wav_io import load_wav
+from .wav_io import read_wav
 
 
 def guarded(module, flag, fn):
@@ -103,11 +103,15 @@ class ForcedAlignmentTask:
     __call__ = forward
 
     def predict_step(self, batch, batch_idx=0):
+        """forced_alignment.py:154-186.  load_wav's resample to the melspec rate (load_wav.py:6-7) runs inside
+        align_batch (``wav_sr``), on the same kernels as the batched CLI, so one file gives identical results on
+        both paths."""
         wav_path, ph_seq, word_seq, ph_idx_to_word_idx = batch
         sr = self.melspec_config["sample_rate"]
-        waveform = load_wav(wav_path, self.device, sr)
-        wav_length = waveform.shape[0] / sr
-        res = self.align_batch(waveform[None], [ph_seq], [word_seq], [ph_idx_to_word_idx])[0]
+        x, file_sr = read_wav(str(wav_path))
+        wave = self.upload(np.ascontiguousarray(x[:1]))                     # channel 0 (load_wav.py:8)
+        wav_length = target_length(x.shape[1], file_sr, sr) / sr           # waveform.shape[0] / sample_rate
+        res = self.align_batch(wave, [ph_seq], [word_seq], [ph_idx_to_word_idx], wav_sr=file_sr)[0]
         return (wav_path, wav_length, res["confidence"], res["ph_seq"], res["ph_intervals"], res["word_seq"],
                 res["word_intervals"])
 
