@@ -279,6 +279,44 @@ def split_flag(device) -> torch.Tensor:
     return _OFLOW[key]
 
 
+class UnetOp(ctypes.Structure):
+    """include/hfa.h hfa_unet_op (one op of the fused UNet + head table)."""
+    _fields_ = [("kind", ctypes.c_int32), ("level", ctypes.c_int32), ("n", ctypes.c_int32),
+                ("groups", ctypes.c_int32), ("nseg", ctypes.c_int32),
+                ("src", ctypes.c_int32 * 2), ("src_ld", ctypes.c_int32 * 2), ("cin", ctypes.c_int32 * 2),
+                ("taps", ctypes.c_int32 * 2), ("gn", ctypes.c_int32 * 2), ("ldw", ctypes.c_int32 * 2),
+                ("res", ctypes.c_int32), ("dst", ctypes.c_int32),
+                ("src_off", ctypes.c_int64 * 2), ("res_off", ctypes.c_int64), ("dst_off", ctypes.c_int64),
+                ("w", ctypes.c_void_p * 2), ("wp", ctypes.c_int64 * 2),
+                ("bias", ctypes.c_void_p), ("gn_gamma", ctypes.c_void_p), ("gn_beta", ctypes.c_void_p),
+                ("ln_gamma", ctypes.c_void_p), ("ln_beta", ctypes.c_void_p)]
+
+
+UNET_NONE, UNET_INPUT, UNET_OUTPUT = -1, -2, -3
+_lib.register("hfa_unet_head", [_I_, _I_, _P_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_, _P_, _P_])
+_lib.register("hfa_unet_lds_bytes", [], restype=ctypes.c_longlong)
+
+
+def unet_head(table, nops, feats, logits, t_pad, workspace, ws_floats, flag, flops=0.0):
+    """The fused UNet + head (unet.hip): ``table`` a device uint8 tensor of ``nops`` UnetOp records, feats
+    [B, Tmax, Cin] f32 (rows >= each t_pad[b] zero), logits [B, Tmax, V+2] f32 out, t_pad int32 [B] device,
+    workspace f32 with ws_floats per utterance."""
+    B, Tmax, _ = feats.shape
+    _need(feats, torch.float32, "feats", contiguous=False)
+    _need(logits, torch.float32, "logits", contiguous=False)
+    _need(t_pad, torch.int32, "t_pad")
+    if feats.stride(2) != 1 or logits.stride(2) != 1:
+        raise ValueError("unet_head: rows must be contiguous")
+
+    def launch():
+        _lib.call("hfa_unet_head", B, Tmax, _ptr(table), nops, _ptr(feats), feats.stride(0), feats.stride(1),
+                  _ptr(logits), logits.stride(0), logits.stride(1), _ptr(t_pad), _ptr(workspace), ws_floats,
+                  _ptr(flag), _stream(feats.device))
+    if PROBE is None:
+        return launch()
+    PROBE("unet_head_kernel", flops, launch)
+
+
 def split(x, out=None, flag=None):
     """f32 [..., C] (row-strided) -> split planes [2, ..., C]; out-of-range values raise ``flag`` (default: the
     device's split_flag)."""

@@ -204,6 +204,42 @@ int hfa_groupnorm_split(int B, int T, int C, int G, const float* x, long long x_
                         uint16_t* ys, long long ys_bs, int ldys, long long sps, int* oflow, void* workspace,
                         hipStream_t stream);
 
+/* ---- fused lattice producer (hubertfa_amd/csrc/unet.hip) ------------------------------------------------------
+ * UNetBackbone + head of LitForcedAlignmentTask (networks/layer/backbone/unet.py:100-119, networks/layer/block/
+ * resnet_block.py:17-50, networks/layer/scaling/stride_conv.py:23-47, networks/task/forced_alignment.py:53-55,
+ * 287-288) as ONE launch: one workgroup per utterance runs the op table in order on its own t_pad[b] rows, with
+ * split-f16 contractions (see hfa_conv_gemm_split), GroupNorm statistics in f64 and LayerNorm in f32 inside the
+ * workgroup.  Slots name f32 tensors of the per-utterance workspace (offsets in floats per Tmax row).
+ *   kind 0 conv1: k3 conv of src[0]; output = the raw conv (the block's GroupNorm statistics are kept in LDS)
+ *   kind 1 conv2: k3 conv of GroupNorm(groups) + Hardswish of src[0] (gn[0] = 1), + Linear shortcut (segment 1)
+ *                 or + residual slot, then LayerNorm + Hardswish
+ *   kind 2 down: k2 s2 conv (src rows read as pairs: cin = 2 C, ldw = 2 C) + bias
+ *   kind 3 up: ConvTranspose k2 s2 as [T, 2 Cout] = [2T, Cout] (+ bias + skip slot)
+ *   kind 4 head: Linear + bias into `logits` (dst = HFA_UNET_OUTPUT)
+ * n <= 384, cin % 32 == 0, t_pad[b] a multiple of 2^(max level); *oflow raised for an operand outside f16 range
+ * or a non-finite output. */
+#define HFA_UNET_NONE (-1)
+#define HFA_UNET_INPUT (-2)
+#define HFA_UNET_OUTPUT (-3)
+typedef struct hfa_unet_op {
+    int32_t kind, level, n, groups, nseg;
+    int32_t src[2], src_ld[2], cin[2], taps[2], gn[2], ldw[2];
+    int32_t res, dst;
+    int64_t src_off[2], res_off, dst_off;
+    const uint16_t* w[2];
+    int64_t wp[2];
+    const float* bias;
+    const float* gn_gamma;
+    const float* gn_beta;
+    const float* ln_gamma;
+    const float* ln_beta;
+} hfa_unet_op;
+int hfa_unet_head(int B, int Tmax, const hfa_unet_op* ops, int nops, const float* feats, long long f_bs, int f_ld,
+                  float* logits, long long l_bs, int l_ld, const int32_t* t_pad, float* workspace, long long ws_bs,
+                  int* oflow, hipStream_t stream);
+/* LDS bytes the fused kernel's workgroup uses (diagnostics). */
+long long hfa_unet_lds_bytes(void);
+
 /* ---- extractor conv0 (hubertfa_amd/csrc/conv.hip) ------------------------------------------------------------
  * x [B, N] -> y [B, T0, 512] channels-last, T0 = (N-10)/5+1.  norm=1: GroupNorm(512,512) + GELU
  * (networks/hubert/model.py:98-99,108; transformers HubertGroupNormConvLayer), needs a workspace of

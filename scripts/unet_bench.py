@@ -21,8 +21,9 @@ def main():
     T = task.head.padded_len(861)
     x = torch.randn(args.B, T, 768, device=d) * 0.5
     flops = task.head.flops(T) * args.B
-    for prec in ("split", "f32", "split"):
+    for prec, fused in (("split", True), ("split", False), ("f32", False), ("split", True)):
         task.head.precision = prec
+        task.head.use_fused = fused
         for _ in range(3):
             task.head.logits(x)
         torch.cuda.synchronize()
@@ -33,9 +34,22 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.reps
-        print(f"head {prec}: {ms:.3f} ms per batch of {args.B} x {T} frames, {flops / ms / 1e9:.1f} TFLOP/s "
+        print(f"head {prec}{' fused' if fused and prec == 'split' else ''}: {ms:.3f} ms per batch of {args.B} x {T} frames, {flops / ms / 1e9:.1f} TFLOP/s "
               f"({flops / 1e9:.1f} GFLOP)", flush=True)
     task.head.precision = "split"
+    task.head.use_fused = True
+    for B in (1, 8, 32, 64):          # fused: one workgroup per utterance
+        xb = x[:1].expand(B, -1, -1).contiguous()
+        for _ in range(2):
+            task.head.logits(xb)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            task.head.logits(xb)
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"fused B={B}: {e0.elapsed_time(e1) / args.reps:.3f} ms", flush=True)
 
 
 if __name__ == "__main__":
