@@ -23,10 +23,12 @@
 // LayerNorm two-pass in f32 (norm.hip's formulas).  A staged value outside f16 range raises *oflow (the caller
 // re-runs on the f32 path).
 //
-// Tile: 8 waves; a row block of BM = 128 output rows x all N output columns (N <= 384): waves 2 (rows) x 4 (columns),
-// a wave owns 64 x N/4 (4 x NJ blocks of 16 x 16).  K runs in steps of 32 channels of one tap: the operand window
-// (BM + taps - 1 rows x 32 channels) is loaded once per channel chunk through registers (transform + split), W's
-// planes for each (tap, chunk) step go global -> LDS by LDS-DMA one step ahead, two stages each.
+// Tile: 8 waves; a row block of 32 NI output rows x all N output columns (N <= 384): waves 2 (rows) x 4 (columns), a
+// wave owns 16 NI x 16 NJ (NI x NJ blocks of 16 x 16, NI NJ <= 12).  K runs in steps of 32 channels of one tap: the
+// operand window (rows + taps - 1 x 32 channels) is loaded once per channel chunk through registers (transform +
+// split) into one of two LDS images, one barrier per chunk; each step's W fragments come from L2 straight into
+// registers one step ahead (the two row waves of a column read the same W; no LDS stage for it, so the k3 convs
+// run 3 steps per barrier).
 #include "hfa_common.h"
 #include "hfa.h"
 
@@ -35,15 +37,18 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// pointers that came through the op table are generic; these make their loads / stores global_* instructions
+typedef const __attribute__((address_space(1))) f16x8 GF16x8;
+typedef const __attribute__((address_space(1))) f32x4 GF32x4;
+typedef const __attribute__((address_space(1))) float GF32;
+typedef __attribute__((address_space(1))) float GF32w;
 
-constexpr int NT = 512, NWV = 8, BM = 128, KS = 32;
+constexpr int NT = 512, BM = 128, KS = 32;
 constexpr int WIN_MAX = BM + 2;                          // k3 conv window rows
 constexpr int A_PLANE = WIN_MAX * 64;                    // bytes of one plane image of the operand window
 constexpr int A_STAGE = 2 * A_PLANE;
 constexpr int N_MAX = 384;
-constexpr int W_PLANE_MAX = N_MAX * 64;
-constexpr int W_STAGE_MAX = 2 * W_PLANE_MAX;
-constexpr int LDS_A = 2 * A_STAGE, LDS_W = 2 * W_STAGE_MAX;
+constexpr int LDS_A = 2 * A_STAGE;
 
 enum { U_CONV1 = 0, U_CONV2 = 1, U_DOWN = 2, U_UP = 3, U_HEAD = 4 };
 
@@ -62,16 +67,18 @@ struct Stage {       // one K-segment of an op: A source (f32 rows), taps, weigh
 
 struct Shared {
     unsigned char a[LDS_A];
-    unsigned char w[LDS_W];
     float red[2][64][4];          // LayerNorm row partials [row half][row][column wave]
     double colsum[2][N_MAX][2];   // GroupNorm column partials [row half][column][sum, sum of squares]
     float gstat[64][2];           // GroupNorm mean, rstd per group
 };
 
 // ---- staging -------------------------------------------------------------------------------------------------
-// Operand window of chunk c0 (32 channels) for output rows [m0, m0 + BM): source rows m0 - pad .. m0 - pad + win - 1
-// -> split planes in LDS image `abuf` (row w at 64 B per plane; chunk slots swizzled).  GroupNorm + Hardswish
-// (gn) with the block's statistics; rows outside [0, rows) are the conv's zero padding (of the transformed value).
+// Operand window of one 32-channel chunk for output rows [m0, m0 + rows_blk): source rows m0 - pad .. m0 - pad + win - 1
+// -> split planes in an LDS image (row w at 64 B per plane; chunk slots swizzled).  GN: the block's GroupNorm +
+// Hardswish on the way in; rows outside [0, rows) are the conv's zero padding (of the transformed value).  A thread
+// always handles the same channel quad (tid & 7) of the chunk, at rows tid/8 + 64 it.  Loads are branch-free (a
+// clamped row is read; store_a zeroes it), and nothing touches the loaded registers before store_a, so the loads
+// stay in flight under the chunk's MFMAs.
 struct ARegs {
     f32x4 v[3];
 };
@@ -80,36 +87,49 @@ __device__ __forceinline__ void load_a(const Stage& s, int m0, int c0, int win, 
     const int tid = threadIdx.x;
 #pragma unroll
     for (int it = 0; it < 3; ++it) {
-        const int idx = tid + it * NT;
-        const int w = idx >> 3, q = idx & 7;
+        const int w = (tid >> 3) + it * (NT / 8), q = tid & 7;
         const int t = m0 - s.pad + w;
-        r.v[it] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (w < win && t >= 0 && t < s.rows)
-            r.v[it] = *reinterpret_cast<const f32x4*>(s.src + (long long)t * s.ld + c0 + q * 4);
+        const int tc = t < 0 ? 0 : (t >= s.rows ? s.rows - 1 : t);
+        r.v[it] = *(const GF32x4*)(s.src + (long long)tc * s.ld + c0 + q * 4);
     }
 }
 
+// GroupNorm + Hardswish of the thread's 4 channels (c0 + 4 (tid & 7) ..): y = x * scale + shift, per channel
+struct GnCoef {
+    f32x4 scale, shift;
+};
+
+__device__ __forceinline__ GnCoef gn_coef(const Shared& sh, const float* gamma, int c0, int cg) {
+    const int c = c0 + (threadIdx.x & 7) * 4;
+    const f32x4 g = *(const GF32x4*)(gamma + c);
+    GnCoef k;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int grp = (c + e) / cg;
+        k.shift[e] = sh.gstat[grp][0];            // (x - mean) * (rstd * gamma) + beta
+        k.scale[e] = sh.gstat[grp][1] * g[e];
+    }
+    return k;
+}
+
+template <bool GN>
 __device__ __forceinline__ void store_a(const Stage& s, int m0, int c0, int win, const ARegs& r, unsigned char* abuf,
-                                        const float* gamma, const float* beta, const Shared& sh, int G, bool& bad) {
-    const int cg = s.gn ? s.cin / G : 1;                  // channels per GroupNorm group of the staged tensor
-    const int tid = threadIdx.x;
+                                        const float* beta, const GnCoef& k, bool& bad) {
+    const int tid = threadIdx.x, q = tid & 7;
+    f32x4 b{0.f, 0.f, 0.f, 0.f};
+    if constexpr (GN) b = *(const GF32x4*)(beta + c0 + q * 4);
 #pragma unroll
     for (int it = 0; it < 3; ++it) {
-        const int idx = tid + it * NT;
-        const int w = idx >> 3, q = idx & 7;
+        const int w = (tid >> 3) + it * (NT / 8);
         if (w >= win) continue;
         const int t = m0 - s.pad + w;
+        const bool ok = t >= 0 && t < s.rows;
         f32x4 v = r.v[it];
-        if (s.gn) {
-            const int c = c0 + q * 4;
-            const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c);
-            const f32x4 b = *reinterpret_cast<const f32x4*>(beta + c);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int grp = (c + e) / cg;
-                const float o = hfa::hardswish((v[e] - sh.gstat[grp][0]) * sh.gstat[grp][1] * g[e] + b[e]);
-                v[e] = (t >= 0 && t < s.rows) ? o : 0.0f;
-            }
+        for (int e = 0; e < 4; ++e) {
+            float o = v[e];
+            if constexpr (GN) o = hfa::hardswish((o - k.shift[e]) * k.scale[e] + b[e]);
+            v[e] = ok ? o : 0.0f;
         }
         f16x4 h1, h2;
 #pragma unroll
@@ -124,33 +144,100 @@ __device__ __forceinline__ void store_a(const Stage& s, int m0, int c0, int win,
     }
 }
 
-// W planes of one (tap, chunk) step: N rows x 64 B per plane, by LDS-DMA (one 1-KiB piece = 16 rows of a plane)
-__device__ __forceinline__ void issue_w(const Stage& s, int N, int k0, unsigned wlds, int wave, int lane) {
-    const int pieces = 2 * ((N + 15) / 16);
-    const int per_plane = pieces / 2;
-    const unsigned plane_bytes = (unsigned)((N + 15) / 16) * 1024u;
-    // the descriptor, the LDS address and the offset go in SGPRs: make their (wave-uniform) values explicit
-    const int wbytes = __builtin_amdgcn_readfirstlane(N * s.ldw * 2);
-    auto uptr = [](const _Float16* p) {
-        const unsigned long long v = reinterpret_cast<unsigned long long>(p);
-        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-        return reinterpret_cast<const _Float16*>(((unsigned long long)hi << 32) | lo);
-    };
-    const __amdgpu_buffer_rsrc_t r1 = hfa::make_rsrc(uptr(s.w), wbytes);
-    const __amdgpu_buffer_rsrc_t r2 = hfa::make_rsrc(uptr(s.w + s.wp), wbytes);
-    for (int p = wave; p < pieces; p += NWV) {
-        const int pl = p / per_plane, rg = p - pl * per_plane;
-        const int n = rg * 16 + (lane >> 2);
-        const unsigned voff = n < N ? (unsigned)((n * s.ldw + k0 + (((lane & 3) ^ swz(n)) * 8)) * 2) : hfa::DMA_OOB;
-        const unsigned lds = __builtin_amdgcn_readfirstlane(wlds + pl * plane_bytes + rg * 1024u);
-        if (pl) hfa::dma16(voff, r2, 0u, lds);
-        else hfa::dma16(voff, r1, 0u, lds);
+// W fragments of one step for a wave's NJ column blocks, straight from global (L2) into registers in the 16x16x32
+// operand map: lane l holds row n = column block base + (l & 15), k = k0 + 8 (l >> 4) .. +7, both planes.  Columns
+// past N read row N - 1 (their outputs are never stored).
+template <int NJ>
+struct WFr {
+    f16x8 w1[NJ], w2[NJ];
+};
+
+template <int NJ>
+__device__ __forceinline__ void load_wf(const Stage& s, int N, int k0, int wn, int lane, WFr<NJ>& f) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        int n = wn * (NJ * 16) + j * 16 + (lane & 15);
+        n = n < N ? n : N - 1;
+        const _Float16* p = s.w + (long long)n * s.ldw + k0 + 8 * (lane >> 4);
+        f.w1[j] = *(const GF16x8*)(p);      // global, not flat: a flat load would also count in
+        f.w2[j] = *(const GF16x8*)(p + s.wp);   // lgkmcnt and every LDS wait would wait for it
     }
 }
 
 __device__ __forceinline__ void wait_all_barrier() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// One K-step: the wave's NI x NJ blocks += A(window rows + tap) . W(cur), three split products each.
+template <int NI, int NJ>
+__device__ __forceinline__ void mfma_step(f32x4 (&acc)[NI][NJ], const f16x8* ab, const WFr<NJ>& cur, int wrow, int tap,
+                                          int lane) {
+    f16x8 w1s[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) w1s[j] = cur.w1[j] * (_Float16)2048.0f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int w = wrow + i * 16 + (lane & 15) + tap;
+        const int slot = w * 4 + ((lane >> 4) ^ swz(w));
+        const f16x8 a1 = ab[slot];
+        const f16x8 a2 = ab[A_PLANE / 16 + slot];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, w1s[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, cur.w2[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, cur.w1[j], acc[i][j], 0, 0, 0);
+        }
+    }
+}
+
+// All K-steps of one segment (TAPS taps x cin/32 chunks) for the row block at m0.  The window of chunk q + 1 and the
+// W fragments of the next step are loaded while step q's MFMAs run (every load unconditional: the last chunk
+// re-reads itself); W alternates between two register sets, so chunks are walked in pairs (TAPS odd flips the
+// parity each chunk).  One barrier per chunk.  On entry the caller has the LDS images free (a barrier behind it).
+template <int NI, int NJ, int TAPS, bool GN>
+__device__ __forceinline__ void kloop(const Stage& s, int N, int m0, f32x4 (&acc)[NI][NJ], Shared& sh,
+                                      const float* gamma, const float* beta, int G, int wm, int wn, int lane,
+                                      bool& bad) {
+    constexpr int BMO = 32 * NI, WIN = BMO + TAPS - 1;
+    const int nch = s.cin / KS;
+    const int cg = GN ? s.cin / G : 1;
+    const f16x8* abase = reinterpret_cast<const f16x8*>(sh.a);
+    const int wrow = wm * (BMO / 2);
+    ARegs ar;
+    WFr<NJ> wa, wb;
+    load_a(s, m0, 0, WIN, ar);
+    load_wf<NJ>(s, N, 0, wn, lane, wa);
+    GnCoef k{};
+    if constexpr (GN) k = gn_coef(sh, gamma, 0, cg);
+    store_a<GN>(s, m0, 0, WIN, ar, sh.a, beta, k, bad);
+    wait_all_barrier();
+    // chunk q with its first W set in X: taps alternate X, Y, X, ...; the next chunk's first set lands in the
+    // other one (Y for TAPS odd)
+    auto chunk = [&](int q, WFr<NJ>& X, WFr<NJ>& Y) {
+        const int qn = q + 1 < nch ? q + 1 : q;
+        const f16x8* ab = abase + (q & 1) * (A_STAGE / 16);
+        load_a(s, m0, qn * KS, WIN, ar);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int tp = 0; tp < TAPS; ++tp) {
+            WFr<NJ>& cur = (tp & 1) ? Y : X;
+            WFr<NJ>& nxt = (tp & 1) ? X : Y;
+            if (tp + 1 < TAPS) load_wf<NJ>(s, N, (tp + 1) * s.cin + q * KS, wn, lane, nxt);
+            else load_wf<NJ>(s, N, qn * KS, wn, lane, nxt);
+            __builtin_amdgcn_sched_barrier(0);          // the prefetch stays ahead of this step's MFMAs
+            mfma_step<NI, NJ>(acc, ab, cur, wrow, tp, lane);
+        }
+        if (q + 1 < nch) {
+            if constexpr (GN) k = gn_coef(sh, gamma, qn * KS, cg);
+            store_a<GN>(s, m0, qn * KS, WIN, ar, sh.a + ((q + 1) & 1) * A_STAGE, beta, k, bad);
+            wait_all_barrier();
+        }
+    };
+    static_assert(TAPS == 1 || TAPS == 3, "taps 1 or 3");
+    for (int q = 0; q < nch; q += 2) {
+        chunk(q, wa, wb);                       // TAPS odd: its last step prefetched chunk q + 1's first set into wb
+        if (q + 1 < nch) chunk(q + 1, wb, wa);
+    }
 }
 
 // ---- one op: all row blocks of one GEMM with its epilogue ---------------------------------------------------------
@@ -179,10 +266,6 @@ __device__ void run_op(const OpArgs& o, Shared& sh, bool& bad) {
     const int wm = wave >> 2, wn = wave & 3;                // 2 x 4 waves
     const int N = o.N;
     const int cg = o.G > 0 ? N / o.G : 1;                  // CONV1: channels per group of its output
-    const unsigned lds_w = hfa::lds_addr(sh.w);
-    const unsigned wstage = (unsigned)((N + 15) / 16) * 2048u;   // bytes per W stage (2 planes)
-    const f16x8* abase = reinterpret_cast<const f16x8*>(sh.a);
-    const f16x8* wbase = reinterpret_cast<const f16x8*>(sh.w);
 
     if (o.kind == U_CONV1) {                                // GroupNorm column sums, accumulated block by block
         for (int i = tid; i < 2 * N_MAX * 2; i += NT) (&sh.colsum[0][0][0])[i] = 0.0;
@@ -196,76 +279,17 @@ __device__ void run_op(const OpArgs& o, Shared& sh, bool& bad) {
 #pragma unroll
             for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-        // step list: for each segment, for each 32-channel chunk, for each tap
-        int seg = 0, c0 = 0, tap = 0, step = 0, chunk = 0;
-        ARegs ar;
-        {
-            const Stage& s = o.st[0];
-            wait_all_barrier();            // every wave is done reading the previous block's / op's LDS images
-            issue_w(s, N, 0, lds_w, wave, lane);
-            load_a(s, m0, 0, BMO + s.taps - 1, ar);
+        // K: segment 0 (the op's operand), then the shortcut segment of a block's second conv
+        wait_all_barrier();                // every wave is done reading the previous block's / op's LDS images
+        if (o.kind == U_CONV1)
+            kloop<NI, NJ, 3, false>(o.st[0], N, m0, acc, sh, o.gamma, o.beta, o.G, wm, wn, lane, bad);
+        else if (o.kind == U_CONV2)
+            kloop<NI, NJ, 3, true>(o.st[0], N, m0, acc, sh, o.gamma, o.beta, o.G, wm, wn, lane, bad);
+        else
+            kloop<NI, NJ, 1, false>(o.st[0], N, m0, acc, sh, o.gamma, o.beta, o.G, wm, wn, lane, bad);
+        if (o.nst > 1) {
             wait_all_barrier();
-            store_a(s, m0, 0, BMO + s.taps - 1, ar, sh.a, o.gamma, o.beta, sh, o.G, bad);
-            wait_all_barrier();
-        }
-        while (true) {
-            const Stage s = seg ? o.st[1] : o.st[0];     // (no dynamic index: the stages stay in registers)
-            // next step
-            int nseg = seg, nc0 = c0, ntap = tap + 1;
-            if (ntap == s.taps) {
-                ntap = 0;
-                nc0 = c0 + KS;
-                if (nc0 >= s.cin) {
-                    nc0 = 0;
-                    ++nseg;
-                }
-            }
-            const bool has_next = nseg < o.nst;
-            const bool new_chunk = has_next && ntap == 0;
-            if (has_next) {
-                const Stage ns = nseg ? o.st[1] : o.st[0];
-                issue_w(ns, N, ntap * ns.cin + nc0, lds_w + ((step + 1) & 1) * wstage, wave, lane);
-                if (new_chunk) load_a(ns, m0, nc0, BMO + ns.taps - 1, ar);
-            }
-            // MFMAs of this step: A rows (window row r + tap), W rows of this wave's columns
-            const f16x8* ab = abase + (chunk & 1) * (A_STAGE / 16);
-            const f16x8* wb = wbase + (step & 1) * (wstage / 16);
-            f16x8 a1[NI], a2[NI];
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int w = wm * (BMO / 2) + i * 16 + (lane & 15) + tap;
-                const int slot = w * 4 + ((lane >> 4) ^ swz(w));
-                a1[i] = ab[slot];
-                a2[i] = ab[A_PLANE / 16 + slot];
-            }
-            const int wplane = ((N + 15) / 16) * 1024 / 16;      // f16x8 units per W plane
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int n = wn * (NJ * 16) + j * 16 + (lane & 15);
-                const int slot = n * 4 + ((lane >> 4) ^ swz(n));
-                const f16x8 w1 = wb[slot];
-                const f16x8 w2 = wb[wplane + slot];
-                const f16x8 w1s = w1 * (_Float16)2048.0f;
-#pragma unroll
-                for (int i = 0; i < NI; ++i) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], w1s, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], w2, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[i], w1, acc[i][j], 0, 0, 0);
-                }
-            }
-            if (!has_next) break;
-            if (new_chunk) {                 // the next chunk's window into the other A image
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const Stage ns = nseg ? o.st[1] : o.st[0];
-                store_a(ns, m0, nc0, BMO + ns.taps - 1, ar, sh.a + ((chunk + 1) & 1) * A_STAGE, o.gamma, o.beta, sh, o.G,
-                        bad);
-                ++chunk;
-            }
-            wait_all_barrier();
-            seg = nseg;
-            c0 = nc0;
-            tap = ntap;
-            ++step;
+            kloop<NI, NJ, 1, false>(o.st[1], N, m0, acc, sh, o.gamma, o.beta, o.G, wm, wn, lane, bad);
         }
 
         // ---- epilogue: rows m0 + wm*64 + 16 i + 4 (lane >> 4) + e, column wn*NJ*16 + 16 j + (lane & 15) -----------
@@ -288,7 +312,7 @@ __device__ void run_op(const OpArgs& o, Shared& sh, bool& bad) {
                         if (col >= N) continue;
                         const float v = acc[i][j][e];
                         bad |= !__builtin_isfinite(v);
-                        o.dst[(long long)row * o.ldd + col] = v;
+                        *(GF32w*)(o.dst + (long long)row * o.ldd + col) = v;
                     }
                 }
             // this block's column sums (valid rows): the lane's rows, then the lanes of a column (bits 4, 5), added
@@ -329,7 +353,7 @@ __device__ void run_op(const OpArgs& o, Shared& sh, bool& bad) {
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
                         const int col = col_base + 16 * j;
-                        if (o.res && row < o.rows_out && col < N) acc[i][j][e] += o.res[(long long)row * N + col];
+                        if (o.res && row < o.rows_out && col < N) acc[i][j][e] += *(const GF32*)(o.res + (long long)row * N + col);
                         if (col < N) s += acc[i][j][e];
                     }
                     rs[i][e] = s;
@@ -397,9 +421,10 @@ __device__ void run_op(const OpArgs& o, Shared& sh, bool& bad) {
                     for (int j = 0; j < NJ; ++j) {
                         const int col = col_base + 16 * j;
                         if (col >= N) continue;
-                        const float v = hfa::hardswish((acc[i][j][e] - mean[i][e]) * rstd * o.ln_g[col] + o.ln_b[col]);
+                        const float v = hfa::hardswish((acc[i][j][e] - mean[i][e]) * rstd * *(const GF32*)(o.ln_g + col) +
+                                                      *(const GF32*)(o.ln_b + col));
                         bad |= !__builtin_isfinite(v);
-                        o.dst[(long long)row * o.ldd + col] = v;
+                        *(GF32w*)(o.dst + (long long)row * o.ldd + col) = v;
                     }
                 }
             __syncthreads();                 // sh.red reused by the next block
@@ -415,10 +440,10 @@ __device__ void run_op(const OpArgs& o, Shared& sh, bool& bad) {
                     for (int j = 0; j < NJ; ++j) {
                         const int col = col_base + 16 * j;
                         if (col >= N) continue;
-                        float v = acc[i][j][e] + o.bias[col];
-                        if (o.res) v += o.res[(long long)row * N + col];
+                        float v = acc[i][j][e] + *(const GF32*)(o.bias + col);
+                        if (o.res) v += *(const GF32*)(o.res + (long long)row * N + col);
                         bad |= !__builtin_isfinite(v);
-                        o.dst[(long long)row * o.ldd + col] = v;
+                        *(GF32w*)(o.dst + (long long)row * o.ldd + col) = v;
                     }
                 }
         }
