@@ -258,8 +258,11 @@ struct OpArgs {
 
 // NI x NJ blocks of 16 x 16 per wave: a row block of 32 NI rows (2 row waves) x 64 NJ columns (4 column waves);
 // NI NJ <= 12 keeps the accumulators at 48 VGPRs
+// Not inlined: each (NI, NJ) instance gets its own register allocation (inlined into one kernel body, the union of
+// the four instances' live ranges spilled inside the MFMA loops).  Returns whether a value left f16 range.
 template <int NI, int NJ>
-__device__ void run_op(const OpArgs& o, Shared& sh, bool& bad) {
+__device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh) {
+    bool bad = false;
     constexpr int BMO = 32 * NI;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -467,6 +470,7 @@ __device__ void run_op(const OpArgs& o, Shared& sh, bool& bad) {
         }
     }
     __syncthreads();
+    return bad;
 }
 
 // ---- the kernel: one workgroup per utterance walks the op table ---------------------------------------------------
@@ -484,6 +488,7 @@ struct UnetArgs {
     long long ws_bs;
     int Tmax;
     int* oflow;
+    long long* prof;          // optional (hfa_unet_profile): workgroup 0's s_memrealtime at every op boundary
 };
 
 __device__ __forceinline__ const float* slot_ptr(const UnetArgs& a, float* wsb, int slot, long long off) {
@@ -499,6 +504,7 @@ __global__ __launch_bounds__(NT, 1) void unet_head_kernel(const UnetArgs a) {
     float* wsb = a.ws + b * a.ws_bs;
     bool bad = false;
     for (int k = 0; k < a.nops; ++k) {
+        if (a.prof && b == 0 && threadIdx.x == 0) a.prof[k] = (long long)__builtin_amdgcn_s_memrealtime();
         const hfa_unet_op& u = a.ops[k];
         OpArgs o;
         o.kind = u.kind;
@@ -534,19 +540,27 @@ __global__ __launch_bounds__(NT, 1) void unet_head_kernel(const UnetArgs a) {
             o.dst = wsb + u.dst_off * a.Tmax;
             o.ldd = u.n;
         }
-        if (o.N <= 128) run_op<4, 2>(o, sh, bad);
-        else if (o.N <= 192) run_op<4, 3>(o, sh, bad);
-        else if (o.N <= 256) run_op<2, 4>(o, sh, bad);
-        else run_op<2, 6>(o, sh, bad);
+        if (o.N <= 128) bad |= run_op<4, 2>(o, sh);
+        else if (o.N <= 192) bad |= run_op<4, 3>(o, sh);
+        else if (o.N <= 256) bad |= run_op<2, 4>(o, sh);
+        else bad |= run_op<2, 6>(o, sh);
     }
+    if (a.prof && b == 0 && threadIdx.x == 0) a.prof[a.nops] = (long long)__builtin_amdgcn_s_memrealtime();
     if (bad && a.oflow) *a.oflow = 1;
 }
+
+thread_local long long* g_prof = nullptr;
 
 }  // namespace
 
 extern "C" {
 
 long long hfa_unet_lds_bytes(void) { return (long long)sizeof(Shared); }
+
+int hfa_unet_profile(long long* buf) {
+    g_prof = buf;
+    return HFA_OK;
+}
 
 int hfa_unet_head(int B, int Tmax, const hfa_unet_op* ops, int nops, const float* feats, long long f_bs, int f_ld,
                   float* logits, long long l_bs, int l_ld, const int32_t* t_pad, float* workspace, long long ws_bs,
@@ -558,7 +572,8 @@ int hfa_unet_head(int B, int Tmax, const hfa_unet_op* ops, int nops, const float
         return HFA_EINVAL;
     }
     if (B == 0) return HFA_OK;
-    UnetArgs a{ops, nops, feats, f_bs, f_ld, logits, l_bs, l_ld, t_pad, workspace, ws_bs, Tmax, oflow};
+    UnetArgs a{ops, nops, feats, f_bs, f_ld, logits, l_bs, l_ld, t_pad, workspace, ws_bs, Tmax, oflow, g_prof};
+    g_prof = nullptr;
     hipLaunchKernelGGL(unet_head_kernel, dim3(B), dim3(NT), 0, stream, a);
     return hfa::check_launch("hfa_unet_head");
 }

@@ -239,6 +239,9 @@ int hfa_unet_head(int B, int Tmax, const hfa_unet_op* ops, int nops, const float
                   int* oflow, hipStream_t stream);
 /* LDS bytes the fused kernel's workgroup uses (diagnostics). */
 long long hfa_unet_lds_bytes(void);
+/* Diagnostics: the calling thread's next hfa_unet_head launch writes workgroup 0's s_memrealtime (100 MHz) at the
+ * start of every op and at the end into buf[0 .. nops] (device memory); the hook resets after that launch. */
+int hfa_unet_profile(long long* buf);
 
 /* ---- extractor conv0 (hubertfa_amd/csrc/conv.hip) ------------------------------------------------------------
  * x [B, N] -> y [B, T0, 512] channels-last, T0 = (N-10)/5+1.  norm=1: GroupNorm(512,512) + GELU
