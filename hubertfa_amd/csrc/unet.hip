@@ -145,8 +145,9 @@ __device__ __forceinline__ void store_a(const Stage& s, int m0, int c0, int win,
 }
 
 // W fragments of one step for a wave's NJ column blocks, straight from global (L2) into registers in the 16x16x32
-// operand map: lane l holds row n = column block base + (l & 15), k = k0 + 8 (l >> 4) .. +7, both planes.  Columns
-// past N read row N - 1 (their outputs are never stored).
+// operand map: lane l holds row n = 16 nb + (l & 15), k = k0 + 8 (l >> 4) .. +7, both planes.  The weights are stored
+// in exactly that order (fragment layout, built at load: [plane][k / 32][n / 16][lane][8 halves]), so a fragment is
+// one contiguous 1 KiB load per wave.  Column blocks past the last read the last one (never stored).
 template <int NJ>
 struct WFr {
     f16x8 w1[NJ], w2[NJ];
@@ -154,11 +155,12 @@ struct WFr {
 
 template <int NJ>
 __device__ __forceinline__ void load_wf(const Stage& s, int N, int k0, int wn, int lane, WFr<NJ>& f) {
+    const int NB = (N + 15) >> 4;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-        int n = wn * (NJ * 16) + j * 16 + (lane & 15);
-        n = n < N ? n : N - 1;
-        const _Float16* p = s.w + (long long)n * s.ldw + k0 + 8 * (lane >> 4);
+        int nb = wn * NJ + j;
+        nb = nb < NB ? nb : NB - 1;
+        const _Float16* p = s.w + ((long long)((k0 >> 5) * NB + nb) * 64 + lane) * 8;
         f.w1[j] = *(const GF16x8*)(p);      // global, not flat: a flat load would also count in
         f.w2[j] = *(const GF16x8*)(p + s.wp);   // lgkmcnt and every LDS wait would wait for it
     }

@@ -186,7 +186,9 @@ class FusedPlan:
         def planes(p):
             if p is None:
                 raise ValueError("no split planes")      # |w| >= 16 somewhere, or K % 32
-            return p
+            f = fragment_layout(p)
+            self.keep.append(f)
+            return f
 
         def op(kind, level, n, segs, dst, res=None, bias=None, gn=None, ln=None):
             o = {"kind": kind, "level": level, "n": n, "segs": segs, "dst": dst, "res": res, "bias": bias, "gn": gn,
@@ -233,7 +235,7 @@ class FusedPlan:
                 op(3, lev, 2 * up.cout, [seg("Y", up.cin, up.cin, 1, up.ws)], slot("X", up.cout >> (lev - 1)),
                    res=f"S{lev - 1}", bias=up.b)
         hw = head.head_w
-        self.head_planes = ops_split(hw, c)
+        self.head_planes = fragment_layout(ops_split(hw, c))
         self.keep.append(self.head_planes)
         out_n = hw.shape[0]
         op(4, 0, out_n, [{"src": "Y", "ld": head.decoders[-1][0].cout, "cin": head.decoders[-1][0].cout, "taps": 1,
@@ -253,7 +255,7 @@ class FusedPlan:
                 r.src[s] = -2 if sg["src"] == "INPUT" else 0
                 r.src_off[s] = 0 if sg["src"] == "INPUT" else off[sg["src"]]
                 r.src_ld[s], r.cin[s], r.taps[s], r.gn[s] = sg["ld"], sg["cin"], sg["taps"], int(sg["gn"])
-                r.ldw[s] = sg["w"].shape[-1]
+                r.ldw[s] = sg["taps"] * sg["cin"]
                 r.w[s] = sg["w"].data_ptr()
                 r.wp[s] = sg["w"].stride(0)
             if o["res"] is None:
@@ -292,6 +294,17 @@ class FusedPlan:
             for sg in o["segs"]:
                 f += sum(2.0 * (int(t) >> o["level"]) * o["n"] * sg["taps"] * sg["cin"] for t in t_pad)
         return f
+
+
+def fragment_layout(planes: torch.Tensor) -> torch.Tensor:
+    """[2, N, K] split planes -> the fused kernel's fragment order [2, K/32, ceil(N/16), 64 lanes, 8] (lane = 16 *
+    (k % 32 // 8) + n % 16): one 16 x 32 MFMA operand is one contiguous 1 KiB piece; padded columns are zero."""
+    _, N, K = planes.shape
+    NB = -(-N // 16)
+    p = torch.zeros((2, NB * 16, K), dtype=planes.dtype, device=planes.device)
+    p[:, :N] = planes
+    p = p.view(2, NB, 16, K // 32, 4, 8).permute(0, 3, 1, 4, 2, 5).contiguous()
+    return p.view(2, K // 32, NB, 64, 8)
 
 
 def ops_split(w, ctx):

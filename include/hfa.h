@@ -216,8 +216,10 @@ int hfa_groupnorm_split(int B, int T, int C, int G, const float* x, long long x_
  *   kind 2 down: k2 s2 conv (src rows read as pairs: cin = 2 C, ldw = 2 C) + bias
  *   kind 3 up: ConvTranspose k2 s2 as [T, 2 Cout] = [2T, Cout] (+ bias + skip slot)
  *   kind 4 head: Linear + bias into `logits` (dst = HFA_UNET_OUTPUT)
- * n <= 384, cin % 32 == 0, t_pad[b] a multiple of 2^(max level); *oflow raised for an operand outside f16 range
- * or a non-finite output. */
+ * Weights w[s] are split planes in fragment order: plane p at w + p * wp halves, [K/32][ceil(n/16)][64][8] halves,
+ * element (k, n) at lane (k % 32 / 8) * 16 + n % 16, position k % 8 (one contiguous 1 KiB MFMA operand per 16 columns
+ * x 32 k); ldw[s] = K.  n <= 384, cin % 32 == 0, t_pad[b] a multiple of 2^(max level); *oflow raised for an operand
+ * outside f16 range or a non-finite output. */
 #define HFA_UNET_NONE (-1)
 #define HFA_UNET_INPUT (-2)
 #define HFA_UNET_OUTPUT (-3)
