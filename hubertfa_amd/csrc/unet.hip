@@ -65,12 +65,15 @@ struct Stage {       // one K-segment of an op: A source (f32 rows), taps, weigh
     int ldw;
 };
 
+constexpr int TILE_FLOATS = 128 * (192 + 16);         // the largest C tile: 128 x 192 (NI 4, NJ 3); 64 x 384 fits
+
 struct Shared {
     unsigned char a[LDS_A];
-    float red[2][64][4];          // LayerNorm row partials [row half][row][column wave]
-    double colsum[2][N_MAX][2];   // GroupNorm column partials [row half][column][sum, sum of squares]
+    float tile[TILE_FLOATS];      // the row block's outputs for the row-wise epilogue (row stride 64 NJ + 16 floats);
+                                  // at the end of a first conv: the waves' GroupNorm column partials (f64)
     float gstat[64][2];           // GroupNorm mean, rstd per group
 };
+static_assert(8 * N_MAX * 2 * sizeof(double) <= TILE_FLOATS * sizeof(float), "GroupNorm partials fit the tile");
 
 // ---- staging -------------------------------------------------------------------------------------------------
 // Operand window of one 32-channel chunk for output rows [m0, m0 + rows_blk): source rows m0 - pad .. m0 - pad + win - 1
@@ -272,9 +275,13 @@ __device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh) {
     const int N = o.N;
     const int cg = o.G > 0 ? N / o.G : 1;                  // CONV1: channels per group of its output
 
-    if (o.kind == U_CONV1) {                                // GroupNorm column sums, accumulated block by block
-        for (int i = tid; i < 2 * N_MAX * 2; i += NT) (&sh.colsum[0][0][0])[i] = 0.0;
-    }
+    // CONV1: this wave's GroupNorm column partials (its rows, columns lane + 64 k), f64
+    constexpr int CPL = (NJ * 64 + 63) / 64;                // columns per lane in the row-wise epilogue
+    double gs[CPL], gss[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) gs[k] = gss[k] = 0.0;
+    constexpr int LDT = NJ * 64 + 16;                       // tile row stride (floats): 64 B off a bank row
+    static_assert(BMO * LDT <= TILE_FLOATS, "tile");
     const int nblk = (o.rows_out + BMO - 1) / BMO;
     for (int blk = 0; blk < nblk; ++blk) {
         const int m0 = blk * BMO;
@@ -285,7 +292,7 @@ __device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh) {
             for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
         // K: segment 0 (the op's operand), then the shortcut segment of a block's second conv
-        wait_all_barrier();                // every wave is done reading the previous block's / op's LDS images
+        wait_all_barrier();                // every wave is done with the previous block's LDS images and tile
         if (o.kind == U_CONV1)
             kloop<NI, NJ, 3, false>(o.st[0], N, m0, acc, sh, o.gamma, o.beta, o.G, wm, wn, lane, bad);
         else if (o.kind == U_CONV2)
@@ -297,172 +304,110 @@ __device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh) {
             kloop<NI, NJ, 1, false>(o.st[1], N, m0, acc, sh, o.gamma, o.beta, o.G, wm, wn, lane, bad);
         }
 
-        // ---- epilogue: rows m0 + wm*64 + 16 i + 4 (lane >> 4) + e, column wn*NJ*16 + 16 j + (lane & 15) -----------
+        // ---- epilogue, 1: the accumulators (scaled back by 2^-11) into the tile: row 16 i + 4 (lane >> 4) + e of
+        // the wave's rows, column 16 j + (lane & 15) of its columns
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) acc[i][j] *= 1.0f / 2048.0f;
-        const int col_base = wn * (NJ * 16) + (lane & 15);
-        const int row_base = m0 + wm * (BMO / 2) + 4 * (lane >> 4);
-        if (o.kind == U_CONV1) {
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
+            for (int j = 0; j < NJ; ++j)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int row = row_base + 16 * i + e;
-                    if (row >= o.rows_out) continue;
+                    const int r = wm * (BMO / 2) + 16 * i + 4 * (lane >> 4) + e;
+                    const int c = wn * (NJ * 16) + 16 * j + (lane & 15);
+                    sh.tile[r * LDT + c] = acc[i][j][e] * (1.0f / 2048.0f);
+                }
+        __syncthreads();
+        // ---- 2: row-wise, one wave per row (rows wave, wave + 8, ...): lane handles columns lane + 64 k, so every
+        // global access is one contiguous 256-B row segment and LayerNorm's statistics are wave reductions
+        const int rows_here = o.rows_out - m0 < BMO ? o.rows_out - m0 : BMO;
+        for (int r = wave; r < rows_here; r += 8) {
+            const int row = m0 + r;
+            float v[CPL];
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        const int col = col_base + 16 * j;
-                        if (col >= N) continue;
-                        const float v = acc[i][j][e];
-                        bad |= !__builtin_isfinite(v);
-                        *(GF32w*)(o.dst + (long long)row * o.ldd + col) = v;
+            for (int k = 0; k < CPL; ++k) {
+                const int c = lane + 64 * k;
+                v[k] = c < N ? sh.tile[r * LDT + c] : 0.0f;
+            }
+            if (o.kind == U_CONV1) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const int c = lane + 64 * k;
+                    if (c < N) {
+                        bad |= !__builtin_isfinite(v[k]);
+                        *(GF32w*)(o.dst + (long long)row * o.ldd + c) = v[k];
+                        gs[k] += (double)v[k];
+                        gss[k] += (double)v[k] * (double)v[k];
                     }
                 }
-            // this block's column sums (valid rows): the lane's rows, then the lanes of a column (bits 4, 5), added
-            // to the workgroup's partials in block order (deterministic)
+            } else if (o.kind == U_CONV2) {
+                // + identity residual, LayerNorm over the row's N columns (two-pass, f32) + Hardswish
+                float s = 0.f;
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                double s = 0.0, ss = 0.0;
-#pragma unroll
-                for (int i = 0; i < NI; ++i)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int row = row_base + 16 * i + e;
-                        if (row < o.rows_out) {
-                            const double v = (double)acc[i][j][e];
-                            s += v;
-                            ss += v * v;
-                        }
+                for (int k = 0; k < CPL; ++k) {
+                    const int c = lane + 64 * k;
+                    if (c < N) {
+                        if (o.res) v[k] += *(const GF32*)(o.res + (long long)row * N + c);
+                        s += v[k];
                     }
-                s += __shfl_xor(s, 16, 64);
-                ss += __shfl_xor(ss, 16, 64);
-                s += __shfl_xor(s, 32, 64);
-                ss += __shfl_xor(ss, 32, 64);
-                const int col = col_base + 16 * j;
-                if (lane < 16 && col < N) {
-                    sh.colsum[wm][col][0] += s;
-                    sh.colsum[wm][col][1] += ss;
+                }
+                const float mean = hfa::wave_sum(s) / (float)N;
+                float ss = 0.f;
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const int c = lane + 64 * k;
+                    if (c < N) {
+                        const float d = v[k] - mean;
+                        ss += d * d;
+                    }
+                }
+                const float rstd = 1.0f / sqrtf(hfa::wave_sum(ss) / (float)N + 1e-5f);
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const int c = lane + 64 * k;
+                    if (c < N) {
+                        const float y = hfa::hardswish((v[k] - mean) * rstd * *(const GF32*)(o.ln_g + c) +
+                                                       *(const GF32*)(o.ln_b + c));
+                        bad |= !__builtin_isfinite(y);
+                        *(GF32w*)(o.dst + (long long)row * o.ldd + c) = y;
+                    }
+                }
+            } else {
+                // DOWN / HEAD: + bias; UP: + bias + skip (its [T, N] rows are bit-for-bit the [2T, N/2] rows)
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const int c = lane + 64 * k;
+                    if (c < N) {
+                        float y = v[k] + *(const GF32*)(o.bias + c);
+                        if (o.res) y += *(const GF32*)(o.res + (long long)row * N + c);
+                        bad |= !__builtin_isfinite(y);
+                        *(GF32w*)(o.dst + (long long)row * o.ldd + c) = y;
+                    }
                 }
             }
-        } else if (o.kind == U_CONV2) {
-            // + identity residual, then LayerNorm over the row's N columns (4 column waves) + Hardswish
-            float rs[NI][4];
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int row = row_base + 16 * i + e;
-                    float s = 0.f;
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        const int col = col_base + 16 * j;
-                        if (o.res && row < o.rows_out && col < N) acc[i][j][e] += *(const GF32*)(o.res + (long long)row * N + col);
-                        if (col < N) s += acc[i][j][e];
-                    }
-                    rs[i][e] = s;
-                }
-            // row sums: over the 16 lanes of a row group, then over the 4 column waves through LDS
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float s = rs[i][e];
-                    s += __shfl_xor(s, 1, 64);
-                    s += __shfl_xor(s, 2, 64);
-                    s += __shfl_xor(s, 4, 64);
-                    s += __shfl_xor(s, 8, 64);
-                    rs[i][e] = s;
-                }
-            if ((lane & 15) == 0) {
-#pragma unroll
-                for (int i = 0; i < NI; ++i)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) sh.red[wm][16 * i + 4 * (lane >> 4) + e][wn] = rs[i][e];
-            }
-            __syncthreads();
-            float (&mean)[NI][4] = rs;       // the row means replace the partial sums
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int r = 16 * i + 4 * (lane >> 4) + e;
-                    mean[i][e] = ((sh.red[wm][r][0] + sh.red[wm][r][1]) + (sh.red[wm][r][2] + sh.red[wm][r][3])) /
-                                 (float)N;
-                }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        const int col = col_base + 16 * j;
-                        if (col < N) {
-                            const float d = acc[i][j][e] - mean[i][e];
-                            s += d * d;
-                        }
-                    }
-                    s += __shfl_xor(s, 1, 64);
-                    s += __shfl_xor(s, 2, 64);
-                    s += __shfl_xor(s, 4, 64);
-                    s += __shfl_xor(s, 8, 64);
-                    if ((lane & 15) == 0) sh.red[wm][16 * i + 4 * (lane >> 4) + e][wn] = s;
-                }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int r = 16 * i + 4 * (lane >> 4) + e;
-                    const int row = row_base + 16 * i + e;
-                    const float var = ((sh.red[wm][r][0] + sh.red[wm][r][1]) + (sh.red[wm][r][2] + sh.red[wm][r][3])) /
-                                      (float)N;
-                    const float rstd = 1.0f / sqrtf(var + 1e-5f);
-                    if (row >= o.rows_out) continue;
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        const int col = col_base + 16 * j;
-                        if (col >= N) continue;
-                        const float v = hfa::hardswish((acc[i][j][e] - mean[i][e]) * rstd * *(const GF32*)(o.ln_g + col) +
-                                                      *(const GF32*)(o.ln_b + col));
-                        bad |= !__builtin_isfinite(v);
-                        *(GF32w*)(o.dst + (long long)row * o.ldd + col) = v;
-                    }
-                }
-            __syncthreads();                 // sh.red reused by the next block
-        } else {
-            // DOWN / HEAD: + bias; UP: + bias + skip (output [T, N] is bit-for-bit the [2T, N/2] rows)
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int row = row_base + 16 * i + e;
-                    if (row >= o.rows_out) continue;
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        const int col = col_base + 16 * j;
-                        if (col >= N) continue;
-                        float v = acc[i][j][e] + *(const GF32*)(o.bias + col);
-                        if (o.res) v += *(const GF32*)(o.res + (long long)row * N + col);
-                        bad |= !__builtin_isfinite(v);
-                        *(GF32w*)(o.dst + (long long)row * o.ldd + col) = v;
-                    }
-                }
         }
     }
 
     if (o.kind == U_CONV1) {
-        // GroupNorm statistics over the utterance: the two row halves and the group's columns in a fixed order
+        // GroupNorm statistics over the utterance: every wave's column partials into the tile space, then per group
+        // the waves and the group's columns in a fixed order (deterministic)
+        __syncthreads();
+        double* part = reinterpret_cast<double*>(sh.tile);         // [8 waves][N][2]
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            const int c = lane + 64 * k;
+            if (c < N) {
+                part[(wave * N + c) * 2] = gs[k];
+                part[(wave * N + c) * 2 + 1] = gss[k];
+            }
+        }
         __syncthreads();
         if (tid < o.G) {
             double S = 0.0, SS = 0.0;
-            for (int c = tid * cg; c < (tid + 1) * cg; ++c) {
-                S += sh.colsum[0][c][0] + sh.colsum[1][c][0];
-                SS += sh.colsum[0][c][1] + sh.colsum[1][c][1];
-            }
+            for (int c = tid * cg; c < (tid + 1) * cg; ++c)
+                for (int w = 0; w < 8; ++w) {
+                    S += part[(w * N + c) * 2];
+                    SS += part[(w * N + c) * 2 + 1];
+                }
             const double n = (double)o.rows_out * cg;
             const double mean_d = o.rows_out > 0 ? S / n : 0.0;
             double var_d = o.rows_out > 0 ? SS / n - mean_d * mean_d : 0.0;
