@@ -42,6 +42,7 @@ typedef const __attribute__((address_space(1))) f16x8 GF16x8;
 typedef const __attribute__((address_space(1))) f32x4 GF32x4;
 typedef const __attribute__((address_space(1))) float GF32;
 typedef __attribute__((address_space(1))) float GF32w;
+typedef __attribute__((address_space(1))) f32x4 GF32x4w;
 
 constexpr int NT = 512, BM = 128, KS = 32;
 constexpr int WIN_MAX = BM + 2;                          // k3 conv window rows
@@ -275,13 +276,26 @@ __device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh) {
     const int N = o.N;
     const int cg = o.G > 0 ? N / o.G : 1;                  // CONV1: channels per group of its output
 
-    // CONV1: this wave's GroupNorm column partials (its rows, columns lane + 64 k), f64
-    constexpr int CPL = (NJ * 64 + 63) / 64;                // columns per lane in the row-wise epilogue
-    double gs[CPL], gss[CPL];
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) gs[k] = gss[k] = 0.0;
+    // Row-wise epilogue geometry: a lane owns the float4 columns 4 lane + 256 k (k < C4; N % 4 == 0)
+    constexpr int C4 = (NJ * 64 + 255) / 256;
     constexpr int LDT = NJ * 64 + 16;                       // tile row stride (floats): 64 B off a bank row
     static_assert(BMO * LDT <= TILE_FLOATS, "tile");
+    // per-column parameters, loaded once per op
+    f32x4 pb[C4], pg[C4], pbt[C4];
+#pragma unroll
+    for (int k = 0; k < C4; ++k) {
+        const int c = 4 * lane + 256 * k;
+        const int cc = c < N ? c : 0;                           // (branch-free: a valid address, value unused)
+        pb[k] = o.bias ? *(const GF32x4*)(o.bias + cc) : f32x4{0.f, 0.f, 0.f, 0.f};
+        pg[k] = o.ln_g ? *(const GF32x4*)(o.ln_g + cc) : f32x4{0.f, 0.f, 0.f, 0.f};
+        pbt[k] = o.ln_b ? *(const GF32x4*)(o.ln_b + cc) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // CONV1: this wave's GroupNorm column partials (its rows, its lane's columns), f64
+    double gs[C4][4], gss[C4][4];
+#pragma unroll
+    for (int k = 0; k < C4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gs[k][e] = gss[k][e] = 0.0;
     const int nblk = (o.rows_out + BMO - 1) / BMO;
     for (int blk = 0; blk < nblk; ++blk) {
         const int m0 = blk * BMO;
@@ -317,70 +331,93 @@ __device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh) {
                     sh.tile[r * LDT + c] = acc[i][j][e] * (1.0f / 2048.0f);
                 }
         __syncthreads();
-        // ---- 2: row-wise, one wave per row (rows wave, wave + 8, ...): lane handles columns lane + 64 k, so every
-        // global access is one contiguous 256-B row segment and LayerNorm's statistics are wave reductions
+        // ---- 2: row-wise, one wave per row (rows wave, wave + 8, ...), two rows at a time: a lane handles the
+        // float4 columns 4 lane + 256 k, so every global access is a contiguous row segment of 16-B pieces, the
+        // residual loads of both rows are in flight together, and LayerNorm's statistics are wave reductions
         const int rows_here = o.rows_out - m0 < BMO ? o.rows_out - m0 : BMO;
-        for (int r = wave; r < rows_here; r += 8) {
-            const int row = m0 + r;
-            float v[CPL];
+        for (int r0 = wave; r0 < rows_here; r0 += 16) {
+            f32x4 v[2][C4], rr[2][C4];
 #pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-                const int c = lane + 64 * k;
-                v[k] = c < N ? sh.tile[r * LDT + c] : 0.0f;
+            for (int h = 0; h < 2; ++h) {
+                const int r = r0 + 8 * h;
+                const int rc = r < rows_here ? r : r0;             // (the second row may not exist: reread the first)
+#pragma unroll
+                for (int k = 0; k < C4; ++k) {
+                    const int c = 4 * lane + 256 * k;
+                    const int cc = c < N ? c : 0;
+                    v[h][k] = *reinterpret_cast<const f32x4*>(&sh.tile[rc * LDT + cc]);
+                    rr[h][k] = o.res ? *(const GF32x4*)(o.res + (long long)(m0 + rc) * N + cc)
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
             }
-            if (o.kind == U_CONV1) {
 #pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const int c = lane + 64 * k;
-                    if (c < N) {
-                        bad |= !__builtin_isfinite(v[k]);
-                        *(GF32w*)(o.dst + (long long)row * o.ldd + c) = v[k];
-                        gs[k] += (double)v[k];
-                        gss[k] += (double)v[k] * (double)v[k];
+            for (int h = 0; h < 2; ++h) {
+                const int r = r0 + 8 * h;
+                if (r >= rows_here) break;                         // (wave-uniform)
+                const int row = m0 + r;
+                if (o.kind == U_CONV1) {
+#pragma unroll
+                    for (int k = 0; k < C4; ++k) {
+                        const int c = 4 * lane + 256 * k;
+                        if (c < N) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                bad |= !__builtin_isfinite(v[h][k][e]);
+                                gs[k][e] += (double)v[h][k][e];
+                                gss[k][e] += (double)v[h][k][e] * (double)v[h][k][e];
+                            }
+                            *(GF32x4w*)(o.dst + (long long)row * o.ldd + c) = v[h][k];
+                        }
                     }
-                }
-            } else if (o.kind == U_CONV2) {
-                // + identity residual, LayerNorm over the row's N columns (two-pass, f32) + Hardswish
-                float s = 0.f;
+                } else if (o.kind == U_CONV2) {
+                    // + identity residual, LayerNorm over the row's N columns (two-pass, f32) + Hardswish
+                    float s = 0.f;
 #pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const int c = lane + 64 * k;
-                    if (c < N) {
-                        if (o.res) v[k] += *(const GF32*)(o.res + (long long)row * N + c);
-                        s += v[k];
+                    for (int k = 0; k < C4; ++k) {
+                        const int c = 4 * lane + 256 * k;
+                        if (c < N) {
+                            v[h][k] += rr[h][k];
+                            s += (v[h][k][0] + v[h][k][1]) + (v[h][k][2] + v[h][k][3]);
+                        }
                     }
-                }
-                const float mean = hfa::wave_sum(s) / (float)N;
-                float ss = 0.f;
+                    const float mean = hfa::wave_sum(s) / (float)N;
+                    float ss = 0.f;
 #pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const int c = lane + 64 * k;
-                    if (c < N) {
-                        const float d = v[k] - mean;
-                        ss += d * d;
+                    for (int k = 0; k < C4; ++k) {
+                        const int c = 4 * lane + 256 * k;
+                        if (c < N) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const float d = v[h][k][e] - mean;
+                                ss += d * d;
+                            }
+                        }
                     }
-                }
-                const float rstd = 1.0f / sqrtf(hfa::wave_sum(ss) / (float)N + 1e-5f);
+                    const float rstd = 1.0f / sqrtf(hfa::wave_sum(ss) / (float)N + 1e-5f);
 #pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const int c = lane + 64 * k;
-                    if (c < N) {
-                        const float y = hfa::hardswish((v[k] - mean) * rstd * *(const GF32*)(o.ln_g + c) +
-                                                       *(const GF32*)(o.ln_b + c));
-                        bad |= !__builtin_isfinite(y);
-                        *(GF32w*)(o.dst + (long long)row * o.ldd + c) = y;
+                    for (int k = 0; k < C4; ++k) {
+                        const int c = 4 * lane + 256 * k;
+                        if (c < N) {
+                            f32x4 y;
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                y[e] = hfa::hardswish((v[h][k][e] - mean) * rstd * pg[k][e] + pbt[k][e]);
+                                bad |= !__builtin_isfinite(y[e]);
+                            }
+                            *(GF32x4w*)(o.dst + (long long)row * o.ldd + c) = y;
+                        }
                     }
-                }
-            } else {
-                // DOWN / HEAD: + bias; UP: + bias + skip (its [T, N] rows are bit-for-bit the [2T, N/2] rows)
+                } else {
+                    // DOWN / HEAD: + bias; UP: + bias + skip (its [T, N] rows are bit-for-bit the [2T, N/2] rows)
 #pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const int c = lane + 64 * k;
-                    if (c < N) {
-                        float y = v[k] + *(const GF32*)(o.bias + c);
-                        if (o.res) y += *(const GF32*)(o.res + (long long)row * N + c);
-                        bad |= !__builtin_isfinite(y);
-                        *(GF32w*)(o.dst + (long long)row * o.ldd + c) = y;
+                    for (int k = 0; k < C4; ++k) {
+                        const int c = 4 * lane + 256 * k;
+                        if (c < N) {
+                            f32x4 y = v[h][k] + pb[k] + rr[h][k];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) bad |= !__builtin_isfinite(y[e]);
+                            *(GF32x4w*)(o.dst + (long long)row * o.ldd + c) = y;
+                        }
                     }
                 }
             }
@@ -393,13 +430,15 @@ __device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh) {
         __syncthreads();
         double* part = reinterpret_cast<double*>(sh.tile);         // [8 waves][N][2]
 #pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-            const int c = lane + 64 * k;
-            if (c < N) {
-                part[(wave * N + c) * 2] = gs[k];
-                part[(wave * N + c) * 2 + 1] = gss[k];
+        for (int k = 0; k < C4; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int c = 4 * lane + 256 * k + e;
+                if (c < N) {
+                    part[(wave * N + c) * 2] = gs[k][e];
+                    part[(wave * N + c) * 2 + 1] = gss[k][e];
+                }
             }
-        }
         __syncthreads();
         if (tid < o.G) {
             double S = 0.0, SS = 0.0;
@@ -513,7 +552,8 @@ int hfa_unet_head(int B, int Tmax, const hfa_unet_op* ops, int nops, const float
                   float* logits, long long l_bs, int l_ld, const int32_t* t_pad, float* workspace, long long ws_bs,
                   int* oflow, hipStream_t stream) {
     if (B < 0 || Tmax < 0 || nops < 1 || nops > 256 || !ops || !feats || !logits || !t_pad || !workspace ||
-        f_ld % 4 || l_ld < 1 || ws_bs < 0 || (reinterpret_cast<uintptr_t>(feats) & 15) || (f_bs % 4)) {
+        f_ld % 4 || l_ld < 1 || l_ld % 4 || l_bs % 4 || ws_bs < 0 || ws_bs % 4 || (reinterpret_cast<uintptr_t>(feats) & 15) ||
+        (reinterpret_cast<uintptr_t>(logits) & 15) || (reinterpret_cast<uintptr_t>(workspace) & 15) || (f_bs % 4)) {
         hfa::set_error("hfa_unet_head: bad arguments (B=%d Tmax=%d nops=%d f_ld=%d l_ld=%d)", B, Tmax, nops, f_ld,
                        l_ld);
         return HFA_EINVAL;

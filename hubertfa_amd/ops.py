@@ -306,8 +306,8 @@ def unet_head(table, nops, feats, logits, t_pad, workspace, ws_floats, flag, flo
     _need(feats, torch.float32, "feats", contiguous=False)
     _need(logits, torch.float32, "logits", contiguous=False)
     _need(t_pad, torch.int32, "t_pad")
-    if feats.stride(2) != 1 or logits.stride(2) != 1:
-        raise ValueError("unet_head: rows must be contiguous")
+    if feats.stride(2) != 1 or logits.stride(2) != 1 or logits.stride(1) % 4 or logits.data_ptr() % 16:
+        raise ValueError("unet_head: contiguous rows, logits rows 16-B aligned")
 
     def launch():
         _lib.call("hfa_unet_head", B, Tmax, _ptr(table), nops, _ptr(feats), feats.stride(0), feats.stride(1),

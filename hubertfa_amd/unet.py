@@ -238,9 +238,12 @@ class FusedPlan:
         self.head_planes = fragment_layout(ops_split(hw, c))
         self.keep.append(self.head_planes)
         out_n = hw.shape[0]
-        op(4, 0, out_n, [{"src": "Y", "ld": head.decoders[-1][0].cout, "cin": head.decoders[-1][0].cout, "taps": 1,
-                          "w": self.head_planes, "gn": False}], "OUTPUT", bias=head.head_b)
-        if any(o["n"] > 384 for o in ops) or any(sg["cin"] % 32 for o in ops for sg in o["segs"]):
+        self.out_ld = -(-out_n // 4) * 4          # the row-wise epilogue moves float4s: head rows padded to 4
+        self.head_bias = torch.zeros(self.out_ld, dtype=torch.float32, device=c.dev)
+        self.head_bias[:out_n] = head.head_b
+        op(4, 0, self.out_ld, [{"src": "Y", "ld": head.decoders[-1][0].cout, "cin": head.decoders[-1][0].cout,
+                                "taps": 1, "w": self.head_planes, "gn": False}], "OUTPUT", bias=self.head_bias)
+        if any(o["n"] > 384 or o["n"] % 4 for o in ops) or any(sg["cin"] % 32 for o in ops for sg in o["segs"]):
             raise ValueError("outputs > 384 columns")
         # slot offsets (floats per Tmax row)
         off, self.ws_floats_per_row = {}, 0
@@ -281,12 +284,12 @@ class FusedPlan:
         """x [B, Tmax, C_in] (rows >= t_pad[b] zero) -> logits [B, Tmax, V+2] (rows >= t_pad[b] not written)."""
         from .hubert import dev_lengths
         B, Tmax, _ = x.shape
-        logits = torch.empty((B, Tmax, self.out_n), dtype=torch.float32, device=x.device)
+        logits = torch.empty((B, Tmax, self.out_ld), dtype=torch.float32, device=x.device)
         ws = torch.empty((B, Tmax * self.ws_floats_per_row), dtype=torch.float32, device=x.device)
         tp = dev_lengths(t_pad, x.device)
         ops.unet_head(self.table, self.nops, x, logits, tp, ws, Tmax * self.ws_floats_per_row, flag,
                       flops=self.flops(t_pad))
-        return logits
+        return logits[:, :, :self.out_n]
 
     def flops(self, t_pad) -> float:
         f = 0.0

@@ -218,8 +218,9 @@ int hfa_groupnorm_split(int B, int T, int C, int G, const float* x, long long x_
  *   kind 4 head: Linear + bias into `logits` (dst = HFA_UNET_OUTPUT)
  * Weights w[s] are split planes in fragment order: plane p at w + p * wp halves, [K/32][ceil(n/16)][64][8] halves,
  * element (k, n) at lane (k % 32 / 8) * 16 + n % 16, position k % 8 (one contiguous 1 KiB MFMA operand per 16 columns
- * x 32 k); ldw[s] = K.  n <= 384, cin % 32 == 0, t_pad[b] a multiple of 2^(max level); *oflow raised for an operand
- * outside f16 range or a non-finite output. */
+ * x 32 k); ldw[s] = K.  n <= 384 and n % 4 == 0 (rows move as float4s: feats, logits and workspace 16-B aligned,
+ * l_ld % 4 == 0), cin % 32 == 0, t_pad[b] a multiple of 2^(max level); *oflow raised for an operand outside f16
+ * range or a non-finite output. */
 #define HFA_UNET_NONE (-1)
 #define HFA_UNET_INPUT (-2)
 #define HFA_UNET_OUTPUT (-3)
