@@ -186,10 +186,31 @@ def step_breakdown(task, wav, ph_seqs, word_seqs, p2ws, k, step_s):
         return (time.perf_counter() - t0) / k * 1e3
     enc_ms = clock(lambda: task.encode_batch(wav, 16000))
     head_ms = clock(lambda: task.decoder.fetch(task.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)))
+    # the side stream's two parts, each overlapped alone with the encoder as in task.submit
+    side = torch.cuda.Stream()
+    logits = task.head.logits(feats)[:, :n_frames]
+    frame, edge = logits[:, :, 2:], logits[:, :, 0]
+
+    def piped(side_work):
+        def run():
+            f2, _, _ = task.encode_batch(wav, 16000)
+            ev = torch.cuda.Event()
+            ev.record()
+            with torch.cuda.stream(side):
+                side.wait_event(ev)
+                side_work(f2)
+        return run
+    unet_piped = clock(piped(lambda f2: task.head.logits(f2)))
+    dp_piped = clock(piped(lambda f2: task.decoder.fetch(task.decoder.decode_batch(frame, edge, wl, ph_seqs, word_seqs,
+                                                                                      p2ws, host=False))))
+    torch.cuda.synchronize()
     return {"pipelined_step_ms": step_s * 1e3, "encoder_only_ms": enc_ms, "head_dp_only_ms": head_ms,
-            "side_stream_cost_ms": step_s * 1e3 - enc_ms,
+            "side_stream_cost_ms": step_s * 1e3 - enc_ms, "encoder_plus_unet_ms": unet_piped,
+            "encoder_plus_lattice_dp_ms": dp_piped,
             "note": "encoder_only / head_dp_only: the step's two halves run alone, serially, k steps each; "
-                    "side_stream_cost = pipelined step - encoder alone (what overlapping the head costs the encoder)"}
+                    "side_stream_cost = pipelined step - encoder alone (what overlapping the head costs the encoder); "
+                    "encoder_plus_unet / encoder_plus_lattice_dp: the encoder with only that part of the side stream "
+                    "beside it"}
 
 
 def config3_batch(args, world: int) -> int:
