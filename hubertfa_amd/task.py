@@ -151,19 +151,31 @@ class ForcedAlignmentTask:
         wl = [n / sr] * waves.shape[0] if lengths is None else [int(m) / sr for m in lengths]
         return feats, n_frames, wl
 
-    def decode_device(self, feats, n_frames, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
-        """Device half 2 (current stream): UNet head + lattice + Viterbi -> the decoder's device outputs."""
+    def head_logits(self, feats, n_frames):
+        """UNet head (current stream): features -> (logits [B, T, V+2], the head's range-flag snapshot or None)."""
         if isinstance(n_frames, (list, tuple)):          # variable-length batch
             t_pad = [self.head.padded_len(int(t)) for t in n_frames]
             logits = self.head.logits(feats, t_pad)[:, :max(n_frames)]
         else:
             logits = self.head.logits(feats)[:, :n_frames]
+        flag = None
+        if self.head.precision == "split":      # the head's own range flag, snapshot on the stream that ran it
+            flag = self.head.flag.clone()
+            self.head.flag.zero_()
+        return logits, flag
+
+    def lattice_dp(self, logits, flag, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
+        """Lattice prologue + Viterbi + backtrack (current stream) -> the decoder's device outputs."""
         frame, edge = logits[:, :, 2:], logits[:, :, 0]      # LatticeHead.split without the unused ctc logits
         dev_out = self.decoder.decode_batch(frame, edge, wav_lengths, ph_seqs, word_seqs, p2ws, host=False)
-        if self.head.precision == "split":      # the head's own range flag, snapshot on the stream that ran it
-            dev_out["split_oflow_head"] = self.head.flag.clone()
-            self.head.flag.zero_()
+        if flag is not None:
+            dev_out["split_oflow_head"] = flag
         return dev_out
+
+    def decode_device(self, feats, n_frames, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
+        """Device half 2 (current stream): UNet head + lattice + Viterbi -> the decoder's device outputs."""
+        logits, flag = self.head_logits(feats, n_frames)
+        return self.lattice_dp(logits, flag, wav_lengths, ph_seqs, word_seqs, p2ws)
 
     def _guard(self, dev_out, redo_args):
         """Split-precision range guard: snapshot (and clear) the split-f16 overflow flag the batch's producers
@@ -216,6 +228,8 @@ class ForcedAlignmentTask:
         pinned = x if x.is_pinned() else x.contiguous().pin_memory()
         return pinned.to(self.device, non_blocking=True)   # (the pinned block is held until this copy ends)
 
+    head_on_main = __import__("os").environ.get("HFA_HEAD_ON_MAIN", "0") == "1"     # (A/B switch)
+
     def submit(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
                on_device=None, lengths=None, chunk_seconds: float | None = None):
         """Two-stream pipelined device pass; returns the decoder's fetch handle (``decoder.assemble`` completes it).
@@ -228,13 +242,21 @@ class ForcedAlignmentTask:
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
         feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds)
+        if self.head_on_main:                    # the UNet head right behind the encoder, only the DP beside it
+            logits, hflag = self.head_logits(feats, n_frames)
         guard = self._guard({}, (waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds))
         ready = torch.cuda.Event()
         ready.record(main)
         with torch.cuda.stream(self._side):
             self._side.wait_event(ready)
-            feats.record_stream(self._side)      # the caching allocator must not recycle it under the side stream
-            dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
+            if self.head_on_main:
+                logits.record_stream(self._side)
+                if hflag is not None:
+                    hflag.record_stream(self._side)
+                dev_out = self.lattice_dp(logits, hflag, wl, ph_seqs, word_seqs, p2ws)
+            else:
+                feats.record_stream(self._side)  # the caching allocator must not recycle it under the side stream
+                dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
             if "split_oflow" in guard:
                 guard["split_oflow"].record_stream(self._side)
             dev_out.update(guard)

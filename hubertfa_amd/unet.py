@@ -432,7 +432,7 @@ class LatticeHead:
                 return out
         return self._chipwide(x, t_pad)
 
-    use_fused = __import__("os").environ.get("HFA_UNET_FUSED", "1") != "0"   # (A/B switch: 0 = chip-wide launches)
+    use_fused = __import__("os").environ.get("HFA_UNET_FUSED", "0") == "1"   # (A/B switch: 1 = the fused kernel)
 
     def _chipwide(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
         hs = self.ctx.use_split(self.head_ws)
