@@ -343,7 +343,14 @@ class LatticeHead:
         self.decoders.append([_Block(sd, f"decoders.{arch.times - 1}.", dev, c)])
         self.head_w = _t(sd["head.weight"]).float().contiguous().to(dev)
         self.head_b = _t(sd["head.bias"]).float().contiguous().to(dev)
-        self.head_ws = c.planes(self.head_w) if self.head_w.shape[0] % 4 == 0 else None   # f32 C rows: 16-B
+        # split path: the head's rows padded with zeros to a multiple of 4 (the split GEMM's f32 C rows are 16-B
+        # aligned); its logits are the leading V+2 columns of the padded output (a strided view)
+        n, n4 = self.head_w.shape[0], -(-self.head_w.shape[0] // 4) * 4
+        self.head_wp = torch.zeros((n4, self.head_w.shape[1]), dtype=torch.float32, device=dev)
+        self.head_wp[:n] = self.head_w
+        self.head_bp = torch.zeros(n4, dtype=torch.float32, device=dev)
+        self.head_bp[:n] = self.head_b
+        self.head_ws = c.planes(self.head_wp)
         self.vocab_size = self.head_w.shape[0] - 2
 
     @property
@@ -435,9 +442,10 @@ class LatticeHead:
     use_fused = __import__("os").environ.get("HFA_UNET_FUSED", "0") == "1"   # (A/B switch: 1 = the fused kernel)
 
     def _chipwide(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
-        hs = self.ctx.use_split(self.head_ws)
-        y, ys = self.backbone(x, t_pad, want_split=True) if hs else (self.backbone(x, t_pad), None)
-        return self.ctx.linear(y, ys, self.head_w, self.head_ws, self.head_b)[0]
+        if self.ctx.use_split(self.head_ws):
+            y, ys = self.backbone(x, t_pad, want_split=True)
+            return self.ctx.linear(y, ys, self.head_wp, self.head_ws, self.head_bp)[0][:, :, :self.head_w.shape[0]]
+        return self.ctx.linear(self.backbone(x, t_pad), None, self.head_w, None, self.head_b)[0]
 
     @staticmethod
     def split(logits: torch.Tensor):
