@@ -79,7 +79,7 @@ def parse():
     ap.add_argument("--host-input", action="store_true",
                     help="waves start in host memory and are uploaded inside every step (task.upload, as infer.py) (PCIe-inclusive "
                          "rate; the headline value keeps inputs resident in HBM)")
-    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r02", "traffic_r02.json"),
+    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r03", "traffic_r03.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
 

@@ -486,7 +486,7 @@ __global__ __launch_bounds__(NT, 1) void unet_head_kernel(const UnetArgs a) {
     __shared__ Shared sh;
     const int b = blockIdx.x;
     const int T0 = a.t_pad[b];
-    if (T0 <= 0) return;
+    if (T0 <= 0 || T0 > a.Tmax) return;
     float* wsb = a.ws + b * a.ws_bs;
     bool bad = false;
     for (int k = 0; k < a.nops; ++k) {
@@ -542,6 +542,54 @@ thread_local long long* g_prof = nullptr;
 extern "C" {
 
 long long hfa_unet_lds_bytes(void) { return (long long)sizeof(Shared); }
+
+int hfa_unet_validate(const hfa_unet_op* ops, int nops, long long wpr, int l_ld) {
+    if (!ops || nops < 1 || nops > 256 || wpr < 0) {
+        hfa::set_error("hfa_unet_validate: bad table (nops=%d)", nops);
+        return HFA_EINVAL;
+    }
+    // floats per Tmax row a level-`lv` tensor of row width `ld` at slot offset `off` reaches
+    auto inside = [&](long long off, int ld, int lv) { return off >= 0 && off + ((long long)ld + (1LL << lv) - 1) / (1LL << lv) <= wpr; };
+    for (int k = 0; k < nops; ++k) {
+        const hfa_unet_op& u = ops[k];
+        const char* why = nullptr;
+        const bool head = u.kind == U_HEAD;
+        if (u.kind < U_CONV1 || u.kind > U_HEAD) why = "kind";
+        else if (u.level < 0 || u.level > 12) why = "level";
+        else if (u.n < 4 || u.n > 384 || u.n % 4) why = "n (4..384, a multiple of 4)";
+        else if (u.nseg < 1 || u.nseg > (u.kind == U_CONV2 ? 2 : 1)) why = "nseg";
+        else if (u.kind == U_CONV1 && (u.groups < 1 || u.n % u.groups)) why = "groups";
+        else if (u.kind == U_CONV2 && (!u.gn_gamma || !u.gn_beta || !u.ln_gamma || !u.ln_beta)) why = "norm parameters";
+        else if (u.kind == U_CONV2 && (k == 0 || ops[k - 1].kind != U_CONV1 || ops[k - 1].n != u.cin[0] ||
+                                       !u.gn[0] || u.groups != ops[k - 1].groups))
+            why = "conv2 without its conv1 (GroupNorm statistics)";
+        else if (head != (u.dst == HFA_UNET_OUTPUT)) why = "dst (HFA_UNET_OUTPUT is the head's only)";
+        else if (head && u.n > l_ld) why = "head n > l_ld";
+        else if (!head && (u.dst < 0 || !inside(u.dst_off, u.n, u.level))) why = "dst slot outside the workspace";
+        else if (u.res != HFA_UNET_NONE && u.res != HFA_UNET_INPUT &&
+                 (u.res < 0 || !inside(u.res_off, u.n, u.level)))
+            why = "res slot outside the workspace";
+        for (int s = 0; s < u.nseg && !why; ++s) {
+            if (u.cin[s] < 32 || u.cin[s] % 32) why = "cin (a multiple of 32)";
+            else if (u.taps[s] != 1 && u.taps[s] != 3) why = "taps (1 or 3)";
+            else if (u.ldw[s] != u.taps[s] * u.cin[s]) why = "ldw != taps * cin";
+            else if (!u.w[s] || (reinterpret_cast<uintptr_t>(u.w[s]) & 15) || u.wp[s] % 8 ||
+                     u.wp[s] < (long long)u.ldw[s] / 32 * ((u.n + 15) / 16) * 512)
+                why = "weight planes";
+            else if (u.gn[s] && (s != 0 || u.kind != U_CONV2)) why = "gn outside conv2's first segment";
+            else if (u.src[s] == HFA_UNET_INPUT) {
+                if (u.level != 0) why = "INPUT read off level 0";
+            } else if (u.src[s] < 0 || u.src_ld[s] < u.cin[s] || u.src_ld[s] % 4 ||
+                       !inside(u.src_off[s], u.src_ld[s], u.level))
+                why = "src slot outside the workspace";
+        }
+        if (why) {
+            hfa::set_error("hfa_unet_validate: op %d: %s", k, why);
+            return HFA_EINVAL;
+        }
+    }
+    return HFA_OK;
+}
 
 int hfa_unet_profile(long long* buf) {
     g_prof = buf;

@@ -295,7 +295,14 @@ class UnetOp(ctypes.Structure):
 UNET_NONE, UNET_INPUT, UNET_OUTPUT = -1, -2, -3
 _lib.register("hfa_unet_head", [_I_, _I_, _P_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_, _P_, _P_])
 _lib.register("hfa_unet_lds_bytes", [], restype=ctypes.c_longlong)
+_lib.register("hfa_unet_validate", [_P_, _I_, _LL_, _I_])
 _lib.register("hfa_unet_profile", [_P_])
+
+
+def unet_validate(table, ws_floats_per_row: int, l_ld: int):
+    """Check a host op table (a ctypes array of UnetOp) before it is uploaded: ValueError (HFAArgumentError) naming
+    the first bad op."""
+    _lib.call("hfa_unet_validate", ctypes.addressof(table), len(table), ws_floats_per_row, l_ld)
 
 
 def unet_head(table, nops, feats, logits, t_pad, workspace, ws_floats, flag, flops=0.0):

@@ -274,6 +274,7 @@ class FusedPlan:
                 r.gn_gamma, r.gn_beta = o["gn"][0].data_ptr(), o["gn"][1].data_ptr()
             if o["ln"] is not None:
                 r.ln_gamma, r.ln_beta = o["ln"][0].data_ptr(), o["ln"][1].data_ptr()
+        ops_unet_validate(table, self.ws_floats_per_row, self.out_ld)
         raw = bytes(table)
         self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(c.dev)
         self.nops = len(ops)
@@ -319,6 +320,10 @@ def ops_split(w, ctx):
 
 def ops_unet_op_type():
     return ops.UnetOp
+
+
+def ops_unet_validate(table, ws_floats_per_row, l_ld):
+    ops.unet_validate(table, ws_floats_per_row, l_ld)
 
 
 class LatticeHead:

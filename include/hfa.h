@@ -219,8 +219,9 @@ int hfa_groupnorm_split(int B, int T, int C, int G, const float* x, long long x_
  * Weights w[s] are split planes in fragment order: plane p at w + p * wp halves, [K/32][ceil(n/16)][64][8] halves,
  * element (k, n) at lane (k % 32 / 8) * 16 + n % 16, position k % 8 (one contiguous 1 KiB MFMA operand per 16 columns
  * x 32 k); ldw[s] = K.  n <= 384 and n % 4 == 0 (rows move as float4s: feats, logits and workspace 16-B aligned,
- * l_ld % 4 == 0), cin % 32 == 0, t_pad[b] a multiple of 2^(max level); *oflow raised for an operand outside f16
- * range or a non-finite output. */
+ * l_ld % 4 == 0), cin % 32 == 0, t_pad[b] a multiple of 2^(max level) and <= Tmax (a workgroup whose t_pad[b] is
+ * <= 0 or > Tmax writes nothing); *oflow raised for an operand outside f16 range or a non-finite output.  Tables
+ * are checked on the host by hfa_unet_validate. */
 #define HFA_UNET_NONE (-1)
 #define HFA_UNET_INPUT (-2)
 #define HFA_UNET_OUTPUT (-3)
@@ -240,6 +241,12 @@ typedef struct hfa_unet_op {
 int hfa_unet_head(int B, int Tmax, const hfa_unet_op* ops, int nops, const float* feats, long long f_bs, int f_ld,
                   float* logits, long long l_bs, int l_ld, const int32_t* t_pad, float* workspace, long long ws_bs,
                   int* oflow, hipStream_t stream);
+/* Host-side check of an op table before it is uploaded (the launch reads the table from device memory, so it cannot
+ * check it): kinds, channel and tap constraints above, weight pointers 16-B aligned with plane strides that hold
+ * [K/32][ceil(n/16)][64][8] halves, the parameters each kind reads present, HFA_UNET_OUTPUT only as the head's
+ * destination with n <= l_ld, and every slot access inside ws_floats_per_row floats per Tmax row (a level-l tensor of
+ * row width ld uses ceil(ld / 2^l) of them).  HFA_OK or HFA_EINVAL with hfa_last_error() naming the op. */
+int hfa_unet_validate(const hfa_unet_op* host_ops, int nops, long long ws_floats_per_row, int l_ld);
 /* LDS bytes the fused kernel's workgroup uses (diagnostics). */
 long long hfa_unet_lds_bytes(void);
 /* Diagnostics: the calling thread's next hfa_unet_head launch writes workgroup 0's s_memrealtime (100 MHz) at the

@@ -156,6 +156,25 @@ int main() {
             std::remove(tmp);
         }
     }
+    // fused UNet + head: launch arguments, and the host check of an op table (a conv1 whose taps are 2)
+    {
+        const hfa_unet_op* dops = reinterpret_cast<const hfa_unet_op*>(0x100000);
+        int* flag = reinterpret_cast<int*>(0x100000);
+        CHECK(hfa_unet_head(1, 64, nullptr, 3, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, flag, st), "unet null ops");
+        CHECK(hfa_unet_head(1, 64, dops, 0, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, flag, st), "unet nops 0");
+        CHECK(hfa_unet_head(1, 64, dops, 3, fp, 64 * 768, 768, fp, 64 * 66, 66, ip, fp, 4096, flag, st), "unet l_ld 66");
+        CHECK(hfa_unet_head(1, 64, dops, 3, fp, 64 * 768, 768, fmis, 64 * 68, 68, ip, fp, 4096, flag, st), "unet logits misaligned");
+        CHECK(hfa_unet_head(-1, 64, dops, 3, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, flag, st), "unet B<0");
+        CHECK(hfa_unet_validate(nullptr, 3, 128, 68), "unet_validate null");
+        hfa_unet_op op;
+        std::memset(&op, 0, sizeof(op));
+        op.kind = 0; op.n = 64; op.groups = 16; op.nseg = 1; op.res = HFA_UNET_NONE; op.dst = 0;
+        op.src[0] = HFA_UNET_INPUT; op.src_ld[0] = 64; op.cin[0] = 64; op.taps[0] = 2; op.ldw[0] = 128;
+        op.w[0] = hp; op.wp[0] = 1 << 20;
+        CHECK(hfa_unet_validate(&op, 1, 128, 68), "unet_validate taps 2");
+        op.taps[0] = 3; op.ldw[0] = 192;
+        if (hfa_unet_validate(&op, 1, 128, 68) != 0) { std::printf("FAIL unet_validate on a valid op\n"); ++g_fail; }
+    }
     // host queries and tuning hooks (thread-local state; name strings stay valid, bounded)
     for (int cfg = 0; cfg < 25; ++cfg) {
         hfa_gemm_split_tuning(cfg);
