@@ -34,13 +34,22 @@ __device__ __forceinline__ float from_lane_below(float v) {
 
 // VEC: Smax % K == 0 and aligned planes, so a lane's K contiguous states are loaded and stored as vectors
 // (dp K x f32, bt K bytes) instead of 2K scattered narrow accesses per time step.
-template <int K, int NW, int G, bool VEC>
+//
+// Emission pipeline: a ring of R groups of G time steps in registers.  Group r is computed, then its slot is
+// refilled for the group R ahead, so (R - 1) * G steps of compute cover a refill's memory latency.  Every load is
+// unconditional (rows past T, lanes past Smax read a clamped, valid address; their values are never used): loads
+// in divergent branches defeat the compiler's vmcnt tracking, which then waits for every outstanding load (the
+// refill just issued included) at the top of each group — the prefetch did nothing and each group paid a full
+// memory round trip.  E and nE of a group are one vector load each (lane u holds step t0 + u) broadcast per step
+// with v_readlane, instead of two scalar loads per step whose lgkmcnt(0) waits also catch the refills.
+template <int K, int NW, int G, int R, bool VEC>
 __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
     const int32_t* __restrict__ padv, const float* __restrict__ prob_log,
     const float* __restrict__ not_edge_log, const float* __restrict__ edge_log, double* __restrict__ curr_io,
     float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id) {
     static_assert(NW == 1 || K >= 2, "multi-wave DP needs >= 2 states per lane");
+    static_assert(G <= 64 && R >= 2, "a group's E / nE fit one wave's lanes; at least two groups in flight");
     __shared__ float xq[2][NW][2];
     const int b = blockIdx.x;
     const int g = threadIdx.x;
@@ -60,6 +69,7 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     const double ratio = (double)T / (double)S;  // `T / S` (alignment_decoder.py:186), f64 true division
 
     const int s0 = g * K;
+    const int sl = s0 < Smax ? s0 : 0;          // load column of this lane (clamped: lanes past Smax load row start)
     float dprev[K];
     double curr[K];
     bool valid[K], zero[K], allow3[K];
@@ -76,117 +86,142 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
         allow3[k] = valid[k] && s >= pad && !((j < S - 1) && ids[j] != 0);
     }
 
-    float Lc[G][K], Ec[G], nEc[G];
-    float Ln[G][K], En[G], nEn[G];
-    auto load_group = [&](int t0, float (&L)[G][K], float (&E)[G], float (&nE)[G]) {
+    float L[R][G][K], EV[R], nEV[R];
+    auto load = [&](float (&Lr)[G][K], float& ev, float& nev, int t0) {
+        const int te = min(t0 + lane, T - 1);
+        ev = Ep[te];
+        nev = nEp[te];
 #pragma unroll
         for (int u = 0; u < G; ++u) {
-            const int t = t0 + u;
-            const bool tv = t < T;
-            E[u] = tv ? Ep[t] : 0.0f;
-            nE[u] = tv ? nEp[t] : 0.0f;
+            const float* src = pl + (size_t)min(t0 + u, T - 1) * Smax;
             if (VEC && K >= 2) {
-                if (tv && s0 < Smax) {
-                    const float* src = pl + (size_t)t * Smax + s0;
 #pragma unroll
-                    for (int k = 0; k < K; k += 2) {
-                        const float2 v = *reinterpret_cast<const float2*>(src + k);
-                        L[u][k] = v.x;
-                        L[u][k + 1] = v.y;
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < K; ++k) L[u][k] = 0.0f;
+                for (int k = 0; k < K; k += 2) {
+                    const float2 v = *reinterpret_cast<const float2*>(src + sl + k);
+                    Lr[u][k] = v.x;
+                    Lr[u][k + 1] = v.y;
                 }
             } else {
 #pragma unroll
-                for (int k = 0; k < K; ++k) L[u][k] = (tv && valid[k]) ? pl[(size_t)t * Smax + s0 + k] : 0.0f;
+                for (int k = 0; k < K; ++k) Lr[u][k] = src[min(s0 + k, Smax - 1)];
             }
         }
     };
-    load_group(1, Lc, Ec, nEc);
+    // dp / bt rows go out through buffer stores: a lane past Smax gets an out-of-range offset, which the hardware
+    // drops, so the stores need no branch either
+    const int st_off = s0 < Smax ? s0 : 0x40000000;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-    for (int t0 = 1; t0 < T; t0 += G) {
-        if (t0 + G < T) load_group(t0 + G, Ln, En, nEn);
+    // one time step t from emission slot (r, u): the reference's arithmetic, state by state (see the header)
+    auto step = [&](const float (&Lu)[K], float E, float nE, int t) __attribute__((always_inline)) {
+        float a[K], q[K];
 #pragma unroll
-        for (int u = 0; u < G; ++u) {
-            const int t = t0 + u;
-            if (t >= T) break;   // uniform over the workgroup
-            const float E = Ec[u], nE = nEc[u];
-            float a[K], q[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                a[k] = __fadd_rn(dprev[k], Lc[u][k]);                                   // dp + L     (f32)
-                const float a2 = __fadd_rn(a[k], E);                                     //  + E       (f32)
-                q[k] = (float)__dadd_rn((double)a2, __dmul_rn(curr[k], ratio));          //  + C*T/S   (f64)
+        for (int k = 0; k < K; ++k) {
+            a[k] = __fadd_rn(dprev[k], Lu[k]);                                       // dp + L     (f32)
+            const float a2 = __fadd_rn(a[k], E);                                     //  + E       (f32)
+            q[k] = (float)__dadd_rn((double)a2, __dmul_rn(curr[k], ratio));          //  + C*T/S   (f64)
+        }
+        // left neighbour lane's last two q values (states s0-1, s0-2)
+        float qm1 = from_lane_below(q[K - 1]);
+        float qm2 = (K >= 2) ? from_lane_below(q[K >= 2 ? K - 2 : 0]) : from_lane_below(qm1);
+        if (NW > 1) {
+            if (lane == 63) {
+                xq[t & 1][wave][0] = q[K - 1];
+                xq[t & 1][wave][1] = q[K >= 2 ? K - 2 : 0];
             }
-            // left neighbour lane's last two q values (states s0-1, s0-2)
-            float qm1 = from_lane_below(q[K - 1]);
-            float qm2 = (K >= 2) ? from_lane_below(q[K >= 2 ? K - 2 : 0]) : from_lane_below(qm1);
-            if (NW > 1) {
-                if (lane == 63) {
-                    xq[t & 1][wave][0] = q[K - 1];
-                    xq[t & 1][wave][1] = q[K >= 2 ? K - 2 : 0];
-                }
-                __syncthreads();
-                if (lane == 0 && wave > 0) {
-                    qm1 = xq[t & 1][wave - 1][0];
-                    qm2 = xq[t & 1][wave - 1][1];
-                }
-            }
-            const size_t row = (size_t)t * Smax;
-            float bestv[K];
-            unsigned long long bidx = 0;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int s = s0 + k;
-                const float p1 = __fadd_rn(a[k], nE);
-                const float src1 = (k >= 1) ? q[k >= 1 ? k - 1 : 0] : qm1;
-                const float src2 = (k >= 2) ? q[k >= 2 ? k - 2 : 0] : (k == 1 ? qm1 : qm2);
-                const float p2 = (s == 0) ? neg_inf() : src1;
-                const float p3 = allow3[k] ? (pad == 1 ? src1 : src2) : neg_inf();
-                float best = p1;
-                int idx = 0;
-                if (p2 > best) { best = p2; idx = 1; }
-                if (p3 > best) { best = p3; idx = 2; }
-                if (VEC) {
-                    bestv[k] = best;
-                    bidx |= (unsigned long long)idx << (8 * k);
-                } else if (valid[k]) {
-                    d[row + s] = best;
-                    bb[row + s] = (int8_t)idx;
-                }
-                const double Ld = (double)Lc[u][k];
-                if (idx == 0) curr[k] = (Ld > curr[k]) ? Ld : curr[k];  // max(curr, L) (:222)
-                else curr[k] = Ld;                                       // (:224)
-                if (zero[k]) curr[k] = 0.0;                              // (:226-228)
-                dprev[k] = best;
-            }
-            if (VEC && s0 < Smax) {     // states past S inside the Smax pitch get don't-care values
-                float* drow = d + row + s0;
-                if (K == 1) {
-                    drow[0] = bestv[0];
-                    bb[row + s0] = (int8_t)bidx;
-                } else if (K == 2) {
-                    *reinterpret_cast<float2*>(drow) = make_float2(bestv[0], bestv[K > 1 ? 1 : 0]);
-                    *reinterpret_cast<uint16_t*>(bb + row + s0) = (uint16_t)bidx;
-                } else {
-#pragma unroll
-                    for (int k = 0; k < K; k += 4)
-                        *reinterpret_cast<float4*>(drow + k) =
-                            make_float4(bestv[k], bestv[k + 1 < K ? k + 1 : 0], bestv[k + 2 < K ? k + 2 : 0],
-                                        bestv[k + 3 < K ? k + 3 : 0]);
-                    if (K == 4) *reinterpret_cast<uint32_t*>(bb + row + s0) = (uint32_t)bidx;
-                    else *reinterpret_cast<unsigned long long*>(bb + row + s0) = bidx;
-                }
+            __syncthreads();
+            if (lane == 0 && wave > 0) {
+                qm1 = xq[t & 1][wave - 1][0];
+                qm2 = xq[t & 1][wave - 1][1];
             }
         }
+        const size_t row = (size_t)t * Smax;
+        float bestv[K];
+        unsigned long long bidx = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int s = s0 + k;
+            const float p1 = __fadd_rn(a[k], nE);
+            const float src1 = (k >= 1) ? q[k >= 1 ? k - 1 : 0] : qm1;
+            const float src2 = (k >= 2) ? q[k >= 2 ? k - 2 : 0] : (k == 1 ? qm1 : qm2);
+            const float p2 = (s == 0) ? neg_inf() : src1;
+            const float p3 = allow3[k] ? (pad == 1 ? src1 : src2) : neg_inf();
+            float best = p1;
+            int idx = 0;
+            if (p2 > best) { best = p2; idx = 1; }
+            if (p3 > best) { best = p3; idx = 2; }
+            if (VEC) {
+                bestv[k] = best;
+                bidx |= (unsigned long long)idx << (8 * k);
+            } else if (valid[k]) {
+                d[row + s] = best;
+                bb[row + s] = (int8_t)idx;
+            }
+            const double Ld = (double)Lu[k];
+            if (idx == 0) curr[k] = (Ld > curr[k]) ? Ld : curr[k];  // max(curr, L) (:222)
+            else curr[k] = Ld;                                       // (:224)
+            if (zero[k]) curr[k] = 0.0;                              // (:226-228)
+            dprev[k] = best;
+        }
+        if (VEC) {     // states past S inside the Smax pitch get don't-care values
+            const __amdgpu_buffer_rsrc_t rd = hfa::make_rsrc(d + row, (long long)Smax * 4);
+            const __amdgpu_buffer_rsrc_t rb = hfa::make_rsrc(bb + row, Smax);
+            const int od = st_off < 0x40000000 ? st_off * 4 : 0x40000000;
+#pragma unroll
+            for (int k = 0; k < K; k += 4) {
+                if (K - k >= 4) {
+                    u32x4 w;
+                    w.x = __float_as_uint(bestv[k]);
+                    w.y = __float_as_uint(bestv[k + 1 < K ? k + 1 : 0]);
+                    w.z = __float_as_uint(bestv[k + 2 < K ? k + 2 : 0]);
+                    w.w = __float_as_uint(bestv[k + 3 < K ? k + 3 : 0]);
+                    __builtin_amdgcn_raw_buffer_store_b128(w, rd, od + 4 * k, 0, 0);
+                } else if (K - k >= 2) {
+                    u32x2 w;
+                    w.x = __float_as_uint(bestv[k]);
+                    w.y = __float_as_uint(bestv[k + 1 < K ? k + 1 : 0]);
+                    __builtin_amdgcn_raw_buffer_store_b64(w, rd, od + 4 * k, 0, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(bestv[k]), rd, od + 4 * k, 0, 0);
+                }
+            }
+            if (K == 1) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bidx, rb, st_off, 0, 0);
+            else if (K == 2) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bidx, rb, st_off, 0, 0);
+            else if (K == 4) __builtin_amdgcn_raw_buffer_store_b32((unsigned int)bidx, rb, st_off, 0, 0);
+            else {
+                u32x2 w;
+                w.x = (unsigned int)bidx;
+                w.y = (unsigned int)(bidx >> 32);
+                __builtin_amdgcn_raw_buffer_store_b64(w, rb, st_off, 0, 0);
+            }
+        }
+    };
+
+#pragma unroll
+    for (int r = 0; r < R; ++r) load(L[r], EV[r], nEV[r], 1 + r * G);
+    int tb = 1;
+    // main loop: whole rounds of R groups, straight-line (no early exits: a branch around a refill would again
+    // cost the vmcnt tracking); slot r holds steps tb + r G .. + G - 1 on entry
+    for (; tb + R * G <= T; tb += R * G) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int u = 0; u < G; ++u)
+                step(L[r][u], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(EV[r]), u)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nEV[r]), u)), tb + r * G + u);
+            load(L[r], EV[r], nEV[r], tb + (r + R) * G);   // refill this slot for the group R ahead
+        }
+    }
+    // tail (< R G steps): the slots already hold them
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
 #pragma unroll
         for (int u = 0; u < G; ++u) {
-            Ec[u] = En[u];
-            nEc[u] = nEn[u];
-#pragma unroll
-            for (int k = 0; k < K; ++k) Lc[u][k] = Ln[u][k];
+            const int t = tb + r * G + u;
+            if (t < T)   // uniform over the workgroup
+                step(L[r][u], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(EV[r]), u)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nEV[r]), u)), t);
         }
     }
 #pragma unroll
@@ -338,37 +373,63 @@ __global__ __launch_bounds__(kBtThreads) void viterbi_backtrack_kernel(
             s = S - 2;
         s_cur = s;
     }
-    // The chased state drops by at most 2 per step, so R rows of the chase only touch columns
-    // [s_top - 2R, s_top]: stage that R x (2R+1) window instead of whole rows (long lattices: S = 1801 moves
-    // 29 KB per 120 steps instead of 32 KB per 18).  Short rows (Smax <= 2R+1) stage whole rows as before.
-    int R = kBtChunkBytes / Smax;
-    if (R < 1 || 2 * R + 1 < Smax) {
-        R = 1;
-        while (2 * (R + 1) + 1 <= Smax && (R + 1) * (2 * (R + 1) + 1) <= kBtChunkBytes) ++R;
-    }
+    // Band staging + run-skipping chase.  The chased state only ever decreases (by 0..2 per frame), so a chunk of
+    // rows [lo, hi] is staged for a band of BW columns ending at the current state (whole rows when Smax <= 128);
+    // when the state leaves the band the next chunk restarts from that frame.  The chase itself is wave-parallel:
+    // the 64 lanes read bt at the current state for the next 64 frames at once and the first non-zero code (a
+    // ballot) ends the run of 'stay' frames — the path moves about once per T/S frames, so one LDS round trip
+    // covers many frames instead of one per frame.
+    const bool whole = Smax <= 128;
+    const int lgb = whole ? (Smax <= 16 ? 4 : 32 - __builtin_clz(Smax - 1)) : 6;   // band: 2^lgb columns
+    const int BW = 1 << lgb;                                       // (the LDS row pitch)
+    const int R = kBtChunkBytes >> lgb;                            // rows per chunk
+    const bool dw = (Smax & 3) == 0 && (reinterpret_cast<uintptr_t>(bb) & 3) == 0;
+    const int lane = tid & 63, wv = tid >> 6;
     __syncthreads();
-    for (int hi = T - 1; hi >= 0; hi -= R) {
-        const int lo = max(0, hi - R + 1);
+    int hi = T - 1;
+    while (hi >= 0) {
         const int top = s_cur;
-        const int c0 = max(0, top - 2 * (hi - lo));
-        const int W = min(Smax - c0, 2 * (hi - lo) + 1);
-        const int nbytes = (hi - lo + 1) * W;
-        for (int i = tid; i < nbytes; i += kBtThreads) {
-            const int r = i / W, c = i - r * W;
-            chunk[i] = bb[(size_t)(lo + r) * Smax + c0 + c];
+        const int lo = max(0, hi - R + 1);
+        const int c0 = whole ? 0 : max(0, (top & ~3) + 4 - BW);    // 4-aligned, the band [c0, top | 3] holds top
+        const int ncol = min(BW, Smax - c0);                       // staged columns (the rest of the band unused)
+        const int total = (hi - lo + 1) << (lgb - 2);              // dwords of the chunk
+        for (int i = tid; i < total; i += kBtThreads) {
+            const int r = i >> (lgb - 2), c = (i & ((BW >> 2) - 1)) << 2;
+            if (c >= ncol) continue;
+            const int8_t* src = bb + (size_t)(lo + r) * Smax + c0 + c;
+            if (dw) {
+                *reinterpret_cast<int*>(chunk + r * BW + c) = *reinterpret_cast<const int*>(src);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) chunk[r * BW + c + j] = c + j < ncol ? src[j] : 0;
+            }
         }
         __syncthreads();
-        if (tid == 0) {
-            int s = top;
-            for (int t = hi; t >= lo; --t) {
-                const int code = (t == 0) ? -1 : (int)chunk[(t - lo) * W + (s - c0)];
-                const int emit = code != 0;
-                if constexpr (GPATH) gpath[t] = (uint32_t)s | ((uint32_t)emit << 31);
-                else path[t] = (uint16_t)(s | (emit << 15));
-                if (emit) s -= code;
+        if (wv == 0) {
+            int s = top, t = hi;
+            while (t >= lo && s >= c0) {
+                const int tl = t - lane;                           // the frame this lane checks, at state s
+                const bool inr = tl >= lo;
+                const int code = !inr ? 0 : (tl == 0 ? -1 : (int)chunk[(tl - lo) * BW + (s - c0)]);
+                const unsigned long long nz = __ballot(code != 0);
+                const int last = min(63, t - lo);                  // the last lane inside the chunk
+                const int first = nz ? __ffsll((long long)nz) - 1 : last;   // lanes 0..first are this run
+                const bool emits = nz != 0;
+                if (lane <= first && inr) {
+                    const int emit = (lane == first && emits) ? 1 : 0;
+                    if constexpr (GPATH) gpath[tl] = (uint32_t)s | ((uint32_t)emit << 31);
+                    else path[tl] = (uint16_t)(s | (emit << 15));
+                }
+                if (emits) s -= __shfl(code, first);
+                if (s < 0) s = 0;                                  // (only a corrupt bt gets here)
+                t -= first + 1;
             }
-            s_cur = s;
-        }
+            if (lane == 0) s_cur = s;
+            hi = t;                                                // next frame to chase (state left the band:
+        }                                                          // restart the band there)
+        if (wv == 0 && lane == 0) s_carry = hi;
+        __syncthreads();
+        hi = s_carry;
         __syncthreads();
     }
     // confidence + ordered compaction of emitted (s, t)
@@ -506,17 +567,17 @@ __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
 
 thread_local int g_force_k = 0;   // hfa_viterbi_tuning: states per lane of the multi-wave DP (0 = automatic)
 
-template <int K, int NW, int G>
+template <int K, int NW, int G, int R>
 int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const int32_t* pad,
                    const float* prob_log, const float* nE, const float* E, double* curr, float* dp, int8_t* bt,
                    const int32_t* ids, hipStream_t st) {
     const bool vec = Smax % K == 0 && ((uintptr_t)prob_log % 16 == 0) && ((uintptr_t)dp % 16 == 0) &&
                      ((uintptr_t)bt % 8 == 0);
     if (vec)
-        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, true>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
+        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, true>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
                            S, pad, prob_log, nE, E, curr, dp, bt, ids);
     else
-        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, false>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
+        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, false>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
                            S, pad, prob_log, nE, E, curr, dp, bt, ids);
     return hfa::check_launch("hfa_viterbi_forward");
 }
@@ -537,37 +598,39 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
     if (B == 0 || Tmax == 0 || Smax == 0) return HFA_OK;
     // one wave while a lane holds <= 8 states; beyond that K states per lane over up to 16 waves (K = 8 by
     // default, or forced to 2/4 by hfa_viterbi_tuning: more waves, fewer states each, one barrier per step)
-#define HFA_FWD(K, NW, G)                                                                                       \
-    return launch_forward<K, NW, G>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log, edge_log, curr, \
-                                    dp, bt, ph_seq_id, stream)
+#define HFA_FWD(K, NW, G, R)                                                                                    \
+    return launch_forward<K, NW, G, R>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log, edge_log, curr, \
+                                       dp, bt, ph_seq_id, stream)
+    // R groups of G steps in flight (K * G * R emission registers per lane, within the VGPR budget of 64 * NW
+    // threads: 512 up to 4 waves, 256 at 8, 128 at 16)
     const int per_lane = (Smax + 63) / 64;
-    if (per_lane <= 1) HFA_FWD(1, 1, 8);
-    if (per_lane <= 2) HFA_FWD(2, 1, 8);
-    if (per_lane <= 4) HFA_FWD(4, 1, 8);
-    if (per_lane <= 8 && g_force_k == 0) HFA_FWD(8, 1, 4);
-    // measured (scripts/dp_bench.py, T = 25 839, S = 1 801): 2 states per lane over 16 waves 0.76 us/step,
-    // 4 over 8 0.78, 8 over 4 1.08 — the per-step critical path (VALU chain of one lane's K states) wins over
-    // the extra barrier participants
-    const int kk = g_force_k ? g_force_k : (Smax <= 2048 ? 2 : (Smax <= 4096 ? 4 : 8));
+    if (per_lane <= 1) HFA_FWD(1, 1, 8, 4);
+    if (per_lane <= 2) HFA_FWD(2, 1, 8, 4);
+    if (per_lane <= 4) HFA_FWD(4, 1, 8, 3);
+    if (per_lane <= 8 && g_force_k == 0) HFA_FWD(8, 1, 4, 4);
+    // measured (scripts/dp_bench.py, T = 25 839, S = 1 801, with the emission ring): 4 states per lane over 8
+    // waves 0.51 us/step, 2 over 16 0.58, 8 over 4 0.65 (before the ring: 0.68 / 0.77 / 0.98) — the step is
+    // VALU-issue bound over the CU's four SIMDs, and 4 states per lane balance that against the barrier's waves
+    const int kk = g_force_k ? g_force_k : (Smax <= 4096 ? 4 : 8);
     if (kk == 2 && Smax <= 2048) {
         const int w = (Smax + 127) / 128;
-        if (w <= 2) HFA_FWD(2, 2, 8);
-        if (w <= 4) HFA_FWD(2, 4, 8);
-        if (w <= 8) HFA_FWD(2, 8, 8);
-        HFA_FWD(2, 16, 8);
+        if (w <= 2) HFA_FWD(2, 2, 8, 4);
+        if (w <= 4) HFA_FWD(2, 4, 8, 4);
+        if (w <= 8) HFA_FWD(2, 8, 8, 4);
+        HFA_FWD(2, 16, 8, 3);
     }
     if (kk == 4 && Smax <= 4096) {
         const int w = (Smax + 255) / 256;
-        if (w <= 2) HFA_FWD(4, 2, 4);
-        if (w <= 4) HFA_FWD(4, 4, 4);
-        if (w <= 8) HFA_FWD(4, 8, 4);
-        HFA_FWD(4, 16, 4);
+        if (w <= 2) HFA_FWD(4, 2, 4, 4);
+        if (w <= 4) HFA_FWD(4, 4, 4, 4);
+        if (w <= 8) HFA_FWD(4, 8, 4, 4);
+        HFA_FWD(4, 16, 4, 3);
     }
     const int waves = (Smax + 511) / 512;
-    if (waves <= 2) HFA_FWD(8, 2, 4);
-    if (waves <= 4) HFA_FWD(8, 4, 4);
-    if (waves <= 8) HFA_FWD(8, 8, 4);
-    if (waves <= 16) HFA_FWD(8, 16, 2);   // 1024 threads cap VGPRs at 128: shorter prefetch ring
+    if (waves <= 2) HFA_FWD(8, 2, 4, 3);
+    if (waves <= 4) HFA_FWD(8, 4, 4, 3);
+    if (waves <= 8) HFA_FWD(8, 8, 4, 3);
+    if (waves <= 16) HFA_FWD(8, 16, 2, 3);   // 1024 threads cap VGPRs at 128: shorter groups
 #undef HFA_FWD
     if (Smax <= 4 * kWideSeg) {  // the segmented form, up to 32768 states (the backtrack's 15-bit path entries)
         hipLaunchKernelGGL(viterbi_forward_wide_kernel, dim3(B), dim3(64 * kWideNW), 0, stream, Tmax, Smax, T, S,

@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c5t -o run -- python3 bench.py --batch 1 --seconds 300 --words 600 --steps 4 --warmup 1 --no-cpu-baseline --chunk-seconds 20 > gpurun_out/c5t.log 2>&1 &&
+python3 scripts/c5_trace_summary.py gpurun_out/c5t/run_kernel_trace.csv > gpurun_out/c5t_summary.txt
