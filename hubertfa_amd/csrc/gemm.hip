@@ -1569,19 +1569,26 @@ inline int split_cfg(const GemmP& p, int Z) {
         return SCFG_256x64_M16;            // grouped positional conv at Cg = 64 (Hubert-large): 1.26x the 128x64 tile
     if (p.N <= 64 || blocks128 < 256) return SCFG_128x64_M16;
     if (blocks256 < 128 || p.N < 512) return SCFG_128x128_M16;
-    // 256 x 192 where the 256 x 256 grid ends in a thin last round and the 192-wide one does not: QKV at N = 2304
-    // (567 tiles = 2.2 rounds -> 756 = 2.95), 12 % faster than 128 x 128 and 256 x 256 (profiles/r02/split_192.txt).
-    // One-round grids (N = 768: 189 vs 252 tiles) gain nothing: the chip is power-limited, and the fewer busy CUs
-    // run a higher clock.
-    const long long blocks192 = (long long)((p.M + 255) / 256) * ((p.N + 191) / 192) * Z;
+    // Large grids: the 256 x 256 tile unless a 192-wide tile fills the last round of CUs much better.  Score =
+    // fill of the rounds (tiles / (rounds x 256 CUs)) x the tile's per-FLOP speed (192-wide tiles 0.92 of 256 x 256),
+    // ties to 256 x 256.  Measured (scripts/split_gemm_bench.py, profiles/r03/split_tiles_c5.txt): QKV at M = 15 968
+    // (567 big tiles = 2.2 rounds) 192 x 256 347 / 256 x 192 339 / 256 x 256 300 / 128 x 128 297 TF/s; at
+    // M = 17 924 (config 5 windows: 639 tiles = 2.5 rounds) 256 x 256 340 / 128 x 128 318; FFN1 at M = 17 924 (852
+    // tiles = 3.3 rounds) 256 x 256 308 / 192 x 256 304 / 128 x 128 276 — a thin last round costs less than its
+    // share (fewer busy CUs hold a higher clock), so the 128 x 128 tile is never the better large-grid choice.
     auto fill = [](long long b) { return (double)b / (double)(((b + 255) / 256) * 256); };
-    if (p.N % 192 == 0 && blocks256 > 256 && fill(blocks256) < 0.85 && fill(blocks192) > fill(blocks256) + 0.1)
-        return SCFG_256x192_M16;
-    // rounds of resident tiles (256 x 256: one per CU; 128 x 128: two per CU) times the time per round, with the
-    // larger tile's 1.12x per-FLOP speed (profiles/r02/split_mf16.txt): QKV (N = 2304, 567 big tiles = 2.2 rounds)
-    // goes to 128 x 128, the extractor convs, FFN and 768-wide projections stay on 256 x 256
-    const double t256 = (double)((blocks256 + 255) / 256) * 4.0 / 1.12, t128 = (double)((blocks128 + 511) / 512) * 2.0;
-    return t256 <= t128 ? SCFG_256x256_M16 : SCFG_128x128_M16;
+    const long long blocks192n = (long long)((p.M + 255) / 256) * ((p.N + 191) / 192) * Z;   // 256 x 192
+    const long long blocks192m = (long long)((p.M + 191) / 192) * ((p.N + 255) / 256) * Z;   // 192 x 256
+    // (one-round grids stay on 256 x 256: N = 768 at 189 vs 252 busy CUs measured equal, the fewer CUs clock higher)
+    double best = fill(blocks256);
+    int cfg = SCFG_256x256_M16;
+    if (blocks256 <= 256) return cfg;
+    if (0.92 * fill(blocks192m) > best + 0.05) {
+        best = 0.92 * fill(blocks192m);
+        cfg = SCFG_192x256_M16;
+    }
+    if (p.N % 192 == 0 && 0.92 * fill(blocks192n) > best + 0.05) cfg = SCFG_256x192_M16;
+    return cfg;
 }
 
 // general taps (Cg % 32 != 0, the grouped positional conv off the window kernel): the tiles with a GT instantiation

@@ -23,6 +23,14 @@ SHAPES = [  # name, Tin, Cin, Cout, k, stride, epi
     ("unet_sc", 864, 768, 192, 1, 1, 0),
     ("unet_down", 864, 192, 384, 2, 2, 0),
     ("unet_up", 216, 384, 384, 1, 1, 0),
+    # flattened [B*T] rows as the encoder launches them (Z = 1): config 2 (32 x 499) and config 5 in 20 s windows
+    # (15 windows x ~1195 frames)
+    ("qkv_c2", 15968, 768, 2304, 1, 1, 0, 1),
+    ("ffn1_c2", 15968, 768, 3072, 1, 1, 1, 1),
+    ("qkv_c5", 17924, 768, 2304, 1, 1, 0, 1),
+    ("ffn1_c5", 17924, 768, 3072, 1, 1, 1, 1),
+    ("ffn2_c5", 17924, 3072, 768, 1, 1, 0, 1),
+    ("outproj_c5", 17924, 768, 768, 1, 1, 0, 1),
 ]
 
 
@@ -49,7 +57,9 @@ def main():
     keep = set(args.shapes.split(",")) if args.shapes else None
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
-    for name, Tin, Cin, Cout, k, s, epi in SHAPES:
+    for shape in SHAPES:
+        name, Tin, Cin, Cout, k, s, epi = shape[:7]
+        B = shape[7] if len(shape) > 7 else globals()["B"]
         if keep and name not in keep:
             continue
         Tout = (Tin - k) // s + 1

@@ -125,3 +125,18 @@ def test_unet_validate_rejects_bad_tables():
         mutate(t)
         with pytest.raises(HFAArgumentError, match=msg):
             ops.unet_validate(t, wpr, l_ld)
+
+
+def test_split_gemm_tile_choice():
+    """The split GEMM's automatic tile for the workload's large grids (host query, no GPU): 256 x 256 unless a
+    192-wide tile fills the last round of CUs much better (profiles/r03/split_tiles_c5.txt)."""
+    pytest.importorskip("torch")
+    from hubertfa_amd import ops
+    tile = lambda M, N, Z=1, epi=0: ops._split_name(M, N, Z, True, epi, 768).split("<")[1].split(",")[1:3]  # noqa: E731
+    assert tile(15968, 2304) == [" 192", " 256"]          # config 2 QKV: 567 big tiles = 2.2 rounds
+    assert tile(15968, 3072, epi=1) == [" 256", " 256"]   # config 2 FFN1: 756 tiles = 2.95 rounds
+    assert tile(17924, 3072, epi=1) == [" 256", " 256"]   # config 5 windows: 852 tiles (was 128 x 128)
+    assert tile(17924, 2304) == [" 256", " 256"]          # 639 tiles (was 128 x 128)
+    assert tile(15968, 768) == [" 256", " 256"]           # out-projection / FFN2: one round
+    assert tile(15999, 512, Z=32, epi=1) == [" 256", " 256"]   # extractor conv1
+    assert tile(864, 192, Z=32) == [" 128", " 128"]       # UNet level 0: small grid
