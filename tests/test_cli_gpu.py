@@ -168,6 +168,23 @@ def test_bench_contract_two_ranks():
     assert d["roofline"]["bound"] == "mfma" and 0 < d["roofline"]["frac"] < 1
 
 
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_config3_block():
+    """An N > 1 bench line carries BASELINE config 3 (512 x 10 s over the node) after its weak-scaling region: the
+    2-rank rehearsal (gloo, both ranks on GPU 0) times 256 utterances per rank and reports them as `config3`."""
+    import json
+    p = _torchrun(["--gpus", "2", "--steps", "1", "--warmup", "1", "--batch", "4", "--seconds", "10",
+                   "--no-cpu-baseline", "--dist-backend", "gloo", "--device", "0"], script="bench.py", timeout=600)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["config"]["global_batch"] == 8
+    c3 = d["config3"]
+    assert c3["per_gpu_batch"] == 256 and c3["global_batch"] == 512 and c3["steps"] == 1
+    assert c3["value"] > 0 and abs(c3["value"] - 512 * 10.0 / (c3["ms_per_step"] * 1e-3)) < 1e-6 * c3["value"]
+
+
 def test_predict_isolates_failing_file(tmp_path):
     """A batch that raises a recoverable error is re-run file by file; the file that fails alone is logged and
     skipped, every other file gets exactly its normal result."""
