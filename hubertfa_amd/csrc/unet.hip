@@ -266,8 +266,10 @@ struct OpArgs {
 // NI NJ <= 12 keeps the accumulators at 48 VGPRs
 // Not inlined: each (NI, NJ) instance gets its own register allocation (inlined into one kernel body, the union of
 // the four instances' live ranges spilled inside the MFMA loops).  Returns whether a value left f16 range.
+// Row blocks [blk0, blk1) of the op (the fused kernel: all of them).  gn_out (tiled CONV1 only): this workgroup's
+// GroupNorm partial sums per group (f64 sum, sum of squares) go to gn_out[G][2] instead of becoming the statistics.
 template <int NI, int NJ>
-__device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh) {
+__device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh, int blk0, int blk1, double* gn_out) {
     bool bad = false;
     constexpr int BMO = 32 * NI;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -296,8 +298,8 @@ __device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh) {
     for (int k = 0; k < C4; ++k)
 #pragma unroll
         for (int e = 0; e < 4; ++e) gs[k][e] = gss[k][e] = 0.0;
-    const int nblk = (o.rows_out + BMO - 1) / BMO;
-    for (int blk = 0; blk < nblk; ++blk) {
+    const int nblk = min((o.rows_out + BMO - 1) / BMO, blk1);
+    for (int blk = blk0; blk < nblk; ++blk) {
         const int m0 = blk * BMO;
         f32x4 acc[NI][NJ];
 #pragma unroll
@@ -447,6 +449,10 @@ __device__ __attribute__((noinline)) bool run_op(const OpArgs& o, Shared& sh) {
                     S += part[(w * N + c) * 2];
                     SS += part[(w * N + c) * 2 + 1];
                 }
+            if (gn_out) {                                          // tiled: the partials of this row block
+                *(__attribute__((address_space(1))) double*)(gn_out + 2 * tid) = S;
+                *(__attribute__((address_space(1))) double*)(gn_out + 2 * tid + 1) = SS;
+            }
             const double n = (double)o.rows_out * cg;
             const double mean_d = o.rows_out > 0 ? S / n : 0.0;
             double var_d = o.rows_out > 0 ? SS / n - mean_d * mean_d : 0.0;
@@ -477,9 +483,56 @@ struct UnetArgs {
     long long* prof;          // optional (hfa_unet_profile): workgroup 0's s_memrealtime at every op boundary
 };
 
-__device__ __forceinline__ const float* slot_ptr(const UnetArgs& a, float* wsb, int slot, long long off) {
-    if (slot == HFA_UNET_INPUT) return a.feats + blockIdx.x * a.f_bs;
+__device__ __forceinline__ const float* slot_ptr(const UnetArgs& a, int b, float* wsb, int slot, long long off) {
+    if (slot == HFA_UNET_INPUT) return a.feats + b * a.f_bs;
     return wsb + off * a.Tmax;
+}
+
+// table entry u -> the op's arguments for utterance b (T0 padded rows, scratch wsb)
+__device__ __forceinline__ void make_op(const UnetArgs& a, const hfa_unet_op& u, int b, int T0, float* wsb, OpArgs& o) {
+    o.kind = u.kind;
+    o.N = u.n;
+    o.G = u.groups;
+    o.nst = u.nseg;
+    const int T = T0 >> u.level;                            // rows of this op's output level (UP: its input level)
+    o.rows_out = T;
+    for (int s = 0; s < 2; ++s) {
+        Stage& st = o.st[s];
+        const int slot = u.src[s];
+        st.src = slot == HFA_UNET_NONE ? nullptr : slot_ptr(a, b, wsb, slot, u.src_off[s]);
+        st.ld = slot == HFA_UNET_INPUT ? a.f_ld : u.src_ld[s];
+        st.cin = u.cin[s];
+        st.taps = u.taps[s];
+        st.pad = st.taps / 2;
+        st.rows = T;
+        st.gn = u.gn[s] != 0;
+        st.w = reinterpret_cast<const _Float16*>(u.w[s]);
+        st.wp = u.wp[s];
+        st.ldw = u.ldw[s];
+    }
+    o.bias = u.bias;
+    o.gamma = u.gn_gamma;
+    o.beta = u.gn_beta;
+    o.ln_g = u.ln_gamma;
+    o.ln_b = u.ln_beta;
+    o.res = u.res == HFA_UNET_NONE ? nullptr : slot_ptr(a, b, wsb, u.res, u.res_off);
+    if (u.dst == HFA_UNET_OUTPUT) {
+        o.dst = a.logits + b * a.l_bs;
+        o.ldd = a.l_ld;
+    } else {
+        o.dst = wsb + u.dst_off * a.Tmax;
+        o.ldd = u.n;
+    }
+}
+
+// rows per row block of an op with N output columns (run_op's NI): the dispatch below and the host's grid agree on it
+__host__ __device__ constexpr int op_block_rows(int N) { return N <= 192 ? 128 : 64; }
+
+__device__ __forceinline__ bool dispatch_op(const OpArgs& o, Shared& sh, int blk0, int blk1, double* gn_out) {
+    if (o.N <= 128) return run_op<4, 2>(o, sh, blk0, blk1, gn_out);
+    if (o.N <= 192) return run_op<4, 3>(o, sh, blk0, blk1, gn_out);
+    if (o.N <= 256) return run_op<2, 4>(o, sh, blk0, blk1, gn_out);
+    return run_op<2, 6>(o, sh, blk0, blk1, gn_out);
 }
 
 __global__ __launch_bounds__(NT, 1) void unet_head_kernel(const UnetArgs a) {
@@ -491,47 +544,49 @@ __global__ __launch_bounds__(NT, 1) void unet_head_kernel(const UnetArgs a) {
     bool bad = false;
     for (int k = 0; k < a.nops; ++k) {
         if (a.prof && b == 0 && threadIdx.x == 0) a.prof[k] = (long long)__builtin_amdgcn_s_memrealtime();
-        const hfa_unet_op& u = a.ops[k];
         OpArgs o;
-        o.kind = u.kind;
-        o.N = u.n;
-        o.G = u.groups;
-        o.nst = u.nseg;
-        const int T = T0 >> u.level;                        // rows of this op's output level (UP: its input level)
-        o.rows_out = T;
-        for (int s = 0; s < 2; ++s) {
-            Stage& st = o.st[s];
-            const int slot = u.src[s];
-            st.src = slot == HFA_UNET_NONE ? nullptr : slot_ptr(a, wsb, slot, u.src_off[s]);
-            st.ld = slot == HFA_UNET_INPUT ? a.f_ld : u.src_ld[s];
-            st.cin = u.cin[s];
-            st.taps = u.taps[s];
-            st.pad = st.taps / 2;
-            st.rows = T;
-            st.gn = u.gn[s] != 0;
-            st.w = reinterpret_cast<const _Float16*>(u.w[s]);
-            st.wp = u.wp[s];
-            st.ldw = u.ldw[s];
-        }
-        o.bias = u.bias;
-        o.gamma = u.gn_gamma;
-        o.beta = u.gn_beta;
-        o.ln_g = u.ln_gamma;
-        o.ln_b = u.ln_beta;
-        o.res = u.res == HFA_UNET_NONE ? nullptr : slot_ptr(a, wsb, u.res, u.res_off);
-        if (u.dst == HFA_UNET_OUTPUT) {
-            o.dst = a.logits + b * a.l_bs;
-            o.ldd = a.l_ld;
-        } else {
-            o.dst = wsb + u.dst_off * a.Tmax;
-            o.ldd = u.n;
-        }
-        if (o.N <= 128) bad |= run_op<4, 2>(o, sh);
-        else if (o.N <= 192) bad |= run_op<4, 3>(o, sh);
-        else if (o.N <= 256) bad |= run_op<2, 4>(o, sh);
-        else bad |= run_op<2, 6>(o, sh);
+        make_op(a, a.ops[k], b, T0, wsb, o);
+        bad |= dispatch_op(o, sh, 0, 1 << 30, nullptr);
     }
     if (a.prof && b == 0 && threadIdx.x == 0) a.prof[a.nops] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (bad && a.oflow) *a.oflow = 1;
+}
+
+// Tiled form: ONE op per launch, one workgroup per (row block, utterance) — the same op engine, spread over the
+// chip in short-lived workgroups instead of one long-lived workgroup per utterance.  A first conv writes its row
+// block's GroupNorm partials to gn[b][blk][G][2]; the block's second conv sums its utterance's nblk_gn partials in
+// block order (deterministic, independent of the batch) before staging.
+__global__ __launch_bounds__(NT, 1) void unet_op_kernel(const UnetArgs a, int k, double* gn, long long gn_bs,
+                                                        int nblk_gn) {
+    __shared__ Shared sh;
+    const int b = blockIdx.y, blk = blockIdx.x;
+    const int T0 = a.t_pad[b];
+    if (T0 <= 0 || T0 > a.Tmax) return;
+    const hfa_unet_op& u = a.ops[k];
+    if (blk * op_block_rows(u.n) >= (T0 >> u.level)) return;      // this utterance has fewer rows
+    float* wsb = a.ws + b * a.ws_bs;
+    OpArgs o;
+    make_op(a, u, b, T0, wsb, o);
+    double* gnb = gn + b * gn_bs;
+    if (o.kind == U_CONV2) {
+        const int rows1 = T0 >> u.level, cg = o.st[0].cin / o.G;
+        const int nb = min(nblk_gn, (rows1 + op_block_rows(o.st[0].cin) - 1) / op_block_rows(o.st[0].cin));
+        if ((int)threadIdx.x < o.G) {
+            double S = 0.0, SS = 0.0;
+            for (int i = 0; i < nb; ++i) {
+                S += gnb[(i * 64 + threadIdx.x) * 2];
+                SS += gnb[(i * 64 + threadIdx.x) * 2 + 1];
+            }
+            const double n = (double)rows1 * cg;
+            const double mean_d = rows1 > 0 ? S / n : 0.0;
+            double var_d = rows1 > 0 ? SS / n - mean_d * mean_d : 0.0;
+            if (var_d < 0) var_d = 0;
+            sh.gstat[threadIdx.x][0] = (float)mean_d;
+            sh.gstat[threadIdx.x][1] = (float)(1.0 / sqrt(var_d + 1e-5));
+        }
+        __syncthreads();
+    }
+    const bool bad = dispatch_op(o, sh, blk, blk + 1, o.kind == U_CONV1 ? gnb + blk * 64 * 2 : nullptr);
     if (bad && a.oflow) *a.oflow = 1;
 }
 
@@ -611,6 +666,37 @@ int hfa_unet_head(int B, int Tmax, const hfa_unet_op* ops, int nops, const float
     g_prof = nullptr;
     hipLaunchKernelGGL(unet_head_kernel, dim3(B), dim3(NT), 0, stream, a);
     return hfa::check_launch("hfa_unet_head");
+}
+
+long long hfa_unet_gn_doubles(int Tmax) {
+    return (long long)((Tmax + 63) / 64) * 64 * 2;            // row blocks of >= 64 rows, 64 groups, (sum, sumsq)
+}
+
+int hfa_unet_head_tiled(int B, int Tmax, const hfa_unet_op* host_ops, const hfa_unet_op* ops, int nops,
+                        const float* feats, long long f_bs, int f_ld, float* logits, long long l_bs, int l_ld,
+                        const int32_t* t_pad, float* workspace, long long ws_bs, double* gn_ws, long long gn_bs,
+                        int* oflow, hipStream_t stream) {
+    if (B < 0 || Tmax < 0 || nops < 1 || nops > 256 || !host_ops || !ops || !feats || !logits || !t_pad ||
+        !workspace || !gn_ws || gn_bs < hfa_unet_gn_doubles(Tmax) || f_ld % 4 || l_ld < 1 || l_ld % 4 ||
+        l_bs % 4 || ws_bs < 0 || ws_bs % 4 || (reinterpret_cast<uintptr_t>(feats) & 15) ||
+        (reinterpret_cast<uintptr_t>(logits) & 15) || (reinterpret_cast<uintptr_t>(workspace) & 15) || (f_bs % 4) ||
+        B > 65535) {
+        hfa::set_error("hfa_unet_head_tiled: bad arguments (B=%d Tmax=%d nops=%d f_ld=%d l_ld=%d gn_bs=%lld)", B,
+                       Tmax, nops, f_ld, l_ld, gn_bs);
+        return HFA_EINVAL;
+    }
+    if (B == 0 || Tmax == 0) return HFA_OK;
+    UnetArgs a{ops, nops, feats, f_bs, f_ld, logits, l_bs, l_ld, t_pad, workspace, ws_bs, Tmax, oflow, nullptr};
+    for (int k = 0; k < nops; ++k) {
+        const hfa_unet_op& u = host_ops[k];
+        const int rows = Tmax >> u.level;
+        const int nblk = (rows + op_block_rows(u.n) - 1) / op_block_rows(u.n);
+        const int nblk_gn = u.kind == U_CONV2 ? (rows + op_block_rows(u.cin[0]) - 1) / op_block_rows(u.cin[0]) : 0;
+        if (nblk < 1) continue;
+        hipLaunchKernelGGL(unet_op_kernel, dim3(nblk, B), dim3(NT), 0, stream, a, k, gn_ws, gn_bs, nblk_gn);
+        if (int rc = hfa::check_launch("hfa_unet_head_tiled")) return rc;
+    }
+    return HFA_OK;
 }
 
 }  // extern "C"

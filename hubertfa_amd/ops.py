@@ -296,6 +296,9 @@ UNET_NONE, UNET_INPUT, UNET_OUTPUT = -1, -2, -3
 _lib.register("hfa_unet_head", [_I_, _I_, _P_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_, _P_, _P_])
 _lib.register("hfa_unet_lds_bytes", [], restype=ctypes.c_longlong)
 _lib.register("hfa_unet_validate", [_P_, _I_, _LL_, _I_])
+_lib.register("hfa_unet_gn_doubles", [_I_], restype=ctypes.c_longlong)
+_lib.register("hfa_unet_head_tiled", [_I_, _I_, _P_, _P_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_, _P_,
+                                      _LL_, _P_, _P_])
 _lib.register("hfa_unet_profile", [_P_])
 
 
@@ -303,6 +306,27 @@ def unet_validate(table, ws_floats_per_row: int, l_ld: int):
     """Check a host op table (a ctypes array of UnetOp) before it is uploaded: ValueError (HFAArgumentError) naming
     the first bad op."""
     _lib.call("hfa_unet_validate", ctypes.addressof(table), len(table), ws_floats_per_row, l_ld)
+
+
+def unet_head_tiled(host_table, table, feats, logits, t_pad, workspace, ws_floats, flag, flops=0.0):
+    """The same op table as one launch per op, one workgroup per (row block, utterance) (unet.hip
+    hfa_unet_head_tiled); ``host_table`` the ctypes UnetOp array the device ``table`` was made from."""
+    B, Tmax, _ = feats.shape
+    _need(feats, torch.float32, "feats", contiguous=False)
+    _need(logits, torch.float32, "logits", contiguous=False)
+    _need(t_pad, torch.int32, "t_pad")
+    if feats.stride(2) != 1 or logits.stride(2) != 1 or logits.stride(1) % 4 or logits.data_ptr() % 16:
+        raise ValueError("unet_head_tiled: contiguous rows, logits rows 16-B aligned")
+    gn_bs = int(_lib.lib().hfa_unet_gn_doubles(Tmax))
+    gn = torch.empty((B, gn_bs), dtype=torch.float64, device=feats.device)
+
+    def launch():
+        _lib.call("hfa_unet_head_tiled", B, Tmax, ctypes.addressof(host_table), _ptr(table), len(host_table),
+                  _ptr(feats), feats.stride(0), feats.stride(1), _ptr(logits), logits.stride(0), logits.stride(1),
+                  _ptr(t_pad), _ptr(workspace), ws_floats, _ptr(gn), gn_bs, _ptr(flag), _stream(feats.device))
+    if PROBE is None:
+        return launch()
+    PROBE("unet_op_kernel", flops, launch)
 
 
 def unet_head(table, nops, feats, logits, t_pad, workspace, ws_floats, flag, flops=0.0):

@@ -275,21 +275,27 @@ class FusedPlan:
             if o["ln"] is not None:
                 r.ln_gamma, r.ln_beta = o["ln"][0].data_ptr(), o["ln"][1].data_ptr()
         ops_unet_validate(table, self.ws_floats_per_row, self.out_ld)
+        self.host_table = table
         raw = bytes(table)
         self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(c.dev)
         self.nops = len(ops)
         self.out_n = out_n
         self.ops = ops
 
-    def __call__(self, x: torch.Tensor, t_pad, flag) -> torch.Tensor:
-        """x [B, Tmax, C_in] (rows >= t_pad[b] zero) -> logits [B, Tmax, V+2] (rows >= t_pad[b] not written)."""
+    def __call__(self, x: torch.Tensor, t_pad, flag, tiled: bool = False) -> torch.Tensor:
+        """x [B, Tmax, C_in] (rows >= t_pad[b] zero) -> logits [B, Tmax, V+2] (rows >= t_pad[b] not written).
+        ``tiled``: one launch per op over (row block, utterance) workgroups instead of one workgroup per utterance."""
         from .hubert import dev_lengths
         B, Tmax, _ = x.shape
         logits = torch.empty((B, Tmax, self.out_ld), dtype=torch.float32, device=x.device)
         ws = torch.empty((B, Tmax * self.ws_floats_per_row), dtype=torch.float32, device=x.device)
         tp = dev_lengths(t_pad, x.device)
-        ops.unet_head(self.table, self.nops, x, logits, tp, ws, Tmax * self.ws_floats_per_row, flag,
-                      flops=self.flops(t_pad))
+        if tiled:
+            ops.unet_head_tiled(self.host_table, self.table, x, logits, tp, ws, Tmax * self.ws_floats_per_row, flag,
+                                flops=self.flops(t_pad))
+        else:
+            ops.unet_head(self.table, self.nops, x, logits, tp, ws, Tmax * self.ws_floats_per_row, flag,
+                          flops=self.flops(t_pad))
         return logits[:, :, :self.out_n]
 
     def flops(self, t_pad) -> float:
@@ -424,6 +430,10 @@ class LatticeHead:
         """x [B, T_pad, C_in] -> logits [B, T_pad, V+2].  Split precision: utterances of up to FusedPlan.MAX_T padded
         frames run on the fused kernel (one workgroup each), longer ones on the chip-wide launches; the choice
         depends on an utterance's own length only, so its result does not depend on the batch."""
+        if self.ctx.precision == "split" and self.use_tiled and self.fused is not None:
+            B, T = x.shape[0], x.shape[1]
+            return self.fused(x, [int(v) for v in t_pad] if t_pad is not None else [T] * B, self.ctx.flag,
+                              tiled=True)
         fp = self.fused if self.ctx.precision == "split" and self.use_fused else None
         if fp is not None:
             B, T = x.shape[0], x.shape[1]
@@ -445,6 +455,7 @@ class LatticeHead:
         return self._chipwide(x, t_pad)
 
     use_fused = __import__("os").environ.get("HFA_UNET_FUSED", "0") == "1"   # (A/B switch: 1 = the fused kernel)
+    use_tiled = __import__("os").environ.get("HFA_UNET_TILED", "0") == "1"   # (A/B: 1 = the op engine, per-op launches)
 
     def _chipwide(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
         if self.ctx.use_split(self.head_ws):

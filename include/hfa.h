@@ -247,6 +247,16 @@ int hfa_unet_head(int B, int Tmax, const hfa_unet_op* ops, int nops, const float
  * destination with n <= l_ld, and every slot access inside ws_floats_per_row floats per Tmax row (a level-l tensor of
  * row width ld uses ceil(ld / 2^l) of them).  HFA_OK or HFA_EINVAL with hfa_last_error() naming the op. */
 int hfa_unet_validate(const hfa_unet_op* host_ops, int nops, long long ws_floats_per_row, int l_ld);
+/* The same op table as one launch PER OP, one workgroup per (row block, utterance): row blocks of 128 rows for
+ * n <= 192, 64 above.  host_ops is the table in host memory (the launch grid of each op is planned from it), ops the
+ * same table in device memory.  gn_ws: per-utterance GroupNorm partials (f64, gn_bs >= hfa_unet_gn_doubles(Tmax)
+ * doubles apart), written by each first conv and summed in row-block order by its second conv (deterministic,
+ * independent of the batch).  Other arguments as hfa_unet_head. */
+long long hfa_unet_gn_doubles(int Tmax);
+int hfa_unet_head_tiled(int B, int Tmax, const hfa_unet_op* host_ops, const hfa_unet_op* ops, int nops,
+                        const float* feats, long long f_bs, int f_ld, float* logits, long long l_bs, int l_ld,
+                        const int32_t* t_pad, float* workspace, long long ws_bs, double* gn_ws, long long gn_bs,
+                        int* oflow, hipStream_t stream);
 /* LDS bytes the fused kernel's workgroup uses (diagnostics). */
 long long hfa_unet_lds_bytes(void);
 /* Diagnostics: the calling thread's next hfa_unet_head launch writes workgroup 0's s_memrealtime (100 MHz) at the

@@ -166,6 +166,14 @@ int main() {
         CHECK(hfa_unet_head(1, 64, dops, 3, fp, 64 * 768, 768, fmis, 64 * 68, 68, ip, fp, 4096, flag, st), "unet logits misaligned");
         CHECK(hfa_unet_head(-1, 64, dops, 3, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, flag, st), "unet B<0");
         CHECK(hfa_unet_validate(nullptr, 3, 128, 68), "unet_validate null");
+        double* gw = reinterpret_cast<double*>(0x100000);
+        const long long gb = hfa_unet_gn_doubles(64);
+        CHECK(hfa_unet_head_tiled(1, 64, nullptr, dops, 3, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, gw, gb,
+                                  flag, st), "unet_tiled null host table");
+        CHECK(hfa_unet_head_tiled(1, 64, dops, dops, 3, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, gw, gb - 1,
+                                  flag, st), "unet_tiled short GroupNorm workspace");
+        CHECK(hfa_unet_head_tiled(1, 64, dops, dops, 3, fp, 64 * 768, 768, fmis, 64 * 68, 68, ip, fp, 4096, gw, gb,
+                                  flag, st), "unet_tiled logits misaligned");
         hfa_unet_op op;
         std::memset(&op, 0, sizeof(op));
         op.kind = 0; op.n = 64; op.groups = 16; op.nseg = 1; op.res = HFA_UNET_NONE; op.dst = 0;

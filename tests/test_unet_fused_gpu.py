@@ -110,3 +110,77 @@ def test_fused_other_encoder_widths(input_dims):
     x = _feats(ua, [216], 216, seed=3)
     e = float((head.logits(x) - head._chipwide(x)).abs().max())
     assert e < 2e-4, e
+
+
+# ---- the tiled form (hfa_unet_head_tiled: one launch per op, one workgroup per row block and utterance) ----------
+
+def _tiled(head, x, tps):
+    return head.fused(x, tps, head.ctx.flag, tiled=True)
+
+
+@pytest.mark.parametrize("tps", [[864], [864, 216, 8], [208, 432], [2304, 512]])
+def test_tiled_matches_chipwide(tps):
+    ua, head = _head()
+    Tmax = max(tps)
+    x = _feats(ua, tps, Tmax, seed=len(tps) + 40)
+    out = _tiled(head, x, tps)
+    ref = head._chipwide(x, t_pad=tps if len(set(tps)) > 1 else None)
+    for b, t in enumerate(tps):
+        e = float((out[b, :t] - ref[b, :t]).abs().max())
+        print(f"T={t}: tiled vs chip-wide max |diff| {e:.2e}")
+        assert e < 2e-4
+
+
+def test_tiled_vs_reference_golden():
+    """unet_head.npz (the reference UNetBackbone + head at T = 203, 862) through the tiled launches."""
+    ua, head = _head()
+    z = np.load(os.path.join(GOLDEN, "unet_head.npz"))
+    from hubertfa_amd import synth
+    for T in (203, 862):
+        x = synth.rng(31 + T).standard_normal((1, T, ua.input_dims)).astype(np.float32)
+        Tp = head.padded_len(T)
+        xp = np.zeros((1, Tp, ua.input_dims), np.float32)
+        xp[:, :T] = x
+        lg = _tiled(head, torch.from_numpy(xp).cuda(), [Tp])[0, :T].cpu().numpy()
+        e = float(np.abs(lg - z[f"T{T}_logits"]).max())
+        print(f"tiled unet T={T}: max err vs the reference {e:.2e}")
+        assert e < 2e-4
+
+
+def test_tiled_batch_invariance_and_determinism():
+    """Each row equals its one-utterance run bit for bit (GroupNorm partials summed in row-block order), and two
+    runs agree bit for bit."""
+    ua, head = _head()
+    tps = [432, 864, 120]
+    x = _feats(ua, tps, 864, seed=9)
+    batch = _tiled(head, x, tps)
+    again = _tiled(head, x, tps)
+    for b, t in enumerate(tps):                      # (rows past t_pad[b] are not written)
+        assert torch.equal(batch[b, :t], again[b, :t])
+    for b, t in enumerate(tps):
+        alone = _tiled(head, x[b:b + 1, :t].contiguous(), [t])
+        assert torch.equal(batch[b, :t], alone[0]), f"row {b} differs from its one-utterance run"
+
+
+def test_tiled_through_logits_switch():
+    """LatticeHead.logits routes to the tiled launches when use_tiled is set (the HFA_UNET_TILED switch)."""
+    ua, head = _head()
+    x = _feats(ua, [864, 432], 864, seed=5)
+    ref = head._chipwide(x, t_pad=[864, 432])
+    head.use_tiled = True
+    try:
+        out = head.logits(x, t_pad=[864, 432])
+    finally:
+        head.use_tiled = False
+    assert float((out[0] - ref[0]).abs().max()) < 2e-4 and float((out[1, :432] - ref[1, :432]).abs().max()) < 2e-4
+
+
+def test_tiled_range_flag():
+    ua, head = _head()
+    x = _feats(ua, [64], 64)
+    x[0, 3, 5] = 1e6
+    head.ctx.flag.zero_()
+    _tiled(head, x, [64])
+    torch.cuda.synchronize()
+    assert int(head.ctx.flag.item()) == 1
+    head.ctx.flag.zero_()
