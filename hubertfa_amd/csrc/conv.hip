@@ -11,8 +11,11 @@
 // re-reading 65 MB, so:
 //   pass 1 (stats):  conv0 on the fly, per-chunk per-channel f64 sum / sum-of-squares partials (no output);
 //   pass 2 (reduce): mean / rstd per (batch, channel);
-//   pass 3 (apply):  conv0 again (bit-identical explicit fmaf chain), normalise, GELU, one coalesced
-//                    channels-last store [B, T0, 512] that conv1's implicit GEMM reads directly.
+//   pass 3 (apply):  conv0 again, normalise, GELU, channels-last split-plane store [B, T0, 512] that conv1's
+//                    implicit GEMM reads directly.  Split-plane output (the encoder's default path): the conv on
+//                    the f16 MFMA with the three split products packed in one K step (conv0_packed_kernel); f32
+//                    output: the explicit fmaf chain on the VALU (conv0_apply_kernel).
+// (Since round 3 passes 1-2 are the lag-product statistics below; the conv re-run is hfa_conv0_tuning mode 1.)
 #include "hfa_common.h"
 
 namespace {
@@ -408,7 +411,127 @@ __global__ __launch_bounds__(MNT) void conv0_apply_mfma_kernel(int N, int T0, co
     if (bad && oflow) *oflow = 1;
 }
 
-thread_local int g_conv0_mode = 0;   // hfa_conv0_tuning: 0 lag-product stats (default), 1 round 1, 2 MFMA apply
+// ---- conv0 on the f16 MFMA, the three split products packed in one K = 32 step (the split-plane apply pass) -------
+// The 10-tap conv of 16 channels x 16 frames is ONE v_mfma_f32_16x16x32_f16: A (rows = channels) holds
+// [2^11 w1 (taps 0-9) | w2 (taps 0-9) | w1 (taps 0-9) | 0 0], B (columns = frames) [x1 | x1 | x2 | 0 0], with
+// w = w1 + 2^-11 w2 and x = x1 + 2^-11 x2 the split-f16 pairs of gemm.hip, so D = 2^11 w1 x1 + w2 x1 + w1 x2 =
+// 2^11 (w . x) to the scheme's 2^-22 (every f16 x f16 product exact in the f32 accumulator).  The accumulator starts
+// at -2^11 mean, so D = 2^11 (v - mean) and GroupNorm is one fma: D (rstd gamma 2^-11) + beta.  What is left on
+// the VALU is GroupNorm, GELU (hfa::gelu_fast, 14 ops), the plane split and the range check: ~21 VALU ops per output
+// against ~36 in conv0_apply8_kernel, whose explicit fmaf chain (and its 72 LDS reads per frame: the compiler
+// re-read the 10 samples for every channel) made that pass VALU-issue bound at ~4.4 TB/s.
+// Block: 8 waves over a CH-frame chunk.  The chunk's B columns are packed once into LDS (64 B per frame: one
+// ds_read_b128 per lane per 16 frames, conflict-free); wave w owns channels 64 w + [0, 64) as four 16-channel MFMA
+// blocks with the row map of conv0_apply_mfma_kernel (lane l then holds channels 64 w + 32 p + 8 (l >> 4) + [0, 8)
+// of frame l & 15 for p = 0, 1: one 16-B piece per plane) and walks the chunk's 16 frame groups.  |w| >= 32
+// overflows 2^11 w1 to inf, which the output check flags (the range guard then re-runs the batch on the f32 path,
+// whose conv0 is the exact VALU kernel).  The f32-output conv0 (hfa_conv0_f32) stays on conv0_apply_kernel.
+constexpr int PNT = 512;
+
+template <int MODE>
+__global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const float* __restrict__ x,
+                                                           long long x_bs, const float* __restrict__ w0,
+                                                           const float* __restrict__ stats,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ bias,
+                                                           _Float16* __restrict__ yh, long long y_bs, long long y_sp,
+                                                           int* __restrict__ oflow) {
+    __shared__ __attribute__((aligned(16))) _Float16 bcol[CH * 32];   // [frame][32 k-slots]
+    const int b = blockIdx.y, chunk = blockIdx.x;
+    const int t0 = chunk * CH;
+    const int nt = min(CH, T0 - t0);
+    {   // pack: thread (frame f, half h) splits samples 5 (t0 + f) + 5 h + [0, 5) into slots k, 10 + k and 20 + k
+        const int f = threadIdx.x >> 1, h = threadIdx.x & 1;
+        const float* xb = x + b * x_bs + (long long)(t0 + f) * ST + 5 * h;
+        const long long rem = (long long)N - ((long long)(t0 + f) * ST + 5 * h);   // samples left in the row
+        _Float16* col = bcol + f * 32;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const float v = (f < nt && i < rem) ? xb[i] : 0.0f;
+            const _Float16 v1 = (_Float16)v;
+            const _Float16 v2 = (_Float16)((v - (float)v1) * 2048.0f);
+            col[5 * h + i] = v1;
+            col[10 + 5 * h + i] = v1;
+            col[20 + 5 * h + i] = v2;
+        }
+        if (h) col[30] = col[31] = (_Float16)0.0f;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+    // A fragments: block 2p + q, row i = lane & 15 -> channel 64 wave + 32 p + 8 (i >> 2) + 4 q + (i & 3);
+    // k-slots 8 g + [0, 8)
+    f16x8 af[4];
+    bool wbad = false;
+#pragma unroll
+    for (int blk = 0; blk < 4; ++blk) {
+        const int i = j;
+        const int ch = 64 * wave + 32 * (blk >> 1) + 8 * (i >> 2) + 4 * (blk & 1) + (i & 3);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = 8 * g + e;
+            const int tap = k < 10 ? k : k < 20 ? k - 10 : k < 30 ? k - 20 : 0;
+            const float w = k < 30 ? w0[ch * KW + tap] : 0.0f;
+            const _Float16 w1 = (_Float16)w;
+            const float w1f = (float)w1;
+            wbad |= !(__builtin_fabsf(w) < 32.0f);
+            af[blk][e] = k < 10 ? (_Float16)(w1f * 2048.0f) : k < 20 ? (_Float16)((w - w1f) * 2048.0f) : k < 30 ? w1
+                                                                                                               : (_Float16)0.0f;
+        }
+    }
+    // per-channel constants of the lane's 16 channels: c = 8 p + e <-> channel 64 wave + 32 p + 8 g + e
+    float cinit[16], sc[16], sh[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int ch = 64 * wave + 32 * (c >> 3) + 8 * g + (c & 7);
+        if (MODE == 0) {
+            cinit[c] = -2048.0f * stats[(b * C0 + ch) * 2];
+            sc[c] = stats[(b * C0 + ch) * 2 + 1] * gamma[ch] * (1.0f / 2048.0f);   // rstd gamma 2^-11
+            sh[c] = beta[ch];
+        } else {
+            cinit[c] = 0.0f;
+            sc[c] = 1.0f / 2048.0f;
+            sh[c] = bias ? bias[ch] : 0.0f;
+        }
+    }
+    __syncthreads();
+    _Float16* yb = yh + b * y_bs + (long long)t0 * C0 + 64 * wave + 8 * g;
+    bool bad = wbad;
+    for (int f0 = 0; f0 < nt; f0 += 16) {
+        const f16x8 bx = *reinterpret_cast<const f16x8*>(bcol + (f0 + j) * 32 + 8 * g);
+        f32x4 d[4];
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) {
+            const int p = blk >> 1, q = blk & 1;
+            const f32x4 c0 = {cinit[8 * p + 4 * q], cinit[8 * p + 4 * q + 1], cinit[8 * p + 4 * q + 2],
+                              cinit[8 * p + 4 * q + 3]};
+            d[blk] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[blk], bx, c0, 0, 0, 0);
+        }
+        const bool live = f0 + j < nt;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            f16x8 h1, h2;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int c = 8 * p + e;
+                float v = fmaf(d[2 * p + (e >> 2)][e & 3], sc[c], sh[c]);
+                if (MODE == 0) v = hfa::gelu_fast(v);
+                asm volatile("" : "+v"(v));   // split the rounded f32 value: no fusing its last fma into the cvt
+                bad |= live && !(__builtin_fabsf(v) < 65504.0f);
+                h1[e] = (_Float16)v;
+                h2[e] = (_Float16)((v - (float)h1[e]) * 2048.0f);
+            }
+            if (live) {
+                _Float16* dst = yb + (long long)(f0 + j) * C0 + 32 * p;
+                *reinterpret_cast<f16x8*>(dst) = h1;
+                *reinterpret_cast<f16x8*>(dst + y_sp) = h2;
+            }
+        }
+    }
+    if (bad && oflow) *oflow = 1;
+}
+
+thread_local int g_conv0_mode = 0;   // hfa_conv0_tuning: 0 packed f16 MFMA apply (default), 1 round 1, 2 f32-MFMA
+                                     // apply, 3 VALU apply (conv0_apply8_kernel)
 
 }  // namespace
 
@@ -452,7 +575,10 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
             hipLaunchKernelGGL(conv0_reduce_kernel, dim3(C0 / 64, B), dim3(NT), 0, stream, T0, nchunk, part, eps,
                                stats, t0_len);
         }
-        if (outs && vec8 && g_conv0_mode == 2)
+        if (outs && vec8 && g_conv0_mode == 0)
+            hipLaunchKernelGGL((conv0_packed_kernel<0>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0, stats,
+                               gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
+        else if (outs && vec8 && g_conv0_mode == 2)
             hipLaunchKernelGGL((conv0_apply_mfma_kernel<0>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
         else if (outs && vec8)
@@ -464,6 +590,9 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
         else
             hipLaunchKernelGGL((conv0_apply_kernel<0, false>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, y, y_bs, y_sp, oflow);
+    } else if (outs && vec8 && g_conv0_mode == 0) {
+        hipLaunchKernelGGL((conv0_packed_kernel<1>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0, nullptr, nullptr,
+                           nullptr, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
     } else if (outs && vec8 && g_conv0_mode == 2) {
         hipLaunchKernelGGL((conv0_apply_mfma_kernel<1>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, nullptr,
                            nullptr, nullptr, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
@@ -501,13 +630,14 @@ int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w
                         t0_len, stream);
 }
 
-// Kernel choice for A/B timing and the parity tests: 0 (default) the lag-product statistics and conv0_apply8_kernel,
-// 1 the round-1 passes (the conv re-run on the VALU for the statistics), 2 the lag-product statistics with the MFMA
-// apply pass (bit-identical to 0; measured 0.575-0.620 vs 0.566-0.571 ms per batch, scripts/conv0_bench.py).  Per
-// calling thread.
+// Kernel choice for A/B timing and the parity tests (split-plane output; the f32 output is always the VALU kernel):
+// 0 (default) the lag-product statistics and the packed f16-MFMA apply pass (conv0_packed_kernel), 1 the round-1
+// passes (the conv re-run on the VALU for the statistics, conv0_apply8_kernel), 2 the lag-product statistics with the
+// f32-MFMA apply pass (bit-identical to 3; measured 0.575-0.620 vs 0.566-0.571 ms per batch, scripts/conv0_bench.py),
+// 3 the lag-product statistics with conv0_apply8_kernel (the round-2 default).  Per calling thread.
 int hfa_conv0_tuning(int mode) {
-    if (mode < 0 || mode > 2) {
-        hfa::set_error("hfa_conv0_tuning: mode %d is not 0, 1 or 2", mode);
+    if (mode < 0 || mode > 3) {
+        hfa::set_error("hfa_conv0_tuning: mode %d is not 0, 1, 2 or 3", mode);
         return HFA_EINVAL;
     }
     g_conv0_mode = mode;

@@ -1,4 +1,5 @@
-"""conv0 + GroupNorm + GELU (split-plane output) at the bench geometry, MFMA conv vs the VALU kernels (GPU box).
+"""conv0 + GroupNorm + GELU (split-plane output) at the bench geometry, the apply-pass variants (GPU box):
+mode 0 packed f16 MFMA (default), 3 VALU (round 2), 2 f32 MFMA, 1 round-1 statistics.
 python scripts/conv0_bench.py [--reps 20] [--B 32] [--seconds 10]"""
 import argparse
 import os
@@ -26,7 +27,9 @@ def main():
     out = torch.empty(2, args.B, T0, 512, dtype=torch.float16, device=d)
     ws = torch.empty(_lib.lib().hfa_conv0_workspace_bytes(args.B, N), dtype=torch.uint8, device=d)
     nbytes = args.B * (4.0 * N + 4.0 * 512 * T0)
-    for mode in (0, 2, 1, 0, 2, 1):
+    names = {0: 'lag-product stats + packed f16-MFMA apply', 1: 'round-1: VALU stats + VALU apply',
+             2: 'lag-product stats + f32-MFMA apply', 3: 'lag-product stats + VALU apply'}
+    for mode in (0, 3, 2, 1, 0, 3, 2, 1):
         _lib.call("hfa_conv0_tuning", mode)
         fn = lambda: ops.conv0(x, w0, gamma=gam, beta=bet, out=out, workspace=ws, out_split=True)  # noqa: E731
         for _ in range(3):
@@ -39,7 +42,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.reps
-        print(f"mode {mode} ({['lag-product stats + VALU apply', 'round-1: VALU stats + VALU apply', 'lag-product stats + MFMA apply'][mode]}): {ms:.3f} ms per batch (stats + reduce + apply), "
+        print(f"mode {mode} ({names[mode]}): {ms:.3f} ms per batch (stats + reduce + apply), "
               f"{nbytes / ms / 1e6:.0f} GB/s of algorithmic bytes", flush=True)
     _lib.call("hfa_conv0_tuning", 0)
 

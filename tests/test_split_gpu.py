@@ -196,7 +196,7 @@ def test_layernorm_split_output(C, act, varlen):
 
 
 def test_conv0_split_output_matches_f32():
-    from hubertfa_amd import ops
+    from hubertfa_amd import ops, _lib
     d = torch.device("cuda")
     B, N = 2, 16000
     x = _r(B, N, seed=8).to(d)
@@ -204,19 +204,29 @@ def test_conv0_split_output_matches_f32():
     g, bb = (1 + 0.1 * _r(512, seed=10)).to(d), (0.1 * _r(512, seed=11)).to(d)
     y32 = ops.conv0(x, w0, gamma=g, beta=bb)
     ys = ops.conv0(x, w0, gamma=g, beta=bb, out_split=True)
-    hi = ys[0].float()
+    back = ys[0].double() + ys[1].double() / 2048.0
+    # the split output's conv runs on the f16 MFMA (3 exact split products, 2^-22 per operand), the f32 output's on
+    # the VALU fmaf chain; GroupNorm scales the conv's rounding by rstd * gamma
+    assert float((back - y32.double()).abs().max()) <= 2e-6 * float(y32.abs().max()) + 1e-9
+    _lib.call("hfa_conv0_tuning", 3)                   # the VALU apply pass: the f32 output's bits, split
+    try:
+        ys3 = ops.conv0(x, w0, gamma=g, beta=bb, out_split=True)
+    finally:
+        _lib.call("hfa_conv0_tuning", 0)
+    hi = ys3[0].float()
     assert torch.equal(hi, y32.half().float())
-    back = hi.double() + ys[1].double() / 2048.0
+    back = hi.double() + ys3[1].double() / 2048.0
     assert float((back - y32.double()).abs().max()) <= 2.0 ** -22 * float(y32.abs().max()) + 1e-9
 
 
 @pytest.mark.parametrize("N,lens", [(16000, None), (12345, None), (16000, [16000, 5003]), (97, None)])
 def test_conv0_mfma_bit_identical_to_valu(N, lens):
     """conv0's taps on v_mfma_f32_16x16x4_f32 (an exact k-ordered fmaf chain, mode 2) give the VALU kernel's bits
-    (mode 0; also the raw conv + bias planes of the LN-conv variant); with GroupNorm, the lag-product statistics
-    (modes 0, 2) and the conv-pass f64 sums (mode 1) agree to f32 rounding, so the normalised outputs agree to a few
-    ulps; the f32 and split outputs of one mode share the statistics and agree bitwise.  Ragged chunk tails and
-    per-row frame counts included."""
+    (mode 3; also the raw conv + bias planes of the LN-conv variant); with GroupNorm, the lag-product statistics
+    (modes 2, 3) and the conv-pass f64 sums (mode 1) agree to f32 rounding, so the normalised outputs agree to a few
+    ulps; the f32 and split outputs of one VALU/f32-MFMA mode share the statistics and agree bitwise.  The default
+    packed f16-MFMA apply pass (mode 0: three split products in one K step) agrees with them to the split scheme's
+    2^-22 per operand.  Ragged chunk tails and per-row frame counts included."""
     from hubertfa_amd import ops, _lib
     from hubertfa_amd.hubert import dev_lengths
     d = torch.device("cuda")
@@ -226,7 +236,7 @@ def test_conv0_mfma_bit_identical_to_valu(N, lens):
     g, bb = (1 + 0.1 * _r(512, seed=33)).to(d), (0.1 * _r(512, seed=34)).to(d)
     tl = None if lens is None else dev_lengths([(n - 10) // 5 + 1 for n in lens], d)
     outs = {}
-    for mode in (0, 1, 2):
+    for mode in (0, 1, 2, 3):
         _lib.call("hfa_conv0_tuning", mode)
         try:
             outs[mode] = (ops.conv0(x, w0, gamma=g, beta=bb, out_split=True, t0_len=tl),
@@ -235,16 +245,19 @@ def test_conv0_mfma_bit_identical_to_valu(N, lens):
         finally:
             _lib.call("hfa_conv0_tuning", 0)
     torch.cuda.synchronize()
-    for a, b in zip(outs[0], outs[2]):                             # MFMA taps = VALU fmaf chain, same statistics
+    for a, b in zip(outs[3], outs[2]):                             # MFMA taps = VALU fmaf chain, same statistics
         assert torch.equal(a, b)
-    assert torch.equal(outs[0][1], outs[1][1])                     # no statistics: bit-identical
-    for i in (0, 2):
-        a = outs[0][i].double() if i == 2 else outs[0][i][0].double() + outs[0][i][1].double() / 2048
-        b = outs[1][i].double() if i == 2 else outs[1][i][0].double() + outs[1][i][1].double() / 2048
-        if tl is not None:                                         # rows past a row's frames are don't-care
+    assert torch.equal(outs[3][1], outs[1][1])                     # no statistics: bit-identical
+
+    def val(o, i):
+        return o[i].double() if i == 2 else o[i][0].double() + o[i][1].double() / 2048
+
+    for m, i, tol in ((1, 0, 1e-5), (1, 2, 1e-5), (0, 0, 2e-6), (0, 1, 2e-6), (0, 2, 0.0)):
+        a, b = val(outs[m], i), val(outs[3], i)
+        if tl is not None and i != 1:                              # rows past a row's frames are don't-care
             a, b = a[:1], b[:1]
-        assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
-    for m in (0, 1, 2):
+        assert float((a - b).abs().max()) <= tol * max(1.0, float(b.abs().max())), (m, i)
+    for m in (1, 2, 3):
         assert torch.equal(outs[m][0][0].float(), outs[m][2].half().float())
 
 
