@@ -181,6 +181,7 @@ __global__ __launch_bounds__(C0) void conv0_gram_stats_kernel(int T0, int nchunk
 // OUTS: write the output as split-f16 planes (gemm.hip gemm_split_kernel operand: hi = f16(v), lo = f16((v - hi)
 // * 2^11), plane 1 at +y_sp halves) instead of f32 — the same bytes, and conv1 then runs on the f16 MFMA.
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int MODE, bool OUTS>
 __global__ __launch_bounds__(NT) void conv0_apply_kernel(int N, int T0, const float* __restrict__ x, long long x_bs,
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(MNT) void conv0_apply_mfma_kernel(int N, int T0, co
                 asm volatile("" : "+v"(v));   // split the rounded f32 value: no fusing its last multiply into the cvt
                 bad |= live && !(__builtin_fabsf(v) < 65504.0f);
                 h1[e] = (_Float16)v;
-                h2[e] = (_Float16)((v - (float)h1[e]) * 2048.0f);
+                h2[e] = (_Float16)fmaf((float)h1[e], -2048.0f, v * 2048.0f);   // exact: 2^11 (v - h1)
             }
             if (live) {
                 _Float16* dst = yb + (long long)(f0 + j) * C0 + 32 * p;
@@ -413,22 +414,31 @@ __global__ __launch_bounds__(MNT) void conv0_apply_mfma_kernel(int N, int T0, co
 
 // ---- conv0 on the f16 MFMA, the three split products packed in one K = 32 step (the split-plane apply pass) -------
 // The 10-tap conv of 16 channels x 16 frames is ONE v_mfma_f32_16x16x32_f16: A (rows = channels) holds
-// [2^11 w1 (taps 0-9) | w2 (taps 0-9) | w1 (taps 0-9) | 0 0], B (columns = frames) [x1 | x1 | x2 | 0 0], with
+// [2^11 w1 (taps 0-9) | w2 (taps 0-9) | w1 (taps 0-9) | mean pair], B (columns = frames) [x1 | x1 | x2 | -1 -1], with
 // w = w1 + 2^-11 w2 and x = x1 + 2^-11 x2 the split-f16 pairs of gemm.hip, so D = 2^11 w1 x1 + w2 x1 + w1 x2 =
-// 2^11 (w . x) to the scheme's 2^-22 (every f16 x f16 product exact in the f32 accumulator).  The accumulator starts
-// at -2^11 mean, so D = 2^11 (v - mean) and GroupNorm is one fma: D (rstd gamma 2^-11) + beta.  What is left on
-// the VALU is GroupNorm, GELU (hfa::gelu_fast, 14 ops), the plane split and the range check: ~21 VALU ops per output
-// against ~36 in conv0_apply8_kernel, whose explicit fmaf chain (and its 72 LDS reads per frame: the compiler
-// re-read the 10 samples for every channel) made that pass VALU-issue bound at ~4.4 TB/s.
+// 2^11 (w . x) to the scheme's 2^-22 (every f16 x f16 product exact in the f32 accumulator).  Slots 30 and 31 carry
+// 2^11 mean as an f16 pair (A) against -1 (B), so D = 2^11 (v - mean) and GroupNorm is one fma: D (rstd gamma
+// 2^-11) + beta (|mean| >= 32 overflows the pair and is flagged like |w| >= 32).  What is left on the VALU is
+// GroupNorm, GELU (hfa::gelu_fast, 13 ops), the plane split (one v_cvt_pk_f16_f32 and two v_fma_mix per pair) and a
+// packed-f16 range check: ~18 VALU ops per output against ~36 in conv0_apply8_kernel, whose explicit fmaf chain (and
+// its 72 LDS reads per frame: the compiler re-read the 10 samples for every channel) made that pass VALU-issue bound.
 // Block: 8 waves over a CH-frame chunk.  The chunk's B columns are packed once into LDS (64 B per frame: one
 // ds_read_b128 per lane per 16 frames, conflict-free); wave w owns channels 64 w + [0, 64) as four 16-channel MFMA
 // blocks with the row map of conv0_apply_mfma_kernel (lane l then holds channels 64 w + 32 p + 8 (l >> 4) + [0, 8)
 // of frame l & 15 for p = 0, 1: one 16-B piece per plane) and walks the chunk's 16 frame groups.  |w| >= 32
 // overflows 2^11 w1 to inf, which the output check flags (the range guard then re-runs the batch on the f32 path,
 // whose conv0 is the exact VALU kernel).  The f32-output conv0 (hfa_conv0_f32) stays on conv0_apply_kernel.
+// Stores (STORE): the MFMA layout gives a store instruction 16 frames x 64 B; STORE 1 (default) passes each wave's
+// 16 x 64 channels through its own XOR-swizzled LDS tile so one instruction writes 8 frames x 128 B (whole lines),
+// STORE 2 through a block-wide double-buffered tile (one 1-KiB row per instruction, one barrier per group), STORE 0
+// stores straight from the accumulator layout.  Measured (scripts/conv0_bench.py, B = 32 x 10 s, conv0 in all):
+// STORE 0 0.51-0.56 ms, 1 0.457-0.466, 2 0.468; the VALU apply pass 0.53-0.55; a persistent-block form (next chunk's
+// samples prefetched into registers) 0.60-0.65.  Ablations of STORE 0: no plane stores 0.35 ms, no GELU 0.47.
 constexpr int PNT = 512;
 
-template <int MODE>
+// ABL (timing ablations only, hfa_conv0_tuning 5 / 6): 1 = no plane stores (the planes are folded into one register
+// and stored once per lane), 2 = no GELU.
+template <int MODE, int STORE, int ABL = 0>
 __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const float* __restrict__ x,
                                                            long long x_bs, const float* __restrict__ w0,
                                                            const float* __restrict__ stats,
@@ -438,6 +448,9 @@ __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const 
                                                            _Float16* __restrict__ yh, long long y_bs, long long y_sp,
                                                            int* __restrict__ oflow) {
     __shared__ __attribute__((aligned(16))) _Float16 bcol[CH * 32];   // [frame][32 k-slots]
+    // STORE 1: [wave][plane][row][8 chunks of 16 B]; STORE 2: [buf][plane][row][64 chunks of 16 B]
+    __shared__ __attribute__((aligned(16))) uint4 otile[STORE == 1 ? PNT / 64 : STORE == 2 ? 2 : 1][2]
+                                                       [STORE == 1 ? 16 * 8 : STORE == 2 ? 16 * 64 : 1];
     const int b = blockIdx.y, chunk = blockIdx.x;
     const int t0 = chunk * CH;
     const int nt = min(CH, T0 - t0);
@@ -455,13 +468,13 @@ __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const 
             col[10 + 5 * h + i] = v1;
             col[20 + 5 * h + i] = v2;
         }
-        if (h) col[30] = col[31] = (_Float16)0.0f;
+        if (h) col[30] = col[31] = (_Float16)-1.0f;   // against the mean's slots of A (zero in mode 1)
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
     // A fragments: block 2p + q, row i = lane & 15 -> channel 64 wave + 32 p + 8 (i >> 2) + 4 q + (i & 3);
     // k-slots 8 g + [0, 8)
     f16x8 af[4];
-    bool wbad = false;
+    bool bad = false;
 #pragma unroll
     for (int blk = 0; blk < 4; ++blk) {
         const int i = j;
@@ -473,60 +486,114 @@ __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const 
             const float w = k < 30 ? w0[ch * KW + tap] : 0.0f;
             const _Float16 w1 = (_Float16)w;
             const float w1f = (float)w1;
-            wbad |= !(__builtin_fabsf(w) < 32.0f);
-            af[blk][e] = k < 10 ? (_Float16)(w1f * 2048.0f) : k < 20 ? (_Float16)((w - w1f) * 2048.0f) : k < 30 ? w1
-                                                                                                               : (_Float16)0.0f;
+            bad |= !(__builtin_fabsf(w) < 32.0f);
+            af[blk][e] = k < 10 ? (_Float16)(w1f * 2048.0f) : k < 20 ? (_Float16)((w - w1f) * 2048.0f) : w1;
+        }
+        if (MODE == 0 && g == 3) {   // slots 30, 31: 2^11 mean as an f16 pair (hi + lo, 22 bits) against B = -1
+            const float m2 = 2048.0f * stats[(b * C0 + ch) * 2];
+            const _Float16 mh = (_Float16)m2;
+            af[blk][6] = mh;
+            af[blk][7] = (_Float16)(m2 - (float)mh);
+            bad |= !(__builtin_fabsf(m2) < 65504.0f);
+        } else if (g == 3) {
+            af[blk][6] = af[blk][7] = (_Float16)0.0f;
         }
     }
     // per-channel constants of the lane's 16 channels: c = 8 p + e <-> channel 64 wave + 32 p + 8 g + e
-    float cinit[16], sc[16], sh[16];
+    float sc[16], sh[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int ch = 64 * wave + 32 * (c >> 3) + 8 * g + (c & 7);
         if (MODE == 0) {
-            cinit[c] = -2048.0f * stats[(b * C0 + ch) * 2];
             sc[c] = stats[(b * C0 + ch) * 2 + 1] * gamma[ch] * (1.0f / 2048.0f);   // rstd gamma 2^-11
             sh[c] = beta[ch];
         } else {
-            cinit[c] = 0.0f;
             sc[c] = 1.0f / 2048.0f;
             sh[c] = bias ? bias[ch] : 0.0f;
         }
     }
     __syncthreads();
-    _Float16* yb = yh + b * y_bs + (long long)t0 * C0 + 64 * wave + 8 * g;
-    bool bad = wbad;
+    // Range check on the packed high planes: |v| >= 65520 rounds to inf, a NaN stays NaN, and h * 0 + acc turns
+    // either into a NaN that persists (the planes represent every |v| < 65520 exactly to the scheme's precision:
+    // the low plane then holds |v - h1| * 2^11 <= 2^15).  Frames past the chunk's nt come from zero samples: finite.
+    const f16x2 zero2 = {(_Float16)0.0f, (_Float16)0.0f};
+    f16x2 nanacc = zero2;
+    const float c2048 = 2048.0f;
+    unsigned abl_sink = 0;
+    int tb = 0;
+    _Float16* yb = yh + b * y_bs + (long long)t0 * C0;
     for (int f0 = 0; f0 < nt; f0 += 16) {
         const f16x8 bx = *reinterpret_cast<const f16x8*>(bcol + (f0 + j) * 32 + 8 * g);
         f32x4 d[4];
 #pragma unroll
-        for (int blk = 0; blk < 4; ++blk) {
-            const int p = blk >> 1, q = blk & 1;
-            const f32x4 c0 = {cinit[8 * p + 4 * q], cinit[8 * p + 4 * q + 1], cinit[8 * p + 4 * q + 2],
-                              cinit[8 * p + 4 * q + 3]};
-            d[blk] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[blk], bx, c0, 0, 0, 0);
-        }
-        const bool live = f0 + j < nt;
+        for (int blk = 0; blk < 4; ++blk)
+            d[blk] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[blk], bx, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-            f16x8 h1, h2;
+            unsigned h1[4], h2[4];   // f16 pairs
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int c = 8 * p + e;
-                float v = fmaf(d[2 * p + (e >> 2)][e & 3], sc[c], sh[c]);
-                if (MODE == 0) v = hfa::gelu_fast(v);
-                asm volatile("" : "+v"(v));   // split the rounded f32 value: no fusing its last fma into the cvt
-                bad |= live && !(__builtin_fabsf(v) < 65504.0f);
-                h1[e] = (_Float16)v;
-                h2[e] = (_Float16)((v - (float)h1[e]) * 2048.0f);
+            for (int e = 0; e < 8; e += 2) {
+                float v[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int c = 8 * p + e + u;
+                    v[u] = fmaf(d[2 * p + ((e + u) >> 2)][(e + u) & 3], sc[c], sh[c]);
+                    if (MODE == 0 && ABL != 2) v[u] = hfa::gelu_fast(v[u]);
+                    asm volatile("" : "+v"(v[u]));   // split the rounded f32 value: no fusing its last fma into the cvt
+                }
+                const f16x2 hp = __builtin_convertvector((f32x2){v[0], v[1]}, f16x2);   // one v_cvt_pk_f16_f32
+                nanacc = hp * zero2 + nanacc;   // stays 0 unless a high plane is inf / NaN (v_pk_fma_f16)
+                h1[e >> 1] = __builtin_bit_cast(unsigned, hp);
+                h2[e >> 1] = hfa::split_lo_pair(h1[e >> 1], v[0] * 2048.0f, v[1] * 2048.0f, c2048);
             }
-            if (live) {
-                _Float16* dst = yb + (long long)(f0 + j) * C0 + 32 * p;
-                *reinterpret_cast<f16x8*>(dst) = h1;
-                *reinterpret_cast<f16x8*>(dst + y_sp) = h2;
+            const uint4 o1 = make_uint4(h1[0], h1[1], h1[2], h1[3]), o2 = make_uint4(h2[0], h2[1], h2[2], h2[3]);
+            if (ABL == 1) {
+                abl_sink ^= o1.x ^ o1.y ^ o1.z ^ o1.w ^ o2.x ^ o2.y ^ o2.z ^ o2.w;
+            } else if (STORE == 1) {   // row j, 16-B chunk 4 p + g of the wave's 128-B row segment, XOR-swizzled
+                const int slot = j * 8 + ((4 * p + g) ^ (j & 7));
+                otile[wave][0][slot] = o1;
+                otile[wave][1][slot] = o2;
+            } else if (STORE == 2) {   // row j, chunk 8 wave + 4 p + g of the 1-KiB row, XOR-swizzled by the row
+                const int slot = j * 64 + ((8 * wave + 4 * p + g) ^ j);
+                otile[tb][0][slot] = o1;
+                otile[tb][1][slot] = o2;
+            } else if (f0 + j < nt) {
+                _Float16* dst = yb + (long long)(f0 + j) * C0 + 64 * wave + 32 * p + 8 * g;
+                *reinterpret_cast<uint4*>(dst) = o1;
+                *reinterpret_cast<uint4*>(dst + y_sp) = o2;
             }
         }
+        if (ABL != 1 && STORE == 1) {   // lane (row r = lane >> 3 + 8 hf, chunk c = lane & 7): 8 rows x 128 B
+            const int c = lane & 7;     // (wave-local tile: LDS ops of one wave complete in order, no barrier)
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int r = (lane >> 3) + 8 * hf;
+                const int slot = r * 8 + (c ^ (r & 7));
+                const uint4 v1 = otile[wave][0][slot], v2 = otile[wave][1][slot];
+                if (f0 + r < nt) {
+                    _Float16* dst = yb + (long long)(f0 + r) * C0 + 64 * wave + 8 * c;
+                    *reinterpret_cast<uint4*>(dst) = v1;
+                    *reinterpret_cast<uint4*>(dst + y_sp) = v2;
+                }
+            }
+        } else if (ABL != 1 && STORE == 2) {   // wave w stores rows 2 w, 2 w + 1: one 1-KiB row per instruction
+            __syncthreads();
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                const int r = 2 * wave + rr;
+                const int slot = r * 64 + (lane ^ r);
+                const uint4 v1 = otile[tb][0][slot], v2 = otile[tb][1][slot];
+                if (f0 + r < nt) {
+                    _Float16* dst = yb + (long long)(f0 + r) * C0 + 8 * lane;
+                    *reinterpret_cast<uint4*>(dst) = v1;
+                    *reinterpret_cast<uint4*>(dst + y_sp) = v2;
+                }
+            }
+            tb ^= 1;   // the other buffer's readers passed this group's barrier before anyone writes it again
+        }
     }
+    bad |= nanacc[0] != nanacc[0] || nanacc[1] != nanacc[1];
+    if (ABL == 1) *reinterpret_cast<unsigned*>(yb + 2 * threadIdx.x) = abl_sink;
     if (bad && oflow) *oflow = 1;
 }
 
@@ -575,9 +642,14 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
             hipLaunchKernelGGL(conv0_reduce_kernel, dim3(C0 / 64, B), dim3(NT), 0, stream, T0, nchunk, part, eps,
                                stats, t0_len);
         }
-        if (outs && vec8 && g_conv0_mode == 0)
-            hipLaunchKernelGGL((conv0_packed_kernel<0>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0, stats,
-                               gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
+#define HFA_PACKED(MODE_, STORE_, ABL_, STATS_)                                                                       \
+    hipLaunchKernelGGL((conv0_packed_kernel<MODE_, STORE_, ABL_>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0,     \
+                       STATS_, gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow)
+        if (outs && vec8 && g_conv0_mode == 0) HFA_PACKED(0, 1, 0, stats);
+        else if (outs && vec8 && g_conv0_mode == 4) HFA_PACKED(0, 0, 0, stats);
+        else if (outs && vec8 && g_conv0_mode == 5) HFA_PACKED(0, 0, 1, stats);
+        else if (outs && vec8 && g_conv0_mode == 6) HFA_PACKED(0, 0, 2, stats);
+        else if (outs && vec8 && g_conv0_mode == 7) HFA_PACKED(0, 2, 0, stats);
         else if (outs && vec8 && g_conv0_mode == 2)
             hipLaunchKernelGGL((conv0_apply_mfma_kernel<0>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
@@ -590,9 +662,8 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
         else
             hipLaunchKernelGGL((conv0_apply_kernel<0, false>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, y, y_bs, y_sp, oflow);
-    } else if (outs && vec8 && g_conv0_mode == 0) {
-        hipLaunchKernelGGL((conv0_packed_kernel<1>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0, nullptr, nullptr,
-                           nullptr, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
+    } else if (outs && vec8 && (g_conv0_mode == 0 || g_conv0_mode >= 4)) {   // the packed modes
+        HFA_PACKED(1, 1, 0, nullptr);
     } else if (outs && vec8 && g_conv0_mode == 2) {
         hipLaunchKernelGGL((conv0_apply_mfma_kernel<1>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, nullptr,
                            nullptr, nullptr, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
@@ -606,6 +677,7 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
         hipLaunchKernelGGL((conv0_apply_kernel<1, false>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, nullptr,
                            nullptr, nullptr, bias, y, y_bs, y_sp, oflow);
     }
+#undef HFA_PACKED
     return hfa::check_launch(fn);
 }
 }  // namespace
@@ -634,10 +706,12 @@ int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w
 // 0 (default) the lag-product statistics and the packed f16-MFMA apply pass (conv0_packed_kernel), 1 the round-1
 // passes (the conv re-run on the VALU for the statistics, conv0_apply8_kernel), 2 the lag-product statistics with the
 // f32-MFMA apply pass (bit-identical to 3; measured 0.575-0.620 vs 0.566-0.571 ms per batch, scripts/conv0_bench.py),
-// 3 the lag-product statistics with conv0_apply8_kernel (the round-2 default).  Per calling thread.
+// 3 the lag-product statistics with conv0_apply8_kernel (the round-2 default), 4 mode 0 with its stores straight
+// from the MFMA layout, 5 / 6 timing ablations of mode 4 (no plane stores; no GELU -- wrong outputs), 7 mode 0 with
+// its stores through a block-wide LDS tile.  Per calling thread.
 int hfa_conv0_tuning(int mode) {
-    if (mode < 0 || mode > 3) {
-        hfa::set_error("hfa_conv0_tuning: mode %d is not 0, 1, 2 or 3", mode);
+    if (mode < 0 || mode > 7) {
+        hfa::set_error("hfa_conv0_tuning: mode %d is not 0 .. 7", mode);
         return HFA_EINVAL;
     }
     g_conv0_mode = mode;

@@ -104,25 +104,39 @@ __device__ __forceinline__ float gelu_erf(float x) {
     return 0.5f * x * (1.0f + erf_nb(x * 0.70710678118654752440f));
 }
 
+// Low planes of two values whose high planes h (f16 pair, from one v_cvt_pk_f16_f32) are known: f16(2^11 v - 2^11 h)
+// for each half, as two v_fma_mix ops that read h's halves in place (the compiler re-converts each value to a
+// scalar f16 first).  x2048 = 2^11 v (exact); the fma is exact (|v - h| <= half an f16 ulp of v), so its one
+// rounding to f16 equals the round-1 form f16((v - f32(h)) * 2^11) bit for bit.  c2048 = 2048.0f in a register
+// (gfx9 VOP3P takes no literal).
+__device__ __forceinline__ unsigned split_lo_pair(unsigned h, float x2048_0, float x2048_1, float c2048) {
+    unsigned r;
+    asm("v_fma_mixlo_f16 %0, -%1, %4, %2 op_sel_hi:[1,0,0]\n\t"
+                 "v_fma_mixhi_f16 %0, -%1, %4, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                 : "=&v"(r)
+                 : "v"(h), "v"(x2048_0), "v"(x2048_1), "v"(c2048));
+    return r;
+}
+
 // The GELU of every fused epilogue.  With E = erfc(|x| / sqrt 2) = 1 - erf(|x| / sqrt 2):
 //   GELU(x) = x - (x / 2) E for x >= 0 and (x / 2) E for x < 0, i.e. max(x, 0) - |x / 2| E  (one fma),
-// and E = exp2(q(a)), a = min(|x|, 3.95 sqrt 2), q(a) = a R8(a) fitted to log2 erfc(a / sqrt 2) on [0, 3.95 sqrt 2]
-// (erfc-weighted least squares toward minimax, scripts/fit_gelu_erf.py): 14 VALU ops (|x| and -|x/2| are source
+// and E = exp2(q(a)), a = min(|x|, 3.95 sqrt 2), q(a) = a R7(a) fitted to log2 erfc(a / sqrt 2) on [0, 3.95 sqrt 2]
+// (erfc-weighted least squares toward minimax, scripts/fit_gelu_erf.py): 13 VALU ops (|x| and -|x/2| are source
 // modifiers; one v_exp_f32), against 19 for the round-1 form 0.5 x (1 + sign(z)(1 - exp(-q))).  In f32 it is within
-// 1.2 |x| 2^-24 of the f64 GELU everywhere (the f32 formula 0.5 x (1 + erf) with a correctly rounded erf: 2 |x|
-// 2^-24, its cancellation floor) and within 4.1 ulp where x > -1.5 (scripts/fit_gelu_erf.py emulates it).  Past the
-// clamp E stays erfc(3.95) = 1.9e-8, i.e. an error <= 1e-8 |x|, inside the same bound.
+// 1.21 |x| 2^-24 of the f64 GELU everywhere (the f32 formula 0.5 x (1 + erf) with a correctly rounded erf: 1.7 |x|
+// 2^-24, its cancellation floor) and within 4.9 ulp where x > -1.5 (scripts/fit_gelu_erf.py emulates it; degree 8
+// buys only 1.19 / 4.0).  Past the clamp E stays erfc(3.95) = 1.9e-8, i.e. an error <= 1e-8 |x|, inside the same
+// bound.  x = +inf gives NaN (the range flags catch both).
 __device__ __forceinline__ float gelu_fast(float x) {
     const float a = fminf(fabsf(x), 5.58614357f);
-    float q = __uint_as_float(0x350df054u);
-    q = fmaf(q, a, __uint_as_float(0xb72439edu));
-    q = fmaf(q, a, __uint_as_float(0x389ff9cau));
-    q = fmaf(q, a, __uint_as_float(0xb9971b7eu));
-    q = fmaf(q, a, __uint_as_float(0x37b31b3bu));
-    q = fmaf(q, a, __uint_as_float(0x3be2ed41u));
-    q = fmaf(q, a, __uint_as_float(0xbd56c2cdu));
-    q = fmaf(q, a, __uint_as_float(0xbeeb1f2au));
-    q = fmaf(q, a, __uint_as_float(0xbf935762u));
+    float q = __uint_as_float(0xb64b3c2au);
+    q = fmaf(q, a, __uint_as_float(0x382ef466u));
+    q = fmaf(q, a, __uint_as_float(0xb94eba72u));
+    q = fmaf(q, a, __uint_as_float(0xb8e94e0eu));
+    q = fmaf(q, a, __uint_as_float(0x3be669ecu));
+    q = fmaf(q, a, __uint_as_float(0xbd56f121u));
+    q = fmaf(q, a, __uint_as_float(0xbeeb1e17u));
+    q = fmaf(q, a, __uint_as_float(0xbf935766u));
     const float e = __builtin_amdgcn_exp2f(a * q);
     return fmaf(-fabsf(0.5f * x), e, fmaxf(x, 0.0f));
 }

@@ -1,7 +1,7 @@
 """Fit of the GELU epilogue's erfc (hfa::gelu_fast in hubertfa_amd/csrc/hfa_common.h) and its f32 accuracy check.
 
 GELU(x) = max(x, 0) - |x / 2| E with E = erfc(|x| / sqrt 2) = exp2(q(a)), a = min(|x|, 3.95 sqrt 2),
-q(a) = a R8(a) ~ log2 erfc(a / sqrt 2), fitted by least squares weighted by the absolute error of E (erfc-weighted),
+q(a) = a R7(a) ~ log2 erfc(a / sqrt 2), fitted by least squares weighted by the absolute error of E (erfc-weighted),
 iteratively re-weighted toward minimax.  Prints the f32 hex coefficients (highest degree first, Horner order of the
 kernel) and the f32-emulated GELU error against fp64, next to the round-1/2 form 0.5 x (1 + sign(z)(1 - exp(-q(|z|)))).
 
@@ -34,8 +34,8 @@ def _irls(A, y, w, scale, iters):
     return c
 
 
-def fit(deg=8, n=400001, iters=30):
-    """q(a) = a R8(a) ~ log2 erfc(a / sqrt 2) on (0, 3.95 sqrt 2]; coefficients lowest degree first."""
+def fit(deg=7, n=400001, iters=30):
+    """q(a) = a R7(a) ~ log2 erfc(a / sqrt 2) on (0, 3.95 sqrt 2]; coefficients lowest degree first."""
     a = np.linspace(0, HI * S2, n)[1:]
     target = np.log2(erfc64(a / S2))
     A = np.vstack([a ** k for k in range(deg + 1)]).T
@@ -76,7 +76,7 @@ def gelu_round1(x, c):
 
 def main():
     r = fit()
-    print("coefficients of R8, highest degree first:")
+    print("coefficients of R7, highest degree first:")
     for k in r[::-1]:
         print(f"  {float(f32(k)): .9e}  0x{struct.unpack('<I', struct.pack('<f', f32(k)))[0]:08x}")
     x = np.concatenate([np.linspace(-12, 12, 2_000_001),

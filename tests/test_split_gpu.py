@@ -225,8 +225,9 @@ def test_conv0_mfma_bit_identical_to_valu(N, lens):
     (mode 3; also the raw conv + bias planes of the LN-conv variant); with GroupNorm, the lag-product statistics
     (modes 2, 3) and the conv-pass f64 sums (mode 1) agree to f32 rounding, so the normalised outputs agree to a few
     ulps; the f32 and split outputs of one VALU/f32-MFMA mode share the statistics and agree bitwise.  The default
-    packed f16-MFMA apply pass (mode 0: three split products in one K step) agrees with them to the split scheme's
-    2^-22 per operand.  Ragged chunk tails and per-row frame counts included."""
+    packed f16-MFMA apply pass (mode 0: three split products in one K step, stores through a per-wave LDS tile; modes
+    4 and 7 store straight from the MFMA layout or through a block-wide tile, the same bits) agrees with them to the
+    split scheme's 2^-22 per operand.  Ragged chunk tails and per-row frame counts included."""
     from hubertfa_amd import ops, _lib
     from hubertfa_amd.hubert import dev_lengths
     d = torch.device("cuda")
@@ -236,7 +237,7 @@ def test_conv0_mfma_bit_identical_to_valu(N, lens):
     g, bb = (1 + 0.1 * _r(512, seed=33)).to(d), (0.1 * _r(512, seed=34)).to(d)
     tl = None if lens is None else dev_lengths([(n - 10) // 5 + 1 for n in lens], d)
     outs = {}
-    for mode in (0, 1, 2, 3):
+    for mode in (0, 1, 2, 3, 4, 7):
         _lib.call("hfa_conv0_tuning", mode)
         try:
             outs[mode] = (ops.conv0(x, w0, gamma=g, beta=bb, out_split=True, t0_len=tl),
@@ -248,6 +249,9 @@ def test_conv0_mfma_bit_identical_to_valu(N, lens):
     for a, b in zip(outs[3], outs[2]):                             # MFMA taps = VALU fmaf chain, same statistics
         assert torch.equal(a, b)
     assert torch.equal(outs[3][1], outs[1][1])                     # no statistics: bit-identical
+    for m in (4, 7):                                               # the store layouts: the same bits
+        for a, b in zip(outs[0], outs[m]):
+            assert torch.equal(a, b)
 
     def val(o, i):
         return o[i].double() if i == 2 else o[i][0].double() + o[i][1].double() / 2048
