@@ -457,11 +457,23 @@ class LatticeHead:
     use_fused = __import__("os").environ.get("HFA_UNET_FUSED", "0") == "1"   # (A/B switch: 1 = the fused kernel)
     use_tiled = __import__("os").environ.get("HFA_UNET_TILED", "0") == "1"   # (A/B: 1 = the op engine, per-op launches)
 
+    unet_tile = int(__import__("os").environ.get("HFA_UNET_TILE", "0"))   # (A/B: a split-GEMM tile for the backbone)
+
     def _chipwide(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
-        if self.ctx.use_split(self.head_ws):
-            y, ys = self.backbone(x, t_pad, want_split=True)
+        if self.unet_tile:
+            from . import _lib
+            _lib.call("hfa_gemm_split_tuning", self.unet_tile)
+        try:
+            if self.ctx.use_split(self.head_ws):
+                y, ys = self.backbone(x, t_pad, want_split=True)
+            else:
+                y, ys = self.backbone(x, t_pad), None
+        finally:
+            if self.unet_tile:
+                _lib.call("hfa_gemm_split_tuning", 0)
+        if ys is not None:
             return self.ctx.linear(y, ys, self.head_wp, self.head_ws, self.head_bp)[0][:, :, :self.head_w.shape[0]]
-        return self.ctx.linear(self.backbone(x, t_pad), None, self.head_w, None, self.head_b)[0]
+        return self.ctx.linear(y, None, self.head_w, None, self.head_b)[0]
 
     @staticmethod
     def split(logits: torch.Tensor):

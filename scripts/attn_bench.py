@@ -35,7 +35,8 @@ def main():
             ops.attention(qkv, qkv[..., H * D:], qkv[..., 2 * H * D:], out, B=B, H=H, L=L, head_dim=D,
                           scale=D ** -0.5, q_bs=L * 3 * H * D, q_ld=3 * H * D, k_bs=L * 3 * H * D, k_ld=3 * H * D,
                           v_bs=L * 3 * H * D, v_ld=3 * H * D, o_bs=L * H * D, o_ld=H * D)
-        for tag, fn, nw in (("f32", go, 0), ("split", go_split, 0), ("spl4w", go_split, 4), ("spl8w", go_split, 8)):
+        for tag, fn, nw in (("f32", go, 0), ("split", go_split, 0), ("spl4w", go_split, 4), ("spl8w", go_split, 8),
+                            ("r2-4w", go_split, 104), ("r2-8w", go_split, 108), ("split", go_split, 0)):
             _lib.call("hfa_attention_split_tuning", nw)
             for _ in range(3):
                 fn()

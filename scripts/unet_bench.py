@@ -37,6 +37,21 @@ def main():
         print(f"head {prec}{' fused' if fused and prec == 'split' else ''}: {ms:.3f} ms per batch of {args.B} x {T} frames, {flops / ms / 1e9:.1f} TFLOP/s "
               f"({flops / 1e9:.1f} GFLOP)", flush=True)
     task.head.precision = "split"
+    task.head.use_fused = False
+    for tile in (0, 23, 19, 18, 17, 0):        # chip-wide backbone, forced split-GEMM tiles (gemm.hip SCFG index)
+        task.head.unet_tile = tile
+        for _ in range(3):
+            task.head.logits(x)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            task.head.logits(x)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.reps
+        print(f"head split chip-wide, backbone tile {tile}: {ms:.3f} ms per batch", flush=True)
+    task.head.unet_tile = 0
     task.head.use_fused = True
     for B in (1, 8, 32, 64):          # fused: one workgroup per utterance
         xb = x[:1].expand(B, -1, -1).contiguous()

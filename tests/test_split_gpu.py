@@ -452,6 +452,32 @@ def test_attention_split_waves_bit_identical(L):
         assert torch.equal(outs[0], outs[1])
 
 
+def test_attention_split_round2_body_agrees():
+    """The round-3 P split (RNE high plane + v_fma_mix remainder) and unrolled tile loop against the round-2 body
+    (truncated high plane; hfa_attention_split_tuning + 100): both within the split kernel's f64 error bar, and
+    within 5e-6 of each other (the two splits of P differ only in the last bits of p's representation)."""
+    from hubertfa_amd import ops, _lib
+    from hubertfa_amd.hubert import dev_lengths
+    B, H, L, D = 2, 3, 333, 64
+    qkv = _r(B, L, 3 * H * D, seed=17, scale=1.5)
+    ref = _attn_ref(qkv, B, L, H, D)
+    d = torch.device("cuda")
+    qs = ops.split(qkv.to(d))
+    outs = []
+    for nw in (4, 104, 8, 108):
+        _lib.call("hfa_attention_split_tuning", nw)
+        try:
+            o = torch.full((2, B, L, H * D), float("nan"), dtype=torch.float16, device=d)
+            ops.attention_split(qs, o, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5)
+            outs.append((o[0].double() + o[1].double() / 2048.0).cpu())
+        finally:
+            _lib.call("hfa_attention_split_tuning", 0)
+    for o in outs:
+        _close(o.float(), ref, 1e-4, 2e-5)
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])   # 4 vs 8 waves: the same bits
+    assert float((outs[0] - outs[1]).abs().max()) < 5e-6
+
+
 def test_attention_split_large_scores():
     """Peaked softmax (scores ~ +-60): the score's own f32-level rounding dominates both kernels' error; the split
     kernel stays within 2x the f32 MFMA kernel's error against f64."""
