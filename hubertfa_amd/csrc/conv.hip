@@ -432,13 +432,15 @@ __global__ __launch_bounds__(MNT) void conv0_apply_mfma_kernel(int N, int T0, co
 // 16 x 64 channels through its own XOR-swizzled LDS tile so one instruction writes 8 frames x 128 B (whole lines),
 // STORE 2 through a block-wide double-buffered tile (one 1-KiB row per instruction, one barrier per group), STORE 0
 // stores straight from the accumulator layout.  Measured (scripts/conv0_bench.py, B = 32 x 10 s, conv0 in all):
-// STORE 0 0.51-0.56 ms, 1 0.457-0.466, 2 0.468; the VALU apply pass 0.53-0.55; a persistent-block form (next chunk's
-// samples prefetched into registers) 0.60-0.65.  Ablations of STORE 0: no plane stores 0.35 ms, no GELU 0.47.
+// STORE 0 0.51-0.56 ms, 1 0.457-0.466 (0.440-0.443 with non-temporal stores, the default), 2 0.468; the VALU apply
+// pass 0.53-0.57; a persistent-block form (next chunk's samples prefetched into registers) 0.60-0.65.  Ablations:
+// STORE 0 without plane stores 0.33-0.35 ms, without GELU 0.47; STORE 1 without GELU 0.43.
 constexpr int PNT = 512;
 
-// ABL (timing ablations only, hfa_conv0_tuning 5 / 6): 1 = no plane stores (the planes are folded into one register
-// and stored once per lane), 2 = no GELU.
-template <int MODE, int STORE, int ABL = 0>
+// ABL (timing ablations only, hfa_conv0_tuning 5 / 6 / 9): 1 = no plane stores (the planes are folded into one
+// register and stored once per lane), 2 = no GELU.  NT: STORE 1's plane stores non-temporal (streaming; the 2.1 GB
+// per batch are far past the 256 MB Infinity Cache anyway): 0.466 -> 0.440 ms per batch (mode 8 = without).
+template <int MODE, int STORE, int ABL = 0, bool NT = true>
 __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const float* __restrict__ x,
                                                            long long x_bs, const float* __restrict__ w0,
                                                            const float* __restrict__ stats,
@@ -572,8 +574,14 @@ __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const 
                 const uint4 v1 = otile[wave][0][slot], v2 = otile[wave][1][slot];
                 if (f0 + r < nt) {
                     _Float16* dst = yb + (long long)(f0 + r) * C0 + 64 * wave + 8 * c;
-                    *reinterpret_cast<uint4*>(dst) = v1;
-                    *reinterpret_cast<uint4*>(dst + y_sp) = v2;
+                    if (NT) {   // non-temporal (streaming) stores
+                        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                        __builtin_nontemporal_store(u32x4{v1.x, v1.y, v1.z, v1.w}, reinterpret_cast<u32x4*>(dst));
+                        __builtin_nontemporal_store(u32x4{v2.x, v2.y, v2.z, v2.w}, reinterpret_cast<u32x4*>(dst + y_sp));
+                    } else {
+                        *reinterpret_cast<uint4*>(dst) = v1;
+                        *reinterpret_cast<uint4*>(dst + y_sp) = v2;
+                    }
                 }
             }
         } else if (ABL != 1 && STORE == 2) {   // wave w stores rows 2 w, 2 w + 1: one 1-KiB row per instruction
@@ -650,6 +658,10 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
         else if (outs && vec8 && g_conv0_mode == 5) HFA_PACKED(0, 0, 1, stats);
         else if (outs && vec8 && g_conv0_mode == 6) HFA_PACKED(0, 0, 2, stats);
         else if (outs && vec8 && g_conv0_mode == 7) HFA_PACKED(0, 2, 0, stats);
+        else if (outs && vec8 && g_conv0_mode == 8)
+            hipLaunchKernelGGL((conv0_packed_kernel<0, 1, 0, false>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0,
+                               stats, gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
+        else if (outs && vec8 && g_conv0_mode == 9) HFA_PACKED(0, 1, 2, stats);
         else if (outs && vec8 && g_conv0_mode == 2)
             hipLaunchKernelGGL((conv0_apply_mfma_kernel<0>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
@@ -708,10 +720,11 @@ int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w
 // f32-MFMA apply pass (bit-identical to 3; measured 0.575-0.620 vs 0.566-0.571 ms per batch, scripts/conv0_bench.py),
 // 3 the lag-product statistics with conv0_apply8_kernel (the round-2 default), 4 mode 0 with its stores straight
 // from the MFMA layout, 5 / 6 timing ablations of mode 4 (no plane stores; no GELU -- wrong outputs), 7 mode 0 with
-// its stores through a block-wide LDS tile.  Per calling thread.
+// its stores through a block-wide LDS tile, 8 mode 0 with plain (not non-temporal) stores, 9 a timing ablation of
+// mode 0 (no GELU).  Per calling thread.
 int hfa_conv0_tuning(int mode) {
-    if (mode < 0 || mode > 7) {
-        hfa::set_error("hfa_conv0_tuning: mode %d is not 0 .. 7", mode);
+    if (mode < 0 || mode > 9) {
+        hfa::set_error("hfa_conv0_tuning: mode %d is not 0 .. 9", mode);
         return HFA_EINVAL;
     }
     g_conv0_mode = mode;

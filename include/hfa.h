@@ -301,11 +301,12 @@ int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hip
 /* conv0 kernel choice for the split-plane output (per calling thread; the f32 output is always the VALU apply
  * pass): 0 = default: GroupNorm statistics from the wave's lag products (S_j, G_jk over the frames: 65 numbers per
  * utterance, f64) and the packed f16-MFMA apply pass (the three split products of the 10 taps in one K = 32 step,
- * stores through a per-wave LDS tile); 1 = the round-1 passes (the conv re-run for f64 sums of its outputs) with the
+ * stores through a per-wave LDS tile, non-temporal); 1 = the round-1 passes (the conv re-run for f64 sums of its outputs) with the
  * VALU apply pass; 2 = lag-product statistics with the taps of the apply pass on the f32-input MFMA (an exact
  * k-ordered fmaf chain: mode 3's bits); 3 = lag-product statistics with the VALU apply pass (the round-2 default);
  * 4 / 7 = mode 0 with its stores straight from the MFMA layout / through a block-wide tile (mode 0's bits); 5 / 6 =
- * timing ablations of mode 4 (no plane stores / no GELU: wrong outputs).  HFA_EINVAL otherwise. */
+ * timing ablations of mode 4 (no plane stores / no GELU: wrong outputs); 8 = mode 0 with plain instead of
+ * non-temporal stores; 9 = a timing ablation of mode 0 (no GELU).  HFA_EINVAL otherwise. */
 int hfa_conv0_tuning(int mode);
 /* Self-test: y = the GELU applied by every fused epilogue (GEMM, LayerNorm/GroupNorm act, conv0). */
 int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream);

@@ -237,7 +237,7 @@ def test_conv0_mfma_bit_identical_to_valu(N, lens):
     g, bb = (1 + 0.1 * _r(512, seed=33)).to(d), (0.1 * _r(512, seed=34)).to(d)
     tl = None if lens is None else dev_lengths([(n - 10) // 5 + 1 for n in lens], d)
     outs = {}
-    for mode in (0, 1, 2, 3, 4, 7):
+    for mode in (0, 1, 2, 3, 4, 7, 8):
         _lib.call("hfa_conv0_tuning", mode)
         try:
             outs[mode] = (ops.conv0(x, w0, gamma=g, beta=bb, out_split=True, t0_len=tl),
@@ -249,7 +249,7 @@ def test_conv0_mfma_bit_identical_to_valu(N, lens):
     for a, b in zip(outs[3], outs[2]):                             # MFMA taps = VALU fmaf chain, same statistics
         assert torch.equal(a, b)
     assert torch.equal(outs[3][1], outs[1][1])                     # no statistics: bit-identical
-    for m in (4, 7):                                               # the store layouts: the same bits
+    for m in (4, 7, 8):                                            # the store layouts: the same bits
         for a, b in zip(outs[0], outs[m]):
             assert torch.equal(a, b)
 
