@@ -632,7 +632,8 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const typename A
                                                 int zb, int zg, int wrow0, int wcol0, int lane, float* slab) {
     _Float16* Cb = p.Ch + zb * p.sCb + zg * p.sCg;
     const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
-    bool bad = false;
+    hfa::h2v nanacc = {(_Float16)0.0f, (_Float16)0.0f};
+    const float c2048 = 2048.0f;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
         const int col0 = wcol0 + j * 32;
@@ -651,13 +652,10 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const typename A
                 const int row = row0 + r, col = col0 + c4;
                 if (row < p.M) {
                     const f32x4 v = *reinterpret_cast<const f32x4*>(slab + r * 36 + c4);
-                    f16x4 v1, v2;
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        bad |= !(__builtin_fabsf(v[t]) < 65504.0f);
-                        v1[t] = (_Float16)v[t];
-                        v2[t] = (_Float16)((v[t] - (float)v1[t]) * 2048.0f);
-                    }
+                    uint2 u1, u2;   // columns past N hold finite zeros (zero W rows): the range check may see them
+                    hfa::split_pair(v[0], v[1], u1.x, u2.x, nanacc, c2048);
+                    hfa::split_pair(v[2], v[3], u1.y, u2.y, nanacc, c2048);
+                    const f16x4 v1 = __builtin_bit_cast(f16x4, u1), v2 = __builtin_bit_cast(f16x4, u2);
                     _Float16* dst = Cb + (long long)row * p.ldc + col;
                     if (col + 3 < p.N) {
                         *reinterpret_cast<f16x4*>(dst) = v1;
@@ -675,7 +673,7 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const typename A
             __builtin_amdgcn_wave_barrier();
         }
     }
-    if (bad && p.oflow) *p.oflow = 1;
+    if (hfa::range_bad(nanacc) && p.oflow) *p.oflow = 1;
 }
 
 // f32 epilogue of the split kernel (+R), through the slab; raises *oflow on a non-finite accumulator.  With p.Ch
@@ -685,6 +683,8 @@ template <int MF, int EPI, int TI, int TJ, int NI, int NJ>
 __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename AccT<MF>::type (&acc)[NI][NJ], int zb,
                                               int zg, int wrow0, int wcol0, int lane, float* slab, bool check) {
     bool bad = false;
+    hfa::h2v nanacc = {(_Float16)0.0f, (_Float16)0.0f};
+    const float c2048 = 2048.0f;
     float* Cb = p.C + zb * p.sCb + zg * p.sCg;
     _Float16* Hb = p.Ch ? p.Ch + zb * p.sCb + zg * p.sCg : nullptr;
     const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
@@ -732,13 +732,14 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
                             }
                     }
                     if (Hb) {
-                        f16x4 v1, v2;
+                        uint2 u1, u2;
+                        if (col + 3 >= p.N)   // columns past N: no residual was added, keep them out of the check
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            bad |= !(__builtin_fabsf(v[t]) < 65504.0f) && col + t < p.N;
-                            v1[t] = (_Float16)v[t];
-                            v2[t] = (_Float16)((v[t] - (float)v1[t]) * 2048.0f);
-                        }
+                            for (int t = 0; t < 4; ++t)
+                                if (col + t >= p.N) v[t] = 0.0f;
+                        hfa::split_pair(v[0], v[1], u1.x, u2.x, nanacc, c2048);
+                        hfa::split_pair(v[2], v[3], u1.y, u2.y, nanacc, c2048);
+                        const f16x4 v1 = __builtin_bit_cast(f16x4, u1), v2 = __builtin_bit_cast(f16x4, u2);
                         _Float16* hd = Hb + (long long)row * p.ldc + col;
                         if (col + 3 < p.N) {
                             *reinterpret_cast<f16x4*>(hd) = v1;
@@ -757,7 +758,7 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
             __builtin_amdgcn_wave_barrier();
         }
     }
-    if (bad && p.oflow) *p.oflow = 1;
+    if ((bad || hfa::range_bad(nanacc)) && p.oflow) *p.oflow = 1;
 }
 
 // GT (general taps): Cg a multiple of 8 but not of 32 (the grouped positional conv, Cg = 48): a K-step's four

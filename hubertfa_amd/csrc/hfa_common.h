@@ -118,6 +118,21 @@ __device__ __forceinline__ unsigned split_lo_pair(unsigned h, float x2048_0, flo
     return r;
 }
 
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// Split-f16 planes of two f32 values (hi = f16(v), lo = f16((v - hi) 2^11), bit for bit the scalar form): one
+// v_cvt_pk_f16_f32 and two v_fma_mix (split_lo_pair) instead of 2 x (cvt, cvt back, sub, mul, cvt).  nanacc: the
+// planes' range check as one v_pk_fma_f16 per pair -- hi * 0 + acc turns an inf (|v| >= 65520) or NaN hi into a
+// NaN that persists; test it once at the end (range_bad).
+__device__ __forceinline__ void split_pair(float a, float b, unsigned& hi, unsigned& lo, h2v& nanacc, float c2048) {
+    const h2v hp = __builtin_convertvector((f2v){a, b}, h2v);
+    nanacc = hp * (h2v){(_Float16)0.0f, (_Float16)0.0f} + nanacc;
+    hi = __builtin_bit_cast(unsigned, hp);
+    lo = split_lo_pair(hi, a * 2048.0f, b * 2048.0f, c2048);
+}
+__device__ __forceinline__ bool range_bad(h2v nanacc) { return nanacc[0] != nanacc[0] || nanacc[1] != nanacc[1]; }
+
 // The GELU of every fused epilogue.  With E = erfc(|x| / sqrt 2) = 1 - erf(|x| / sqrt 2):
 //   GELU(x) = x - (x / 2) E for x >= 0 and (x / 2) E for x < 0, i.e. max(x, 0) - |x / 2| E  (one fma),
 // and E = exp2(q(a)), a = min(|x|, 3.95 sqrt 2), q(a) = a R7(a) fitted to log2 erfc(a / sqrt 2) on [0, 3.95 sqrt 2]

@@ -13,6 +13,8 @@ B = 32
 SHAPES = [  # name, Tin, Cin, Cout, k, stride, epi
     ("conv1", 31999, 512, 512, 3, 2, 1),
     ("conv5", 1999, 512, 512, 2, 2, 1),
+    ("conv6", 999, 512, 512, 2, 2, 1),
+    ("conv4", 3999, 512, 512, 3, 2, 1),
     ("qkv", 499, 768, 2304, 1, 1, 0),
     ("outproj", 499, 768, 768, 1, 1, 0),
     ("ffn1", 499, 768, 3072, 1, 1, 1),
