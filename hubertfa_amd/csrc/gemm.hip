@@ -1569,7 +1569,9 @@ inline int split_cfg(const GemmP& p, int Z) {
     if (p.N == 64 && p.Cg % 32 == 0 && (long long)((p.M + 255) / 256) * Z >= 256)
         return SCFG_256x64_M16;            // grouped positional conv at Cg = 64 (Hubert-large): 1.26x the 128x64 tile
     if (p.N <= 64 || blocks128 < 256) return SCFG_128x64_M16;
-    if (blocks256 < 128 || p.N < 512) return SCFG_128x128_M16;
+    // (a half-filled single round of big tiles loses to 128 x 128: extractor conv6, 128 big tiles, 227 vs 288 TF/s;
+    // at 189 big tiles -- the N = 768 projections -- 256 x 256 still wins, 300 vs 275, profiles/r03/conv6_tiles.txt)
+    if (blocks256 <= 128 || p.N < 512) return SCFG_128x128_M16;
     // Large grids: the 256 x 256 tile unless a 192-wide tile fills the last round of CUs much better.  Score =
     // fill of the rounds (tiles / (rounds x 256 CUs)) x the tile's per-FLOP speed (192-wide tiles 0.92 of 256 x 256),
     // ties to 256 x 256.  Measured (scripts/split_gemm_bench.py, profiles/r03/split_tiles_c5.txt): QKV at M = 15 968

@@ -82,7 +82,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
     const float var = hfa::wave_sum(ss) / (float)C;
     const float rstd = 1.0f / sqrtf(var + eps);
     float* yr = y ? y + wave * ldy : nullptr;      // y NULL: split planes only (the residual is read from them)
-    bool bad = false;
+    hfa::h2v nanacc = {(_Float16)0.0f, (_Float16)0.0f};   // the planes' range check (hfa::split_pair)
+    const float c2048 = 2048.0f;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
         const int c = (lane + i * 64) * 4;
@@ -94,19 +95,15 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
             for (int e = 0; e < 4; ++e) o[e] = act_apply((v[i][e] - mean) * rstd * g[e] + bb[e], act);
             if (yr) *reinterpret_cast<f32x4*>(yr + c) = o;
             if (ys) {
-                f16x4 h1, h2;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    bad |= !(__builtin_fabsf(o[e]) < 65504.0f);
-                    h1[e] = (_Float16)o[e];
-                    h2[e] = (_Float16)((o[e] - (float)h1[e]) * 2048.0f);
-                }
-                *reinterpret_cast<f16x4*>(ys + wave * ldys + c) = h1;
-                *reinterpret_cast<f16x4*>(ys + sps + wave * ldys + c) = h2;
+                uint2 h1, h2;
+                hfa::split_pair(o[0], o[1], h1.x, h2.x, nanacc, c2048);
+                hfa::split_pair(o[2], o[3], h1.y, h2.y, nanacc, c2048);
+                *reinterpret_cast<uint2*>(ys + wave * ldys + c) = h1;
+                *reinterpret_cast<uint2*>(ys + sps + wave * ldys + c) = h2;
             }
         }
     }
-    if (bad && oflow) *oflow = 1;
+    if (hfa::range_bad(nanacc) && oflow) *oflow = 1;
 }
 
 // GroupNorm over a channels-last [T, C] slab per batch item: group g = channels [g*Cg, (g+1)*Cg) over all T.
@@ -305,7 +302,8 @@ __global__ __launch_bounds__(256) void gn_rows_apply_kernel(int T, int C, int G,
     const float mean = stat[g][0], rstd = stat[g][1];
     const f32x4 gm = *reinterpret_cast<const f32x4*>(gamma + c), bt = *reinterpret_cast<const f32x4*>(beta + c);
     const int t0 = pi * kGnRows, t1 = min(T, t0 + kGnRows);
-    bool bad = false;
+    hfa::h2v nanacc = {(_Float16)0.0f, (_Float16)0.0f};   // the planes' range check (hfa::split_pair)
+    const float c2048 = 2048.0f;
     for (int t = t0 + r0; t < t1; t += rstep) {
         f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
         if (t < Tb) {
@@ -315,19 +313,15 @@ __global__ __launch_bounds__(256) void gn_rows_apply_kernel(int T, int C, int G,
         }
         if (y) *reinterpret_cast<f32x4*>(y + b * y_bs + (long long)t * ldy + c) = o;
         if (ys) {
-            f16x4 h1, h2;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                bad |= !(__builtin_fabsf(o[e]) < 65504.0f);
-                h1[e] = (_Float16)o[e];
-                h2[e] = (_Float16)((o[e] - (float)h1[e]) * 2048.0f);
-            }
+            uint2 h1, h2;
+            hfa::split_pair(o[0], o[1], h1.x, h2.x, nanacc, c2048);
+            hfa::split_pair(o[2], o[3], h1.y, h2.y, nanacc, c2048);
             _Float16* d = ys + b * ys_bs + (long long)t * ldys + c;
-            *reinterpret_cast<f16x4*>(d) = h1;
-            *reinterpret_cast<f16x4*>(d + sps) = h2;
+            *reinterpret_cast<uint2*>(d) = h1;
+            *reinterpret_cast<uint2*>(d + sps) = h2;
         }
     }
-    if (bad && oflow) *oflow = 1;
+    if (hfa::range_bad(nanacc) && oflow) *oflow = 1;
 }
 
 }  // namespace

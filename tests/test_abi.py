@@ -139,4 +139,5 @@ def test_split_gemm_tile_choice():
     assert tile(17924, 2304) == [" 256", " 256"]          # 639 tiles (was 128 x 128)
     assert tile(15968, 768) == [" 256", " 256"]           # out-projection / FFN2: one round
     assert tile(15999, 512, Z=32, epi=1) == [" 256", " 256"]   # extractor conv1
+    assert tile(499, 512, Z=32, epi=1) == [" 128", " 128"]     # extractor conv6: 128 big tiles, half a round
     assert tile(864, 192, Z=32) == [" 128", " 128"]       # UNet level 0: small grid
