@@ -301,6 +301,9 @@ def main():
     from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
 
     rank, world, local = env_rank_world()
+    if os.environ.get("HFA_VITERBI_TUNING"):            # (A/B switch: hfa_viterbi_tuning of the DP kernel choice)
+        from hubertfa_amd import _lib
+        _lib.call("hfa_viterbi_tuning", int(os.environ["HFA_VITERBI_TUNING"]))
     if args.device is not None:          # rehearsal of the N>1 path on a 1-GPU box (all ranks on one device)
         local = args.device
     torch.cuda.set_device(local)
