@@ -78,9 +78,11 @@ def test_forward_batched_bit_exact():
                                                 (3000, 1801, 4, True), (3000, 1801, 8, True), (2500, 4100, 4, False),
                                                 (700, 300, 2, False), (70000, 61, 0, True), (65537, 300, 0, False),
                                                 (65536, 31, 0, True), (64000, 31, 0, True), (2000, 9000, 0, True),
-                                                (1500, 20000, 0, False), (1200, 32767, 0, True), (9000, 8500, 2, False)])
+                                                (1500, 20000, 0, False), (1200, 32767, 0, True), (9000, 8500, 2, False),
+                                                (861, 91, 1, True), (861, 91, 5, True), (1000, 77, 1, False)])
 def test_forward_many_states_vs_oracle(T, S, force_k, pitch8):
-    """Single- and multi-wave DP variants (S up to 8192; 2/4/8 states per lane; scalar and vector state pitch), the
+    """Single- and multi-wave DP variants (S up to 8192; 2/4/8 states per lane, the short emission rings 1/5; scalar
+    and vector state pitch), the
     segmented form past 8192 states (up to the backtrack's 32767), all bit-exact with the pinned C oracle, and the
     windowed backtrack with it (T > 64000: the path kept in global memory instead of LDS; the reference takes any T
     and S)."""
