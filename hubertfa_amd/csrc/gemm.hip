@@ -593,7 +593,8 @@ template <> struct AccT<16> { typedef f32x4 type; };
 // an accumulator is not finite.
 template <int MF, int NI, int NJ>
 __device__ __forceinline__ bool fill_slab(const typename AccT<MF>::type (&acc)[NI][NJ], int i, int j, int epi,
-                                          const float* biasb, int col0, int N, int lane, float* slab) {
+                                          const float* biasb, int col0, int N, int lane, float* slab,
+                                          float scale = 1.0f) {
     bool bad = false;
     if constexpr (MF == 32) {
         const int r32 = lane & 31, h = lane >> 5;
@@ -617,7 +618,7 @@ __device__ __forceinline__ bool fill_slab(const typename AccT<MF>::type (&acc)[N
                 for (int e = 0; e < 4; ++e) {
                     const float a = acc[2 * i + ii][2 * j + jj][e];
                     bad |= !__builtin_isfinite(a);
-                    float v = a + bv;
+                    float v = __builtin_fmaf(a, scale, bv);   // scale: the single accumulator's 2^-11 (exact)
                     if (epi == EPI_GELU) v = hfa::gelu_fast(v);
                     slab[(16 * ii + 4 * g + e) * 36 + col] = v;
                 }
@@ -629,7 +630,8 @@ __device__ __forceinline__ bool fill_slab(const typename AccT<MF>::type (&acc)[N
 // Split-plane epilogue: TI x TJ blocks of 32 x 32 per wave, each through the slab (16-B row pieces out).
 template <int MF, int TI, int TJ, int NI, int NJ>
 __device__ __forceinline__ void store_split_lds(const GemmP& p, const typename AccT<MF>::type (&acc)[NI][NJ], int EPI_,
-                                                int zb, int zg, int wrow0, int wcol0, int lane, float* slab) {
+                                                int zb, int zg, int wrow0, int wcol0, int lane, float* slab,
+                                                float scale = 1.0f) {
     _Float16* Cb = p.Ch + zb * p.sCb + zg * p.sCg;
     const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
     hfa::h2v nanacc = {(_Float16)0.0f, (_Float16)0.0f};
@@ -642,7 +644,7 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const typename A
         for (int i = 0; i < TI; ++i) {
             const int row0 = wrow0 + i * 32;
             if (row0 >= p.M) continue;
-            fill_slab<MF>(acc, i, j, EPI_, biasb, col0, p.N, lane, slab);
+            fill_slab<MF>(acc, i, j, EPI_, biasb, col0, p.N, lane, slab, scale);
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
@@ -681,7 +683,8 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const typename A
 // positional conv's input next to its f32 residual copy), with the planes' range check.
 template <int MF, int EPI, int TI, int TJ, int NI, int NJ>
 __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename AccT<MF>::type (&acc)[NI][NJ], int zb,
-                                              int zg, int wrow0, int wcol0, int lane, float* slab, bool check) {
+                                              int zg, int wrow0, int wcol0, int lane, float* slab, bool check,
+                                              float scale = 1.0f) {
     bool bad = false;
     hfa::h2v nanacc = {(_Float16)0.0f, (_Float16)0.0f};
     const float c2048 = 2048.0f;
@@ -698,7 +701,7 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
         for (int i = 0; i < TI; ++i) {
             const int row0 = wrow0 + i * 32;
             if (row0 >= p.M) continue;
-            bad |= fill_slab<MF>(acc, i, j, EPI, biasb, col0, p.N, lane, slab) && check;
+            bad |= fill_slab<MF>(acc, i, j, EPI, biasb, col0, p.N, lane, slab, scale) && check;
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
@@ -995,22 +998,19 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
             }
             stage = stage + 1 == NS ? 0 : stage + 1;
         }
-        if constexpr (!F16) {
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) acc[i][j] *= 1.0f / 2048.0f;
-        }
+        // the single accumulator's 2^-11 goes into the epilogue's bias fma (exact scaling: the same bits as a
+        // separate multiply, one VALU op per output fewer)
+        constexpr float kScale = F16 ? 1.0f : 1.0f / 2048.0f;
         static_assert(NW * 32 * 36 * 4 <= NS * STAGE * 2, "epilogue slabs exceed the staging LDS");
         __syncthreads();
         float* slab = reinterpret_cast<float*>(smem) + wave * (32 * 36);
         constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
         if constexpr (OUT_SPLIT)
             store_split_lds<16, TI, TJ>(p, acc, EPI, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
-                                        slab);
+                                        slab, kScale);
         else
             store_f32_lds<16, EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
-                                           slab, true);
+                                           slab, true, kScale);
         return;
     } else {
     const int r32 = lane & 31, h = lane >> 5;
