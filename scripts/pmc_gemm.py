@@ -24,7 +24,7 @@ def load(d):
                 continue
             k = int(r["Dispatch_Id"])
             e = out[k]
-            e["name"] = r["Kernel_Name"].split("(anonymous namespace)::")[1].split("(")[0]
+            e["name"] = r["Kernel_Name"].split("(anonymous namespace)::")[-1].split("(")[0][:60]
             e["grid"] = int(r["Grid_Size"])
             e["ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
