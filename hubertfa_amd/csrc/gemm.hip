@@ -591,7 +591,7 @@ template <> struct AccT<16> { typedef f32x4 type; };
 // bias and GELU applied, from either accumulator layout: MF 32 = one 32x32x16 accumulator (col lane&31, row (e&3) +
 // 8(e>>2) + 4(lane>>5)), MF 16 = 2 x 2 16x16x32 accumulators (col lane&15, row 4(lane>>4) + e).  Returns true when
 // an accumulator is not finite.
-template <int MF, int NI, int NJ>
+template <int MF, int NI, int NJ, int S = 36>
 __device__ __forceinline__ bool fill_slab(const typename AccT<MF>::type (&acc)[NI][NJ], int i, int j, int epi,
                                           const float* biasb, int col0, int N, int lane, float* slab,
                                           float scale = 1.0f) {
@@ -604,7 +604,7 @@ __device__ __forceinline__ bool fill_slab(const typename AccT<MF>::type (&acc)[N
             bad |= !__builtin_isfinite(acc[i][j][e]);
             float v = acc[i][j][e] + bv;
             if (epi == EPI_GELU) v = hfa::gelu_fast(v);
-            slab[((e & 3) + 8 * (e >> 2) + 4 * h) * 36 + r32] = v;
+            slab[((e & 3) + 8 * (e >> 2) + 4 * h) * S + r32] = v;
         }
     } else {
         const int c16 = lane & 15, g = lane >> 4;
@@ -620,7 +620,7 @@ __device__ __forceinline__ bool fill_slab(const typename AccT<MF>::type (&acc)[N
                     bad |= !__builtin_isfinite(a);
                     float v = __builtin_fmaf(a, scale, bv);   // scale: the single accumulator's 2^-11 (exact)
                     if (epi == EPI_GELU) v = hfa::gelu_fast(v);
-                    slab[(16 * ii + 4 * g + e) * 36 + col] = v;
+                    slab[(16 * ii + 4 * g + e) * S + col] = v;
                 }
         }
     }
@@ -663,6 +663,66 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const typename A
                         *reinterpret_cast<f16x4*>(dst) = v1;
                         *reinterpret_cast<f16x4*>(dst + p.sCp) = v2;
                     } else {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            if (col + t < p.N) {
+                                dst[t] = v1[t];
+                                dst[t + p.sCp] = v2[t];
+                            }
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (hfa::range_bad(nanacc) && p.oflow) *p.oflow = 1;
+}
+
+// Split-plane epilogue over PAIRS of 32 x 32 blocks (TJ even): the two blocks side by side in a [32][68] slab, so a
+// store instruction writes 4 rows x 128 B per plane (whole cache lines) instead of 8 rows x 64 B.  Row stride 68:
+// the fill's 4 rows of 16 columns land on disjoint banks (68 x 4 = 16 mod 64).  Same values as store_split_lds.
+constexpr int kSlab2 = 68;
+#ifndef HFA_SPLIT_PAIRS
+#define HFA_SPLIT_PAIRS 1
+#endif
+constexpr bool kSplitPairs = HFA_SPLIT_PAIRS;   // (A/B build switch: -DHFA_SPLIT_PAIRS=0 -> store_split_lds)
+template <int MF, int TI, int TJ, int NI, int NJ>
+__device__ __forceinline__ void store_split_lds2(const GemmP& p, const typename AccT<MF>::type (&acc)[NI][NJ],
+                                                 int EPI_, int zb, int zg, int wrow0, int wcol0, int lane,
+                                                 float* slab, float scale) {
+    static_assert(TJ % 2 == 0, "pairs of column blocks");
+    _Float16* Cb = p.Ch + zb * p.sCb + zg * p.sCg;
+    const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+    hfa::h2v nanacc = {(_Float16)0.0f, (_Float16)0.0f};
+    const float c2048 = 2048.0f;
+#pragma unroll
+    for (int j = 0; j < TJ; j += 2) {
+        const int col0 = wcol0 + j * 32;
+        if (col0 >= p.N) continue;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const int row0 = wrow0 + i * 32;
+            if (row0 >= p.M) continue;
+            fill_slab<MF, NI, NJ, kSlab2>(acc, i, j, EPI_, biasb, col0, p.N, lane, slab, scale);
+            fill_slab<MF, NI, NJ, kSlab2>(acc, i, j + 1, EPI_, biasb, col0 + 32, p.N, lane, slab + 32, scale);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int idx = lane + k * 64;
+                const int r = idx >> 4, c4 = (idx & 15) * 4;
+                const int row = row0 + r, col = col0 + c4;
+                if (row < p.M) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(slab + r * kSlab2 + c4);
+                    uint2 u1, u2;   // columns past N hold finite zeros (zero W rows): the range check may see them
+                    hfa::split_pair(v[0], v[1], u1.x, u2.x, nanacc, c2048);
+                    hfa::split_pair(v[2], v[3], u1.y, u2.y, nanacc, c2048);
+                    _Float16* dst = Cb + (long long)row * p.ldc + col;
+                    if (col + 3 < p.N) {
+                        *reinterpret_cast<uint2*>(dst) = u1;
+                        *reinterpret_cast<uint2*>(dst + p.sCp) = u2;
+                    } else {
+                        const f16x4 v1 = __builtin_bit_cast(f16x4, u1), v2 = __builtin_bit_cast(f16x4, u2);
 #pragma unroll
                         for (int t = 0; t < 4; ++t)
                             if (col + t < p.N) {
@@ -1001,11 +1061,16 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         // the single accumulator's 2^-11 goes into the epilogue's bias fma (exact scaling: the same bits as a
         // separate multiply, one VALU op per output fewer)
         constexpr float kScale = F16 ? 1.0f : 1.0f / 2048.0f;
-        static_assert(NW * 32 * 36 * 4 <= NS * STAGE * 2, "epilogue slabs exceed the staging LDS");
-        __syncthreads();
-        float* slab = reinterpret_cast<float*>(smem) + wave * (32 * 36);
         constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
-        if constexpr (OUT_SPLIT)
+        constexpr bool PAIRS = OUT_SPLIT && TJ % 2 == 0 && kSplitPairs;   // 128-B row segments (store_split_lds2)
+        constexpr int SLAB = PAIRS ? 32 * kSlab2 : 32 * 36;
+        static_assert(NW * SLAB * 4 <= NS * STAGE * 2, "epilogue slabs exceed the staging LDS");
+        __syncthreads();
+        float* slab = reinterpret_cast<float*>(smem) + wave * SLAB;
+        if constexpr (PAIRS)
+            store_split_lds2<16, TI, TJ>(p, acc, EPI, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN),
+                                         lane, slab, kScale);
+        else if constexpr (OUT_SPLIT)
             store_split_lds<16, TI, TJ>(p, acc, EPI, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
                                         slab, kScale);
         else
