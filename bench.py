@@ -304,6 +304,9 @@ def main():
     if os.environ.get("HFA_VITERBI_TUNING"):            # (A/B switch: hfa_viterbi_tuning of the DP kernel choice)
         from hubertfa_amd import _lib
         _lib.call("hfa_viterbi_tuning", int(os.environ["HFA_VITERBI_TUNING"]))
+    if os.environ.get("HFA_CONV0_TUNING"):              # (A/B switch: hfa_conv0_tuning of the conv0 apply pass)
+        from hubertfa_amd import _lib
+        _lib.call("hfa_conv0_tuning", int(os.environ["HFA_CONV0_TUNING"]))
     if args.device is not None:          # rehearsal of the N>1 path on a 1-GPU box (all ranks on one device)
         local = args.device
     torch.cuda.set_device(local)

@@ -662,6 +662,9 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
             hipLaunchKernelGGL((conv0_packed_kernel<0, 1, 0, false>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0,
                                stats, gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
         else if (outs && vec8 && g_conv0_mode == 9) HFA_PACKED(0, 1, 2, stats);
+        else if (outs && vec8 && g_conv0_mode == 10)   // mode 0 held to 2 workgroups per CU (16 KiB of unused LDS)
+            hipLaunchKernelGGL((conv0_packed_kernel<0, 1, 0, true>), grid, dim3(PNT), 16 * 1024, stream, N, T0, x, x_bs,
+                               w0, stats, gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
         else if (outs && vec8 && g_conv0_mode == 2)
             hipLaunchKernelGGL((conv0_apply_mfma_kernel<0>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
@@ -721,10 +724,11 @@ int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w
 // 3 the lag-product statistics with conv0_apply8_kernel (the round-2 default), 4 mode 0 with its stores straight
 // from the MFMA layout, 5 / 6 timing ablations of mode 4 (no plane stores; no GELU -- wrong outputs), 7 mode 0 with
 // its stores through a block-wide LDS tile, 8 mode 0 with plain (not non-temporal) stores, 9 a timing ablation of
-// mode 0 (no GELU).  Per calling thread.
+// mode 0 (no GELU), 10 mode 0 at 2 workgroups per CU (room for a side-stream GEMM workgroup beside it).  Per calling
+// thread.
 int hfa_conv0_tuning(int mode) {
-    if (mode < 0 || mode > 9) {
-        hfa::set_error("hfa_conv0_tuning: mode %d is not 0 .. 9", mode);
+    if (mode < 0 || mode > 10) {
+        hfa::set_error("hfa_conv0_tuning: mode %d is not 0 .. 10", mode);
         return HFA_EINVAL;
     }
     g_conv0_mode = mode;

@@ -307,7 +307,8 @@ int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hip
  * k-ordered fmaf chain: mode 3's bits); 3 = lag-product statistics with the VALU apply pass (the round-2 default);
  * 4 / 7 = mode 0 with its stores straight from the MFMA layout / through a block-wide tile (mode 0's bits); 5 / 6 =
  * timing ablations of mode 4 (no plane stores / no GELU: wrong outputs); 8 = mode 0 with plain instead of
- * non-temporal stores; 9 = a timing ablation of mode 0 (no GELU).  HFA_EINVAL otherwise. */
+ * non-temporal stores; 9 = a timing ablation of mode 0 (no GELU); 10 = mode 0 held to 2 workgroups per CU.
+ * HFA_EINVAL otherwise. */
 int hfa_conv0_tuning(int mode);
 /* Self-test: y = the GELU applied by every fused epilogue (GEMM, LayerNorm/GroupNorm act, conv0). */
 int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream);
