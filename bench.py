@@ -259,7 +259,10 @@ def host_io(wav_np, res, seconds, budget_s=3.0):
                                           "writes each batch's TextGrids, while the GPU runs the neighbouring batch)"}
 
 
-SECONDARY = ("viterbi_forward_kernel", "hfa_conv0_f32", "attn_fwd_split_kernel", "attn_fwd_f32_kernel")
+SECONDARY = ("viterbi_forward_kernel", "hfa_conv0_split", "hfa_conv0_f32", "attn_fwd_split_kernel", "attn_fwd_f32_kernel")
+SECONDARY_NOTE = {"hfa_conv0_split": "one hfa_conv0_split call: conv0_gram_kernel + conv0_gram_stats_kernel + "
+                                     "conv0_packed_kernel (statistics and the apply pass)",
+                  "hfa_conv0_f32": "one hfa_conv0_f32 call (the f32 path: statistics + the VALU apply pass)"}
 
 
 def secondary_rooflines(iso, pipe, T, S):
@@ -285,6 +288,8 @@ def secondary_rooflines(iso, pipe, T, S):
                 e["us_per_time_step"] = ps["avg_ms"] * 1e3 / T
                 e["states"] = S
         pp = pipe.summary(name)
+        if name in SECONDARY_NOTE:
+            e["covers"] = SECONDARY_NOTE[name]
         e.update({"launches": ps["launches"], "avg_launch_ms": ps["avg_ms"], "timing": "isolated serial steps",
                   "in_pipeline_avg_launch_ms": pp["avg_ms"] if pp["launches"] else None})
         out.append(e)

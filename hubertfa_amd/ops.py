@@ -562,7 +562,8 @@ def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, worksp
     if PROBE is None:
         launch()
     else:                       # wave in (4 B/sample) + activations out (4 B x 512 x T0)
-        PROBE("hfa_conv0_f32", B * (4.0 * N + 4.0 * 512 * T0), launch, kind="bytes")
+        PROBE("hfa_conv0_split" if out_split else "hfa_conv0_f32", B * (4.0 * N + 4.0 * 512 * T0), launch,
+              kind="bytes")
     return out
 
 
