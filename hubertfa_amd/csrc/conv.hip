@@ -437,10 +437,10 @@ __global__ __launch_bounds__(MNT) void conv0_apply_mfma_kernel(int N, int T0, co
 // STORE 0 without plane stores 0.33-0.35 ms, without GELU 0.47; STORE 1 without GELU 0.43.
 constexpr int PNT = 512;
 
-// ABL (timing ablations only, hfa_conv0_tuning 5 / 6 / 9): 1 = no plane stores (the planes are folded into one
-// register and stored once per lane), 2 = no GELU.  NT: STORE 1's plane stores non-temporal (streaming; the 2.1 GB
-// per batch are far past the 256 MB Infinity Cache anyway): 0.466 -> 0.440 ms per batch (mode 8 = without).
-template <int MODE, int STORE, int ABL = 0, bool NT = true>
+// NT: STORE 1's plane stores non-temporal (streaming; the 2.1 GB per batch are far past the 256 MB Infinity Cache
+// anyway): 0.466 -> 0.440 ms per batch (mode 8 = without).  (The timing ablations quoted above -- no plane stores,
+// no GELU -- were builds of this kernel for measurement only; they are not in the library.)
+template <int MODE, int STORE, bool NT = true>
 __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const float* __restrict__ x,
                                                            long long x_bs, const float* __restrict__ w0,
                                                            const float* __restrict__ stats,
@@ -521,7 +521,6 @@ __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const 
     const f16x2 zero2 = {(_Float16)0.0f, (_Float16)0.0f};
     f16x2 nanacc = zero2;
     const float c2048 = 2048.0f;
-    unsigned abl_sink = 0;
     int tb = 0;
     _Float16* yb = yh + b * y_bs + (long long)t0 * C0;
     for (int f0 = 0; f0 < nt; f0 += 16) {
@@ -540,7 +539,7 @@ __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const 
                 for (int u = 0; u < 2; ++u) {
                     const int c = 8 * p + e + u;
                     v[u] = fmaf(d[2 * p + ((e + u) >> 2)][(e + u) & 3], sc[c], sh[c]);
-                    if (MODE == 0 && ABL != 2) v[u] = hfa::gelu_fast(v[u]);
+                    if (MODE == 0) v[u] = hfa::gelu_fast(v[u]);
                     asm volatile("" : "+v"(v[u]));   // split the rounded f32 value: no fusing its last fma into the cvt
                 }
                 const f16x2 hp = __builtin_convertvector((f32x2){v[0], v[1]}, f16x2);   // one v_cvt_pk_f16_f32
@@ -549,9 +548,7 @@ __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const 
                 h2[e >> 1] = hfa::split_lo_pair(h1[e >> 1], v[0] * 2048.0f, v[1] * 2048.0f, c2048);
             }
             const uint4 o1 = make_uint4(h1[0], h1[1], h1[2], h1[3]), o2 = make_uint4(h2[0], h2[1], h2[2], h2[3]);
-            if (ABL == 1) {
-                abl_sink ^= o1.x ^ o1.y ^ o1.z ^ o1.w ^ o2.x ^ o2.y ^ o2.z ^ o2.w;
-            } else if (STORE == 1) {   // row j, 16-B chunk 4 p + g of the wave's 128-B row segment, XOR-swizzled
+            if (STORE == 1) {   // row j, 16-B chunk 4 p + g of the wave's 128-B row segment, XOR-swizzled
                 const int slot = j * 8 + ((4 * p + g) ^ (j & 7));
                 otile[wave][0][slot] = o1;
                 otile[wave][1][slot] = o2;
@@ -565,7 +562,7 @@ __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const 
                 *reinterpret_cast<uint4*>(dst + y_sp) = o2;
             }
         }
-        if (ABL != 1 && STORE == 1) {   // lane (row r = lane >> 3 + 8 hf, chunk c = lane & 7): 8 rows x 128 B
+        if (STORE == 1) {   // lane (row r = lane >> 3 + 8 hf, chunk c = lane & 7): 8 rows x 128 B
             const int c = lane & 7;     // (wave-local tile: LDS ops of one wave complete in order, no barrier)
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
@@ -584,7 +581,7 @@ __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const 
                     }
                 }
             }
-        } else if (ABL != 1 && STORE == 2) {   // wave w stores rows 2 w, 2 w + 1: one 1-KiB row per instruction
+        } else if (STORE == 2) {   // wave w stores rows 2 w, 2 w + 1: one 1-KiB row per instruction
             __syncthreads();
 #pragma unroll
             for (int rr = 0; rr < 2; ++rr) {
@@ -601,7 +598,6 @@ __global__ __launch_bounds__(PNT) void conv0_packed_kernel(int N, int T0, const 
         }
     }
     bad |= nanacc[0] != nanacc[0] || nanacc[1] != nanacc[1];
-    if (ABL == 1) *reinterpret_cast<unsigned*>(yb + 2 * threadIdx.x) = abl_sink;
     if (bad && oflow) *oflow = 1;
 }
 
@@ -650,20 +646,17 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
             hipLaunchKernelGGL(conv0_reduce_kernel, dim3(C0 / 64, B), dim3(NT), 0, stream, T0, nchunk, part, eps,
                                stats, t0_len);
         }
-#define HFA_PACKED(MODE_, STORE_, ABL_, STATS_)                                                                       \
-    hipLaunchKernelGGL((conv0_packed_kernel<MODE_, STORE_, ABL_>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0,     \
+#define HFA_PACKED(MODE_, STORE_, STATS_)                                                                             \
+    hipLaunchKernelGGL((conv0_packed_kernel<MODE_, STORE_>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0,           \
                        STATS_, gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow)
-        if (outs && vec8 && g_conv0_mode == 0) HFA_PACKED(0, 1, 0, stats);
-        else if (outs && vec8 && g_conv0_mode == 4) HFA_PACKED(0, 0, 0, stats);
-        else if (outs && vec8 && g_conv0_mode == 5) HFA_PACKED(0, 0, 1, stats);
-        else if (outs && vec8 && g_conv0_mode == 6) HFA_PACKED(0, 0, 2, stats);
-        else if (outs && vec8 && g_conv0_mode == 7) HFA_PACKED(0, 2, 0, stats);
+        if (outs && vec8 && g_conv0_mode == 0) HFA_PACKED(0, 1, stats);
+        else if (outs && vec8 && g_conv0_mode == 4) HFA_PACKED(0, 0, stats);
+        else if (outs && vec8 && g_conv0_mode == 7) HFA_PACKED(0, 2, stats);
         else if (outs && vec8 && g_conv0_mode == 8)
-            hipLaunchKernelGGL((conv0_packed_kernel<0, 1, 0, false>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0,
+            hipLaunchKernelGGL((conv0_packed_kernel<0, 1, false>), grid, dim3(PNT), 0, stream, N, T0, x, x_bs, w0,
                                stats, gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
-        else if (outs && vec8 && g_conv0_mode == 9) HFA_PACKED(0, 1, 2, stats);
         else if (outs && vec8 && g_conv0_mode == 10)   // mode 0 held to 2 workgroups per CU (16 KiB of unused LDS)
-            hipLaunchKernelGGL((conv0_packed_kernel<0, 1, 0, true>), grid, dim3(PNT), 16 * 1024, stream, N, T0, x, x_bs,
+            hipLaunchKernelGGL((conv0_packed_kernel<0, 1, true>), grid, dim3(PNT), 16 * 1024, stream, N, T0, x, x_bs,
                                w0, stats, gamma, beta, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
         else if (outs && vec8 && g_conv0_mode == 2)
             hipLaunchKernelGGL((conv0_apply_mfma_kernel<0>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, stats,
@@ -678,7 +671,7 @@ int conv0_launch(int B, int N, const float* x, long long x_bs, const float* w0, 
             hipLaunchKernelGGL((conv0_apply_kernel<0, false>), grid, dim3(NT), 0, stream, N, T0, x, x_bs, w0, stats,
                                gamma, beta, bias, y, y_bs, y_sp, oflow);
     } else if (outs && vec8 && (g_conv0_mode == 0 || g_conv0_mode >= 4)) {   // the packed modes
-        HFA_PACKED(1, 1, 0, nullptr);
+        HFA_PACKED(1, 1, nullptr);
     } else if (outs && vec8 && g_conv0_mode == 2) {
         hipLaunchKernelGGL((conv0_apply_mfma_kernel<1>), grid, dim3(MNT), 0, stream, N, T0, x, x_bs, w0, nullptr,
                            nullptr, nullptr, bias, reinterpret_cast<_Float16*>(y), y_bs, y_sp, oflow);
@@ -722,13 +715,12 @@ int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w
 // passes (the conv re-run on the VALU for the statistics, conv0_apply8_kernel), 2 the lag-product statistics with the
 // f32-MFMA apply pass (bit-identical to 3; measured 0.575-0.620 vs 0.566-0.571 ms per batch, scripts/conv0_bench.py),
 // 3 the lag-product statistics with conv0_apply8_kernel (the round-2 default), 4 mode 0 with its stores straight
-// from the MFMA layout, 5 / 6 timing ablations of mode 4 (no plane stores; no GELU -- wrong outputs), 7 mode 0 with
-// its stores through a block-wide LDS tile, 8 mode 0 with plain (not non-temporal) stores, 9 a timing ablation of
-// mode 0 (no GELU), 10 mode 0 at 2 workgroups per CU (room for a side-stream GEMM workgroup beside it).  Per calling
-// thread.
+// from the MFMA layout, 7 with its stores through a block-wide LDS tile, 8 with plain (not non-temporal) stores, 10
+// held to 2 workgroups per CU (room for a side-stream GEMM workgroup beside it); 5, 6 and 9 were timing ablations
+// (wrong outputs by construction) and are rejected.  Per calling thread.
 int hfa_conv0_tuning(int mode) {
-    if (mode < 0 || mode > 10) {
-        hfa::set_error("hfa_conv0_tuning: mode %d is not 0 .. 10", mode);
+    if (mode < 0 || mode > 10 || mode == 5 || mode == 6 || mode == 9) {
+        hfa::set_error("hfa_conv0_tuning: mode %d is not 0-4, 7, 8 or 10", mode);
         return HFA_EINVAL;
     }
     g_conv0_mode = mode;

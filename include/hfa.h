@@ -305,10 +305,9 @@ int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hip
  * stores through a per-wave LDS tile, non-temporal); 1 = the round-1 passes (the conv re-run for f64 sums of its outputs) with the
  * VALU apply pass; 2 = lag-product statistics with the taps of the apply pass on the f32-input MFMA (an exact
  * k-ordered fmaf chain: mode 3's bits); 3 = lag-product statistics with the VALU apply pass (the round-2 default);
- * 4 / 7 = mode 0 with its stores straight from the MFMA layout / through a block-wide tile (mode 0's bits); 5 / 6 =
- * timing ablations of mode 4 (no plane stores / no GELU: wrong outputs); 8 = mode 0 with plain instead of
- * non-temporal stores; 9 = a timing ablation of mode 0 (no GELU); 10 = mode 0 held to 2 workgroups per CU.
- * HFA_EINVAL otherwise. */
+ * 4 / 7 = mode 0 with its stores straight from the MFMA layout / through a block-wide tile (mode 0's bits); 8 =
+ * mode 0 with plain instead of non-temporal stores; 10 = mode 0 held to 2 workgroups per CU.  HFA_EINVAL otherwise
+ * (5, 6 and 9 were measurement-only ablations). */
 int hfa_conv0_tuning(int mode);
 /* Self-test: y = the GELU applied by every fused epilogue (GEMM, LayerNorm/GroupNorm act, conv0). */
 int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream);

@@ -27,12 +27,12 @@ def main():
     out = torch.empty(2, args.B, T0, 512, dtype=torch.float16, device=d)
     ws = torch.empty(_lib.lib().hfa_conv0_workspace_bytes(args.B, N), dtype=torch.uint8, device=d)
     nbytes = args.B * (4.0 * N + 4.0 * 512 * T0)
-    names = {0: 'lag-product stats + packed f16-MFMA apply (per-wave LDS tile, non-temporal stores)', 1: 'round-1: VALU stats + VALU apply',
-             2: 'lag-product stats + f32-MFMA apply', 3: 'lag-product stats + VALU apply',
-             4: 'packed apply, stores from the MFMA layout', 5: 'ablation: mode 4 without plane stores',
-             6: 'ablation: mode 4 without GELU', 7: 'packed apply, block-wide LDS stores',
-             8: 'mode 0 with plain (temporal) stores', 9: 'ablation: mode 0 without GELU', 5: 'ablation: mode 4 without plane stores'}
-    for mode in (0, 8, 9, 5, 3, 0, 8, 9, 5, 3):
+    names = {0: 'lag-product stats + packed f16-MFMA apply (per-wave LDS tile, non-temporal stores)',
+             1: 'round-1: VALU stats + VALU apply', 2: 'lag-product stats + f32-MFMA apply',
+             3: 'lag-product stats + VALU apply', 4: 'packed apply, stores from the MFMA layout',
+             7: 'packed apply, block-wide LDS stores', 8: 'mode 0 with plain (temporal) stores',
+             10: 'mode 0 at 2 workgroups per CU'}
+    for mode in (0, 8, 4, 3, 2, 0, 8, 4, 3, 2):
         _lib.call("hfa_conv0_tuning", mode)
         fn = lambda: ops.conv0(x, w0, gamma=gam, beta=bet, out=out, workspace=ws, out_split=True)  # noqa: E731
         for _ in range(3):
