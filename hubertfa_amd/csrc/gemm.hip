@@ -682,10 +682,6 @@ __device__ __forceinline__ void store_split_lds(const GemmP& p, const typename A
 // store instruction writes 4 rows x 128 B per plane (whole cache lines) instead of 8 rows x 64 B.  Row stride 68:
 // the fill's 4 rows of 16 columns land on disjoint banks (68 x 4 = 16 mod 64).  Same values as store_split_lds.
 constexpr int kSlab2 = 68;
-#ifndef HFA_SPLIT_PAIRS
-#define HFA_SPLIT_PAIRS 1
-#endif
-constexpr bool kSplitPairs = HFA_SPLIT_PAIRS;   // (A/B build switch: -DHFA_SPLIT_PAIRS=0 -> store_split_lds)
 template <int MF, int TI, int TJ, int NI, int NJ>
 __device__ __forceinline__ void store_split_lds2(const GemmP& p, const typename AccT<MF>::type (&acc)[NI][NJ],
                                                  int EPI_, int zb, int zg, int wrow0, int wcol0, int lane,
@@ -1062,7 +1058,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         // separate multiply, one VALU op per output fewer)
         constexpr float kScale = F16 ? 1.0f : 1.0f / 2048.0f;
         constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
-        constexpr bool PAIRS = OUT_SPLIT && TJ % 2 == 0 && kSplitPairs;   // 128-B row segments (store_split_lds2)
+        constexpr bool PAIRS = OUT_SPLIT && TJ % 2 == 0;   // 128-B row segments (store_split_lds2)
         constexpr int SLAB = PAIRS ? 32 * kSlab2 : 32 * 36;
         static_assert(NW * SLAB * 4 <= NS * STAGE * 2, "epilogue slabs exceed the staging LDS");
         __syncthreads();
