@@ -173,6 +173,7 @@ def step_breakdown(task, wav, ph_seqs, word_seqs, p2ws, k, step_s):
     the pipelined step: the same k steps with the encoder alone (main stream, nothing beside it), and the head + DP
     alone on the encoder's output (serial).  Outside the timed region."""
     import torch
+    from hubertfa_amd import ops
     feats, n_frames, wl = task.encode_batch(wav, 16000)
     torch.cuda.synchronize()
 
@@ -198,12 +199,15 @@ def step_breakdown(task, wav, ph_seqs, word_seqs, p2ws, k, step_s):
             ev.record()
             with torch.cuda.stream(side):
                 side.wait_event(ev)
+                f2.record_stream(side)      # the next iteration's encoder must not reuse f2 under the side stream
                 side_work(f2)
         return run
     unet_piped = clock(piped(lambda f2: task.head.logits(f2)))
     dp_piped = clock(piped(lambda f2: task.decoder.fetch(task.decoder.decode_batch(frame, edge, wl, ph_seqs, word_seqs,
                                                                                       p2ws, host=False))))
     torch.cuda.synchronize()
+    task.head.flag.zero_()                  # nothing from these measurement runs may reach the later steps' guard
+    ops.split_flag(task.device).zero_()
     return {"pipelined_step_ms": step_s * 1e3, "encoder_only_ms": enc_ms, "head_dp_only_ms": head_ms,
             "side_stream_cost_ms": step_s * 1e3 - enc_ms, "encoder_plus_unet_ms": unet_piped,
             "encoder_plus_lattice_dp_ms": dp_piped,
@@ -306,12 +310,6 @@ def main():
     from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
 
     rank, world, local = env_rank_world()
-    if os.environ.get("HFA_VITERBI_TUNING"):            # (A/B switch: hfa_viterbi_tuning of the DP kernel choice)
-        from hubertfa_amd import _lib
-        _lib.call("hfa_viterbi_tuning", int(os.environ["HFA_VITERBI_TUNING"]))
-    if os.environ.get("HFA_CONV0_TUNING"):              # (A/B switch: hfa_conv0_tuning of the conv0 apply pass)
-        from hubertfa_amd import _lib
-        _lib.call("hfa_conv0_tuning", int(os.environ["HFA_CONV0_TUNING"]))
     if args.device is not None:          # rehearsal of the N>1 path on a 1-GPU box (all ranks on one device)
         local = args.device
     torch.cuda.set_device(local)

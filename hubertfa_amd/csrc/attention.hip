@@ -262,11 +262,11 @@ __device__ __forceinline__ f16x4 lds_tr(const _Float16* base, int byte_off) {
         const_cast<__attribute__((address_space(3))) s16x4*>(ptr)));
 }
 
-// V2 (default since round 3): P's planes as one v_cvt_pk_f16_f32 per pair (2^11 p1 = RNE f16 of q) and the exact
-// remainder by two v_fma_mix (hfa::split_lo_pair: f16(q - p1) read straight from the packed pair), 1.5 VALU ops per
-// score instead of and + cvt + sub + cvt (4); and the tile loop unrolled by two with the current and next score
-// tiles in swapped register sets (no 32-register copy per tile).  V2 = false is the round-2 loop (A/B timing).
-template <int SNW, bool V2 = true>
+// Since round 3: P's planes as one v_cvt_pk_f16_f32 per pair (2^11 p1 = RNE f16 of q) and the exact remainder by
+// two v_fma_mix (hfa::split_lo_pair: f16(q - p1) read straight from the packed pair), 1.5 VALU ops per score instead
+// of and + cvt + sub + cvt (4); and the tile loop unrolled by two with the current and next score tiles in swapped
+// register sets (no 32-register copy per tile).  (The round-2 loop is in git history.)
+template <int SNW>
 __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnSP p) {
     // Software-pipelined: iteration t issues the score MFMAs of tile t+1, then runs tile t's softmax (VALU) while
     // those MFMAs execute, then tile t's PV MFMAs.  K runs one tile further ahead than V in separate 2-stage rings
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
         q1s[kb] = q1[kb] * (_Float16)kLo;
         q2s[kb] = q2[kb] * (_Float16)kLo;
     }
-    auto scores = [&](const _Float16* sK, f32x16 (&sM)[2], f32x16 (&)[2]) {
+    auto scores = [&](const _Float16* sK, f32x16 (&sM)[2]) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
@@ -391,11 +391,6 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
             }
         }
     };
-    auto combine = [&](const f32x16 (&sM)[2], const f32x16 (&)[2], f32x16 (&sc)[2]) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) sc[kt] = sM[kt];
-    };
-
     f32x16 o[2];
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[0][e] = o[1][e] = 0.f;
@@ -406,16 +401,16 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
     issueV(0, 0);
     if (nkb > 1) issueK(1, SKB);
     hfa::wait_vm_barrier<0>();
-    f32x16 sA[2], sB[2], nC[2];
-    scores(smem, sA, nC);
+    f32x16 sA[2], sB[2];
+    scores(smem, sA);
     __syncthreads();                                       // every wave's K(0) reads done before K(2) lands there
     const float one = 1.0f;
-    // tile t: s holds its scores, the next tile's go to nM (V2: the caller swaps the two sets every tile)
+    // tile t: s holds its scores, the next tile's go to nM (the caller swaps the two sets every tile)
     auto step = [&](int t, f32x16 (&s)[2], f32x16 (&nM)[2]) {
         const int st = t & 1;
         if (t + 2 < nkb) issueK(st, (t + 2) * SKB);        // K(t) was read by iteration t - 1's scores
         if (t + 1 < nkb) issueV(st ^ 1, (t + 1) * SKB);    // V(t - 1) was read by iteration t - 1's PV
-        if (t + 1 < nkb) scores(smem + (st ^ 1) * KST, nM, nC);   // tile t + 1, in flight during softmax(t)
+        if (t + 1 < nkb) scores(smem + (st ^ 1) * KST, nM);   // tile t + 1, in flight during softmax(t)
         const int key0 = t * SKB;
         if (key0 + SKB > L) {
 #pragma unroll
@@ -459,29 +454,17 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 f16x8 p1, p2, p1s;
-                if (V2) {
-                    // 2^11 p1 = f16(q) (round to nearest), 2^11 (p - p1) = f16(q - 2^11 p1): the exact f32 remainder
-                    // rounded once (v_fma_mix reads the f16 half of the packed pair in place)
-                    unsigned w1[4], w2[4];
+                // 2^11 p1 = f16(q) (round to nearest), 2^11 (p - p1) = f16(q - 2^11 p1): the exact f32 remainder
+                // rounded once (v_fma_mix reads the f16 half of the packed pair in place)
+                unsigned w1[4], w2[4];
 #pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const float q0 = s[kt][8 * ks + 2 * jj], q1 = s[kt][8 * ks + 2 * jj + 1];
-                        w1[jj] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){q0, q1}, f16x2));
-                        w2[jj] = hfa::split_lo_pair(w1[jj], q0, q1, one);
-                    }
-                    p1s = __builtin_bit_cast(f16x8, make_uint4(w1[0], w1[1], w1[2], w1[3]));
-                    p2 = __builtin_bit_cast(f16x8, make_uint4(w2[0], w2[1], w2[2], w2[3]));
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        // 2^11 p1 = q with the low 13 mantissa bits cleared (an f16 value for q >= 2^-14),
-                        // 2^11 (p - p1) = the exact f32 remainder, rounded to f16
-                        const float qv = s[kt][8 * ks + j];
-                        const float qt = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, qv) & 0xFFFFE000u);
-                        p1s[j] = (_Float16)qt;
-                        p2[j] = (_Float16)(qv - qt);
-                    }
+                for (int jj = 0; jj < 4; ++jj) {
+                    const float q0 = s[kt][8 * ks + 2 * jj], q1 = s[kt][8 * ks + 2 * jj + 1];
+                    w1[jj] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){q0, q1}, f16x2));
+                    w2[jj] = hfa::split_lo_pair(w1[jj], q0, q1, one);
                 }
+                p1s = __builtin_bit_cast(f16x8, make_uint4(w1[0], w1[1], w1[2], w1[3]));
+                p2 = __builtin_bit_cast(f16x8, make_uint4(w2[0], w2[1], w2[2], w2[3]));
                 p1 = p1s * (_Float16)kLo;
                 const int rb = (32 * kt + 16 * ks) * (DH * 2);
 #pragma unroll
@@ -498,17 +481,12 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
                 }
             }
         if (t + 1 < nkb) {
-            if (!V2) combine(nM, nC, s);
             hfa::wait_vm_barrier<0>();                     // K(t+2), V(t+1) landed; K(t+1), V(t) reads done
         }
     };
-    if (V2) {
-        for (int t = 0; t < nkb; t += 2) {
-            step(t, sA, sB);
-            if (t + 1 < nkb) step(t + 1, sB, sA);
-        }
-    } else {
-        for (int t = 0; t < nkb; ++t) step(t, sA, sB);
+    for (int t = 0; t < nkb; t += 2) {
+        step(t, sA, sB);
+        if (t + 1 < nkb) step(t + 1, sB, sA);
     }
 
     __syncthreads();
@@ -549,7 +527,6 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
 
 namespace {
 thread_local int g_attn_waves = 0;   // hfa_attention_split_tuning override (0: automatic)
-thread_local bool g_attn_v1 = false;   // hfa_attention_split_tuning + 100: the round-2 kernel body
 // Waves (x 32 queries) per workgroup of the split attention: 8 where that still leaves >= 2 workgroups per
 // (batch, head) row of queries, else 4.
 inline int split_attn_waves(int L) {
@@ -622,27 +599,20 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
         hfa::set_error("hfa_attention_split: grid too large");
         return HFA_EINVAL;
     }
-    if (nw == 8 && g_attn_v1)
-        hipLaunchKernelGGL((attn_fwd_split_kernel<8, false>), dim3((unsigned)nblk), dim3(8 * 64), 0, stream, p);
-    else if (nw == 8)
-        hipLaunchKernelGGL((attn_fwd_split_kernel<8, true>), dim3((unsigned)nblk), dim3(8 * 64), 0, stream, p);
-    else if (g_attn_v1)
-        hipLaunchKernelGGL((attn_fwd_split_kernel<4, false>), dim3((unsigned)nblk), dim3(4 * 64), 0, stream, p);
+    if (nw == 8)
+        hipLaunchKernelGGL((attn_fwd_split_kernel<8>), dim3((unsigned)nblk), dim3(8 * 64), 0, stream, p);
     else
-        hipLaunchKernelGGL((attn_fwd_split_kernel<4, true>), dim3((unsigned)nblk), dim3(4 * 64), 0, stream, p);
+        hipLaunchKernelGGL((attn_fwd_split_kernel<4>), dim3((unsigned)nblk), dim3(4 * 64), 0, stream, p);
     return hfa::check_launch("hfa_attention_split");
 }
 
-// Waves per workgroup of hfa_attention_split: 4 or 8, 0 = automatic (benchmarks and the 4/8 parity test); + 100:
-// the round-2 P split and tile loop (attn_fwd_split_kernel<.., false>, A/B timing).
+// Waves per workgroup of hfa_attention_split: 4 or 8, 0 = automatic (benchmarks and the 4/8 parity test).
 int hfa_attention_split_tuning(int waves) {
-    const int w = waves % 100;
-    if (waves < 0 || waves >= 200 || (w != 0 && w != 4 && w != 8)) {
-        hfa::set_error("hfa_attention_split_tuning: waves must be 0, 4 or 8 (+ 100)");
+    if (waves != 0 && waves != 4 && waves != 8) {
+        hfa::set_error("hfa_attention_split_tuning: waves must be 0, 4 or 8");
         return HFA_EINVAL;
     }
-    g_attn_waves = w;
-    g_attn_v1 = waves >= 100;
+    g_attn_waves = waves;
     return HFA_OK;
 }
 

@@ -604,8 +604,6 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
     // R groups of G steps in flight (K * G * R emission registers per lane, within the VGPR budget of 64 * NW
     // threads: 512 up to 4 waves, 256 at 8, 128 at 16)
     const int per_lane = (Smax + 63) / 64;
-    if (g_force_k == 1 && per_lane <= 2) HFA_FWD(2, 1, 4, 2);   // (A/B: a short emission ring, fewer VGPRs)
-    if (g_force_k == 5 && per_lane <= 2) HFA_FWD(2, 1, 8, 2);
     if (per_lane <= 1) HFA_FWD(1, 1, 8, 4);
     if (per_lane <= 2) HFA_FWD(2, 1, 8, 4);
     if (per_lane <= 4) HFA_FWD(4, 1, 8, 3);
@@ -644,9 +642,8 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
 }
 
 int hfa_viterbi_tuning(int force_k) {
-    if (force_k != 0 && force_k != 1 && force_k != 2 && force_k != 4 && force_k != 5 && force_k != 8) {
-        hfa::set_error("hfa_viterbi_tuning: states per lane must be 0 (automatic), 2, 4 or 8, or 1 / 5 (the "
-                       "one-wave DP with a short emission ring, 4 x 2 / 8 x 2 steps) (got %d)", force_k);
+    if (force_k != 0 && force_k != 2 && force_k != 4 && force_k != 8) {
+        hfa::set_error("hfa_viterbi_tuning: states per lane must be 0 (automatic), 2, 4 or 8 (got %d)", force_k);
         return HFA_EINVAL;
     }
     g_force_k = force_k;

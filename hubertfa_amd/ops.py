@@ -145,7 +145,6 @@ _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_
 _lib.register("hfa_attention_split", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _LL_,
                                       _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _P_])
 _lib.register("hfa_attention_split_tuning", [_I_])
-_lib.register("hfa_conv0_tuning", [_I_])
 _lib.register("hfa_layernorm_split", [_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_,
                                       _LL_, _P_, _P_])
 _lib.register("hfa_layernorm_f32",[_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_])
@@ -188,7 +187,7 @@ class KernelProbe:
     def dominant(self) -> str:
         return max(self.census, key=self.census.get)
 
-    def __call__(self, name: str, work: float, launch, kind: str = "flops"):
+    def __call__(self, name: str, work: float, launch, kind: str = "flops", shape=None):
         if self.name is None:
             if kind == "flops":
                 self.census[name] = self.census.get(name, 0.0) + work
@@ -279,76 +278,6 @@ def split_flag(device) -> torch.Tensor:
     return _OFLOW[key]
 
 
-class UnetOp(ctypes.Structure):
-    """include/hfa.h hfa_unet_op (one op of the fused UNet + head table)."""
-    _fields_ = [("kind", ctypes.c_int32), ("level", ctypes.c_int32), ("n", ctypes.c_int32),
-                ("groups", ctypes.c_int32), ("nseg", ctypes.c_int32),
-                ("src", ctypes.c_int32 * 2), ("src_ld", ctypes.c_int32 * 2), ("cin", ctypes.c_int32 * 2),
-                ("taps", ctypes.c_int32 * 2), ("gn", ctypes.c_int32 * 2), ("ldw", ctypes.c_int32 * 2),
-                ("res", ctypes.c_int32), ("dst", ctypes.c_int32),
-                ("src_off", ctypes.c_int64 * 2), ("res_off", ctypes.c_int64), ("dst_off", ctypes.c_int64),
-                ("w", ctypes.c_void_p * 2), ("wp", ctypes.c_int64 * 2),
-                ("bias", ctypes.c_void_p), ("gn_gamma", ctypes.c_void_p), ("gn_beta", ctypes.c_void_p),
-                ("ln_gamma", ctypes.c_void_p), ("ln_beta", ctypes.c_void_p)]
-
-
-UNET_NONE, UNET_INPUT, UNET_OUTPUT = -1, -2, -3
-_lib.register("hfa_unet_head", [_I_, _I_, _P_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_, _P_, _P_])
-_lib.register("hfa_unet_lds_bytes", [], restype=ctypes.c_longlong)
-_lib.register("hfa_unet_validate", [_P_, _I_, _LL_, _I_])
-_lib.register("hfa_unet_gn_doubles", [_I_], restype=ctypes.c_longlong)
-_lib.register("hfa_unet_head_tiled", [_I_, _I_, _P_, _P_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_, _P_,
-                                      _LL_, _P_, _P_])
-_lib.register("hfa_unet_profile", [_P_])
-
-
-def unet_validate(table, ws_floats_per_row: int, l_ld: int):
-    """Check a host op table (a ctypes array of UnetOp) before it is uploaded: ValueError (HFAArgumentError) naming
-    the first bad op."""
-    _lib.call("hfa_unet_validate", ctypes.addressof(table), len(table), ws_floats_per_row, l_ld)
-
-
-def unet_head_tiled(host_table, table, feats, logits, t_pad, workspace, ws_floats, flag, flops=0.0):
-    """The same op table as one launch per op, one workgroup per (row block, utterance) (unet.hip
-    hfa_unet_head_tiled); ``host_table`` the ctypes UnetOp array the device ``table`` was made from."""
-    B, Tmax, _ = feats.shape
-    _need(feats, torch.float32, "feats", contiguous=False)
-    _need(logits, torch.float32, "logits", contiguous=False)
-    _need(t_pad, torch.int32, "t_pad")
-    if feats.stride(2) != 1 or logits.stride(2) != 1 or logits.stride(1) % 4 or logits.data_ptr() % 16:
-        raise ValueError("unet_head_tiled: contiguous rows, logits rows 16-B aligned")
-    gn_bs = int(_lib.lib().hfa_unet_gn_doubles(Tmax))
-    gn = torch.empty((B, gn_bs), dtype=torch.float64, device=feats.device)
-
-    def launch():
-        _lib.call("hfa_unet_head_tiled", B, Tmax, ctypes.addressof(host_table), _ptr(table), len(host_table),
-                  _ptr(feats), feats.stride(0), feats.stride(1), _ptr(logits), logits.stride(0), logits.stride(1),
-                  _ptr(t_pad), _ptr(workspace), ws_floats, _ptr(gn), gn_bs, _ptr(flag), _stream(feats.device))
-    if PROBE is None:
-        return launch()
-    PROBE("unet_op_kernel", flops, launch)
-
-
-def unet_head(table, nops, feats, logits, t_pad, workspace, ws_floats, flag, flops=0.0):
-    """The fused UNet + head (unet.hip): ``table`` a device uint8 tensor of ``nops`` UnetOp records, feats
-    [B, Tmax, Cin] f32 (rows >= each t_pad[b] zero), logits [B, Tmax, V+2] f32 out, t_pad int32 [B] device,
-    workspace f32 with ws_floats per utterance."""
-    B, Tmax, _ = feats.shape
-    _need(feats, torch.float32, "feats", contiguous=False)
-    _need(logits, torch.float32, "logits", contiguous=False)
-    _need(t_pad, torch.int32, "t_pad")
-    if feats.stride(2) != 1 or logits.stride(2) != 1 or logits.stride(1) % 4 or logits.data_ptr() % 16:
-        raise ValueError("unet_head: contiguous rows, logits rows 16-B aligned")
-
-    def launch():
-        _lib.call("hfa_unet_head", B, Tmax, _ptr(table), nops, _ptr(feats), feats.stride(0), feats.stride(1),
-                  _ptr(logits), logits.stride(0), logits.stride(1), _ptr(t_pad), _ptr(workspace), ws_floats,
-                  _ptr(flag), _stream(feats.device))
-    if PROBE is None:
-        return launch()
-    PROBE("unet_head_kernel", flops, launch)
-
-
 def split(x, out=None, flag=None):
     """f32 [..., C] (row-strided) -> split planes [2, ..., C]; out-of-range values raise ``flag`` (default: the
     device's split_flag)."""
@@ -397,7 +326,8 @@ def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0
         _lib.call("hfa_conv_gemm_split", *args, _stream(dev))
     if PROBE is None:
         return launch()
-    PROBE(_split_name(M, N, Zb * G, Cs is not None and C is None, epilogue, Cg or K), 2.0 * M * N * K * Zb * G, launch)
+    PROBE(_split_name(M, N, Zb * G, Cs is not None and C is None, epilogue, Cg or K), 2.0 * M * N * K * Zb * G, launch,
+          shape=(M, N, K, Zb * G))
 
 
 def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, out_split=False, flag=None,
@@ -471,7 +401,8 @@ def attention_split(qkv_s, out_s, *, B, H, L, head_dim, scale, key_len=None):
     if PROBE is None:
         launch()
     else:
-        PROBE("attn_fwd_split_kernel", 4.0 * B * H * L * L * head_dim, launch, kind="flops_aux")
+        PROBE("attn_fwd_split_kernel", 4.0 * B * H * L * L * head_dim, launch, kind="flops_aux",
+              shape=(B, H, L, head_dim))
     return out_s
 
 

@@ -228,9 +228,6 @@ class ForcedAlignmentTask:
         pinned = x if x.is_pinned() else x.contiguous().pin_memory()
         return pinned.to(self.device, non_blocking=True)   # (the pinned block is held until this copy ends)
 
-    head_on_main = __import__("os").environ.get("HFA_HEAD_ON_MAIN", "0") == "1"     # (A/B switch)
-    side_prio = __import__("os").environ.get("HFA_SIDE_PRIO", "same")   # (A/B: same | high | low, vs the encoder)
-
     def submit(self, waves: torch.Tensor, ph_seqs, word_seqs=None, p2ws=None, wav_sr: int | None = None,
                on_device=None, lengths=None, chunk_seconds: float | None = None):
         """Two-stream pipelined device pass; returns the decoder's fetch handle (``decoder.assemble`` completes it).
@@ -239,36 +236,17 @@ class ForcedAlignmentTask:
         waits for it, so a batch's small-grid tail (UNet GEMMs on a few hundred workgroups, one DP workgroup per
         utterance) overlaps the next batch's extractor convs instead of idling most of the chip.  ``on_device``
         (e.g. the RCCL boundary gather) runs on the side stream after the backtrack."""
-        caller = torch.cuda.current_stream(self.device)
+        main = torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(self.device, priority=-1 if self.side_prio == "high" else 0)
-            self._hi = torch.cuda.Stream(self.device, priority=-1) if self.side_prio == "low" else None
-        main = caller
-        if self._hi is not None:                 # the encoder on a high-priority stream, the side stream below it
-            main = self._hi
-            main.wait_stream(caller)
-            if isinstance(waves, torch.Tensor) and waves.is_cuda:
-                waves.record_stream(main)
-        with torch.cuda.stream(main):
-            feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds)
-            if self.head_on_main:                # the UNet head right behind the encoder, only the DP beside it
-                logits, hflag = self.head_logits(feats, n_frames)
-            guard = self._guard({}, (waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds))
+            self._side = torch.cuda.Stream(self.device)
+        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds)
+        guard = self._guard({}, (waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds))
         ready = torch.cuda.Event()
         ready.record(main)
-        if main is not caller:
-            caller.wait_stream(main)
-            feats.record_stream(caller)
         with torch.cuda.stream(self._side):
             self._side.wait_event(ready)
-            if self.head_on_main:
-                logits.record_stream(self._side)
-                if hflag is not None:
-                    hflag.record_stream(self._side)
-                dev_out = self.lattice_dp(logits, hflag, wl, ph_seqs, word_seqs, p2ws)
-            else:
-                feats.record_stream(self._side)  # the caching allocator must not recycle it under the side stream
-                dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
+            feats.record_stream(self._side)      # the caching allocator must not recycle it under the side stream
+            dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
             if "split_oflow" in guard:
                 guard["split_oflow"].record_stream(self._side)
             dev_out.update(guard)

@@ -161,177 +161,6 @@ class _Up:
         return y.view(B, T * self.f, self.cout), (ys.view(2, B, T * self.f, self.cout) if ys is not None else None)
 
 
-class FusedPlan:
-    """Op table of the fused kernel (unet.hip, ``hfa_unet_head``): the same layers as LatticeHead.backbone + head,
-    in the same order, one workgroup per utterance.  Slots are f32 tensors of the per-utterance workspace, each
-    given as floats per Tmax row (a tensor of C channels at level l needs C >> l of them); ping-pong slots X
-    (down / up outputs, block inputs), H (first conv outputs), Y (block outputs) and one skip slot per encoder
-    level.  Built once per head (weights are static); None when a weight has no split planes (|w| >= 16) or the
-    geometry is outside the kernel (channels % 32, outputs > 384)."""
-
-    MAX_T = 2048      # utterances with more padded frames (> 23.8 s) take the chip-wide path (the fused kernel runs
-                      # one utterance per CU: its time grows with T, while the chip-wide launches spread it)
-
-    def __init__(self, head: "LatticeHead"):
-        a = head.arch
-        c = head.ctx
-        self.keep = []                  # tensors whose device pointers the table holds
-        ops = []
-        widths = {}
-
-        def slot(name, w):
-            widths[name] = max(widths.get(name, 0), w)
-            return name
-
-        def planes(p):
-            if p is None:
-                raise ValueError("no split planes")      # |w| >= 16 somewhere, or K % 32
-            f = fragment_layout(p)
-            self.keep.append(f)
-            return f
-
-        def op(kind, level, n, segs, dst, res=None, bias=None, gn=None, ln=None):
-            o = {"kind": kind, "level": level, "n": n, "segs": segs, "dst": dst, "res": res, "bias": bias, "gn": gn,
-                 "ln": ln}
-            ops.append(o)
-            return o
-
-        def seg(src, ld, cin, taps, w, gn=False):
-            if cin % 32 or (w is not None and w.shape[-1] % 32):
-                raise ValueError("channels % 32")
-            return {"src": src, "ld": ld, "cin": cin, "taps": taps, "w": planes(w), "gn": gn}
-
-        def block(bl, level, src, src_ld, dst):
-            h = slot("H", bl.hid >> level)
-            op(0, level, bl.hid, [seg(src, src_ld, bl.cin, 3, bl.w1s)], h)
-            segs = [seg(h, bl.hid, bl.hid, 3, bl.w2s, gn=True)]
-            res = None
-            if bl.sc is not None:
-                segs.append(seg(src, src_ld, bl.cin, 1, bl.scs))
-            else:
-                res = src
-            op(1, level, bl.cout, segs, slot(dst, bl.cout >> level), res=res, gn=bl.gn, ln=bl.ln)
-
-        inp = "INPUT"
-        e0 = head.encoders[0][0]
-        block(e0, 0, inp, e0.cin, "S0")
-        for i in range(1, a.times):
-            dn, bl = head.encoders[i]
-            op(2, i, dn.cout, [seg(f"S{i - 1}", 2 * dn.cin, 2 * dn.cin, 1, dn.ws)], slot("X", dn.cout >> i), bias=dn.b)
-            block(bl, i, "X", dn.cout, f"S{i}")
-        bd, bb, bu = head.bottleneck
-        lv = a.times
-        op(2, lv, bd.cout, [seg(f"S{lv - 1}", 2 * bd.cin, 2 * bd.cin, 1, bd.ws)], slot("X", bd.cout >> lv), bias=bd.b)
-        block(bb, lv, "X", bd.cout, "Y")
-        # transposed conv: [T, 2 Cout] rows of the input level = the [2T, Cout] rows of the level above, + the skip
-        op(3, lv, 2 * bu.cout, [seg("Y", bu.cin, bu.cin, 1, bu.ws)], slot("X", bu.cout >> (lv - 1)),
-           res=f"S{lv - 1}", bias=bu.b)
-        for i, dec in enumerate(head.decoders):
-            lev = a.times - 1 - i
-            bl = dec[0]
-            block(bl, lev, "X", bl.cin, "Y")
-            if len(dec) > 1:
-                up = dec[1]
-                op(3, lev, 2 * up.cout, [seg("Y", up.cin, up.cin, 1, up.ws)], slot("X", up.cout >> (lev - 1)),
-                   res=f"S{lev - 1}", bias=up.b)
-        hw = head.head_w
-        self.head_planes = fragment_layout(ops_split(hw, c))
-        self.keep.append(self.head_planes)
-        out_n = hw.shape[0]
-        self.out_ld = -(-out_n // 4) * 4          # the row-wise epilogue moves float4s: head rows padded to 4
-        self.head_bias = torch.zeros(self.out_ld, dtype=torch.float32, device=c.dev)
-        self.head_bias[:out_n] = head.head_b
-        op(4, 0, self.out_ld, [{"src": "Y", "ld": head.decoders[-1][0].cout, "cin": head.decoders[-1][0].cout,
-                                "taps": 1, "w": self.head_planes, "gn": False}], "OUTPUT", bias=self.head_bias)
-        if any(o["n"] > 384 or o["n"] % 4 for o in ops) or any(sg["cin"] % 32 for o in ops for sg in o["segs"]):
-            raise ValueError("outputs > 384 columns")
-        # slot offsets (floats per Tmax row)
-        off, self.ws_floats_per_row = {}, 0
-        for name in sorted(widths):
-            off[name] = self.ws_floats_per_row
-            self.ws_floats_per_row += -(-widths[name] // 4) * 4        # 16-B aligned rows of every slot
-        table = (ops_unet_op_type() * len(ops))()
-        for k, o in enumerate(ops):
-            r = table[k]
-            r.kind, r.level, r.n, r.groups, r.nseg = o["kind"], o["level"], o["n"], 16, len(o["segs"])
-            for s, sg in enumerate(o["segs"]):
-                r.src[s] = -2 if sg["src"] == "INPUT" else 0
-                r.src_off[s] = 0 if sg["src"] == "INPUT" else off[sg["src"]]
-                r.src_ld[s], r.cin[s], r.taps[s], r.gn[s] = sg["ld"], sg["cin"], sg["taps"], int(sg["gn"])
-                r.ldw[s] = sg["taps"] * sg["cin"]
-                r.w[s] = sg["w"].data_ptr()
-                r.wp[s] = sg["w"].stride(0)
-            if o["res"] is None:
-                r.res = -1
-            else:
-                r.res, r.res_off = (-2, 0) if o["res"] == "INPUT" else (0, off[o["res"]])
-            if o["dst"] == "OUTPUT":
-                r.dst = -3
-            else:
-                r.dst, r.dst_off = 0, off[o["dst"]]
-            r.bias = o["bias"].data_ptr() if o["bias"] is not None else None
-            if o["gn"] is not None:
-                r.gn_gamma, r.gn_beta = o["gn"][0].data_ptr(), o["gn"][1].data_ptr()
-            if o["ln"] is not None:
-                r.ln_gamma, r.ln_beta = o["ln"][0].data_ptr(), o["ln"][1].data_ptr()
-        ops_unet_validate(table, self.ws_floats_per_row, self.out_ld)
-        self.host_table = table
-        raw = bytes(table)
-        self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(c.dev)
-        self.nops = len(ops)
-        self.out_n = out_n
-        self.ops = ops
-
-    def __call__(self, x: torch.Tensor, t_pad, flag, tiled: bool = False) -> torch.Tensor:
-        """x [B, Tmax, C_in] (rows >= t_pad[b] zero) -> logits [B, Tmax, V+2] (rows >= t_pad[b] not written).
-        ``tiled``: one launch per op over (row block, utterance) workgroups instead of one workgroup per utterance."""
-        from .hubert import dev_lengths
-        B, Tmax, _ = x.shape
-        logits = torch.empty((B, Tmax, self.out_ld), dtype=torch.float32, device=x.device)
-        ws = torch.empty((B, Tmax * self.ws_floats_per_row), dtype=torch.float32, device=x.device)
-        tp = dev_lengths(t_pad, x.device)
-        if tiled:
-            ops.unet_head_tiled(self.host_table, self.table, x, logits, tp, ws, Tmax * self.ws_floats_per_row, flag,
-                                flops=self.flops(t_pad))
-        else:
-            ops.unet_head(self.table, self.nops, x, logits, tp, ws, Tmax * self.ws_floats_per_row, flag,
-                          flops=self.flops(t_pad))
-        return logits[:, :, :self.out_n]
-
-    def flops(self, t_pad) -> float:
-        f = 0.0
-        for o in self.ops:
-            for sg in o["segs"]:
-                f += sum(2.0 * (int(t) >> o["level"]) * o["n"] * sg["taps"] * sg["cin"] for t in t_pad)
-        return f
-
-
-def fragment_layout(planes: torch.Tensor) -> torch.Tensor:
-    """[2, N, K] split planes -> the fused kernel's fragment order [2, K/32, ceil(N/16), 64 lanes, 8] (lane = 16 *
-    (k % 32 // 8) + n % 16): one 16 x 32 MFMA operand is one contiguous 1 KiB piece; padded columns are zero."""
-    _, N, K = planes.shape
-    NB = -(-N // 16)
-    p = torch.zeros((2, NB * 16, K), dtype=planes.dtype, device=planes.device)
-    p[:, :N] = planes
-    p = p.view(2, NB, 16, K // 32, 4, 8).permute(0, 3, 1, 4, 2, 5).contiguous()
-    return p.view(2, K // 32, NB, 64, 8)
-
-
-def ops_split(w, ctx):
-    """Split planes of a weight for the fused kernel (|w| < 16 as the split GEMM's single-accumulator form)."""
-    if not bool(w.abs().max() < 16) or w.shape[-1] % 32:
-        raise ValueError("head weight outside the split range")
-    return ops.split(w, flag=ctx.flag)
-
-
-def ops_unet_op_type():
-    return ops.UnetOp
-
-
-def ops_unet_validate(table, ws_floats_per_row, l_ld):
-    ops.unet_validate(table, ws_floats_per_row, l_ld)
-
-
 class LatticeHead:
     """UNet backbone + linear head: features [B, T_pad, C_in] -> logits [B, T_pad, V+2]."""
 
@@ -414,65 +243,15 @@ class LatticeHead:
                 t = dec[1](t[0], L(lev), xs=t[1], want_split=True, skip=h[n_enc - 1 - i][0])
         return t if want_split else t[0]
 
-    @property
-    def fused(self):
-        """The fused one-kernel plan (split precision), built on first use; None when the weights or geometry
-        keep the head on the chip-wide path."""
-        if getattr(self, "_fused", False) is False:
-            try:
-                self._fused = FusedPlan(self) if self.ctx.dev.type == "cuda" else None
-            except ValueError:
-                self._fused = None
-        return self._fused
-
     @torch.no_grad()
     def logits(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
-        """x [B, T_pad, C_in] -> logits [B, T_pad, V+2].  Split precision: utterances of up to FusedPlan.MAX_T padded
-        frames run on the fused kernel (one workgroup each), longer ones on the chip-wide launches; the choice
-        depends on an utterance's own length only, so its result does not depend on the batch."""
-        if self.ctx.precision == "split" and self.use_tiled and self.fused is not None:
-            B, T = x.shape[0], x.shape[1]
-            return self.fused(x, [int(v) for v in t_pad] if t_pad is not None else [T] * B, self.ctx.flag,
-                              tiled=True)
-        fp = self.fused if self.ctx.precision == "split" and self.use_fused else None
-        if fp is not None:
-            B, T = x.shape[0], x.shape[1]
-            tp = [int(v) for v in t_pad] if t_pad is not None else [T] * B
-            short = [b for b in range(B) if tp[b] <= FusedPlan.MAX_T]
-            if len(short) == B:
-                return fp(x, tp, self.ctx.flag)
-            if short:
-                longr = [b for b in range(B) if tp[b] > FusedPlan.MAX_T]
-                out = torch.empty((B, T, fp.out_n), dtype=torch.float32, device=x.device)
-                from .hubert import dev_lengths
-                si, li = dev_lengths(short, x.device).long(), dev_lengths(longr, x.device).long()
-                tshort = max(tp[b] for b in short)
-                out[si, :tshort] = fp(x.index_select(0, si)[:, :tshort].contiguous(), [tp[b] for b in short],
-                                      self.ctx.flag)
-                xl = x.index_select(0, li)
-                out[li] = self._chipwide(xl, [tp[b] for b in longr] if t_pad is not None else None)
-                return out
-        return self._chipwide(x, t_pad)
-
-    use_fused = __import__("os").environ.get("HFA_UNET_FUSED", "0") == "1"   # (A/B switch: 1 = the fused kernel)
-    use_tiled = __import__("os").environ.get("HFA_UNET_TILED", "0") == "1"   # (A/B: 1 = the op engine, per-op launches)
-
-    unet_tile = int(__import__("os").environ.get("HFA_UNET_TILE", "0"))   # (A/B: a split-GEMM tile for the backbone)
-
-    def _chipwide(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
-        if self.unet_tile:
-            from . import _lib
-            _lib.call("hfa_gemm_split_tuning", self.unet_tile)
-        try:
-            if self.ctx.use_split(self.head_ws):
-                y, ys = self.backbone(x, t_pad, want_split=True)
-            else:
-                y, ys = self.backbone(x, t_pad), None
-        finally:
-            if self.unet_tile:
-                _lib.call("hfa_gemm_split_tuning", 0)
-        if ys is not None:
+        """x [B, T_pad, C_in] -> logits [B, T_pad, V+2] on the chip-wide launches (every GEMM spreads over the whole
+        chip; a row's result depends on its own length only).  The one-kernel and per-op-engine forms of round 3
+        were parity-green but slower in the pipeline; they are in git history."""
+        if self.ctx.use_split(self.head_ws):
+            y, ys = self.backbone(x, t_pad, want_split=True)
             return self.ctx.linear(y, ys, self.head_wp, self.head_ws, self.head_bp)[0][:, :, :self.head_w.shape[0]]
+        y = self.backbone(x, t_pad)
         return self.ctx.linear(y, None, self.head_w, None, self.head_b)[0]
 
     @staticmethod

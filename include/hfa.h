@@ -61,9 +61,8 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
                         const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,
                         hipStream_t stream);
 
-/* Tuning hook (benchmarks): states per lane of the multi-wave forward DP, 2 / 4 / 8, 0 = automatic (2 up to 2048
- * states, 4 up to 4096, then 8); 1 / 5 = the one-wave DP (<= 128 states) with a short emission ring (4 x 2 / 8 x 2
- * steps in flight: 69 / 109 VGPRs instead of 177; measured no different in the pipeline). */
+/* Tuning hook (tests, benchmarks): states per lane of the multi-wave forward DP, 2 / 4 / 8, 0 = automatic (4 up
+ * to 4096 states, then 8); the same bits whatever the choice. */
 int hfa_viterbi_tuning(int force_k);
 
 /* hfa_viterbi_backtrack replaces the backward half of AlignmentDecoder._decode,
@@ -169,8 +168,7 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
                         const uint16_t* v, long long v_sp, long long v_bs, int v_ld, uint16_t* o, long long o_sp,
                         long long o_bs, int o_ld, const int32_t* key_len, hipStream_t stream);
 /* Waves (x 32 queries) per workgroup of hfa_attention_split: 4 or 8, 0 = automatic (8 for L >= 512).  Results
- * do not depend on it (every query row sees the same tiles in the same order).  + 100: the round-2 kernel body
- * (truncated high plane of P, one tile per loop trip), for A/B timing. */
+ * do not depend on it (every query row sees the same tiles in the same order). */
 int hfa_attention_split_tuning(int waves);
 
 /* ---- normalisation (hubertfa_amd/csrc/norm.hip); act: 0 none, 1 erf-GELU, 2 Hardswish -----------------------
@@ -206,65 +204,6 @@ int hfa_groupnorm_split(int B, int T, int C, int G, const float* x, long long x_
                         uint16_t* ys, long long ys_bs, int ldys, long long sps, int* oflow, void* workspace,
                         hipStream_t stream);
 
-/* ---- fused lattice producer (hubertfa_amd/csrc/unet.hip) ------------------------------------------------------
- * UNetBackbone + head of LitForcedAlignmentTask (networks/layer/backbone/unet.py:100-119, networks/layer/block/
- * resnet_block.py:17-50, networks/layer/scaling/stride_conv.py:23-47, networks/task/forced_alignment.py:53-55,
- * 287-288) as ONE launch: one workgroup per utterance runs the op table in order on its own t_pad[b] rows, with
- * split-f16 contractions (see hfa_conv_gemm_split), GroupNorm statistics in f64 and LayerNorm in f32 inside the
- * workgroup.  Slots name f32 tensors of the per-utterance workspace (offsets in floats per Tmax row).
- *   kind 0 conv1: k3 conv of src[0]; output = the raw conv (the block's GroupNorm statistics are kept in LDS)
- *   kind 1 conv2: k3 conv of GroupNorm(groups) + Hardswish of src[0] (gn[0] = 1), + Linear shortcut (segment 1)
- *                 or + residual slot, then LayerNorm + Hardswish
- *   kind 2 down: k2 s2 conv (src rows read as pairs: cin = 2 C, ldw = 2 C) + bias
- *   kind 3 up: ConvTranspose k2 s2 as [T, 2 Cout] = [2T, Cout] (+ bias + skip slot)
- *   kind 4 head: Linear + bias into `logits` (dst = HFA_UNET_OUTPUT)
- * Weights w[s] are split planes in fragment order: plane p at w + p * wp halves, [K/32][ceil(n/16)][64][8] halves,
- * element (k, n) at lane (k % 32 / 8) * 16 + n % 16, position k % 8 (one contiguous 1 KiB MFMA operand per 16 columns
- * x 32 k); ldw[s] = K.  n <= 384 and n % 4 == 0 (rows move as float4s: feats, logits and workspace 16-B aligned,
- * l_ld % 4 == 0), cin % 32 == 0, t_pad[b] a multiple of 2^(max level) and <= Tmax (a workgroup whose t_pad[b] is
- * <= 0 or > Tmax writes nothing); *oflow raised for an operand outside f16 range or a non-finite output.  Tables
- * are checked on the host by hfa_unet_validate. */
-#define HFA_UNET_NONE (-1)
-#define HFA_UNET_INPUT (-2)
-#define HFA_UNET_OUTPUT (-3)
-typedef struct hfa_unet_op {
-    int32_t kind, level, n, groups, nseg;
-    int32_t src[2], src_ld[2], cin[2], taps[2], gn[2], ldw[2];
-    int32_t res, dst;
-    int64_t src_off[2], res_off, dst_off;
-    const uint16_t* w[2];
-    int64_t wp[2];
-    const float* bias;
-    const float* gn_gamma;
-    const float* gn_beta;
-    const float* ln_gamma;
-    const float* ln_beta;
-} hfa_unet_op;
-int hfa_unet_head(int B, int Tmax, const hfa_unet_op* ops, int nops, const float* feats, long long f_bs, int f_ld,
-                  float* logits, long long l_bs, int l_ld, const int32_t* t_pad, float* workspace, long long ws_bs,
-                  int* oflow, hipStream_t stream);
-/* Host-side check of an op table before it is uploaded (the launch reads the table from device memory, so it cannot
- * check it): kinds, channel and tap constraints above, weight pointers 16-B aligned with plane strides that hold
- * [K/32][ceil(n/16)][64][8] halves, the parameters each kind reads present, HFA_UNET_OUTPUT only as the head's
- * destination with n <= l_ld, and every slot access inside ws_floats_per_row floats per Tmax row (a level-l tensor of
- * row width ld uses ceil(ld / 2^l) of them).  HFA_OK or HFA_EINVAL with hfa_last_error() naming the op. */
-int hfa_unet_validate(const hfa_unet_op* host_ops, int nops, long long ws_floats_per_row, int l_ld);
-/* The same op table as one launch PER OP, one workgroup per (row block, utterance): row blocks of 128 rows for
- * n <= 192, 64 above.  host_ops is the table in host memory (the launch grid of each op is planned from it), ops the
- * same table in device memory.  gn_ws: per-utterance GroupNorm partials (f64, gn_bs >= hfa_unet_gn_doubles(Tmax)
- * doubles apart), written by each first conv and summed in row-block order by its second conv (deterministic,
- * independent of the batch).  Other arguments as hfa_unet_head. */
-long long hfa_unet_gn_doubles(int Tmax);
-int hfa_unet_head_tiled(int B, int Tmax, const hfa_unet_op* host_ops, const hfa_unet_op* ops, int nops,
-                        const float* feats, long long f_bs, int f_ld, float* logits, long long l_bs, int l_ld,
-                        const int32_t* t_pad, float* workspace, long long ws_bs, double* gn_ws, long long gn_bs,
-                        int* oflow, hipStream_t stream);
-/* LDS bytes the fused kernel's workgroup uses (diagnostics). */
-long long hfa_unet_lds_bytes(void);
-/* Diagnostics: the calling thread's next hfa_unet_head launch writes workgroup 0's s_memrealtime (100 MHz) at the
- * start of every op and at the end into buf[0 .. nops] (device memory); the hook resets after that launch. */
-int hfa_unet_profile(long long* buf);
-
 /* ---- extractor conv0 (hubertfa_amd/csrc/conv.hip) ------------------------------------------------------------
  * x [B, N] -> y [B, T0, 512] channels-last, T0 = (N-10)/5+1.  norm=1: GroupNorm(512,512) + GELU
  * (networks/hubert/model.py:98-99,108; transformers HubertGroupNormConvLayer), needs a workspace of
@@ -299,16 +238,6 @@ int hfa_pad_rows_f32(int B, int N, const float* x, long long x_bs, int left, int
                      hipStream_t stream);
 /* Self-test: y_nb = the branch-free erf of every GELU epilogue, y_ref = device erff (must be bit-identical). */
 int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hipStream_t stream);
-/* conv0 kernel choice for the split-plane output (per calling thread; the f32 output is always the VALU apply
- * pass): 0 = default: GroupNorm statistics from the wave's lag products (S_j, G_jk over the frames: 65 numbers per
- * utterance, f64) and the packed f16-MFMA apply pass (the three split products of the 10 taps in one K = 32 step,
- * stores through a per-wave LDS tile, non-temporal); 1 = the round-1 passes (the conv re-run for f64 sums of its outputs) with the
- * VALU apply pass; 2 = lag-product statistics with the taps of the apply pass on the f32-input MFMA (an exact
- * k-ordered fmaf chain: mode 3's bits); 3 = lag-product statistics with the VALU apply pass (the round-2 default);
- * 4 / 7 = mode 0 with its stores straight from the MFMA layout / through a block-wide tile (mode 0's bits); 8 =
- * mode 0 with plain instead of non-temporal stores; 10 = mode 0 held to 2 workgroups per CU.  HFA_EINVAL otherwise
- * (5, 6 and 9 were measurement-only ablations). */
-int hfa_conv0_tuning(int mode);
 /* Self-test: y = the GELU applied by every fused epilogue (GEMM, LayerNorm/GroupNorm act, conv0). */
 int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream);
 /* out = a + b (UNet skip connection, networks/layer/backbone/unet.py:114). */

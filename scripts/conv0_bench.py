@@ -1,5 +1,5 @@
-"""conv0 + GroupNorm + GELU (split-plane output) at the bench geometry, the apply-pass variants (GPU box):
-hfa_conv0_tuning modes (conv.hip).
+"""conv0 + GroupNorm + GELU (split-plane output) at the bench geometry (GPU box): the shipped kernels (lag-product
+statistics + the packed f16-MFMA apply pass, conv.hip); the round-3 alternatives are in git history.
 python scripts/conv0_bench.py [--reps 20] [--B 32] [--seconds 10]"""
 import argparse
 import os
@@ -27,13 +27,7 @@ def main():
     out = torch.empty(2, args.B, T0, 512, dtype=torch.float16, device=d)
     ws = torch.empty(_lib.lib().hfa_conv0_workspace_bytes(args.B, N), dtype=torch.uint8, device=d)
     nbytes = args.B * (4.0 * N + 4.0 * 512 * T0)
-    names = {0: 'lag-product stats + packed f16-MFMA apply (per-wave LDS tile, non-temporal stores)',
-             1: 'round-1: VALU stats + VALU apply', 2: 'lag-product stats + f32-MFMA apply',
-             3: 'lag-product stats + VALU apply', 4: 'packed apply, stores from the MFMA layout',
-             7: 'packed apply, block-wide LDS stores', 8: 'mode 0 with plain (temporal) stores',
-             10: 'mode 0 at 2 workgroups per CU'}
-    for mode in (0, 8, 4, 3, 2, 0, 8, 4, 3, 2):
-        _lib.call("hfa_conv0_tuning", mode)
+    for rep in range(3):
         fn = lambda: ops.conv0(x, w0, gamma=gam, beta=bet, out=out, workspace=ws, out_split=True)  # noqa: E731
         for _ in range(3):
             fn()
@@ -45,9 +39,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.reps
-        print(f"mode {mode} ({names[mode]}): {ms:.3f} ms per batch (stats + reduce + apply), "
+        print(f"run {rep}: {ms:.3f} ms per batch (stats + apply), "
               f"{nbytes / ms / 1e6:.0f} GB/s of algorithmic bytes", flush=True)
-    _lib.call("hfa_conv0_tuning", 0)
 
 
 if __name__ == "__main__":

@@ -1,6 +1,6 @@
 """The pipelined config-2 step alone (task.submit + assemble, as bench.py's run()), for a rocprof kernel trace of
 the encoder stream beside the side stream: rocprofv3 --kernel-trace -d OUT -o run -- python3 scripts/pipe_trace.py
-[--steps 8].  HFA_UNET_FUSED etc. select the variant."""
+[--steps 8]."""
 import argparse
 import os
 import sys

@@ -87,7 +87,6 @@ int main() {
     CHECK(hfa_attention_split(1, 12, 10, 96, 0.125f, hp, 0, 0, 64, hp, 0, 0, 64, hp, 0, 0, 64, hp, 0, 0, 64,
                                    nullptr, st), "attention_split head_dim");
     CHECK(hfa_attention_split_tuning(3), "attention tuning waves=3");
-    CHECK(hfa_conv0_tuning(11), "conv0 tuning mode=11");
     // norms
     CHECK(hfa_layernorm_f32(10, 6, fp, 8, nullptr, 0, fp, fp, 1e-5f, 0, fp, 8, 0, nullptr, st), "LN C%4");
     CHECK(hfa_layernorm_f32(10, 8, fmis, 8, nullptr, 0, fp, fp, 1e-5f, 0, fp, 8, 0, nullptr, st),
@@ -155,33 +154,6 @@ int main() {
             }
             std::remove(tmp);
         }
-    }
-    // fused UNet + head: launch arguments, and the host check of an op table (a conv1 whose taps are 2)
-    {
-        const hfa_unet_op* dops = reinterpret_cast<const hfa_unet_op*>(0x100000);
-        int* flag = reinterpret_cast<int*>(0x100000);
-        CHECK(hfa_unet_head(1, 64, nullptr, 3, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, flag, st), "unet null ops");
-        CHECK(hfa_unet_head(1, 64, dops, 0, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, flag, st), "unet nops 0");
-        CHECK(hfa_unet_head(1, 64, dops, 3, fp, 64 * 768, 768, fp, 64 * 66, 66, ip, fp, 4096, flag, st), "unet l_ld 66");
-        CHECK(hfa_unet_head(1, 64, dops, 3, fp, 64 * 768, 768, fmis, 64 * 68, 68, ip, fp, 4096, flag, st), "unet logits misaligned");
-        CHECK(hfa_unet_head(-1, 64, dops, 3, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, flag, st), "unet B<0");
-        CHECK(hfa_unet_validate(nullptr, 3, 128, 68), "unet_validate null");
-        double* gw = reinterpret_cast<double*>(0x100000);
-        const long long gb = hfa_unet_gn_doubles(64);
-        CHECK(hfa_unet_head_tiled(1, 64, nullptr, dops, 3, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, gw, gb,
-                                  flag, st), "unet_tiled null host table");
-        CHECK(hfa_unet_head_tiled(1, 64, dops, dops, 3, fp, 64 * 768, 768, fp, 64 * 68, 68, ip, fp, 4096, gw, gb - 1,
-                                  flag, st), "unet_tiled short GroupNorm workspace");
-        CHECK(hfa_unet_head_tiled(1, 64, dops, dops, 3, fp, 64 * 768, 768, fmis, 64 * 68, 68, ip, fp, 4096, gw, gb,
-                                  flag, st), "unet_tiled logits misaligned");
-        hfa_unet_op op;
-        std::memset(&op, 0, sizeof(op));
-        op.kind = 0; op.n = 64; op.groups = 16; op.nseg = 1; op.res = HFA_UNET_NONE; op.dst = 0;
-        op.src[0] = HFA_UNET_INPUT; op.src_ld[0] = 64; op.cin[0] = 64; op.taps[0] = 2; op.ldw[0] = 128;
-        op.w[0] = hp; op.wp[0] = 1 << 20;
-        CHECK(hfa_unet_validate(&op, 1, 128, 68), "unet_validate taps 2");
-        op.taps[0] = 3; op.ldw[0] = 192;
-        if (hfa_unet_validate(&op, 1, 128, 68) != 0) { std::printf("FAIL unet_validate on a valid op\n"); ++g_fail; }
     }
     // host queries and tuning hooks (thread-local state; name strings stay valid, bounded)
     for (int cfg = 0; cfg < 25; ++cfg) {

@@ -74,59 +74,6 @@ def test_no_packed_f32_in_device_code():
         assert n_mfma > 0, "disassembly found no MFMA: extraction failed"
 
 
-def _unet_table(ops):
-    """A three-op fused-UNet table (conv1 INPUT -> H, conv2 H -> Y with the input as residual, head Y -> logits) at
-    level 0 with fake, aligned device pointers (hfa_unet_validate never dereferences them)."""
-    import ctypes
-    t = (ops.UnetOp * 3)()
-    fake = 0x10000
-
-    def seg(r, s, src, off, ld, cin, taps, gn=0):
-        r.src[s], r.src_off[s], r.src_ld[s], r.cin[s], r.taps[s], r.gn[s] = src, off, ld, cin, taps, gn
-        r.ldw[s] = taps * cin
-        r.w[s] = fake
-        r.wp[s] = taps * cin // 32 * ((r.n + 15) // 16) * 512
-    c1, c2, hd = t
-    c1.kind, c1.level, c1.n, c1.groups, c1.nseg, c1.res, c1.dst, c1.dst_off = 0, 0, 64, 16, 1, -1, 0, 0
-    seg(c1, 0, ops.UNET_INPUT, 0, 64, 64, 3)
-    c2.kind, c2.level, c2.n, c2.groups, c2.nseg, c2.res, c2.dst, c2.dst_off = 1, 0, 64, 16, 1, ops.UNET_INPUT, 0, 64
-    seg(c2, 0, 0, 0, 64, 64, 3, gn=1)
-    c2.gn_gamma = c2.gn_beta = c2.ln_gamma = c2.ln_beta = fake
-    hd.kind, hd.level, hd.n, hd.groups, hd.nseg, hd.res, hd.dst = 4, 0, 68, 16, 1, -1, ops.UNET_OUTPUT
-    seg(hd, 0, 0, 64, 64, 64, 1)
-    hd.bias = fake
-    assert ctypes.sizeof(t) == 3 * ctypes.sizeof(ops.UnetOp)
-    return t
-
-
-def test_unet_validate_rejects_bad_tables():
-    """hfa_unet_validate (the host check of a fused-UNet op table): a well-formed table passes; each corruption the
-    kernel could not survive (slot past the workspace, misaligned weights, bad taps / channels, the head's output
-    wider than the logits rows, a conv2 without its conv1) is refused with a message naming the op."""
-    torch = pytest.importorskip("torch")  # noqa: F841
-    from hubertfa_amd import ops
-    from hubertfa_amd._lib import HFAArgumentError
-    ops.unet_validate(_unet_table(ops), 128, 68)
-    cases = [
-        (lambda t: setattr(t[1], "dst_off", 100), 128, 68, "op 1"),          # Y past 128 floats per row
-        (lambda t: None, 127, 68, "op 1"),                                     # workspace one float short
-        (lambda t: setattr(t[2], "n", 72), 128, 68, "op 2: head n"),           # head wider than the logits rows
-        (lambda t: t[0].taps.__setitem__(0, 2), 128, 68, "op 0: taps"),
-        (lambda t: t[0].cin.__setitem__(0, 48), 128, 68, "op 0"),              # cin % 32
-        (lambda t: t[1].w.__setitem__(0, 0x10008), 128, 68, "op 1: weight"),  # 8-B aligned weight planes
-        (lambda t: t[1].wp.__setitem__(0, 512), 128, 68, "op 1: weight"),      # plane stride too short
-        (lambda t: setattr(t[0], "kind", 2), 128, 68, "op 1: conv2 without"),  # conv2 not after its conv1
-        (lambda t: setattr(t[1], "ln_gamma", None), 128, 68, "op 1: norm"),
-        (lambda t: setattr(t[0], "dst", ops.UNET_OUTPUT), 128, 68, "op 0: dst"),
-        (lambda t: setattr(t[0], "n", 66), 128, 68, "op 0: n"),
-    ]
-    for mutate, wpr, l_ld, msg in cases:
-        t = _unet_table(ops)
-        mutate(t)
-        with pytest.raises(HFAArgumentError, match=msg):
-            ops.unet_validate(t, wpr, l_ld)
-
-
 def test_split_gemm_tile_choice():
     """The split GEMM's automatic tile for the workload's large grids (host query, no GPU): 256 x 256 unless a
     192-wide tile fills the last round of CUs much better (profiles/r03/split_tiles_c5.txt)."""
