@@ -217,6 +217,38 @@ def step_breakdown(task, wav, ph_seqs, word_seqs, p2ws, k, step_s):
                     "beside it"}
 
 
+def chunk_agreement(task, wav, ph_seqs, word_seqs, p2ws, chunk_seconds):
+    """Chunked long-form against its anchor, the unchunked run of the same utterances (the
+    reference encodes each wave whole, tools/encoder.py:36-60): per utterance, the share of phone boundaries whose
+    frame is within 0 / 2 / 5 DP frames of the unchunked run's, and the largest per-frame log-prob difference on
+    the [T, S] lattice (and its mean).  Outside the timed region."""
+    import numpy as np
+    import torch
+    full = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False)
+    chnk = task.align_batch(wav, ph_seqs, word_seqs, p2ws, wav_sr=16000, host=False, chunk_seconds=chunk_seconds)
+    torch.cuda.synchronize()
+    out = []
+    for b in range(len(ph_seqs)):
+        T, S = full["T"][b], len(ph_seqs[b])
+        dl = (full["lattice"]["prob_log"][b, :T, :S] - chnk["lattice"]["prob_log"][b, :T, :S]).abs()
+        n_a, n_b = int(full["n"][b]), int(chnk["n"][b])
+        ia, ta = full["ph_idx_seq"][b, :n_a].cpu().numpy(), full["ph_time_int"][b, :n_a].cpu().numpy()
+        ib, tb = chnk["ph_idx_seq"][b, :n_b].cpu().numpy(), chnk["ph_time_int"][b, :n_b].cpu().numpy()
+        common, xa, xb = np.intersect1d(ia, ib, return_indices=True)
+        d = np.abs(ta[xa].astype(np.int64) - tb[xb].astype(np.int64))
+        out.append({"T": int(T), "states": S, "boundaries": int(n_a), "boundaries_chunked": int(n_b),
+                    "phones_in_both": int(len(common)),
+                    "within_0": float(np.mean(d == 0)) if len(d) else None,
+                    "within_2": float(np.mean(d <= 2)) if len(d) else None,
+                    "within_5": float(np.mean(d <= 5)) if len(d) else None,
+                    "max_frame_shift": int(d.max()) if len(d) else None,
+                    "max_logprob_diff": float(dl.max()), "mean_logprob_diff": float(dl.mean())})
+    return {"chunk_seconds": chunk_seconds, "anchor": "the unchunked run of the same utterance (the reference "
+            "encodes each wave whole, tools/encoder.py:36-60)", "utterances": out,
+            "note": "random-init weights: the agreement says little about a trained model's; it measures what the "
+                    "windows' lost attention context changes on this workload"}
+
+
 def config3_batch(args, world: int) -> int:
     """Per-GPU batch of BASELINE config 3 (512 x 10 s over the node) when this multi-GPU run's own global batch is
     not already 512; 0 when there is nothing extra to measure."""
@@ -465,6 +497,8 @@ def main():
                           "global_batch": world * c3, "steps": args.steps, "ms_per_step": el3 / args.steps * 1e3,
                           "value": world * c3 * args.seconds * args.steps / el3, "unit": "audio_s/s",
                           "frames_per_s": world * c3 * n_frames * args.steps / el3}
+    if args.chunk_seconds is not None:
+        out["chunk_agreement"] = chunk_agreement(task, wav_dev, ph_seqs, word_seqs, p2ws, args.chunk_seconds)
     if world == 1 and args.chunk_seconds is None and not args.serial:
         out["step_breakdown"] = step_breakdown(task, wav_dev, ph_seqs, word_seqs, p2ws, args.steps, el / args.steps)
     iso = ops.KernelProbe("-", extra=SECONDARY)       # isolated serial steps for the secondary rooflines

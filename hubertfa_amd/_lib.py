@@ -25,7 +25,8 @@ _SIGS = {
     # alignment decoder (viterbi.hip)
     "hfa_viterbi_forward": [I, I, I, P, P, P, P, P, P, P, P, P, P, P],
     "hfa_viterbi_backtrack": [I, I, I, P, P, P, P, P, P, P, P, P, P],
-    "hfa_lattice_prologue": [I, I, I, I, P, P, P, LL, LL, P, LL, LL, P, P, P, P, P, P, P, P, P],
+    "hfa_lattice_prologue": [I, I, I, I, P, P, P, LL, LL, P, LL, LL, P, P, P, P, P, P, P, P, P, P, P],
+    "hfa_viterbi_init": [I, I, I, P, P, P, P, P, P, P],
     "hfa_viterbi_tuning": [I],
     # WAV front end (wav.cpp, host memory)
     "hfa_wav_info": [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32),

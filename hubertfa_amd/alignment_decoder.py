@@ -91,17 +91,15 @@ class AlignmentDecoder:
         ids_pad = np.zeros((B, Smax), np.int32)
         for b, i in enumerate(ids):
             ids_pad[b, :len(i)] = i
-        # one pinned staging buffer -> one async H2D copy (keeps the stream free-running)
-        meta = np.zeros((B, Smax + 2), np.int32)
-        meta[:, 0] = Ts
-        meta[:, 1] = [len(i) for i in ids]
-        meta[:, 2:] = ids_pad
+        # one pinned staging buffer -> one async H2D copy (keeps the stream free-running); T, S and the ids are
+        # contiguous slices of it (no copy kernels)
+        meta = np.concatenate([np.asarray(Ts, np.int32), np.array([len(i) for i in ids], np.int32), ids_pad.ravel()])
         meta_t = torch.from_numpy(meta).pin_memory().to(dev, non_blocking=True)
-        T_t = meta_t[:, 0].contiguous()
-        S_t = meta_t[:, 1].contiguous()
-        ids_t = meta_t[:, 2:].contiguous()
-        lat = ops.lattice_prologue(frame_logits, edge_logits, ids_t, T_t, S_t, want_frame_probs=keep_frame_probs)
-        dp, bt, curr = self.init_dp(lat["prob_log"], ids_t, S_t)
+        T_t, S_t, ids_t = meta_t[:B], meta_t[B:2 * B], meta_t[2 * B:].view(B, Smax)
+        # the lattice prologue also writes _decode's dp / curr initialisation (one launch, no ATen glue)
+        lat = ops.lattice_prologue(frame_logits, edge_logits, ids_t, T_t, S_t, want_frame_probs=keep_frame_probs,
+                                   init_dp=True)
+        dp, bt, curr = lat.pop("dp"), lat.pop("bt"), lat.pop("curr")
         ops.viterbi_forward(lat["prob_log"], lat["not_edge_log"], lat["edge_log"], curr, dp, bt, ids_t, T_t, S_t)
         idx, tint, n, fc = ops.viterbi_backtrack(dp, bt, ids_t, T_t, S_t)
         dev_out = dict(ph_idx_seq=idx, ph_time_int=tint, n=n, frame_confidence=fc, edge_diff=lat["edge_diff"],
@@ -168,29 +166,6 @@ class AlignmentDecoder:
             out.append(r)
         return out
 
-    @staticmethod
-    def init_dp(prob_log: torch.Tensor, ids_t: torch.Tensor, S_t: torch.Tensor):
-        """dp/bt/curr initialisation of _decode (alignment_decoder.py:244-254), on device."""
-        B, Tmax, Smax = prob_log.shape
-        dev = prob_log.device
-        # rows 1.. of dp/bt are fully written by the forward kernel for every valid (t, s); row 0 of bt is
-        # never read (the backtrack always emits at t == 0), so only dp row 0 and curr need initialising.
-        dp = torch.empty((B, Tmax, Smax), dtype=torch.float32, device=dev)
-        bt = torch.empty((B, Tmax, Smax), dtype=torch.int8, device=dev)
-        curr = torch.full((B, Smax), float("-inf"), dtype=torch.float64, device=dev)
-        if Tmax == 0 or Smax == 0:
-            return dp, bt, curr
-        dp[:, 0, :] = float("-inf")
-        if Tmax == 0 or Smax == 0:
-            return dp, bt, curr
-        dp[:, 0, 0] = prob_log[:, 0, 0]
-        curr[:, 0] = prob_log[:, 0, 0].double()
-        if Smax > 1:
-            two = (ids_t[:, 0] == 0) & (S_t > 1)
-            dp[:, 0, 1] = torch.where(two, prob_log[:, 0, 1], dp[:, 0, 1])
-            curr[:, 1] = torch.where(two, prob_log[:, 0, 1].double(), curr[:, 1])
-        return dp, bt, curr
-
     # -- reference static/numpy API on the GPU --------------------------------------------------------------
     @staticmethod
     def forward_pass(T, S, prob_log, not_edge_prob_log, edge_prob_log, curr_ph_max_prob_log, dp, backtrack_s,
@@ -230,7 +205,7 @@ class AlignmentDecoder:
         ids = torch.from_numpy(ph_seq_id.astype(np.int32))[None].to(dev)
         T_t = torch.tensor([T], dtype=torch.int32, device=dev)
         S_t = torch.tensor([S], dtype=torch.int32, device=dev)
-        dp, bt, curr = self.init_dp(pl, ids, S_t)
+        dp, bt, curr = ops.viterbi_init(pl, ids, T_t, S_t)
         ops.viterbi_forward(pl, torch.from_numpy(nE)[None].to(dev), torch.from_numpy(E)[None].to(dev), curr, dp,
                             bt, ids, T_t, S_t)
         idx, tint, n, fc = ops.viterbi_backtrack(dp, bt, ids, T_t, S_t)

@@ -2006,8 +2006,8 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
                                 : launch_split<EPI_NONE, false>(p, Z, cfg, stream, f16);
 }
 
-const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue, int Cg) {
-    GemmP p = make_params(M, N, 32, 1, nullptr, 0, 0, 0, 1, 0, Cg, 1, nullptr, 0, 0);
+const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split, int epilogue, int Cg) {
+    GemmP p = make_params(M, N, K, 1, nullptr, 0, 0, 0, 1, 0, Cg, 1, nullptr, 0, 0);
     p.Ch = out_split ? reinterpret_cast<_Float16*>(g_name) : nullptr;    // only its null-ness is read
     g_win_nb = N / 16;
     const bool f16 = (epilogue & HFA_GEMM_F16) != 0 && Cg % 32 == 0;

@@ -17,6 +17,14 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 //   index[k] = clamp(round(f32(ratio) * f32(k)), max=U-1) (torch f32 promotion, round half to even);
 //   out[b, k, :] = units[b, index[k], :] for k < n_frames; rows n_frames..T_pad-1 are zero (UNet pad,
 //   networks/layer/backbone/unet.py:103-106).  One wavefront per output row, float4 copies.
+// Snapshot-and-clear of device flags (the split range guard's per-batch flags): snap[i] = flags[i], flags[i] = 0.
+__global__ __launch_bounds__(64) void flag_take_kernel(int n, int* __restrict__ flags, int* __restrict__ snap) {
+    for (int i = threadIdx.x; i < n; i += 64) {
+        snap[i] = flags[i];
+        flags[i] = 0;
+    }
+}
+
 __global__ __launch_bounds__(256) void units_gather_kernel(int U, int C, const float* __restrict__ units,
                                                            long long u_bs, int u_ld, int n_frames, int T_pad,
                                                            float ratio, float* __restrict__ out, long long o_bs,
@@ -261,6 +269,16 @@ int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream)
     if (n == 0) return HFA_OK;
     hipLaunchKernelGGL(gelu_check_kernel, dim3(grid1d(n)), dim3(256), 0, stream, n, x, y);
     return hfa::check_launch("hfa_selftest_gelu");
+}
+
+int hfa_flag_take(int n, int* flags, int* snap, hipStream_t stream) {
+    if (n < 0 || (n > 0 && (!flags || !snap))) {
+        hfa::set_error("hfa_flag_take: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (n == 0) return HFA_OK;
+    hipLaunchKernelGGL(flag_take_kernel, dim3(1), dim3(64), 0, stream, n, flags, snap);
+    return hfa::check_launch("hfa_flag_take");
 }
 
 int hfa_add_f32(long long n, const float* a, const float* b, float* out, hipStream_t stream) {

@@ -499,12 +499,41 @@ __global__ __launch_bounds__(kBtThreads) void viterbi_backtrack_kernel(
 constexpr int kProThreads = 256;
 constexpr int kMaxV = 1024;
 
+// _decode's initialisation (tools/alignment_decoder.py:244-254): dp[0, 0] = L[0, 0] and curr[0] = L[0, 0]; if
+// ph_seq_id[0] == 0 (and S > 1) also dp[0, 1] = curr[1] = L[0, 1]; every other dp[0, s] and curr[s] = -inf (curr in
+// f64, as the reference's np.full).  row0 = {L[0, 0], L[0, 1]}, or null for an all -inf row (T = 0).  Threads
+// i0, i0 + step, ... of the caller cover s < Smax (rows 1.. of dp and bt are written by the forward kernel).
+__device__ __forceinline__ void dp_row0(int b, int Tmax, int Smax, int S, const int32_t* ids, const float* row0,
+                                        int i0, int step, float* dp, double* curr) {
+    const bool two = row0 && S > 1 && ids[0] == 0;
+    for (int s = i0; s < Smax; s += step) {
+        float v = neg_inf();
+        if (row0 && s == 0) v = row0[0];
+        else if (two && s == 1) v = row0[1];
+        dp[(size_t)b * Tmax * Smax + s] = v;
+        curr[(size_t)b * Smax + s] = (double)v;
+    }
+}
+
+__global__ __launch_bounds__(256) void viterbi_init_kernel(int Tmax, int Smax, const int32_t* __restrict__ Tv,
+                                                           const int32_t* __restrict__ Sv,
+                                                           const float* __restrict__ prob_log,
+                                                           const int32_t* __restrict__ ph_seq_id,
+                                                           float* __restrict__ dp, double* __restrict__ curr) {
+    const int b = blockIdx.x;
+    const float* L0 = prob_log + (size_t)b * Tmax * Smax;
+    const int S = Sv[b];
+    const float row0[2] = {L0[0], Smax > 1 ? L0[1] : 0.0f};
+    dp_row0(b, Tmax, Smax, S, ph_seq_id + (size_t)b * Smax, Tv[b] > 0 ? row0 : nullptr, threadIdx.x, 256, dp, curr);
+}
+
 __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
     int Tmax, int V, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
     const float* __restrict__ frame_logits, long long f_ld, long long f_bs, const float* __restrict__ edge_logits,
     long long e_ld, long long e_bs, const int32_t* __restrict__ ph_seq_id, float* __restrict__ ph_prob_log,
     float* __restrict__ ph_frame_pred, float* __restrict__ prob_log, float* __restrict__ edge_log,
-    float* __restrict__ not_edge_log, float* __restrict__ edge_diff, double* __restrict__ edge_prob_out) {
+    float* __restrict__ not_edge_log, float* __restrict__ edge_diff, double* __restrict__ edge_prob_out,
+    float* __restrict__ dp, double* __restrict__ curr) {
     __shared__ unsigned char allowed[kMaxV];
     __shared__ float lsm[kProThreads / 64][kMaxV];
     const int b = blockIdx.y;
@@ -520,7 +549,10 @@ __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
     __syncthreads();
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int t = blockIdx.x * (kProThreads / 64) + w;
-    if (t >= T) return;
+    if (t >= T) {
+        if (t == 0 && dp) dp_row0(b, Tmax, Smax, 0, ids, nullptr, lane, 64, dp, curr);   // T = 0: an all -inf row
+        return;
+    }
     const float* xr = frame_logits + b * f_bs + t * f_ld;
     float m = neg_inf();
     for (int v = lane; v < V; v += 64) {
@@ -545,6 +577,11 @@ __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
     for (int s = lane; s < S; s += 64) {
         const int v = ids[s];
         prob_log[((size_t)b * Tmax + t) * Smax + s] = lsm[w][v];
+    }
+    if (t == 0 && dp) {          // _decode's dp / curr initialisation from this frame's lattice row (no extra launch)
+        const float l0 = lsm[w][ids[0]], l1 = S > 1 ? lsm[w][ids[1]] : 0.0f;
+        const float row0[2] = {l0, l1};
+        dp_row0(b, Tmax, Smax, S, ids, row0, lane, 64, dp, curr);
     }
     if (lane == 0) {
         const float* er = edge_logits + b * e_bs;
@@ -685,22 +722,36 @@ int hfa_lattice_prologue(int B, int Tmax, int V, int Smax, const int32_t* T, con
                          const float* frame_logits, long long frame_ld, long long frame_bs,
                          const float* edge_logits, long long edge_ld, long long edge_bs, const int32_t* ph_seq_id,
                          float* ph_prob_log, float* ph_frame_pred, float* prob_log, float* edge_log,
-                         float* not_edge_log, float* edge_diff, double* edge_prob, hipStream_t stream) {
+                         float* not_edge_log, float* edge_diff, double* edge_prob, float* dp, double* curr,
+                         hipStream_t stream) {
     if (B < 0 || Tmax < 0 || V <= 0 || V > kMaxV || Smax < 0) {
         hfa::set_error("hfa_lattice_prologue: bad sizes (0 < V <= %d)", kMaxV);
         return HFA_EINVAL;
     }
     if (B == 0 || Tmax == 0) return HFA_OK;
     if (!T || !S || !frame_logits || !edge_logits || !ph_seq_id || !prob_log || !edge_log || !not_edge_log ||
-        !edge_diff) {
-        hfa::set_error("hfa_lattice_prologue: null pointer");
+        !edge_diff || (!dp != !curr)) {
+        hfa::set_error("hfa_lattice_prologue: null pointer (dp and curr go together)");
         return HFA_EINVAL;
     }
     dim3 grid((Tmax + kProThreads / 64 - 1) / (kProThreads / 64), B);
     hipLaunchKernelGGL(lattice_prologue_kernel, grid, dim3(kProThreads), 0, stream, Tmax, V, Smax, T, S,
                        frame_logits, frame_ld, frame_bs, edge_logits, edge_ld, edge_bs, ph_seq_id, ph_prob_log,
-                       ph_frame_pred, prob_log, edge_log, not_edge_log, edge_diff, edge_prob);
+                       ph_frame_pred, prob_log, edge_log, not_edge_log, edge_diff, edge_prob, dp, curr);
     return hfa::check_launch("hfa_lattice_prologue");
+}
+
+int hfa_viterbi_init(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const float* prob_log,
+                     const int32_t* ph_seq_id, float* dp, double* curr, hipStream_t stream) {
+    if (B < 0 || Tmax < 0 || Smax < 0 || (B > 0 && Tmax > 0 && Smax > 0 &&
+                                          (!T || !S || !prob_log || !ph_seq_id || !dp || !curr))) {
+        hfa::set_error("hfa_viterbi_init: bad arguments");
+        return HFA_EINVAL;
+    }
+    if (B == 0 || Tmax == 0 || Smax == 0) return HFA_OK;
+    hipLaunchKernelGGL(viterbi_init_kernel, dim3(B), dim3(256), 0, stream, Tmax, Smax, T, S, prob_log, ph_seq_id, dp,
+                       curr);
+    return hfa::check_launch("hfa_viterbi_init");
 }
 
 }  // extern "C"

@@ -88,10 +88,12 @@ def viterbi_backtrack(dp, bt, ph_seq_id, T, S):
     return idx, tint, n, fc
 
 
-def lattice_prologue(frame_logits, edge_logits, ph_seq_id, T, S, want_frame_probs: bool = False):
+def lattice_prologue(frame_logits, edge_logits, ph_seq_id, T, S, want_frame_probs: bool = False,
+                     init_dp: bool = False):
     """Mask + log_softmax/softmax + edge sigmoid/diff/prob + gather to the [T,S] lattice (alignment_decoder.py
     :35-84, 239-242).  frame_logits [B,Tl,V] and edge_logits [B,Tl] may be strided views (last dim unit stride).
-    """
+    ``init_dp``: also allocate the DP's dp / bt / curr and write _decode's initialisation (:244-254) in the same
+    launch (out["dp"], out["bt"], out["curr"], ready for viterbi_forward)."""
     B, Tl, V = frame_logits.shape
     Smax = ph_seq_id.shape[1]
     _need(frame_logits, torch.float32, "frame_logits", contiguous=False)
@@ -111,13 +113,33 @@ def lattice_prologue(frame_logits, edge_logits, ph_seq_id, T, S, want_frame_prob
         "edge_prob": torch.empty((B, Tmax), dtype=torch.float64, device=dev),
         "ph_prob_log": torch.empty((B, Tmax, V), dtype=torch.float32, device=dev) if want_frame_probs else None,
         "ph_frame_pred": torch.empty((B, Tmax, V), dtype=torch.float32, device=dev) if want_frame_probs else None,
+        "dp": torch.empty((B, Tmax, Smax), dtype=torch.float32, device=dev) if init_dp else None,
+        "bt": torch.empty((B, Tmax, Smax), dtype=torch.int8, device=dev) if init_dp else None,
+        "curr": torch.empty((B, Smax), dtype=torch.float64, device=dev) if init_dp else None,
     }
     _lib.call("hfa_lattice_prologue", B, Tmax, V, Smax, _ptr(T), _ptr(S), _ptr(frame_logits),
               frame_logits.stride(1), frame_logits.stride(0), _ptr(edge_logits), edge_logits.stride(1),
               edge_logits.stride(0), _ptr(ph_seq_id), _ptr(out["ph_prob_log"]), _ptr(out["ph_frame_pred"]),
               _ptr(out["prob_log"]), _ptr(out["edge_log"]), _ptr(out["not_edge_log"]), _ptr(out["edge_diff"]),
-              _ptr(out["edge_prob"]), _stream(dev))
+              _ptr(out["edge_prob"]), _ptr(out["dp"]), _ptr(out["curr"]), _stream(dev))
     return out
+
+
+def viterbi_init(prob_log, ph_seq_id, T, S):
+    """_decode's dp / bt / curr initialisation (alignment_decoder.py:244-254) for a lattice that did not come
+    through lattice_prologue: returns (dp, bt, curr) ready for viterbi_forward."""
+    B, Tmax, Smax = prob_log.shape
+    _need(prob_log, torch.float32, "prob_log")
+    _need(ph_seq_id, torch.int32, "ph_seq_id")
+    _need(T, torch.int32, "T")
+    _need(S, torch.int32, "S")
+    dev = prob_log.device
+    dp = torch.empty((B, Tmax, Smax), dtype=torch.float32, device=dev)
+    bt = torch.empty((B, Tmax, Smax), dtype=torch.int8, device=dev)
+    curr = torch.empty((B, Smax), dtype=torch.float64, device=dev)
+    _lib.call("hfa_viterbi_init", B, Tmax, Smax, _ptr(T), _ptr(S), _ptr(prob_log), _ptr(ph_seq_id), _ptr(dp),
+              _ptr(curr), _stream(dev))
+    return dp, bt, curr
 
 
 # ------------------------------------------------------------------------------------------------------------
@@ -136,7 +158,7 @@ _lib.register("hfa_gemm_kernel_name", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_,
 _lib.register("hfa_conv_gemm_split", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, _LL_, _I_, _I_, _I_, _I_, _I_, _P_,
                                        _LL_, _LL_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _P_, _P_, _LL_,
                                        _LL_, _LL_, _I_, _I_, _P_, _P_])
-_lib.register("hfa_gemm_split_kernel_name", [_I_, _I_, _I_, _I_, _I_, _I_], ctypes.c_char_p)
+_lib.register("hfa_gemm_split_kernel_name", [_I_, _I_, _I_, _I_, _I_, _I_, _I_], ctypes.c_char_p)
 _lib.register("hfa_gemm_split_tuning", [_I_])
 _lib.register("hfa_split_f16", [_I_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _P_, _P_])
 _lib.register("hfa_gemm_f32", [_I_, _I_, _I_, _P_, _I_, _P_, _I_, _P_, _P_, _I_, _P_, _I_, _I_, _P_])
@@ -295,8 +317,8 @@ def split(x, out=None, flag=None):
     return out
 
 
-def _split_name(M, N, Z, out_split, epilogue, Cg) -> str:
-    return _lib.lib().hfa_gemm_split_kernel_name(M, N, Z, int(out_split), epilogue, Cg).decode()
+def _split_name(M, N, K, Z, out_split, epilogue, Cg) -> str:
+    return _lib.lib().hfa_gemm_split_kernel_name(M, N, K, Z, int(out_split), epilogue, Cg).decode()
 
 
 def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0, ldx, stride=1, pad=0, Cg=None,
@@ -326,7 +348,7 @@ def conv_gemm_split(As, Ws, C=None, Cs=None, *, M, N, K, Zb=1, G=1, sAb=0, sAg=0
         _lib.call("hfa_conv_gemm_split", *args, _stream(dev))
     if PROBE is None:
         return launch()
-    PROBE(_split_name(M, N, Zb * G, Cs is not None and C is None, epilogue, Cg or K), 2.0 * M * N * K * Zb * G, launch,
+    PROBE(_split_name(M, N, K, Zb * G, Cs is not None and C is None, epilogue, Cg or K), 2.0 * M * N * K * Zb * G, launch,
           shape=(M, N, K, Zb * G))
 
 
@@ -540,6 +562,17 @@ def pad_rows(x, left, n_out, out=None):
     _lib.call("hfa_pad_rows_f32", B, N, _ptr(x), x.stride(0), left, n_out, _ptr(out), out.stride(0),
               _stream(x.device))
     return out
+
+
+_lib.register("hfa_flag_take", [_I_, _P_, _P_, _P_])
+
+
+def flag_take(flag: torch.Tensor) -> torch.Tensor:
+    """Snapshot of a device int32 flag tensor, which is cleared (stream-ordered, one launch)."""
+    _need(flag, torch.int32, "flag")
+    snap = torch.empty_like(flag)
+    _lib.call("hfa_flag_take", flag.numel(), _ptr(flag), _ptr(snap), _stream(flag.device))
+    return snap
 
 
 def add(a, b, out=None):

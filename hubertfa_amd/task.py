@@ -160,8 +160,7 @@ class ForcedAlignmentTask:
             logits = self.head.logits(feats)[:, :n_frames]
         flag = None
         if self.head.precision == "split":      # the head's own range flag, snapshot on the stream that ran it
-            flag = self.head.flag.clone()
-            self.head.flag.zero_()
+            flag = ops.flag_take(self.head.flag)
         return logits, flag
 
     def lattice_dp(self, logits, flag, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
@@ -186,9 +185,7 @@ class ForcedAlignmentTask:
         if not enc_split and self.head.precision != "split":
             return dev_out
         if enc_split:
-            flag = ops.split_flag(self.device)
-            dev_out["split_oflow"] = flag.clone()
-            flag.zero_()
+            dev_out["split_oflow"] = ops.flag_take(ops.split_flag(self.device))
         dev_out["redo"] = lambda: self._align_f32(*redo_args)
         return dev_out
 

@@ -78,12 +78,21 @@ int hfa_viterbi_backtrack(int B, int Tmax, int Smax, const int32_t* T, const int
  * (V contiguous floats); edge logit at edge_logits + b*edge_bs + t*edge_ld.
  * Outputs: prob_log [B,Tmax,Smax] (= ph_prob_log[:, ph_seq_id]), edge_log/not_edge_log [B,Tmax] f32,
  * edge_diff [B,Tmax] f32, edge_prob [B,Tmax] f64 (may be NULL), ph_prob_log/ph_frame_pred [B,Tmax,V] (may be
- * NULL).  V <= 1024. */
+ * NULL).  V <= 1024.  dp [B,Tmax,Smax] f32 / curr [B,Smax] f64 (both or neither): also _decode's DP
+ * initialisation, tools/alignment_decoder.py:244-254 (dp row 0 and curr, as hfa_viterbi_init), from frame 0's
+ * lattice row, so hfa_viterbi_forward can follow directly. */
 int hfa_lattice_prologue(int B, int Tmax, int V, int Smax, const int32_t* T, const int32_t* S,
                          const float* frame_logits, long long frame_ld, long long frame_bs,
                          const float* edge_logits, long long edge_ld, long long edge_bs, const int32_t* ph_seq_id,
                          float* ph_prob_log, float* ph_frame_pred, float* prob_log, float* edge_log,
-                         float* not_edge_log, float* edge_diff, double* edge_prob, hipStream_t stream);
+                         float* not_edge_log, float* edge_diff, double* edge_prob, float* dp, double* curr,
+                         hipStream_t stream);
+/* hfa_viterbi_init replaces _decode's initialisation, tools/alignment_decoder.py:244-254, for a lattice that did not
+ * come through hfa_lattice_prologue: dp[b,0,0] = curr[b,0] = prob_log[b,0,0]; if ph_seq_id[b,0] == 0 and S[b] > 1
+ * also dp[b,0,1] = curr[b,1] = prob_log[b,0,1]; every other dp[b,0,s] and curr[b,s] (s < Smax) = -inf; T[b] = 0:
+ * the whole row -inf. */
+int hfa_viterbi_init(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const float* prob_log,
+                     const int32_t* ph_seq_id, float* dp, double* curr, hipStream_t stream);
 
 /* ---- dense contractions (hubertfa_amd/csrc/gemm.hip): f32 MFMA implicit GEMM ---------------------------------
  * C[z](m,n) = epi(sum_k A[z](m,k) W[z](n,k) + bias[zg*sBg + n]) + R[z](m,n),  z = zb*G + zg,
@@ -133,8 +142,9 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
                         long long sRb, long long sRg, int ldr, const uint16_t* Rs, long long sRp, float* C,
                         uint16_t* Cs, long long sCp, long long sCb, long long sCg, int ldc, int epilogue, int* oflow,
                         hipStream_t stream);
-/* rocprof symbol stem of the split instantiation for an M x N output over Z = Zb*G (out_split: planes out). */
-const char* hfa_gemm_split_kernel_name(int M, int N, int Z, int out_split, int epilogue, int Cg);
+/* rocprof symbol stem of the split instantiation for an M x N x K contraction over Z = Zb*G (out_split: planes out;
+ * stride 1 assumed, as the grouped positional conv's window kernel needs). */
+const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split, int epilogue, int Cg);
 /* Tile override for the split GEMM: 0 auto, 1 128x128, 2 128x64, 3 256x128 (8 waves), 4/5 128x128 with 3/4
  * stages (one workgroup per CU), 6 256x128 with 3 stages, 7 256x256 single accumulator (8 waves of 128x64),
  * 8 256x128 single accumulator (4 waves), 9 128x128 single accumulator, 10 128x64 single accumulator, 11/12
@@ -240,6 +250,9 @@ int hfa_pad_rows_f32(int B, int N, const float* x, long long x_bs, int left, int
 int hfa_selftest_erf(long long n, const float* x, float* y_nb, float* y_ref, hipStream_t stream);
 /* Self-test: y = the GELU applied by every fused epilogue (GEMM, LayerNorm/GroupNorm act, conv0). */
 int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream);
+/* Range-guard bookkeeping (no reference counterpart: the split-f16 arithmetic's per-batch overflow flags): snap[i] =
+ * flags[i], then flags[i] = 0, for i < n, stream-ordered (the batch's snapshot travels with its outputs). */
+int hfa_flag_take(int n, int* flags, int* snap, hipStream_t stream);
 /* out = a + b (UNet skip connection, networks/layer/backbone/unet.py:114). */
 int hfa_add_f32(long long n, const float* a, const float* b, float* out, hipStream_t stream);
 /* torchaudio.transforms.Resample (sinc_interp_hann) as pad + MFMA GEMM (tools/load_wav.py:7,

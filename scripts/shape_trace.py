@@ -8,7 +8,8 @@ rooflines from a rocprofv3 kernel trace or PMC pass:
 The log lists, in host launch order, every launch the ops layer reports to its probe hook during the LAST
 ``--steps`` steps (name, shape, algorithmic work); shape_table.py pairs them with the trace's dispatches (same
 host order) to label each GEMM dispatch by its role (out-proj vs FFN2 share one instantiation and grid).
-``--serial``: encoder + head + DP on one stream (no overlap), for the isolated figures."""
+``--mode serial``: encoder + head + DP on one stream (no overlap); ``--mode encoder``: the encoder alone (what each
+encoder kernel takes with nothing beside it: against ``pipe``, the per-kernel cost of the overlapped side stream)."""
 import argparse
 import json
 import os
@@ -36,7 +37,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--encoder", default="base", choices=["base", "large"])
-    ap.add_argument("--serial", action="store_true")
+    ap.add_argument("--mode", default="pipe", choices=["pipe", "serial", "encoder"])
     ap.add_argument("--log", required=True)
     args = ap.parse_args()
     import bench
@@ -51,7 +52,11 @@ def main():
     wav = torch.from_numpy(wav_np).to(d)
 
     def run(k):
-        if args.serial:
+        if args.mode == "encoder":
+            for _ in range(k):
+                task.encode_batch(wav, 16000)
+            return
+        if args.mode == "serial":
             for _ in range(k):
                 task.decoder.assemble(task.align_batch(wav, ph, ws, pw, wav_sr=16000, host=False), ph, ws, pw)
             return
@@ -72,7 +77,7 @@ def main():
     torch.cuda.synchronize()
     os.makedirs(os.path.dirname(os.path.abspath(args.log)), exist_ok=True)
     with open(args.log, "w") as f:
-        json.dump({"steps": args.steps, "batch": args.batch, "encoder": enc, "serial": args.serial,
+        json.dump({"steps": args.steps, "batch": args.batch, "encoder": enc, "mode": args.mode,
                    "launches": log.entries}, f)
     print(f"logged {len(log.entries)} launches over {args.steps} steps", flush=True)
 

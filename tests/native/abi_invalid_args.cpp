@@ -55,10 +55,14 @@ int main() {
     CHECK(hfa_viterbi_backtrack(2, 70000, 8, ip, ip, fp, bp, ip, nullptr, nullptr, nullptr, fp, st),
                "backtrack NULL out");
     CHECK(hfa_viterbi_backtrack(-3, 10, 8, ip, ip, fp, bp, ip, op, op, op, fp, st), "backtrack B<0");
-    CHECK(hfa_lattice_prologue(-1, 10, 60, 8, ip, ip, fp, 60, 600, fp, 1, 10, ip, fp, fp, fp, fp, fp, fp, dp, st),
-               "prologue B<0");
+    CHECK(hfa_lattice_prologue(-1, 10, 60, 8, ip, ip, fp, 60, 600, fp, 1, 10, ip, fp, fp, fp, fp, fp, fp, dp,
+                               nullptr, nullptr, st), "prologue B<0");
     CHECK(hfa_lattice_prologue(1, 10, 60, 8, ip, ip, nullptr, 60, 600, fp, 1, 10, ip, fp, fp, fp, fp, fp, fp,
-                                    dp, st), "prologue NULL logits");
+                               dp, nullptr, nullptr, st), "prologue NULL logits");
+    CHECK(hfa_lattice_prologue(1, 10, 60, 8, ip, ip, fp, 60, 600, fp, 1, 10, ip, fp, fp, fp, fp, fp, fp, dp, fp,
+                               nullptr, st), "prologue dp without curr");
+    CHECK(hfa_viterbi_init(-1, 10, 8, ip, ip, fp, ip, fp, dp, st), "viterbi_init B<0");
+    CHECK(hfa_viterbi_init(1, 10, 8, ip, ip, fp, ip, nullptr, dp, st), "viterbi_init NULL dp");
     // GEMMs
     CHECK(hfa_conv_gemm_f32(-1, 64, 64, 1, 1, fp, 0, 0, 64, 1, 0, 64, 1, fp, 0, 64, nullptr, 0, nullptr, 0, 0,
                                  0, fp, 0, 0, 64, 0, st), "conv_gemm_f32 M<0");
@@ -121,6 +125,8 @@ int main() {
     CHECK(hfa_mask_rows_f32(-1, 10, 4, fp, 40, 4, ip, st), "mask B<0");
     CHECK(hfa_pad_rows_f32(1, 10, nullptr, 10, 2, 14, fp, 14, st), "pad NULL x");
     CHECK(hfa_add_f32(-4, fp, fp, fp, st), "add n<0");
+    CHECK(hfa_flag_take(-1, op, op, st), "flag_take n<0");
+    CHECK(hfa_flag_take(1, nullptr, op, st), "flag_take NULL flags");
     CHECK(hfa_selftest_erf(-1, fp, fp, fp, st), "erf n<0");
     CHECK(hfa_selftest_gelu(-1, fp, fp, st), "gelu n<0");
     CHECK(hfa_resample_f32(1, 100, fp, 100, 0, 441, fp, 16, 6, ws, fp, 300, st), "resample orig=0");
@@ -158,7 +164,7 @@ int main() {
     // host queries and tuning hooks (thread-local state; name strings stay valid, bounded)
     for (int cfg = 0; cfg < 25; ++cfg) {
         hfa_gemm_split_tuning(cfg);
-        const char* n = hfa_gemm_split_kernel_name(15968, 3072, 1, 1, 1, 768);
+        const char* n = hfa_gemm_split_kernel_name(15968, 3072, 768, 1, 1, 1, 768);
         if (!n || std::strlen(n) == 0 || std::strlen(n) >= 128) { std::printf("FAIL split name cfg %d\n", cfg); ++g_fail; }
     }
     hfa_gemm_split_tuning(0);

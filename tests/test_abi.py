@@ -79,7 +79,7 @@ def test_split_gemm_tile_choice():
     192-wide tile fills the last round of CUs much better (profiles/r03/split_tiles_c5.txt)."""
     pytest.importorskip("torch")
     from hubertfa_amd import ops
-    tile = lambda M, N, Z=1, epi=0: ops._split_name(M, N, Z, True, epi, 768).split("<")[1].split(",")[1:3]  # noqa: E731
+    tile = lambda M, N, Z=1, epi=0: ops._split_name(M, N, 768, Z, True, epi, 768).split("<")[1].split(",")[1:3]  # noqa: E731
     assert tile(15968, 2304) == [" 192", " 256"]          # config 2 QKV: 567 big tiles = 2.2 rounds
     assert tile(15968, 3072, epi=1) == [" 256", " 256"]   # config 2 FFN1: 756 tiles = 2.95 rounds
     assert tile(17924, 3072, epi=1) == [" 256", " 256"]   # config 5 windows: 852 tiles (was 128 x 128)
@@ -88,3 +88,5 @@ def test_split_gemm_tile_choice():
     assert tile(15999, 512, Z=32, epi=1) == [" 256", " 256"]   # extractor conv1
     assert tile(499, 512, Z=32, epi=1) == [" 128", " 128"]     # extractor conv6: 128 big tiles, half a round
     assert tile(864, 192, Z=32) == [" 128", " 128"]       # UNet level 0: small grid
+    # the grouped positional conv (Cg = 48, k = 128): the LDS-window kernel, named as launched (the K argument)
+    assert ops._split_name(499, 48, 6144, 512, False, 1, 48) == "posconv_split_kernel<1, 3>"

@@ -97,3 +97,8 @@ def test_300s_chunked_properties():
     iv = res["ph_intervals"]
     assert np.all(iv[:, 1] > iv[:, 0]) and iv[0, 0] >= 0 and iv[-1, 1] <= 300.0 + 1e-6
     assert np.all(np.diff(iv[:, 0]) > 0)
+    # quantified against the anchor, the unchunked run (bench.chunk_agreement; the same numbers go into the
+    # config-5c bench line): printed, and bounded loosely -- random weights, so only gross breakage is asserted
+    agr = bench.chunk_agreement(task, torch.from_numpy(wav).to(dev), ph_seqs, word_seqs, p2ws, 20.0)["utterances"][0]
+    print(f"chunked vs unchunked at 300 s: {agr}")
+    assert agr["phones_in_both"] > 0 and agr["within_5"] is not None and np.isfinite(agr["max_logprob_diff"])

@@ -189,3 +189,36 @@ def test_decode_end_to_end_matches_reference():
         np.testing.assert_allclose(ph_iv, zz[f"c{ci}_ph_intervals"], atol=1e-6)
         np.testing.assert_allclose(w_iv, zz[f"c{ci}_word_intervals"], atol=1e-6)
         np.testing.assert_allclose(conf, case["total_confidence"], rtol=1e-4)
+
+
+@pytest.mark.parametrize("first_sp", [True, False])
+def test_dp_initialisation_in_prologue(first_sp):
+    """_decode's initialisation (alignment_decoder.py:244-254) written by the lattice prologue (init_dp) and by
+    hfa_viterbi_init: dp[0, 0] = curr[0] = L[0, 0]; with an id-0 first phone and S > 1 also dp[0, 1] = curr[1] =
+    L[0, 1]; every other state of row 0 (padding pitch included) and of curr -inf; a row with T = 0 all -inf; S = 1
+    keeps only state 0.  Bit-exact, in a batch with unequal T and S."""
+    from hubertfa_amd import ops
+    dev = torch.device("cuda")
+    rng = np.random.default_rng(5)
+    V = 20
+    Ts, Ss = [7, 0, 5, 9], [5, 3, 1, 2]
+    B, Tmax, Smax = len(Ts), max(Ts), 8
+    ids = rng.integers(1, V, (B, Smax)).astype(np.int32)
+    if first_sp:
+        ids[:, 0] = 0
+    logits = torch.from_numpy(rng.normal(0, 3, (B, Tmax, V + 2)).astype(np.float32)).to(dev)
+    T_t = torch.tensor(Ts, dtype=torch.int32, device=dev)
+    S_t = torch.tensor(Ss, dtype=torch.int32, device=dev)
+    ids_t = torch.from_numpy(ids).to(dev)
+    out = ops.lattice_prologue(logits[:, :, 2:], logits[:, :, 0], ids_t, T_t, S_t, init_dp=True)
+    dp2, _, cu2 = ops.viterbi_init(out["prob_log"], ids_t, T_t, S_t)
+    pl = out["prob_log"].cpu().numpy()
+    for b in range(B):
+        exp = np.full(Smax, -np.inf)
+        if Ts[b] > 0:
+            exp[0] = pl[b, 0, 0]
+            if first_sp and Ss[b] > 1:
+                exp[1] = pl[b, 0, 1]
+        for dp, cu in ((out["dp"], out["curr"]), (dp2, cu2)):
+            assert np.array_equal(dp[b, 0].cpu().numpy(), exp.astype(np.float32)), b
+            assert np.array_equal(cu[b].cpu().numpy(), exp.astype(np.float32).astype(np.float64)), b
