@@ -386,12 +386,13 @@ def main():
         """k steps, software-pipelined: the host assembles batch i while the GPU runs batch i+1."""
         pending, res = None, None
         for _ in range(k):
-            t0 = time.perf_counter()
+            t0, c0, p0 = time.perf_counter(), time.thread_time(), time.process_time()
             h = launch(inp)
-            t1 = time.perf_counter()
+            t1, c1 = time.perf_counter(), time.thread_time()
             if pending is not None:
                 res = finish(pending, inp)
-            host_t.append((t1 - t0, time.perf_counter() - t1))
+            host_t.append((t1 - t0, time.perf_counter() - t1, c1 - c0, time.thread_time() - c1,
+                           time.process_time() - p0))
             pending = h
         return finish(pending, inp) if pending is not None else res
 
@@ -412,7 +413,7 @@ def main():
             e = float(tt.item())
         return r, e
 
-    host_t = []   # (enqueue, wait + assemble) seconds per step, reported on stderr
+    host_t = []   # per step: enqueue / wait + assemble wall seconds, their CPU seconds (this thread), process CPU
 
     census = ops.KernelProbe(None)
     ops.PROBE = census
@@ -510,6 +511,14 @@ def main():
     torch.cuda.synchronize()
     ops.PROBE = None
     out["secondary"] = secondary_rooflines(iso, probe, n_frames, len(ph_seqs[0]))
+    ht = host_t[max(args.warmup, 1):max(args.warmup, 1) + args.steps]      # the timed steps
+    avg = lambda i: 1e3 * sum(h[i] for h in ht) / max(len(ht), 1)  # noqa: E731
+    out["host_cpu"] = {
+        "enqueue_cpu_ms_per_step": avg(2), "assemble_cpu_ms_per_step": avg(3), "process_cpu_ms_per_step": avg(4),
+        "enqueue_wall_ms_per_step": avg(0), "wait_assemble_wall_ms_per_step": avg(1),
+        "note": "rank 0's host cost per timed step: CPU seconds of the launching thread for the GPU half's enqueue "
+                "(ctypes launches, allocator, events) and for the previous batch's wait + interval assembly, and "
+                "the whole process's CPU (all threads); the GPU step is ms_per_step"}
     if rank == 0:
         import contextlib
         with contextlib.redirect_stdout(sys.stderr):         # the writers' progress prints stay off the JSON line
@@ -518,8 +527,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(wav_np, ph_seqs, word_seqs, p2ws, ckpt, args.cpu_sample_s, encoder)
     if rank == 0:
         ht = host_t[-args.steps:]
-        print(f"host per step: enqueue {1e3 * sum(a for a, _ in ht) / len(ht):.2f} ms, wait+assemble "
-              f"{1e3 * sum(b for _, b in ht) / len(ht):.2f} ms", file=sys.stderr, flush=True)
+        print(f"host per step: enqueue {1e3 * sum(h[0] for h in ht) / len(ht):.2f} ms, wait+assemble "
+              f"{1e3 * sum(h[1] for h in ht) / len(ht):.2f} ms", file=sys.stderr, flush=True)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -749,73 +749,97 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
     const float* Rb = p.R ? p.R + zb * p.sRb + zg * p.sRg : nullptr;
     const _Float16* Rhb = p.Rh ? p.Rh + zb * p.sRb + zg * p.sRg : nullptr;
     const float* biasb = p.bias ? p.bias + zg * p.sBg : nullptr;
+    // The residual planes (out-projection, FFN2: the LayerNorm's planes) are loaded one 32 x 32 block ahead: block
+    // b + 1's loads are issued before block b's slab pass, so their latency hides under it instead of stalling every
+    // block (the epilogue runs with the matrix pipe idle).  Vector rows only (col + 3 < N, aligned C); the ragged
+    // column tail reads its residual directly below.
+    constexpr int NB = TI * TJ;
+    f16x4 rn1[4], rn2[4];
+    auto load_res = [&](int b, f16x4 (&r1)[4], f16x4 (&r2)[4]) {
+        const int row0 = wrow0 + (b % TI) * 32, col0 = wcol0 + (b / TI) * 32;
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) {
+        for (int k = 0; k < 4; ++k) {
+            const int idx = lane + k * 64;
+            const int row = row0 + (idx >> 3), col = col0 + (idx & 7) * 4;
+            if (row < p.M && col + 3 < p.N && p.cvec) {
+                const _Float16* rh = Rhb + (long long)row * p.ldr + col;
+                r1[k] = *reinterpret_cast<const f16x4*>(rh);
+                r2[k] = *reinterpret_cast<const f16x4*>(rh + p.sRp);
+            }
+        }
+    };
+    if (Rhb) load_res(0, rn1, rn2);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int i = b % TI, j = b / TI;
         const int col0 = wcol0 + j * 32;
-        if (col0 >= p.N) continue;
-#pragma unroll
-        for (int i = 0; i < TI; ++i) {
-            const int row0 = wrow0 + i * 32;
-            if (row0 >= p.M) continue;
-            bad |= fill_slab<MF>(acc, i, j, EPI, biasb, col0, p.N, lane, slab, scale) && check;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        const int row0 = wrow0 + i * 32;
+        f16x4 rc1[4], rc2[4];
+        if (Rhb) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int idx = lane + k * 64;
-                const int r = idx >> 3, c4 = (idx & 7) * 4;
-                const int row = row0 + r, col = col0 + c4;
-                if (row < p.M) {
-                    f32x4 v = *reinterpret_cast<const f32x4*>(slab + r * 36 + c4);
-                    float* dst = Cb + (long long)row * p.ldc + col;
-                    if (col + 3 < p.N && p.cvec) {
-                        if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + (long long)row * p.ldr + col);
-                        if (Rhb) {          // residual planes: hi + 2^-11 lo (exact in f32), one rounding in the add
-                            const _Float16* rh = Rhb + (long long)row * p.ldr + col;
-                            const f16x4 r1 = *reinterpret_cast<const f16x4*>(rh);
-                            const f16x4 r2 = *reinterpret_cast<const f16x4*>(rh + p.sRp);
+                rc1[k] = rn1[k];
+                rc2[k] = rn2[k];
+            }
+            if (b + 1 < NB) load_res(b + 1, rn1, rn2);
+        }
+        if (col0 >= p.N || row0 >= p.M) continue;
+        bad |= fill_slab<MF>(acc, i, j, EPI, biasb, col0, p.N, lane, slab, scale) && check;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
-                            for (int t = 0; t < 4; ++t) v[t] += __builtin_fmaf((float)r2[t], 1.0f / 2048.0f, (float)r1[t]);
+        for (int k = 0; k < 4; ++k) {
+            const int idx = lane + k * 64;
+            const int r = idx >> 3, c4 = (idx & 7) * 4;
+            const int row = row0 + r, col = col0 + c4;
+            if (row < p.M) {
+                f32x4 v = *reinterpret_cast<const f32x4*>(slab + r * 36 + c4);
+                float* dst = Cb + (long long)row * p.ldc + col;
+                if (col + 3 < p.N && p.cvec) {
+                    if (Rb) v += *reinterpret_cast<const f32x4*>(Rb + (long long)row * p.ldr + col);
+                    if (Rhb) {          // residual planes: hi + 2^-11 lo (exact in f32), one rounding in the add
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            v[t] += __builtin_fmaf((float)rc2[k][t], 1.0f / 2048.0f, (float)rc1[k][t]);
+                    }
+                    *reinterpret_cast<f32x4*>(dst) = v;
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if (col + t < p.N) {
+                            v[t] += Rb ? Rb[(long long)row * p.ldr + col + t] : 0.0f;
+                            if (Rhb) {
+                                const _Float16* rh = Rhb + (long long)row * p.ldr + col + t;
+                                v[t] += __builtin_fmaf((float)rh[p.sRp], 1.0f / 2048.0f, (float)rh[0]);
+                            }
+                            dst[t] = v[t];
                         }
-                        *reinterpret_cast<f32x4*>(dst) = v;
+                }
+                if (Hb) {
+                    uint2 u1, u2;
+                    if (col + 3 >= p.N)   // columns past N: no residual was added, keep them out of the check
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            if (col + t >= p.N) v[t] = 0.0f;
+                    hfa::split_pair(v[0], v[1], u1.x, u2.x, nanacc, c2048);
+                    hfa::split_pair(v[2], v[3], u1.y, u2.y, nanacc, c2048);
+                    const f16x4 v1 = __builtin_bit_cast(f16x4, u1), v2 = __builtin_bit_cast(f16x4, u2);
+                    _Float16* hd = Hb + (long long)row * p.ldc + col;
+                    if (col + 3 < p.N) {
+                        *reinterpret_cast<f16x4*>(hd) = v1;
+                        *reinterpret_cast<f16x4*>(hd + p.sCp) = v2;
                     } else {
 #pragma unroll
                         for (int t = 0; t < 4; ++t)
                             if (col + t < p.N) {
-                                v[t] += Rb ? Rb[(long long)row * p.ldr + col + t] : 0.0f;
-                                if (Rhb) {
-                                    const _Float16* rh = Rhb + (long long)row * p.ldr + col + t;
-                                    v[t] += __builtin_fmaf((float)rh[p.sRp], 1.0f / 2048.0f, (float)rh[0]);
-                                }
-                                dst[t] = v[t];
+                                hd[t] = v1[t];
+                                hd[t + p.sCp] = v2[t];
                             }
-                    }
-                    if (Hb) {
-                        uint2 u1, u2;
-                        if (col + 3 >= p.N)   // columns past N: no residual was added, keep them out of the check
-#pragma unroll
-                            for (int t = 0; t < 4; ++t)
-                                if (col + t >= p.N) v[t] = 0.0f;
-                        hfa::split_pair(v[0], v[1], u1.x, u2.x, nanacc, c2048);
-                        hfa::split_pair(v[2], v[3], u1.y, u2.y, nanacc, c2048);
-                        const f16x4 v1 = __builtin_bit_cast(f16x4, u1), v2 = __builtin_bit_cast(f16x4, u2);
-                        _Float16* hd = Hb + (long long)row * p.ldc + col;
-                        if (col + 3 < p.N) {
-                            *reinterpret_cast<f16x4*>(hd) = v1;
-                            *reinterpret_cast<f16x4*>(hd + p.sCp) = v2;
-                        } else {
-#pragma unroll
-                            for (int t = 0; t < 4; ++t)
-                                if (col + t < p.N) {
-                                    hd[t] = v1[t];
-                                    hd[t + p.sCp] = v2[t];
-                                }
-                        }
                     }
                 }
             }
-            __builtin_amdgcn_wave_barrier();
         }
+        __builtin_amdgcn_wave_barrier();
     }
     if ((bad || hfa::range_bad(nanacc)) && p.oflow) *p.oflow = 1;
 }
@@ -1602,6 +1626,8 @@ constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {256, 64, 4, 1, 2, 2, true, 32, 16}, {256, 128, 4, 2, 3, 1, true, 32, 16}, {128, 256, 2, 4, 3, 1, true, 32, 16},
     {256, 192, 4, 2, 2, 1, true, 32, 16}, {192, 256, 2, 4, 2, 1, true, 32, 16}};
 thread_local int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
+thread_local int g_split_fill = 0;  // A/B (hfa_gemm_split_fill): 1 = one-round big-tile grids take the CU's whole LDS,
+                                    // 2 = every big-tile grid does (no other kernel's workgroup can share the CU)
 thread_local int g_win_nb = 3;   // column blocks of the window kernel the name query reports (N / 16)
 
 // Measured on the workload's shapes (scripts/split_gemm_bench.py, profiles/r01/split_gemm_cfgs.txt): the 256 x 256
@@ -1682,9 +1708,23 @@ int launch_split_cfg(GemmP p, int Z, hipStream_t st) {
     constexpr SplitGeom g = kSplitGeom[CFG];
     dim3 grid;
     if (int rc = set_grid(p, g.BM, g.BN, grid, Z)) return rc;
-    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE, g.BK,
-                                          g.MF ? g.MF : 32, F16>),
-                       grid, dim3(64 * g.WM * g.WN), 0, st, p);
+    auto kern = gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE, g.BK, g.MF ? g.MF : 32,
+                                  F16>;
+    unsigned dyn = 0;
+    if (g_split_fill && g.OCC == 1 && (g_split_fill == 2 || (long long)grid.x * grid.z <= 256)) {
+        constexpr unsigned stat = (unsigned)(g.NS * (2 * g.BM * g.BK + 2 * g.BN * g.BK) * 2);
+        dyn = 160u * 1024u - stat;
+        static thread_local bool attr_set = false;     // per instantiation
+        if (!attr_set) {
+            hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+            if (e != hipSuccess) {
+                hfa::set_error("hfa_conv_gemm_split: cannot reserve the CU's LDS: %s", hipGetErrorString(e));
+                return -(int)e;
+            }
+            attr_set = true;
+        }
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(64 * g.WM * g.WN), dyn, st, p);
     return hfa::check_launch("hfa_conv_gemm_split");
 }
 
@@ -2019,6 +2059,15 @@ const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split
 
 int hfa_gemm_split_tuning(int cfg) {
     g_split_cfg = cfg;
+    return HFA_OK;
+}
+
+int hfa_gemm_split_fill(int mode) {
+    if (mode < 0 || mode > 2) {
+        hfa::set_error("hfa_gemm_split_fill: mode %d is not 0, 1 or 2", mode);
+        return HFA_EINVAL;
+    }
+    g_split_fill = mode;
     return HFA_OK;
 }
 

@@ -156,6 +156,10 @@ const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split
  * B*T = 15968 rows).  The automatic choice uses single-accumulator tiles only: results then do not depend on the
  * tile. */
 int hfa_gemm_split_tuning(int cfg);
+/* Scheduling experiment (A/B; default 0): 1 = a one-round grid of one-workgroup-per-CU split tiles reserves the
+ * whole 160 KiB of LDS, so no workgroup of another stream's kernel can share a CU it runs on; 2 = every such grid.
+ * Results do not change. */
+int hfa_gemm_split_fill(int mode);
 /* x [rows, cols] f32 (row stride ldx) -> split planes y (row stride ldy, plane 1 at +sp); raises *oflow (if
  * non-NULL) for |x| >= 65504 or a non-finite x. */
 int hfa_split_f16(int rows, int cols, const float* x, long long ldx, uint16_t* y, long long ldy, long long sp,
