@@ -1612,7 +1612,7 @@ enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_
        SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_256x64_1 = 14,
        SCFG_N48 = 15, SCFG_WIN = 16, SCFG_256x256_M16 = 17, SCFG_128x128_M16 = 18, SCFG_128x64_M16 = 19,
        SCFG_256x64_M16 = 20, SCFG_256x128_M16_S3 = 21, SCFG_128x256_M16_S3 = 22, SCFG_256x192_M16 = 23,
-       SCFG_192x256_M16 = 24, SCFG_COUNT = 25 };
+       SCFG_192x256_M16 = 24, SCFG_128x192_M16 = 25, SCFG_192x128_M16 = 26, SCFG_COUNT = 27 };
 struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; int MF; };
 constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 128, 2, 2, 2, 2, false, 32}, {128, 128, 2, 2, 2, 2, false, 32}, {128, 64, 2, 2, 2, 2, false, 32},
@@ -1624,7 +1624,10 @@ constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {256, 48, 8, 1, 3, 1, true, 32},       // SCFG_WIN: posconv_split_kernel (LDS-resident input window)
     {256, 256, 2, 4, 2, 1, true, 32, 16}, {128, 128, 2, 2, 2, 2, true, 32, 16}, {128, 64, 2, 2, 2, 2, true, 32, 16},
     {256, 64, 4, 1, 2, 2, true, 32, 16}, {256, 128, 4, 2, 3, 1, true, 32, 16}, {128, 256, 2, 4, 3, 1, true, 32, 16},
-    {256, 192, 4, 2, 2, 1, true, 32, 16}, {192, 256, 2, 4, 2, 1, true, 32, 16}};
+    {256, 192, 4, 2, 2, 1, true, 32, 16}, {192, 256, 2, 4, 2, 1, true, 32, 16},
+    // two workgroups per CU (2 x 80 KiB of LDS): 500 / 504 tiles fill the 512 slots of an N = 768 grid at
+    // B*L = 15968 rows in one balanced round (the 256 x 256 tile: 189 tiles on 256 CUs)
+    {128, 192, 2, 2, 2, 2, true, 32, 16}, {192, 128, 2, 2, 2, 2, true, 32, 16}};
 thread_local int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 thread_local int g_split_fill = 0;  // A/B (hfa_gemm_split_fill): 1 = one-round big-tile grids take the CU's whole LDS,
                                     // 2 = every big-tile grid does (no other kernel's workgroup can share the CU)
@@ -1787,6 +1790,8 @@ int launch_split(GemmP p, int Z, int cfg, hipStream_t st, bool f16) {
         case SCFG_128x256_M16_S3: return launch_split_cfg<EPI, OUTS, SCFG_128x256_M16_S3>(p, Z, st);
         case SCFG_256x192_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x192_M16>(p, Z, st);
         case SCFG_192x256_M16: return launch_split_cfg<EPI, OUTS, SCFG_192x256_M16>(p, Z, st);
+        case SCFG_128x192_M16: return launch_split_cfg<EPI, OUTS, SCFG_128x192_M16>(p, Z, st);
+        case SCFG_192x128_M16: return launch_split_cfg<EPI, OUTS, SCFG_192x128_M16>(p, Z, st);
         default: return launch_split_cfg<EPI, OUTS, SCFG_128x128>(p, Z, st);
     }
 }

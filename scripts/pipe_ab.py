@@ -65,9 +65,11 @@ def setters(task):
                 g()
         return f
     return {
-        "base": combo(lambda: L.hfa_gemm_split_fill(0), side("plain")),
+        "base": combo(lambda: L.hfa_gemm_split_fill(0), side("plain"), lambda: setattr(task, "interleave", True)),
         "fill1": lambda: L.hfa_gemm_split_fill(1),
         "fill2": lambda: L.hfa_gemm_split_fill(2),
+        "serialside": lambda: setattr(task, "interleave", False),
+        "serialsidefill1": combo(lambda: setattr(task, "interleave", False), lambda: L.hfa_gemm_split_fill(1)),
         "mask64": side(64),
         "mask32": side(32),
         "mask64fill1": combo(side(64), lambda: L.hfa_gemm_split_fill(1)),
