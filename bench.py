@@ -79,8 +79,10 @@ def parse():
     ap.add_argument("--host-input", action="store_true",
                     help="waves start in host memory and are uploaded inside every step (task.upload, as infer.py) (PCIe-inclusive "
                          "rate; the headline value keeps inputs resident in HBM)")
-    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r03", "traffic_r03.json"),
-                    help="PMC-derived HBM bytes per launch of the probed kernel (written by tools/pmc_traffic.py)")
+    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r04", "traffic_r04.json"),
+                    help="PMC-derived HBM bytes per launch of the probed kernel (written by scripts/pmc_traffic.py)")
+    ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "r04", "pmc_r04.json"),
+                    help="PMC-derived MFMA busy and clock per kernel (written by scripts/pmc_kernels.py)")
     return ap.parse_args()
 
 
@@ -435,6 +437,13 @@ def main():
     hub_flops = task.unitsEncoder.model.flops(int(round(args.seconds * 16000)))
     head_flops = task.head.flops(task.head.padded_len(n_frames))
 
+    pmc = None
+    if os.path.exists(args.pmc_file):
+        try:
+            with open(args.pmc_file) as f:
+                pmc = json.load(f).get("kernels", {}).get(probe_name)
+        except Exception:  # noqa: BLE001
+            pmc = None
     traffic = None
     if os.path.exists(args.traffic_file):
         try:
@@ -476,7 +485,10 @@ def main():
                                     "MAC, 2516.6 TF f16 dense / 3" if probe_name.startswith("gemm_split_kernel")
                                     else "f32 MFMA dense peak"),
                      "traffic": traffic, "launches": ps["launches"], "avg_launch_ms": ps["avg_ms"],
-                     "flops_per_launch": ps["avg_flops"]},
+                     "flops_per_launch": ps["avg_flops"],
+                     "mfma_busy": pmc.get("mfma_busy") if pmc else None,
+                     "clock_ghz": pmc.get("clock_ghz") if pmc else None,
+                     "pmc_source": os.path.relpath(args.pmc_file, REPO) if pmc else None},
     }
     if probe_name.startswith("gemm_split_kernel") and achieved:
         # context, not the contract's peak: MI355X_MICROARCH.md 'DVFS give-back' item 1 measures a plain bf16 GEMM

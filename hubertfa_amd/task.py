@@ -275,6 +275,7 @@ class ForcedAlignmentTask:
         return work.handle
 
     interleave = True
+    gate_points = ("ffn2",)      # where the next encoder takes a step of the held side work (HubertEncoder gates)
 
     def flush(self):
         """Enqueue any side work still held for interleaving (the pipeline's last batch)."""
@@ -325,8 +326,8 @@ class _SideWork:
     def gate(self, main):
         """Callable for the next encoder's FFN2 gates: the side stream waits for the main stream to reach that point,
         then takes one step."""
-        def g():
-            if self.done:
+        def g(point):
+            if self.done or point not in self.task.gate_points:
                 return
             ev = torch.cuda.Event()
             ev.record(main)

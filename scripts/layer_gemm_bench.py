@@ -8,7 +8,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from hubertfa_amd import ops  # noqa: E402
+from hubertfa_amd import ops, _lib  # noqa: E402
 
 SPLIT_PEAK = 2516.6 / 3
 
@@ -63,7 +63,12 @@ def main():
         o = torch.empty((2, B, L, H), dtype=torch.float16, device=d)
         cases.append(("attention (split)", 4.0 * B * H * L * L,
                       lambda: ops.attention_split(qs, o, B=B, H=H // 64, L=L, head_dim=64, scale=0.125)))
-    from hubertfa_amd import _lib
+
+        def attn8():
+            _lib.lib().hfa_attention_split_tuning(8)
+            ops.attention_split(qs, o, B=B, H=H // 64, L=L, head_dim=64, scale=0.125)
+            _lib.lib().hfa_attention_split_tuning(0)
+        cases.append(("attention (split, 8 waves)", 4.0 * B * H * L * L, attn8))
     for cfg in [int(c) for c in args.cfgs.split(",")]:
         _lib.lib().hfa_gemm_split_tuning(cfg)
         for name, flop, fn in cases:

@@ -65,10 +65,12 @@ def setters(task):
                 g()
         return f
     return {
-        "base": combo(lambda: L.hfa_gemm_split_fill(0), side("plain"), lambda: setattr(task, "interleave", True)),
+        "base": combo(lambda: L.hfa_gemm_split_fill(0), side("plain"), lambda: setattr(task, "interleave", True),
+                      lambda: setattr(task, "gate_points", ("ffn2",))),
         "fill1": lambda: L.hfa_gemm_split_fill(1),
         "fill2": lambda: L.hfa_gemm_split_fill(2),
         "serialside": lambda: setattr(task, "interleave", False),
+        "gatestart": lambda: setattr(task, "gate_points", ("extractor", "ffn2")),
         "serialsidefill1": combo(lambda: setattr(task, "interleave", False), lambda: L.hfa_gemm_split_fill(1)),
         "mask64": side(64),
         "mask32": side(32),
