@@ -1629,8 +1629,6 @@ constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     // B*L = 15968 rows in one balanced round (the 256 x 256 tile: 189 tiles on 256 CUs)
     {128, 192, 2, 2, 2, 2, true, 32, 16}, {192, 128, 2, 2, 2, 2, true, 32, 16}};
 thread_local int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
-thread_local int g_split_fill = 0;  // A/B (hfa_gemm_split_fill): 1 = one-round big-tile grids take the CU's whole LDS,
-                                    // 2 = every big-tile grid does (no other kernel's workgroup can share the CU)
 thread_local int g_win_nb = 3;   // column blocks of the window kernel the name query reports (N / 16)
 
 // Measured on the workload's shapes (scripts/split_gemm_bench.py, profiles/r01/split_gemm_cfgs.txt): the 256 x 256
@@ -1672,10 +1670,13 @@ inline int split_cfg(const GemmP& p, int Z) {
     auto fill = [](long long b) { return (double)b / (double)(((b + 255) / 256) * 256); };
     const long long blocks192n = (long long)((p.M + 255) / 256) * ((p.N + 191) / 192) * Z;   // 256 x 192
     const long long blocks192m = (long long)((p.M + 191) / 192) * ((p.N + 255) / 256) * Z;   // 192 x 256
-    // (one-round grids stay on 256 x 256: N = 768 at 189 vs 252 busy CUs measured equal, the fewer CUs clock higher)
+    // One-round grids: the 192 x 256 tile when it still makes one round and busies more CUs -- the N = 768 family
+    // at B*L = 15968 rows, 252 instead of 189 tiles on 256 CUs: FFN2 228 -> 208 us, the out-projection 77 -> 69 us,
+    // measured as hubert.py launches them (profiles/r04/layer_tiles.txt; round 2's per-utterance Z-batched
+    // microbenchmark had not shown it).
     double best = fill(blocks256);
     int cfg = SCFG_256x256_M16;
-    if (blocks256 <= 256) return cfg;
+    if (blocks256 <= 256) return (blocks192m <= 256 && blocks192m > blocks256) ? SCFG_192x256_M16 : cfg;
     if (0.92 * fill(blocks192m) > best + 0.05) {
         best = 0.92 * fill(blocks192m);
         cfg = SCFG_192x256_M16;
@@ -1711,23 +1712,9 @@ int launch_split_cfg(GemmP p, int Z, hipStream_t st) {
     constexpr SplitGeom g = kSplitGeom[CFG];
     dim3 grid;
     if (int rc = set_grid(p, g.BM, g.BN, grid, Z)) return rc;
-    auto kern = gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE, g.BK, g.MF ? g.MF : 32,
-                                  F16>;
-    unsigned dyn = 0;
-    if (g_split_fill && g.OCC == 1 && (g_split_fill == 2 || (long long)grid.x * grid.z <= 256)) {
-        constexpr unsigned stat = (unsigned)(g.NS * (2 * g.BM * g.BK + 2 * g.BN * g.BK) * 2);
-        dyn = 160u * 1024u - stat;
-        static thread_local bool attr_set = false;     // per instantiation
-        if (!attr_set) {
-            hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-            if (e != hipSuccess) {
-                hfa::set_error("hfa_conv_gemm_split: cannot reserve the CU's LDS: %s", hipGetErrorString(e));
-                return -(int)e;
-            }
-            attr_set = true;
-        }
-    }
-    hipLaunchKernelGGL(kern, grid, dim3(64 * g.WM * g.WN), dyn, st, p);
+    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE, g.BK,
+                                          g.MF ? g.MF : 32, F16>),
+                       grid, dim3(64 * g.WM * g.WN), 0, st, p);
     return hfa::check_launch("hfa_conv_gemm_split");
 }
 
@@ -2064,15 +2051,6 @@ const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split
 
 int hfa_gemm_split_tuning(int cfg) {
     g_split_cfg = cfg;
-    return HFA_OK;
-}
-
-int hfa_gemm_split_fill(int mode) {
-    if (mode < 0 || mode > 2) {
-        hfa::set_error("hfa_gemm_split_fill: mode %d is not 0, 1 or 2", mode);
-        return HFA_EINVAL;
-    }
-    g_split_fill = mode;
     return HFA_OK;
 }
 

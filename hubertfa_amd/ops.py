@@ -160,7 +160,6 @@ _lib.register("hfa_conv_gemm_split", [_I_, _I_, _I_, _I_, _I_, _P_, _LL_, _LL_, 
                                        _LL_, _LL_, _I_, _I_, _P_, _P_])
 _lib.register("hfa_gemm_split_kernel_name", [_I_, _I_, _I_, _I_, _I_, _I_, _I_], ctypes.c_char_p)
 _lib.register("hfa_gemm_split_tuning", [_I_])
-_lib.register("hfa_gemm_split_fill", [_I_])
 _lib.register("hfa_split_f16", [_I_, _I_, _P_, _LL_, _P_, _LL_, _LL_, _P_, _P_])
 _lib.register("hfa_gemm_f32", [_I_, _I_, _I_, _P_, _I_, _P_, _I_, _P_, _P_, _I_, _P_, _I_, _I_, _P_])
 _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_,

@@ -153,13 +153,9 @@ const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split
  * with f32 output, e.g. the grouped positional conv at Cg = 48), 16 the LDS-window positional conv kernel, 17-20
  * the 256x256 / 128x128 / 128x64 / 256x64 single-accumulator tiles on v_mfma_f32_16x16x32_f16, 21/22 256x128 /
  * 128x256 likewise with 3 stages, 23/24 256x192 / 192x256 likewise (one round of 252 tiles for N = 768 at
- * B*T = 15968 rows).  The automatic choice uses single-accumulator tiles only: results then do not depend on the
+ * B*T = 15968 rows), 25/26 128x192 / 192x128 with two workgroups per CU.  The automatic choice uses single-accumulator tiles only: results then do not depend on the
  * tile. */
 int hfa_gemm_split_tuning(int cfg);
-/* Scheduling experiment (A/B; default 0): 1 = a one-round grid of one-workgroup-per-CU split tiles reserves the
- * whole 160 KiB of LDS, so no workgroup of another stream's kernel can share a CU it runs on; 2 = every such grid.
- * Results do not change. */
-int hfa_gemm_split_fill(int mode);
 /* x [rows, cols] f32 (row stride ldx) -> split planes y (row stride ldy, plane 1 at +sp); raises *oflow (if
  * non-NULL) for |x| >= 65504 or a non-finite x. */
 int hfa_split_f16(int rows, int cols, const float* x, long long ldx, uint16_t* y, long long ldy, long long sp,

@@ -1,7 +1,7 @@
 """Interleaved A/B of the pipelined config-2 step (bench.py's run(): task.submit + assemble, two streams) across
-scheduling / kernel variants selected through libhfa's thread-local tuning hooks, on one box:
+scheduling variants, on one box (add a variant as a setter in setters()):
 
-    python scripts/pipe_ab.py --variants base,fill1,fill2 --rounds 4 --steps 20
+    python scripts/pipe_ab.py --variants base,mask64 --rounds 4 --steps 20
 
 Prints ms per step per variant per round and the median; with --encoder-only also the encoder alone."""
 import argparse
@@ -42,8 +42,6 @@ def masked_stream(device, n_cus: int, total: int = 256):
 
 
 def setters(task):
-    from hubertfa_amd import _lib
-    L = _lib.lib()
     plain = {}
 
     def side(kind):
@@ -59,29 +57,16 @@ def setters(task):
                 task._side = plain[key]
         return f
 
-    def combo(*fs):
-        def f():
-            for g in fs:
-                g()
-        return f
     return {
-        "base": combo(lambda: L.hfa_gemm_split_fill(0), side("plain"), lambda: setattr(task, "interleave", True),
-                      lambda: setattr(task, "gate_points", ("ffn2",))),
-        "fill1": lambda: L.hfa_gemm_split_fill(1),
-        "fill2": lambda: L.hfa_gemm_split_fill(2),
-        "serialside": lambda: setattr(task, "interleave", False),
-        "gatestart": lambda: setattr(task, "gate_points", ("extractor", "ffn2")),
-        "serialsidefill1": combo(lambda: setattr(task, "interleave", False), lambda: L.hfa_gemm_split_fill(1)),
+        "base": side("plain"),
         "mask64": side(64),
         "mask32": side(32),
-        "mask64fill1": combo(side(64), lambda: L.hfa_gemm_split_fill(1)),
-        "mask64fill2": combo(side(64), lambda: L.hfa_gemm_split_fill(2)),
     }
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="base,fill1,fill2")
+    ap.add_argument("--variants", default="base,mask64")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--encoder-only", action="store_true")

@@ -84,7 +84,8 @@ def test_split_gemm_tile_choice():
     assert tile(15968, 3072, epi=1) == [" 256", " 256"]   # config 2 FFN1: 756 tiles = 2.95 rounds
     assert tile(17924, 3072, epi=1) == [" 256", " 256"]   # config 5 windows: 852 tiles (was 128 x 128)
     assert tile(17924, 2304) == [" 256", " 256"]          # 639 tiles (was 128 x 128)
-    assert tile(15968, 768) == [" 256", " 256"]           # out-projection / FFN2: one round
+    assert tile(15968, 768) == [" 192", " 256"]           # out-projection / FFN2: one round of 252 tiles (not 189)
+    assert tile(17924, 768) == [" 256", " 256"]           # config 5 windows: 192 x 256 would take a second round
     assert tile(15999, 512, Z=32, epi=1) == [" 256", " 256"]   # extractor conv1
     assert tile(499, 512, Z=32, epi=1) == [" 128", " 128"]     # extractor conv6: 128 big tiles, half a round
     assert tile(864, 192, Z=32) == [" 128", " 128"]       # UNet level 0: small grid
