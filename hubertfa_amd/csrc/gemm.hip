@@ -1480,18 +1480,23 @@ __global__ __launch_bounds__(256, 2) void gemm_split48_kernel(const GemmP p) {
 // DMA per kFLOP.  The window is chunk-major ([plane][8-channel chunk][row], 16 B per cell), so a 16x16x32 operand
 // read (16 consecutive rows of one chunk per 16 lanes) covers all 64 banks once; the K index is the flattened
 // (tap, channel) of the im2col weight rows, each lane's 8-wide chunk mapping to its own (tap, chunk) pair.
-// 8 waves x (32 rows x 48 columns) on v_mfma_f32_16x16x32_f16, split-f16 single-accumulator arithmetic.
-constexpr int kWinRows = 384;
+// 8 waves x (16 RB rows x 16 NB columns) on v_mfma_f32_16x16x32_f16, split-f16 single-accumulator arithmetic.
+// RB (row blocks of 16 per wave): 2 -> 256-row tiles; 4 -> 512-row tiles (Cg = 48, round 4): a wave then reads 8 A
+// and 6 W operands per 36 MFMAs instead of 4 and 6 per 18 -- the LDS operand reads, not the MFMAs, bounded the
+// 256-row form (~140 B of LDS reads per cycle per CU wanted against 128) -- and one tile covers a 10 s utterance's
+// 499 frames (one window load per (batch, group) instead of two overlapping ones).
+constexpr int win_rows(int RB) { return RB == 4 ? 640 : 384; }  // 128 RB + k - 1 (k <= 128), 64-row pieces
 
-template <int EPI, int NB>
+template <int EPI, int NB, int RB = 2>
 __global__ __launch_bounds__(512, 1) void posconv_split_kernel(const GemmP p) {
-    constexpr int BM = 256, BN = 16 * NB, BK = 32, NW = 8, NS = 3;   // NB = 3 (Cg 48) or 4 (Cg 64)
+    constexpr int BM = 128 * RB, BN = 16 * NB, BK = 32, NW = 8, NS = 3;   // NB = 3 (Cg 48) or 4 (Cg 64)
+    constexpr int kWinRows = win_rows(RB);
     constexpr int PW = BN * BK;                                  // halves per W plane image
     constexpr int WSTAGE = 2 * PW;
-    const int CC = p.Cg / 8;                                     // 8-channel chunks per row (<= 8)
-    __shared__ __attribute__((aligned(16))) _Float16 dsm[2 * 8 * kWinRows * 8 + NS * WSTAGE];
+    const int CC = p.Cg / 8;                                     // 8-channel chunks per row (<= 2 NB)
+    __shared__ __attribute__((aligned(16))) _Float16 dsm[2 * 2 * NB * kWinRows * 8 + NS * WSTAGE];
     _Float16* win = dsm;                                         // [2][CC][kWinRows] x 8 halves
-    _Float16* wst = dsm + 2 * 8 * kWinRows * 8;                  // NS stages of [2][BN][32]
+    _Float16* wst = dsm + 2 * 2 * NB * kWinRows * 8;             // NS stages of [2][BN][32]
 
     const int nwg = gridDim.x, orig = blockIdx.x;
     const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -1511,9 +1516,10 @@ __global__ __launch_bounds__(512, 1) void posconv_split_kernel(const GemmP p) {
 
     // input window: pieces of 64 rows of one (plane, chunk); window row r <-> input row t0 + r
     const int t0 = tm * BM - p.pad;
-    const int npieces = 2 * CC * (kWinRows / 64);
+    constexpr int GP = kWinRows / 64;                            // 64-row pieces per (plane, chunk)
+    const int npieces = 2 * CC * GP;
     for (int pc = wave; pc < npieces; pc += NW) {
-        const int plane = pc / (CC * 6), rest = pc - plane * CC * 6, c = rest / 6, g = rest - c * 6;
+        const int plane = pc / (CC * GP), rest = pc - plane * CC * GP, c = rest / GP, g = rest - c * GP;
         const int t = t0 + g * 64 + lane;
         const unsigned vo = (t >= 0 && t < p.Tin) ? (unsigned)((t * p.ldx + c * 8) * 2) : hfa::DMA_OOB;
         hfa::dma16(vo, plane ? rA2 : rA1, 0u, lds_win + ((plane * CC + c) * kWinRows + g * 64) * 16);
@@ -1532,17 +1538,17 @@ __global__ __launch_bounds__(512, 1) void posconv_split_kernel(const GemmP p) {
     if (nk > 1) issueW(1, 1);
     hfa::wait_vm_barrier<0>();                                   // window and steps 0, 1 landed
 
-    // per-lane operand addressing: output row l = 32 wave + 16 b + r16, chunk q = lane >> 4 (k 8q..8q+7 of a step)
+    // per-lane operand addressing: output row l = 16 RB wave + 16 b + r16, chunk q = lane >> 4 (k 8q..8q+7 of a step)
     const int r16 = lane & 15, q = lane >> 4;
     int tap = 0, ch = q;                                         // (tap, 8-channel chunk) of this lane's k
     while (ch >= CC) { ch -= CC; ++tap; }
     const f16x8* w8 = reinterpret_cast<const f16x8*>(wst);
     const f16x8* a8 = reinterpret_cast<const f16x8*>(win);
     const int rdW = (r16 * 4) + (q ^ swz(r16));                  // + cb * 64, + plane * PW / 8, + stage * WSTAGE / 8
-    const int lrow = 32 * wave + r16;
-    f32x4 acc[2][NB];
+    const int lrow = 16 * RB * wave + r16;
+    f32x4 acc[RB][NB];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RB; ++i)
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -1550,9 +1556,9 @@ __global__ __launch_bounds__(512, 1) void posconv_split_kernel(const GemmP p) {
     for (int s = 0; s < nk; ++s) {
         if (s + 2 < nk) issueW(stage == 0 ? 2 : stage - 1, s + 2);    // into the stage read at step s - 1
         const f16x8* st = w8 + stage * (WSTAGE / 8);
-        f16x8 a1[2], a2[2], w1[NB], w2[NB], w1s[NB];
+        f16x8 a1[RB], a2[RB], w1[NB], w2[NB], w1s[NB];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < RB; ++b) {
             const int cell = ch * kWinRows + lrow + 16 * b + tap;
             a1[b] = a8[cell];
             a2[b] = a8[CC * kWinRows + cell];
@@ -1564,7 +1570,7 @@ __global__ __launch_bounds__(512, 1) void posconv_split_kernel(const GemmP p) {
             w1s[j] = w1[j] * (_Float16)2048.0f;
         }
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < RB; ++i)
 #pragma unroll
             for (int j = 0; j < NB; ++j) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], w1s[j], acc[i][j], 0, 0, 0);
@@ -1589,10 +1595,10 @@ __global__ __launch_bounds__(512, 1) void posconv_split_kernel(const GemmP p) {
         const int col = j * 16 + r16;
         const float bv = biasb ? biasb[col] : 0.0f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < RB; ++i)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const int row = tm * BM + 32 * wave + i * 16 + 4 * q + e;
+                const int row = tm * BM + 16 * RB * wave + i * 16 + 4 * q + e;
                 const float a = acc[i][j][e] * (1.0f / 2048.0f);
                 bad |= !__builtin_isfinite(a);
                 if (row < p.M) {
@@ -1630,6 +1636,7 @@ constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
     {128, 192, 2, 2, 2, 2, true, 32, 16}, {192, 128, 2, 2, 2, 2, true, 32, 16}};
 thread_local int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 thread_local int g_win_nb = 3;   // column blocks of the window kernel the name query reports (N / 16)
+thread_local int g_win_rb = 2;   // and its row blocks per wave
 
 // Measured on the workload's shapes (scripts/split_gemm_bench.py, profiles/r01/split_gemm_cfgs.txt): the 256 x 256
 // single-accumulator tile is 7-15 % faster than 128 x 128 on the extractor convs, FFN and out-projection (even at
@@ -1640,8 +1647,10 @@ thread_local int g_win_nb = 3;   // column blocks of the window kernel the name 
 // automatic tile is a 16x16x32 (MF 16) tile; the 32x32x16 tiles stay as tuning choices.
 inline bool win_ok(const GemmP& p) {   // posconv_split_kernel: stride 1, N 48 or 64, Cg % 8, Cg <= 64, window fits
     return (p.N == 48 || p.N == 64) && p.Ch == nullptr && p.stride == 1 && p.Cg % 8 == 0 && p.Cg >= 32 &&
-           p.Cg <= 64 && p.K % p.Cg == 0 && 256 + p.K / p.Cg - 1 <= kWinRows;
+           p.Cg <= 2 * (p.N / 16) * 8 && p.K % p.Cg == 0 && 256 + p.K / p.Cg - 1 <= win_rows(2);
 }
+// 512-row tiles (RB 4) for N = 48 when the rows fill more than one 256-row tile and the 640-row window holds the taps
+inline bool win_rb4(const GemmP& p) { return p.N == 48 && p.M > 256 && 512 + p.K / p.Cg - 1 <= win_rows(4); }
 
 inline int split_cfg(const GemmP& p, int Z) {
     const bool n48 = p.N == 48 && p.Ch == nullptr && p.Cg % 8 == 0 && p.Cg >= 32;
@@ -1697,7 +1706,8 @@ inline void split_name(int cfg, int epi, bool outs, bool gt, bool f16, char* buf
         return;
     }
     if (cfg == SCFG_WIN) {
-        snprintf(buf, len, "posconv_split_kernel<%d, %d>", epi, g_win_nb);
+        if (g_win_rb == 4) snprintf(buf, len, "posconv_split_kernel<%d, %d, 4>", epi, g_win_nb);
+        else snprintf(buf, len, "posconv_split_kernel<%d, %d, 2>", epi, g_win_nb);
         return;
     }
     if (gt) cfg = gt_cfg(cfg);
@@ -2015,8 +2025,13 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
         return HFA_EINVAL;
     }
     if (cfg == SCFG_WIN) {                     // grouped positional conv: LDS-resident input window
-        dim3 grid((unsigned)((M + 255) / 256), 1, Z);
-        if (N == 48 && epilogue == EPI_GELU)
+        const bool rb4 = win_rb4(p);
+        dim3 grid((unsigned)((M + (rb4 ? 511 : 255)) / (rb4 ? 512 : 256)), 1, Z);
+        if (rb4 && epilogue == EPI_GELU)
+            hipLaunchKernelGGL((posconv_split_kernel<EPI_GELU, 3, 4>), grid, dim3(512), 0, stream, p);
+        else if (rb4)
+            hipLaunchKernelGGL((posconv_split_kernel<EPI_NONE, 3, 4>), grid, dim3(512), 0, stream, p);
+        else if (N == 48 && epilogue == EPI_GELU)
             hipLaunchKernelGGL((posconv_split_kernel<EPI_GELU, 3>), grid, dim3(512), 0, stream, p);
         else if (N == 48)
             hipLaunchKernelGGL((posconv_split_kernel<EPI_NONE, 3>), grid, dim3(512), 0, stream, p);
@@ -2042,6 +2057,7 @@ const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split
     GemmP p = make_params(M, N, K, 1, nullptr, 0, 0, 0, 1, 0, Cg, 1, nullptr, 0, 0);
     p.Ch = out_split ? reinterpret_cast<_Float16*>(g_name) : nullptr;    // only its null-ness is read
     g_win_nb = N / 16;
+    g_win_rb = win_rb4(p) ? 4 : 2;
     const bool f16 = (epilogue & HFA_GEMM_F16) != 0 && Cg % 32 == 0;
     int cfg = split_cfg(p, Z);
     if (f16 && cfg != SCFG_WIN && cfg != SCFG_N48) cfg = f16_cfg(cfg);

@@ -90,4 +90,6 @@ def test_split_gemm_tile_choice():
     assert tile(499, 512, Z=32, epi=1) == [" 128", " 128"]     # extractor conv6: 128 big tiles, half a round
     assert tile(864, 192, Z=32) == [" 128", " 128"]       # UNet level 0: small grid
     # the grouped positional conv (Cg = 48, k = 128): the LDS-window kernel, named as launched (the K argument)
-    assert ops._split_name(499, 48, 6144, 512, False, 1, 48) == "posconv_split_kernel<1, 3>"
+    assert ops._split_name(499, 48, 6144, 512, False, 1, 48) == "posconv_split_kernel<1, 3, 4>"   # 512-row tiles
+    assert ops._split_name(200, 48, 6144, 512, False, 1, 48) == "posconv_split_kernel<1, 3, 2>"
+    assert ops._split_name(499, 64, 8192, 512, False, 1, 64) == "posconv_split_kernel<1, 4, 2>"   # Hubert-large

@@ -127,6 +127,30 @@ def test_split_grouped_posconv_general_taps(H, G, k, L, cfg):
     _close(out, ref, 2e-5, 2e-5)
 
 
+def test_posconv_window_tiles_bit_identical():
+    """The window positional conv's 512-row tiles (M > 256, Cg = 48) and 256-row tiles run every output row through
+    the same MFMA chain: rows whose 128-tap window lies inside the first 256 frames come out bit-identical from a
+    499-frame call (512-row tile) and a 256-frame call (256-row tile)."""
+    from hubertfa_amd import ops
+    B, H, G, k = 2, 768, 16, 128
+    Cg = H // G
+    d = torch.device("cuda")
+    x = _r(B, 499, H, seed=21).to(d)
+    w = ops.split((_r(H, Cg, k, seed=22, scale=(Cg * k) ** -0.5)).permute(0, 2, 1).reshape(H, k * Cg).contiguous().to(d))
+    b = (_r(H, seed=23) * 0.1).to(d)
+
+    def run(L):
+        xl = x[:, :L].contiguous()
+        out = torch.empty(B, L, H, device=d)
+        ops.conv_gemm_split(ops.split(xl), w, C=out, M=L, N=Cg, K=k * Cg, Zb=B, G=G, sAb=L * H, sAg=Cg, ldx=H,
+                            stride=1, pad=k // 2, Cg=Cg, Tin=L, sWg=Cg * k * Cg, bias=b, sBg=Cg, R=xl, sRb=L * H,
+                            sRg=Cg, ldr=H, sCb=L * H, sCg=Cg, ldc=H, epilogue=ops.EPI_GELU)
+        return out
+    assert ops._split_name(499, Cg, k * Cg, B * G, False, 1, Cg).endswith(", 4>")
+    assert ops._split_name(256, Cg, k * Cg, B * G, False, 1, Cg).endswith(", 2>")
+    assert torch.equal(run(499)[:, :192], run(256)[:, :192])
+
+
 @pytest.mark.parametrize("outs", [False, True])
 @pytest.mark.parametrize("cfgs", [(0, 17, 18, 19, 20, 23, 24), (7, 9, 10, 8, 11, 12, 13, 14)])
 def test_split_single_acc_tiles_bit_identical(outs, cfgs):
