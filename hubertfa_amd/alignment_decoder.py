@@ -126,7 +126,7 @@ class AlignmentDecoder:
             h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
             h.copy_(t, non_blocking=True)
             host[k] = h
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(blocking=True)    # the host sleeps in assemble's wait instead of spinning a core
         ev.record()
         out = {"T": dev_out["T"], "host": host, "event": ev}
         if "redo" in dev_out:

@@ -6,6 +6,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/final
 mkdir -p $O
+(nproc; lscpu) > $O/host_cpu.txt 2>&1 || true
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputests.log 2>&1 || { echo "GPU TESTS FAIL"; tail -40 $O/gputests.log; exit 1; }
   tail -2 $O/gputests.log
@@ -28,6 +29,11 @@ python scripts/shape_table.py --trace $O/trace --log $O/trace/launch_log.json --
 python scripts/pmc_kernels.py --mfma $O/pmc_mfma --wait $O/pmc_wait --out $O/pmc_r04.json > $O/pmc_kernels.txt 2>&1 || { echo "PMC KERNELS FAIL"; cat $O/pmc_kernels.txt; }
 rm -rf $O/pmc_mfma/*.csv.bak
 head -12 $O/shape_table.txt
+rm -rf $O/serial
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/serial -o run -- python3 scripts/shape_trace.py --mode serial --steps 6 --warmup 3 --log $O/serial/launch_log.json > $O/serial.log 2>&1 || { echo "SERIAL TRACE FAIL"; tail -20 $O/serial.log; exit 1; }
+python scripts/shape_table.py --trace $O/serial --log $O/serial/launch_log.json --csv $O/shape_serial.csv > $O/shape_serial.txt 2>&1 || { echo "SERIAL TABLE FAIL"; cat $O/shape_serial.txt; }
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --traffic-file $O/traffic_r04.json --pmc-file $O/pmc_r04.json > $O/bench.json 2> $O/bench.err || { echo "BENCH FAIL"; tail -20 $O/bench.err; exit 1; }
 tail -c 1500 $O/bench.json
+timeout -k 10 200 python scripts/attn_len_sweep.py > $O/attn_len.txt 2>&1 || { echo "ATTN SWEEP FAIL"; tail -5 $O/attn_len.txt; exit 1; }
+cat $O/attn_len.txt
 echo ALLOK
