@@ -1685,7 +1685,14 @@ inline int split_cfg(const GemmP& p, int Z) {
     // microbenchmark had not shown it).
     double best = fill(blocks256);
     int cfg = SCFG_256x256_M16;
-    if (blocks256 <= 256) return (blocks192m <= 256 && blocks192m > blocks256) ? SCFG_192x256_M16 : cfg;
+    if (blocks256 <= 256) {
+        // Short K (the out-projection and the feature projection, K <= 1024): two 128 x 192 workgroups per CU when
+        // they still make one round of the 512 slots, so one tile's epilogue runs beside the other's main loop
+        // (out-projection 69 -> 68 us in isolation, profiles/r04/layer_tiles.txt; FFN2's K = 3072 stays on 192 x 256)
+        const long long blocks128x192 = (long long)((p.M + 127) / 128) * ((p.N + 191) / 192) * Z;
+        if (p.K <= 1024 && blocks128x192 <= 512 && blocks128x192 > 2 * blocks256) return SCFG_128x192_M16;
+        return (blocks192m <= 256 && blocks192m > blocks256) ? SCFG_192x256_M16 : cfg;
+    }
     if (0.92 * fill(blocks192m) > best + 0.05) {
         best = 0.92 * fill(blocks192m);
         cfg = SCFG_192x256_M16;

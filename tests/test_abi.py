@@ -79,12 +79,13 @@ def test_split_gemm_tile_choice():
     192-wide tile fills the last round of CUs much better (profiles/r03/split_tiles_c5.txt)."""
     pytest.importorskip("torch")
     from hubertfa_amd import ops
-    tile = lambda M, N, Z=1, epi=0: ops._split_name(M, N, 768, Z, True, epi, 768).split("<")[1].split(",")[1:3]  # noqa: E731
+    tile = lambda M, N, Z=1, epi=0, K=768: ops._split_name(M, N, K, Z, True, epi, 768).split("<")[1].split(",")[1:3]  # noqa: E731
     assert tile(15968, 2304) == [" 192", " 256"]          # config 2 QKV: 567 big tiles = 2.2 rounds
     assert tile(15968, 3072, epi=1) == [" 256", " 256"]   # config 2 FFN1: 756 tiles = 2.95 rounds
     assert tile(17924, 3072, epi=1) == [" 256", " 256"]   # config 5 windows: 852 tiles (was 128 x 128)
     assert tile(17924, 2304) == [" 256", " 256"]          # 639 tiles (was 128 x 128)
-    assert tile(15968, 768) == [" 192", " 256"]           # out-projection / FFN2: one round of 252 tiles (not 189)
+    assert tile(15968, 768, K=3072) == [" 192", " 256"]   # FFN2: one round of 252 tiles (not 189)
+    assert tile(15968, 768) == [" 128", " 192"]           # out-projection (K = 768): 500 tiles, two per CU
     assert tile(17924, 768) == [" 256", " 256"]           # config 5 windows: 192 x 256 would take a second round
     assert tile(15999, 512, Z=32, epi=1) == [" 256", " 256"]   # extractor conv1
     assert tile(499, 512, Z=32, epi=1) == [" 128", " 128"]     # extractor conv6: 128 big tiles, half a round

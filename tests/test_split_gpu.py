@@ -42,7 +42,7 @@ def test_split_planes_and_flag():
     flag.zero_()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13, 14, 15, 17, 18, 19, 20])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13, 14, 15, 17, 18, 19, 20, 23, 24, 25, 26])
 @pytest.mark.parametrize("M,N,K,epi,res,outs", [(300, 200, 128, 0, False, False), (1000, 768, 768, 1, False, False),
                                                 (257, 72, 192, 0, True, False), (4096, 3072, 768, 1, False, True),
                                                 (130, 2304, 768, 0, False, True), (64, 768, 3072, 0, True, False)])
@@ -152,10 +152,10 @@ def test_posconv_window_tiles_bit_identical():
 
 
 @pytest.mark.parametrize("outs", [False, True])
-@pytest.mark.parametrize("cfgs", [(0, 17, 18, 19, 20, 23, 24), (7, 9, 10, 8, 11, 12, 13, 14)])
+@pytest.mark.parametrize("cfgs", [(0, 17, 18, 19, 20, 23, 24, 25, 26), (7, 9, 10, 8, 11, 12, 13, 14)])
 def test_split_single_acc_tiles_bit_identical(outs, cfgs):
-    """Every automatic tile (17 = 256x256, 18 = 128x128, 19 = 128x64, 20 = 256x64, 23 = 256x192, 24 = 192x256:
-    single-accumulator 16x16x32 tiles) gives the same bits, so a row's result does not depend on the batch (and so the grid) it runs in; the
+    """Every automatic tile (17 = 256x256, 18 = 128x128, 19 = 128x64, 20 = 256x64, 23 = 256x192, 24 = 192x256,
+    25 = 128x192, 26 = 192x128: single-accumulator 16x16x32 tiles) gives the same bits, so a row's result does not depend on the batch (and so the grid) it runs in; the
     32x32x16 tiles (tuning only) agree among themselves the same way."""
     from hubertfa_amd import ops, _lib
     d = torch.device("cuda")
@@ -174,7 +174,7 @@ def test_split_single_acc_tiles_bit_identical(outs, cfgs):
 
 
 @pytest.mark.parametrize("cfg,outs", [(7, False), (8, False), (9, True), (10, False), (17, False), (18, True),
-                                      (19, False), (20, True), (23, True), (24, False)])
+                                      (19, False), (20, True), (23, True), (24, False), (25, True), (26, False)])
 def test_split_single_acc_weight_range_flag(cfg, outs):
     """Single-accumulator tiles form 2^11 * hi(w) in f16: a weight with |w| >= 32 overflows there, and the
     non-finite result raises the split flag (the caller re-runs on the f32 GEMM) instead of passing silently."""
@@ -451,6 +451,37 @@ def test_attention_split_waves_bit_identical(L):
             finally:
                 _lib.call("hfa_attention_split_tuning", 0)
         assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("B,L,nw", [(32, 499, 0), (16, 700, 8), (24, 300, 4)])
+def test_attention_split_persistent_bit_identical(B, L, nw):
+    """The persistent grid (a workgroup walks items wgid, wgid + G, ...: seams between items of different rows and
+    heads, padding items of a variable-length batch zeroed on the way) gives the same bits as one item per
+    workgroup, and rows agree with f64."""
+    from hubertfa_amd import ops, _lib
+    from hubertfa_amd.hubert import dev_lengths
+    H, D = 12, 64
+    d = torch.device("cuda")
+    qkv = _r(B, L, 3 * H * D, seed=17, scale=2.0)
+    qs = ops.split(qkv.to(d))
+    lens = [L - (37 * b) % (L - 1) for b in range(B)]
+    for kl in (None, dev_lengths(lens, d)):
+        outs = []
+        for mode in (nw, nw + 100):
+            _lib.call("hfa_attention_split_tuning", mode)
+            try:
+                o = torch.full((2, B, L, H * D), float("nan"), dtype=torch.float16, device=d)
+                ops.attention_split(qs, o, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5, key_len=kl)
+                outs.append(o)
+            finally:
+                _lib.call("hfa_attention_split_tuning", 0)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1])
+    got = (outs[0][0].float() + outs[0][1].float() / 2048.0).cpu()
+    for b in (0, B // 2, B - 1):
+        ref = _attn_ref(qkv[b:b + 1, :lens[b]], 1, lens[b], H, D)
+        _close(got[b:b + 1, :lens[b]], ref, 1e-4, 2e-5)
+        assert bool((got[b, lens[b]:] == 0).all())
 
 
 def test_attention_split_large_scores():
