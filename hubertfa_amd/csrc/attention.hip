@@ -241,6 +241,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int SKB = 64;              // keys per tile
 constexpr int SNS = 2;               // LDS stages
 constexpr int SPLANE = SKB * DH;     // halves per plane image (8 KiB)
+constexpr int SSTAGE = 4 * SPLANE;   // K1, K2, V1, V2
 constexpr float kLo = 1.0f / 2048.0f;
 
 struct AttnSP {
@@ -252,27 +253,6 @@ struct AttnSP {
     _Float16* o; long long o_sp, o_bs; int o_ld;
     const int32_t* key_len;
 };
-
-// LDS-DMA of 64 x 16 B (hfa::dma16) with the buffer descriptor assembled from wave-uniform words at the issue
-// (base address, no stride, num_records = bytes, the raw-buffer flags of hfa::make_rsrc): in the persistent item loop
-// the compiler took a descriptor held across items for a divergent value and could not give it the SGPRs the
-// instruction needs
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void dma16u(unsigned voff, const void* base, long long bytes, unsigned lds) {
-    const unsigned long long a = (unsigned long long)(uintptr_t)base;
-    const u32x4 rs{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a),
-                   (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32) & 0xffffu),
-                   (unsigned)__builtin_amdgcn_readfirstlane((unsigned)bytes), 0x00020000u};
-    unsigned keep;   // M0 is compiler-reserved: set and restore it inside the statement that uses it
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds) : "memory");
-}
-
-__device__ __forceinline__ long long uniform64(long long x) {
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)x), hi = __builtin_amdgcn_readfirstlane((unsigned)(x >> 32));
-    return (long long)(((unsigned long long)hi << 32) | lo);
-}
 
 __device__ __forceinline__ f16x4 lds_tr(const _Float16* base, int byte_off) {
     const auto* ptr = reinterpret_cast<const __attribute__((address_space(3))) s16x4*>(
@@ -293,82 +273,56 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
     // (K(t+1) must have landed when iteration t starts, V(t) only by its PV), so the LDS stays 64 KiB (2 per CU).
     // The output uses one accumulator at scale 2^11: P is taken relative to m_run + kSlack (p <= 1, so 2^11 p1 is
     // exact in f16) and O += V1 (2^11 P1) + V1 P2 + V2 P1.
-    // SNW waves of 32 queries share each K/V tile (8 waves halve the LDS-DMA stream per query at L ~ 500).
-    // Persistent (round 4): a workgroup walks items (batch, head, query block) wgid, wgid + G, ... of a grid of G
-    // workgroups; at each seam the next item's Q loads and first K/V tiles are issued before the finished item's
-    // epilogue (through a slab in the idle V stage), so the epilogue runs under their latency and no workgroup is
-    // re-launched.  G = the item count is the one-item-per-workgroup kernel.
+    // SNW waves of 32 queries share each K/V tile (8 waves halve the LDS-DMA stream per query at L ~ 500)
     constexpr int KST = 2 * SPLANE;                      // halves per K (or V) stage, both planes
     constexpr int NW = SNW, PPW = 8 / SNW;               // 1-KiB DMA pieces (8 keys) per plane per wave
     static_assert(SNW == 4 || SNW == 8, "4 or 8 waves");
-    // K0, K1, V0, V1, and 512 B for the epilogue slab (4 waves: 4 x 32 x 33 f32 from V1 on, under the next item's
-    // loads; 8 waves: 8 x 32 x 33 f32 from K0 on, before them)
-    constexpr bool kOverlap = SNW == 4;
-    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * KST + 256];
-    static_assert(!kOverlap || NW * QW * 33 * 4 <= KST * 2 + 512, "epilogue slab");
+    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * KST];   // K0, K1, V0, V1
 
     const int nwg = gridDim.x, orig = blockIdx.x;
     const int xcd = orig & 7, xq = nwg >> 3, xr = nwg & 7;
     const int wgid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (orig >> 3);
     const int nqb = (p.L + QW * NW - 1) / (QW * NW);
-    const int nitems = p.B * p.H * nqb;
+    const int bh = wgid / nqb, qb = wgid - bh * nqb;
+    const int b = bh / p.H, hd = bh - b * p.H;
+    const int L = p.key_len ? p.key_len[b] : p.L;
+    if (qb * (QW * NW) >= L) {                           // whole workgroup is padding: zero its O rows, exit
+        for (int i = threadIdx.x; i < QW * NW * (DH / 4); i += NW * 64) {
+            const int qq = qb * (QW * NW) + i / (DH / 4), c4 = (i % (DH / 4)) * 4;
+            if (qq < p.L) {
+                _Float16* dst = p.o + b * p.o_bs + (long long)qq * p.o_ld + hd * DH + c4;
+                const f16x4 z{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+                *reinterpret_cast<f16x4*>(dst) = z;
+                *reinterpret_cast<f16x4*>(dst + p.o_sp) = z;
+            }
+        }
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r32 = lane & 31, half = lane >> 5;
+    const int q0 = qb * (QW * NW) + wave * QW;
+    const int qi = q0 + r32;
 
-    // the next item >= it (stride nwg) with rows to compute; items wholly past their row's length only zero their
-    // O rows (padding of a variable-length batch)
-    auto next_item = [&](int it) -> int {
-        for (; it < nitems; it += nwg) {
-            const int bh = it / nqb, qb = it - bh * nqb;
-            const int ib = bh / p.H, ih = bh - ib * p.H;
-            const int iL = __builtin_amdgcn_readfirstlane(p.key_len ? p.key_len[ib] : p.L);
-            if (qb * (QW * NW) < iL) return it;
-            for (int i = threadIdx.x; i < QW * NW * (DH / 4); i += NW * 64) {
-                const int qq = qb * (QW * NW) + i / (DH / 4), c4 = (i % (DH / 4)) * 4;
-                if (qq < p.L) {
-                    _Float16* dst = p.o + ib * p.o_bs + (long long)qq * p.o_ld + ih * DH + c4;
-                    const f16x4 z{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
-                    *reinterpret_cast<f16x4*>(dst) = z;
-                    *reinterpret_cast<f16x4*>(dst + p.o_sp) = z;
-                }
-            }
-        }
-        return nitems;
-    };
-    int it = __builtin_amdgcn_readfirstlane(next_item(wgid));
-    if (it >= nitems) return;
+    const _Float16* Q = p.q + b * p.q_bs + hd * DH;
+    const _Float16* Kp = p.k + b * p.k_bs + hd * DH;
+    const _Float16* Vp = p.v + b * p.v_bs + hd * DH;
+    const long long kbytes = ((long long)(L - 1) * p.k_ld + DH) * 2, vbytes = ((long long)(L - 1) * p.v_ld + DH) * 2;
+    const __amdgpu_buffer_rsrc_t rK1 = hfa::make_rsrc(Kp, kbytes), rK2 = hfa::make_rsrc(Kp + p.k_sp, kbytes);
+    const __amdgpu_buffer_rsrc_t rV1 = hfa::make_rsrc(Vp, vbytes), rV2 = hfa::make_rsrc(Vp + p.v_sp, vbytes);
 
-    // per-item coordinates (wave-uniform) and the K/V buffer descriptors
-    int b = 0, hd = 0, L = 0, q0 = 0, nkb = 0;
-    long long koff = 0, voff = 0, kbytes = 0, vbytes = 0;   // K/V element offsets and spans of the item's (b, head)
     f16x8 q1[DH / 16], q2[DH / 16];
-    auto setup = [&](int item) {                          // (readfirstlane: keep the descriptors in SGPRs)
-        item = __builtin_amdgcn_readfirstlane(item);
-        const int bh = item / nqb, qb = item - bh * nqb;
-        b = bh / p.H;
-        hd = bh - b * p.H;
-        L = __builtin_amdgcn_readfirstlane(p.key_len ? p.key_len[b] : p.L);
-        q0 = qb * (QW * NW) + wave * QW;
-        nkb = (L + SKB - 1) / SKB;
-        koff = uniform64(b * p.k_bs + hd * DH);
-        voff = uniform64(b * p.v_bs + hd * DH);
-        kbytes = uniform64(((long long)(L - 1) * p.k_ld + DH) * 2);
-        vbytes = uniform64(((long long)(L - 1) * p.v_ld + DH) * 2);
-        const _Float16* Q = p.q + b * p.q_bs + hd * DH;
-        const int qi = q0 + r32;
 #pragma unroll
-        for (int kb = 0; kb < DH / 16; ++kb) {
-            if (qi < L) {
-                const _Float16* src = Q + (long long)qi * p.q_ld + kb * 16 + half * 8;
-                q1[kb] = *reinterpret_cast<const f16x8*>(src);
-                q2[kb] = *reinterpret_cast<const f16x8*>(src + p.q_sp);
-            } else {
+    for (int kb = 0; kb < DH / 16; ++kb) {
+        if (qi < L) {
+            const _Float16* src = Q + (long long)qi * p.q_ld + kb * 16 + half * 8;
+            q1[kb] = *reinterpret_cast<const f16x8*>(src);
+            q2[kb] = *reinterpret_cast<const f16x8*>(src + p.q_sp);
+        } else {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) q1[kb][j] = q2[kb][j] = (_Float16)0.0f;
-            }
+            for (int j = 0; j < 8; ++j) q1[kb][j] = q2[kb][j] = (_Float16)0.0f;
         }
-    };
+    }
 
     int rowd[PPW], kch[PPW], vch[PPW];
 #pragma unroll
@@ -384,8 +338,8 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
         for (int d = 0; d < PPW; ++d) {
             const int key = key0 + rowd[d];
             const unsigned ko = key < L ? (unsigned)((key * p.k_ld + kch[d] * 8) * 2) : hfa::DMA_OOB;
-            dma16u(ko, p.k + koff, kbytes, base + d * 1024);
-            dma16u(ko, p.k + koff + p.k_sp, kbytes, base + SPLANE * 2 + d * 1024);
+            hfa::dma16(ko, rK1, 0u, base + d * 1024);
+            hfa::dma16(ko, rK2, 0u, base + SPLANE * 2 + d * 1024);
         }
     };
     auto issueV = [&](int stage, int key0) {
@@ -394,14 +348,9 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
         for (int d = 0; d < PPW; ++d) {
             const int key = key0 + rowd[d];
             const unsigned vo = key < L ? (unsigned)((key * p.v_ld + vch[d] * 8) * 2) : hfa::DMA_OOB;
-            dma16u(vo, p.v + voff, vbytes, base + d * 1024);
-            dma16u(vo, p.v + voff + p.v_sp, vbytes, base + SPLANE * 2 + d * 1024);
+            hfa::dma16(vo, rV1, 0u, base + d * 1024);
+            hfa::dma16(vo, rV2, 0u, base + SPLANE * 2 + d * 1024);
         }
-    };
-    auto prologue = [&]() {                                // the item's Q, K(0), V(0), K(1) in flight
-        issueK(0, 0);
-        issueV(0, 0);
-        if (nkb > 1) issueK(1, SKB);
     };
 
     int kofs[DH / 16];
@@ -417,11 +366,16 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
 
     const float qscale = p.scale * 1.44269504088896340736f;
     // One score accumulator: k1 q1 + k1 (2^-11 q2) + k2 (2^-11 q1), the two small products on Q planes pre-scaled
-    // once per item (2^-11 q2 is the exact residual q - q1; an f16 subnormal below 2^-14, i.e. an absolute error
+    // once per wave (2^-11 q2 is the exact residual q - q1; an f16 subnormal below 2^-14, i.e. an absolute error
     // <= 2^-25 |k| per product, under the f32 score's own rounding) -- no second accumulator, no combine pass.
     // Against the two-accumulator form (main + correction, combined by one FMA per score): 0.092 -> 0.087 ms per
     // layer (base), 0.118 -> 0.112 (large), 215 -> 204 VGPRs (profiles/r02/attn_single_acc_ab.txt).
     f16x8 q1s[DH / 16], q2s[DH / 16];
+#pragma unroll
+    for (int kb = 0; kb < DH / 16; ++kb) {
+        q1s[kb] = q1[kb] * (_Float16)kLo;
+        q2s[kb] = q2[kb] * (_Float16)kLo;
+    }
     auto scores = [&](const _Float16* sK, f32x16 (&sM)[2]) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
@@ -438,8 +392,18 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
         }
     };
     f32x16 o[2];
-    float m_run, l_run;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[0][e] = o[1][e] = 0.f;
+    float m_run = -__builtin_inff(), l_run = 0.0f;
+
+    const int nkb = (L + SKB - 1) / SKB;
+    issueK(0, 0);
+    issueV(0, 0);
+    if (nkb > 1) issueK(1, SKB);
+    hfa::wait_vm_barrier<0>();
     f32x16 sA[2], sB[2];
+    scores(smem, sA);
+    __syncthreads();                                       // every wave's K(0) reads done before K(2) lands there
     const float one = 1.0f;
     // tile t: s holds its scores, the next tile's go to nM (the caller swaps the two sets every tile)
     auto step = [&](int t, f32x16 (&s)[2], f32x16 (&nM)[2]) {
@@ -495,9 +459,9 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
                 unsigned w1[4], w2[4];
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
-                    const float x0 = s[kt][8 * ks + 2 * jj], x1 = s[kt][8 * ks + 2 * jj + 1];
-                    w1[jj] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x0, x1}, f16x2));
-                    w2[jj] = hfa::split_lo_pair(w1[jj], x0, x1, one);
+                    const float q0 = s[kt][8 * ks + 2 * jj], q1 = s[kt][8 * ks + 2 * jj + 1];
+                    w1[jj] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){q0, q1}, f16x2));
+                    w2[jj] = hfa::split_lo_pair(w1[jj], q0, q1, one);
                 }
                 p1s = __builtin_bit_cast(f16x8, make_uint4(w1[0], w1[1], w1[2], w1[3]));
                 p2 = __builtin_bit_cast(f16x8, make_uint4(w2[0], w2[1], w2[2], w2[3]));
@@ -520,82 +484,42 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
             hfa::wait_vm_barrier<0>();                     // K(t+2), V(t+1) landed; K(t+1), V(t) reads done
         }
     };
-    // O^T (the finished item's) normalised and written back as split planes through a per-wave 32 x 33 f32 slab in
-    // V stage 1 (which no DMA targets at a seam) and the 512 B past it.  Every lane-dependent address is derived from
-    // a lane id read inside (an opaque v_mbcnt): loop-invariant, the compiler would otherwise hoist ~50 of them out of
-    // the item loop and hold them in VGPRs through every tile.
-    auto epilogue = [&](int eb, int ehd, int eq0, int eL, float inv) {
-        int ln;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-        const int er = ln & 31, eh = ln >> 5;
-        float* slab = reinterpret_cast<float*>(smem + (kOverlap ? 3 * KST : 0)) + wave * (QW * 33);
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) slab[er * 33 + 4 * eh + (e & 3) + 8 * (e >> 2)] = o[db][e] * inv;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = (ln >> 3) + 8 * i, c4 = (ln & 7) * 4;
-                const int qq = eq0 + row;
-                if (qq < p.L) {                 // rows past this row's length: zeros (padding of a varlen batch)
-                    f16x4 h1, h2;
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const float x = qq < eL ? slab[row * 33 + c4 + t] : 0.0f;
-                        h1[t] = (_Float16)x;
-                        h2[t] = (_Float16)((x - (float)h1[t]) * 2048.0f);
-                    }
-                    _Float16* dst = p.o + eb * p.o_bs + (long long)qq * p.o_ld + ehd * DH + db * 32 + c4;
-                    *reinterpret_cast<f16x4*>(dst) = h1;
-                    *reinterpret_cast<f16x4*>(dst + p.o_sp) = h2;
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-    };
+    for (int t = 0; t < nkb; t += 2) {
+        step(t, sA, sB);
+        if (t + 1 < nkb) step(t + 1, sB, sA);
+    }
 
-    setup(it);
-    prologue();
-    for (;;) {
-        hfa::wait_vm_barrier<0>();                         // Q, K(0), V(0), K(1) landed (and the last epilogue's stores)
+    __syncthreads();
+    const float inv = 1.0f / l_run;                        // o and l both carry the 2^11 scale
+    float* slab = reinterpret_cast<float*>(smem) + wave * (QW * 33);
 #pragma unroll
-        for (int kb = 0; kb < DH / 16; ++kb) {
-            q1s[kb] = q1[kb] * (_Float16)kLo;
-            q2s[kb] = q2[kb] * (_Float16)kLo;
-        }
+    for (int db = 0; db < 2; ++db) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) o[0][e] = o[1][e] = 0.f;
-        m_run = -__builtin_inff();
-        l_run = 0.0f;
-        scores(smem, sA);
-        __syncthreads();                                   // every wave's K(0) reads done before K(2) lands there
-        for (int t = 0; t < nkb; t += 2) {
-            step(t, sA, sB);
-            if (t + 1 < nkb) step(t + 1, sB, sA);
+        for (int e = 0; e < 16; ++e) {
+            const int d = (e & 3) + 8 * (e >> 2) + 4 * half;
+            slab[r32 * 33 + d] = o[db][e] * inv;
         }
-        // seam: the finished item's coordinates, then the next item's loads in flight under its epilogue
-        const int eb = b, ehd = hd, eq0 = q0, eL = L;
-        const float inv = 1.0f / l_run;                    // o and l both carry the 2^11 scale
-        const int nit = __builtin_amdgcn_readfirstlane(next_item(it + nwg));
-        __syncthreads();                                   // every wave's PV reads done: all four stages free
-        if (kOverlap) {
-            if (nit < nitems) {
-                setup(nit);
-                prologue();
-            }
-            epilogue(eb, ehd, eq0, eL, inv);
-        } else {
-            epilogue(eb, ehd, eq0, eL, inv);
-            if (nit < nitems) {
-                __syncthreads();                           // every wave's slab reads done before the DMA lands
-                setup(nit);
-                prologue();
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int idx = lane + i * 64;
+            const int row = idx >> 3, c4 = (idx & 7) * 4;
+            const int qq = q0 + row;
+            if (qq < p.L) {                     // rows past this row's length: zeros (padding of a varlen batch)
+                f16x4 h1, h2;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float x = qq < L ? slab[row * 33 + c4 + t] : 0.0f;
+                    h1[t] = (_Float16)x;
+                    h2[t] = (_Float16)((x - (float)h1[t]) * 2048.0f);
+                }
+                _Float16* dst = p.o + b * p.o_bs + (long long)qq * p.o_ld + hd * DH + db * 32 + c4;
+                *reinterpret_cast<f16x4*>(dst) = h1;
+                *reinterpret_cast<f16x4*>(dst + p.o_sp) = h2;
             }
         }
-        if (nit >= nitems) break;
-        it = nit;
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -603,26 +527,11 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
 
 namespace {
 thread_local int g_attn_waves = 0;   // hfa_attention_split_tuning override (0: automatic)
-thread_local bool g_attn_item_grid = false;   // hfa_attention_split_tuning(+100): one item per workgroup
 // Waves (x 32 queries) per workgroup of the split attention: 8 where that still leaves >= 2 workgroups per
 // (batch, head) row of queries, else 4.
 inline int split_attn_waves(int L) {
     if (g_attn_waves == 4 || g_attn_waves == 8) return g_attn_waves;
     return L >= 2 * 8 * QW ? 8 : 4;
-}
-// The persistent grid: as many workgroups as the chip holds at once (2 per CU at 4 waves, 1 at 8: 64 KiB of LDS and
-// ~210 VGPRs per wave), never more than the items
-inline long long split_attn_grid(long long items, int nw) {
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return items;
-    if (cus[dev] == 0) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return items;
-        cus[dev] = n;
-    }
-    const long long cap = (long long)cus[dev] * (nw == 4 ? 2 : 1);
-    return g_attn_item_grid || items < cap ? items : cap;
 }
 }  // namespace
 
@@ -690,24 +599,20 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
         hfa::set_error("hfa_attention_split: grid too large");
         return HFA_EINVAL;
     }
-    const unsigned grid = (unsigned)split_attn_grid(nblk, nw);
     if (nw == 8)
-        hipLaunchKernelGGL((attn_fwd_split_kernel<8>), dim3(grid), dim3(8 * 64), 0, stream, p);
+        hipLaunchKernelGGL((attn_fwd_split_kernel<8>), dim3((unsigned)nblk), dim3(8 * 64), 0, stream, p);
     else
-        hipLaunchKernelGGL((attn_fwd_split_kernel<4>), dim3(grid), dim3(4 * 64), 0, stream, p);
+        hipLaunchKernelGGL((attn_fwd_split_kernel<4>), dim3((unsigned)nblk), dim3(4 * 64), 0, stream, p);
     return hfa::check_launch("hfa_attention_split");
 }
 
-// Waves per workgroup of hfa_attention_split: 4 or 8, 0 = automatic; + 100: one item (query block) per workgroup
-// instead of the persistent grid (benchmarks and the parity tests: the results are the same bits).
+// Waves per workgroup of hfa_attention_split: 4 or 8, 0 = automatic (benchmarks and the 4/8 parity test).
 int hfa_attention_split_tuning(int waves) {
-    const int w = waves >= 100 ? waves - 100 : waves;
-    if (w != 0 && w != 4 && w != 8) {
-        hfa::set_error("hfa_attention_split_tuning: waves must be 0, 4 or 8 (+100 for one item per workgroup)");
+    if (waves != 0 && waves != 4 && waves != 8) {
+        hfa::set_error("hfa_attention_split_tuning: waves must be 0, 4 or 8");
         return HFA_EINVAL;
     }
-    g_attn_waves = w;
-    g_attn_item_grid = waves >= 100;
+    g_attn_waves = waves;
     return HFA_OK;
 }
 

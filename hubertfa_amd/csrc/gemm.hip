@@ -1688,7 +1688,8 @@ inline int split_cfg(const GemmP& p, int Z) {
     if (blocks256 <= 256) {
         // Short K (the out-projection and the feature projection, K <= 1024): two 128 x 192 workgroups per CU when
         // they still make one round of the 512 slots, so one tile's epilogue runs beside the other's main loop
-        // (out-projection 69 -> 68 us in isolation, profiles/r04/layer_tiles.txt; FFN2's K = 3072 stays on 192 x 256)
+        // (out-projection 70-72 -> 69-70 us, three interleaved pairs, profiles/r04/attn_persistent_ab.txt; FFN2's
+        // K = 3072 stays on 192 x 256: 208 vs 219 us, profiles/r04/layer_tiles.txt)
         const long long blocks128x192 = (long long)((p.M + 127) / 128) * ((p.N + 191) / 192) * Z;
         if (p.K <= 1024 && blocks128x192 <= 512 && blocks128x192 > 2 * blocks256) return SCFG_128x192_M16;
         return (blocks192m <= 256 && blocks192m > blocks256) ? SCFG_192x256_M16 : cfg;

@@ -1,8 +1,8 @@
 """Split attention at equal work, growing row length (GPU): B x L^2 held at config 2's 32 x 499^2, 12 heads of 64,
 so a longer row means fewer, longer query blocks per (batch, head).  What the L = 499 point loses against the long
-rows is the per-block cost (prologue loads, epilogue stores, the padded last tile) -- what the persistent grid hides.
-``--modes``: hfa_attention_split_tuning values to compare (0 = automatic, the persistent grid; 100 = one item per
-workgroup).   python scripts/attn_len_sweep.py [--reps 200] [--modes 0,100]"""
+rows is the per-block cost (prologue loads, epilogue stores, the padded last tile).  ``--modes``:
+hfa_attention_split_tuning values to compare (0 = automatic, 4 / 8 waves).
+    python scripts/attn_len_sweep.py [--reps 200] [--modes 0,4,8]"""
 import argparse
 import math
 import os
