@@ -334,6 +334,40 @@ def secondary_rooflines(iso, pipe, T, S):
     return out
 
 
+def thread_cpu():
+    """{native thread id: (name, user + system CPU seconds)} of this process (Linux /proc; {} elsewhere)."""
+    out = {}
+    base = f"/proc/{os.getpid()}/task"
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        return out
+    tck = os.sysconf("SC_CLK_TCK")
+    for t in tids:
+        try:
+            with open(f"{base}/{t}/stat") as f:
+                st = f.read()
+            name = st[st.index("(") + 1:st.rindex(")")]
+            fields = st[st.rindex(")") + 2:].split()
+            out[int(t)] = (name, (int(fields[11]) + int(fields[12])) / tck)
+        except (OSError, ValueError, IndexError):
+            continue
+    return out
+
+
+def thread_cpu_diff(a, b, steps, top=5):
+    """The busiest threads' CPU ms per step between two thread_cpu() snapshots."""
+    import threading
+    main_id = threading.get_native_id()
+    rows = []
+    for tid, (name, t1) in b.items():
+        d = t1 - a.get(tid, (name, 0.0))[1]
+        if d > 0:
+            rows.append(("main" if tid == main_id else name, round(1e3 * d / max(steps, 1), 2)))
+    rows.sort(key=lambda r: -r[1])
+    return rows[:top]
+
+
 def main():
     args = parse()
     import numpy as np
@@ -425,7 +459,9 @@ def main():
     probe_name = census.dominant() if args.probe == "auto" else args.probe
     probe = ops.KernelProbe(probe_name, extra=SECONDARY)
     ops.PROBE = probe
+    thr0 = thread_cpu()
     res, el = timed(args.steps)
+    thr1 = thread_cpu()
     ops.PROBE = None
 
     n_frames = res[0]["T"]
@@ -528,9 +564,11 @@ def main():
     out["host_cpu"] = {
         "enqueue_cpu_ms_per_step": avg(2), "assemble_cpu_ms_per_step": avg(3), "process_cpu_ms_per_step": avg(4),
         "enqueue_wall_ms_per_step": avg(0), "wait_assemble_wall_ms_per_step": avg(1),
+        "threads_cpu_ms_per_step": thread_cpu_diff(thr0, thr1, args.steps),
         "note": "rank 0's host cost per timed step: CPU seconds of the launching thread for the GPU half's enqueue "
                 "(ctypes launches, allocator, events) and for the previous batch's wait + interval assembly, and "
-                "the whole process's CPU (all threads); the GPU step is ms_per_step"}
+                "the whole process's CPU (all threads; per thread over the timed region in threads_cpu_ms_per_step, "
+                "'main' = the launching thread); the GPU step is ms_per_step"}
     if rank == 0:
         import contextlib
         with contextlib.redirect_stdout(sys.stderr):         # the writers' progress prints stay off the JSON line

@@ -10,6 +10,8 @@ only the O(#phones) interval/word assembly, in numpy, with the reference's dtype
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 
@@ -126,7 +128,7 @@ class AlignmentDecoder:
             h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
             h.copy_(t, non_blocking=True)
             host[k] = h
-        ev = torch.cuda.Event(blocking=True)    # the host sleeps in assemble's wait instead of spinning a core
+        ev = torch.cuda.Event()
         ev.record()
         out = {"T": dev_out["T"], "host": host, "event": ev}
         if "redo" in dev_out:
@@ -141,7 +143,9 @@ class AlignmentDecoder:
         the CLI's export workers, rank 0 after the multi-GPU gather)."""
         if "host" not in dev_out:
             dev_out = self.fetch(dev_out, keep_frame_probs)
-        dev_out["event"].synchronize()
+        ev = dev_out["event"]
+        while not ev.query():          # poll and sleep: a HIP event wait spins a core (~12 ms of CPU per 15.6 ms
+            time.sleep(2e-4)           # step); the batch lands while the GPU runs the next one, so 0.2 ms is slack
         hd = {k: v.numpy() for k, v in dev_out["host"].items()}
         if "redo" in dev_out and any(int(hd[k][0]) for k in ("split_oflow", "split_oflow_head") if k in hd):
             # a split-f16 operand left f16 range: this batch is recomputed with f32 GEMMs
