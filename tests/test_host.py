@@ -350,10 +350,11 @@ def _gloo_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_boundary_gather_world2_gloo_unequal_shapes():
+@pytest.mark.parametrize("world", [2, 8])
+def test_boundary_gather_world2_gloo_unequal_shapes(world):
     """all_gather of each rank's (B, Tmax), then a padded all_gather_into_tensor per array; ranks
     hold different batch sizes and lengths, and rank 0 gets every rank's arrays back unpadded (and the CLI's
-    record tables survive the round trip bit for bit)."""
+    record tables survive the round trip bit for bit).  World 8 rehearses the driver's 8-GPU node on gloo."""
     import multiprocessing as mp
     import socket
     s = socket.socket()
@@ -362,17 +363,22 @@ def test_boundary_gather_world2_gloo_unequal_shapes():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_gloo_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res, recs = q.get(timeout=120)
+    res, recs = q.get(timeout=180)
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert np.array(res["ph_idx_seq"][0]).shape == (3, 7) and np.array(res["ph_idx_seq"][1]).shape == (4, 11)
-    assert res["n"][0] == [1, 1, 1] and res["n"][1] == [2, 2, 2, 2]
-    assert np.array(res["ph_time_int"][1])[0, 0] == 100 and np.array(res["ph_time_int"][1])[3, 10] == 143
-    want = {**_records(0), **_records(1)}
+    for r in range(world):
+        B, T = 3 + r, 7 + 4 * r
+        assert np.array(res["ph_idx_seq"][r]).shape == (B, T) and bool((np.array(res["ph_idx_seq"][r]) == r).all())
+        assert res["n"][r] == [r + 1] * B
+        assert np.array(res["ph_time_int"][r])[0, 0] == 100 * r
+        assert np.array(res["ph_time_int"][r])[B - 1, T - 1] == 100 * r + B * T - 1
+    want = {}
+    for r in range(world):
+        want.update(_records(r))
     assert sorted(recs) == sorted(want)
     for k, r in want.items():
         for f, v in r.items():
