@@ -143,24 +143,20 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_split64_kernel(const Attn
             q1s[h][kb] = q1[h][kb] * (_Float16)kLo;
             q2s[h][kb] = q2[h][kb] * (_Float16)kLo;
         }
-    // both halves' score tiles from one pass over the K fragments
-    auto scores = [&](const _Float16* sK, f32x16 (&sM)[NH][2]) {
+    // one half's score tile (the K fragments are read once per half: the halves are interleaved with each other's
+    // softmax, not with each other's MFMAs)
+    auto scores = [&](const _Float16* sK, f32x16 (&sM)[2], int h) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-            for (int h = 0; h < NH; ++h)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) sM[h][kt][e] = 0.f;
+            for (int e = 0; e < 16; ++e) sM[kt][e] = 0.f;
 #pragma unroll
             for (int kb = 0; kb < DH / 16; ++kb) {
                 const f16x8 k1 = *reinterpret_cast<const f16x8*>(sK + kt * 32 * DH + kofs[kb]);
                 const f16x8 k2 = *reinterpret_cast<const f16x8*>(sK + SPLANE + kt * 32 * DH + kofs[kb]);
-#pragma unroll
-                for (int h = 0; h < NH; ++h) {
-                    sM[h][kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q1[h][kb], sM[h][kt], 0, 0, 0);
-                    sM[h][kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q2s[h][kb], sM[h][kt], 0, 0, 0);
-                    sM[h][kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k2, q1s[h][kb], sM[h][kt], 0, 0, 0);
-                }
+                sM[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q1[h][kb], sM[kt], 0, 0, 0);
+                sM[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, q2s[h][kb], sM[kt], 0, 0, 0);
+                sM[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(k2, q1s[h][kb], sM[kt], 0, 0, 0);
             }
         }
     };
@@ -199,10 +195,12 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_split64_kernel(const Attn
         bm = fmaxf(bm, __shfl_xor(bm, 32, 64)) * qscale;
         const float m_cand = fmaxf(mr, bm);
         const bool move = m_cand > mr + kSlack;
-        if (__builtin_amdgcn_ballot_w64(move)) {
+        {   // branch-free (alpha = 1 exactly where the max does not move: the same bits), so the scheduler can
+            // interleave this half's softmax with the other half's MFMAs
             const float m_new = move ? m_cand : mr;
             const float alpha = __builtin_amdgcn_exp2f(mr - m_new);
             lr *= alpha;
+            asm volatile("" : "+v"(lr));   // keep l's rescale a separate rounding (no FMA with the sum below)
 #pragma unroll
             for (int e = 0; e < 16; ++e) { oh[0][e] *= alpha; oh[1][e] *= alpha; }
             mr = m_new;
@@ -229,14 +227,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_split64_kernel(const Attn
             issueK(st ^ 1, (t + 1) * SKB);
             issueV(st ^ 1, (t + 1) * SKB);
         }
-        scores(smem + st * KST, sc);
-        f32x16 (&s)[NH][2] = sc;
+        const _Float16* sK = smem + st * KST;
         const _Float16* sV = smem + (2 + st) * KST;
-        // one half at a time (its exp'd tile and P planes only live until its PV MFMAs; the V fragments are re-read
-        // for the second half)
-#pragma unroll
-        for (int h = 0; h < NH; ++h) {
-            softmax(t, s[h], m_run[h], l_run[h], o[h]);
+        auto pv = [&](int h) {
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -244,7 +237,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_split64_kernel(const Attn
                     unsigned w1[4], w2[4];
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj) {
-                        const float x0 = s[h][kt][8 * ks + 2 * jj], x1 = s[h][kt][8 * ks + 2 * jj + 1];
+                        const float x0 = sc[h][kt][8 * ks + 2 * jj], x1 = sc[h][kt][8 * ks + 2 * jj + 1];
                         w1[jj] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x0, x1}, f16x2));
                         w2[jj] = hfa::split_lo_pair(w1[jj], x0, x1, one);
                     }
@@ -265,7 +258,14 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_split64_kernel(const Attn
                         o[h][db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v2, p1, o[h][db], 0, 0, 0);
                     }
                 }
-        }
+        };
+        // half A's softmax beside half B's score MFMAs, half B's softmax beside half A's PV MFMAs
+        scores(sK, sc[0], 0);
+        softmax(t, sc[0], m_run[0], l_run[0], o[0]);
+        scores(sK, sc[1], 1);
+        pv(0);
+        softmax(t, sc[1], m_run[1], l_run[1], o[1]);
+        pv(1);
         if (t + 1 < nkb) {
             hfa::wait_vm_barrier<0>();                     // K(t+1), V(t+1) landed; K(t), V(t) reads done
         }

@@ -2,7 +2,7 @@
 # identity with the 4/8-wave kernel and the f64 tests), then the equal-work length sweep and the layer microbenchmark.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r04l
+O=${OUT:-gpurun_out/r04l}
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_split_gpu.py -x -q --timeout 120 --timeout-method thread -k attention > $O/tests.log 2>&1 || { echo "TESTS FAIL"; tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
