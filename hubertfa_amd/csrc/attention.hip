@@ -15,7 +15,6 @@
 // the running reference max moves only when a query's max exceeds it by more than 8 (log2 units), so the
 // output rescale runs about once per row.
 #include "hfa_common.h"
-#include "attn_params.h"
 
 namespace {
 
@@ -244,6 +243,16 @@ constexpr int SNS = 2;               // LDS stages
 constexpr int SPLANE = SKB * DH;     // halves per plane image (8 KiB)
 constexpr int SSTAGE = 4 * SPLANE;   // K1, K2, V1, V2
 constexpr float kLo = 1.0f / 2048.0f;
+
+struct AttnSP {
+    int B, H, L;
+    float scale;
+    const _Float16* q; long long q_sp, q_bs; int q_ld;
+    const _Float16* k; long long k_sp, k_bs; int k_ld;
+    const _Float16* v; long long v_sp, v_bs; int v_ld;
+    _Float16* o; long long o_sp, o_bs; int o_ld;
+    const int32_t* key_len;
+};
 
 __device__ __forceinline__ f16x4 lds_tr(const _Float16* base, int byte_off) {
     const auto* ptr = reinterpret_cast<const __attribute__((address_space(3))) s16x4*>(
@@ -521,7 +530,7 @@ thread_local int g_attn_waves = 0;   // hfa_attention_split_tuning override (0: 
 // Waves (x 32 queries) per workgroup of the split attention: 8 where that still leaves >= 2 workgroups per
 // (batch, head) row of queries, else 4.
 inline int split_attn_waves(int L) {
-    if (g_attn_waves == 4 || g_attn_waves == 8 || g_attn_waves == 64) return g_attn_waves;
+    if (g_attn_waves == 4 || g_attn_waves == 8) return g_attn_waves;
     return L >= 2 * 8 * QW ? 8 : 4;
 }
 }  // namespace
@@ -585,10 +594,6 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
     AttnSP p{B, H, L, scale, (const _Float16*)q, q_sp, q_bs, q_ld, (const _Float16*)k, k_sp, k_bs, k_ld,
              (const _Float16*)v, v_sp, v_bs, v_ld, (_Float16*)o, o_sp, o_bs, o_ld, key_len};
     const int nw = split_attn_waves(L);
-    if (nw == 64) {                                    // 64 queries per wave (attention64.hip)
-        launch_attn_split64(p, stream);
-        return hfa::check_launch("hfa_attention_split");
-    }
     const long long nblk = (long long)((L + QW * nw - 1) / (QW * nw)) * B * H;
     if (nblk > 0x7fffffffLL) {
         hfa::set_error("hfa_attention_split: grid too large");
@@ -603,8 +608,8 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
 
 // Waves per workgroup of hfa_attention_split: 4 or 8, 0 = automatic (benchmarks and the 4/8 parity test).
 int hfa_attention_split_tuning(int waves) {
-    if (waves != 0 && waves != 4 && waves != 8 && waves != 64) {
-        hfa::set_error("hfa_attention_split_tuning: waves must be 0, 4, 8 or 64 (64 queries per wave)");
+    if (waves != 0 && waves != 4 && waves != 8) {
+        hfa::set_error("hfa_attention_split_tuning: waves must be 0, 4 or 8");
         return HFA_EINVAL;
     }
     g_attn_waves = waves;

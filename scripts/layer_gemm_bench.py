@@ -69,12 +69,6 @@ def main():
             ops.attention_split(qs, o, B=B, H=H // 64, L=L, head_dim=64, scale=0.125)
             _lib.lib().hfa_attention_split_tuning(0)
         cases.append(("attention (split, 8 waves)", 4.0 * B * H * L * L, attn8))
-
-        def attn64():
-            _lib.lib().hfa_attention_split_tuning(64)
-            ops.attention_split(qs, o, B=B, H=H // 64, L=L, head_dim=64, scale=0.125)
-            _lib.lib().hfa_attention_split_tuning(0)
-        cases.append(("attention (split, 64 q/wave)", 4.0 * B * H * L * L, attn64))
     for cfg in [int(c) for c in args.cfgs.split(",")]:
         _lib.lib().hfa_gemm_split_tuning(cfg)
         for name, flop, fn in cases:

@@ -433,8 +433,8 @@ def test_attention_split_repeatable():
 
 @pytest.mark.parametrize("L", [499, 700])
 def test_attention_split_waves_bit_identical(L):
-    """4- and 8-wave workgroups and the 64-queries-per-wave kernel (attention64.hip) give bit-identical planes
-    (each query row sees the same key tiles in the same order), with and without per-row key lengths."""
+    """4- and 8-wave workgroups give bit-identical planes (each query row sees the same key tiles in the same
+    order), with and without per-row key lengths."""
     from hubertfa_amd import ops, _lib
     from hubertfa_amd.hubert import dev_lengths
     B, H, D = 3, 4, 64
@@ -442,7 +442,7 @@ def test_attention_split_waves_bit_identical(L):
     qs = ops.split(_r(B, L, 3 * H * D, seed=13, scale=2.0).to(d))
     for kl in (None, dev_lengths([L, L - 200, 65], d)):
         outs = []
-        for nw in (4, 8, 64):
+        for nw in (4, 8):
             _lib.call("hfa_attention_split_tuning", nw)
             try:
                 o = torch.full((2, B, L, H * D), float("nan"), dtype=torch.float16, device=d)
@@ -450,7 +450,7 @@ def test_attention_split_waves_bit_identical(L):
                 outs.append(o)
             finally:
                 _lib.call("hfa_attention_split_tuning", 0)
-        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+        assert torch.equal(outs[0], outs[1])
 
 
 def test_attention_split_large_scores():
