@@ -141,9 +141,6 @@ class AlignmentDecoder:
         interval/word assembly.  ``intervals=False`` returns the raw boundary records only (T, ph_idx_seq,
         ph_time_int, frame_confidence, edge_diff), for callers that assemble them elsewhere (``utterance_result``:
         the CLI's export workers, rank 0 after the multi-GPU gather)."""
-        resolve = dev_out.pop("resolve", None)
-        if resolve is not None:              # a pipelined handle whose side work is still held (task.submit)
-            resolve()
         if "host" not in dev_out:
             dev_out = self.fetch(dev_out, keep_frame_probs)
         ev = dev_out["event"]

@@ -285,12 +285,9 @@ class HubertEncoder:
         return ops.layernorm(x, w, b, eps, out=out), None
 
     def layer(self, h: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None, hs: torch.Tensor | None = None,
-              want_split: bool = False, gate=None):
+              want_split: bool = False):
         """One encoder layer: (h, hs) -> (h', hs').  ``hs``: h's split planes if its producer wrote them;
-        ``want_split``: also return the output's planes (the next layer's QKV operand), else None.  ``gate``
-        (optional callable) is called with "ffn2" right before the FFN2 launch: the point where another stream's work
-        may be enqueued to run beside FFN2's one round of tiles (task.submit); forward() also calls it with
-        "extractor" before conv0."""
+        ``want_split``: also return the output's planes (the next layer's QKV operand), else None."""
         sp = self.precision == "split" and L_.w1_s is not None and L_.w2_s is not None
         if not self.arch.stable_layer_norm:   # post-LN (HubertEncoderLayer / nn.TransformerEncoderLayer)
             # split path: the residual stream rides in the LayerNorms' split planes (hi + 2^-11 lo, 22 significand
@@ -300,8 +297,6 @@ class HubertEncoder:
             h1 = self._out_proj(o, L_, res)
             h1, h1s = self._ln(h1, L_.ln1_w, L_.ln1_b, out=h1, split=sp, planes_only=sp)
             f = self._linear(h1, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp, xs=h1s)
-            if gate is not None:
-                gate("ffn2")
             h2 = self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h1s, xs=f) if sp else \
                 ops.linear(f, L_.w2, L_.b2, residual=h1)
             return self._ln(h2, L_.ln2_w, L_.ln2_b, out=h2, split=want_split, planes_only=want_split)
@@ -314,15 +309,13 @@ class HubertEncoder:
         h = self._out_proj(o, L_, h)
         a_, a_s = self._ln(h, L_.ln2_w, L_.ln2_b, split=sp, planes_only=sp)
         f = self._linear(a_, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp, xs=a_s)
-        if gate is not None:
-            gate("ffn2")
         if sp:
             return self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h, xs=f), None
         return ops.linear(f, L_.w2, L_.b2, residual=h), None
 
     @torch.no_grad()
     def forward(self, wav: torch.Tensor, n_layers: int | None = None, lengths=None,
-                normalized: bool = False, gate=None) -> torch.Tensor:
+                normalized: bool = False) -> torch.Tensor:
         """wav [B, N] -> units [B, L, C].  ``lengths`` (optional, host ints [B]): samples per row of a
         variable-length batch (rows zero-padded to N); row b's units are valid for frame_lengths(lengths[b])
         frames and equal what that utterance gives alone.  ``normalized``: the caller already applied the
@@ -346,8 +339,6 @@ class HubertEncoder:
             x = ops.wav_normalize(x, 1e-7, lens=ns)
         if a.wav_pad:
             x = ops.pad_rows(x, a.wav_pad, x.shape[1] + 2 * a.wav_pad)
-        if gate is not None:
-            gate("extractor")           # the HBM-bound conv0 pass runs next: room for another stream's MFMA work
         feats = self.feature_extractor(x, lens0)
         fln, flns = self._ln(feats, self.fp_ln[0], self.fp_ln[1], split=self.fp_ws is not None)
         # uniform batch: the projection also writes its output as planes (the positional conv's operand; the f32
@@ -366,8 +357,7 @@ class HubertEncoder:
             h, hs = self._ln(h, self.enc_ln[0], self.enc_ln[1], out=h, split=bool(layers), planes_only=first)
         for i, L_ in enumerate(layers):
             nxt = i + 1 < len(layers)
-            h, hs = self.layer(h, L_, lensL, hs, want_split=nxt and (a.stable_layer_norm or planes_in(layers[i + 1])),
-                               gate=gate)
+            h, hs = self.layer(h, L_, lensL, hs, want_split=nxt and (a.stable_layer_norm or planes_in(layers[i + 1])))
         if a.stable_layer_norm:
             h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
         if self.proj is not None:

@@ -24,15 +24,6 @@ from .unet import LatticeHead
 from .wav_io import read_wav
 
 
-def _drain(gen):
-    """Run a step generator to its end and return its result."""
-    while True:
-        try:
-            next(gen)
-        except StopIteration as e:
-            return e.value
-
-
 def guarded(module, flag, fn):
     """Run ``fn`` (one pass of ``module``'s kernels) under the split-f16 range guard, synchronously: clear
     ``flag``, run, and if a split producer raised it, clear it and run ``fn`` again with ``module.precision`` =
@@ -133,7 +124,7 @@ class ForcedAlignmentTask:
 
     @torch.no_grad()
     def encode_batch(self, waves: torch.Tensor, wav_sr: int | None = None, lengths=None,
-                     chunk_seconds: float | None = None, gate=None):
+                     chunk_seconds: float | None = None):
         """Device half 1 (current stream): waves [B, N] -> (features [B, T_pad, C], DP frames, wav lengths).
 
         ``lengths`` (optional host ints [B]): samples per row of a variable-length batch, rows zero-padded to N
@@ -156,21 +147,17 @@ class ForcedAlignmentTask:
         n = waves.shape[-1]
         chunk = None if chunk_seconds is None else max(1, int(round(chunk_seconds * 50)))
         feats, n_frames = self.unitsEncoder.encode_frames(waves, sr, hop, pad_to=self.head.divisible,
-                                                          lengths=lengths, chunk_frames=chunk, gate=gate)
+                                                          lengths=lengths, chunk_frames=chunk)
         wl = [n / sr] * waves.shape[0] if lengths is None else [int(m) / sr for m in lengths]
         return feats, n_frames, wl
 
     def head_logits(self, feats, n_frames):
         """UNet head (current stream): features -> (logits [B, T, V+2], the head's range-flag snapshot or None)."""
-        return _drain(self.head_logits_steps(feats, n_frames))
-
-    def head_logits_steps(self, feats, n_frames):
-        """``head_logits`` as a generator yielding between the UNet's modules (LatticeHead.logits_steps)."""
         if isinstance(n_frames, (list, tuple)):          # variable-length batch
             t_pad = [self.head.padded_len(int(t)) for t in n_frames]
-            logits = (yield from self.head.logits_steps(feats, t_pad))[:, :max(n_frames)]
+            logits = self.head.logits(feats, t_pad)[:, :max(n_frames)]
         else:
-            logits = (yield from self.head.logits_steps(feats))[:, :n_frames]
+            logits = self.head.logits(feats)[:, :n_frames]
         flag = None
         if self.head.precision == "split":      # the head's own range flag, snapshot on the stream that ran it
             flag = ops.flag_take(self.head.flag)
@@ -186,12 +173,7 @@ class ForcedAlignmentTask:
 
     def decode_device(self, feats, n_frames, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
         """Device half 2 (current stream): UNet head + lattice + Viterbi -> the decoder's device outputs."""
-        return _drain(self.decode_steps(feats, n_frames, wav_lengths, ph_seqs, word_seqs, p2ws))
-
-    def decode_steps(self, feats, n_frames, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
-        """``decode_device`` as a generator: one step per UNet module, then the head, then the lattice + DP."""
-        logits, flag = yield from self.head_logits_steps(feats, n_frames)
-        yield
+        logits, flag = self.head_logits(feats, n_frames)
         return self.lattice_dp(logits, flag, wav_lengths, ph_seqs, word_seqs, p2ws)
 
     def _guard(self, dev_out, redo_args):
@@ -247,98 +229,29 @@ class ForcedAlignmentTask:
                on_device=None, lengths=None, chunk_seconds: float | None = None):
         """Two-stream pipelined device pass; returns the decoder's fetch handle (``decoder.assemble`` completes it).
 
-        The encoder runs on the caller's current stream and the head + lattice + Viterbi on a side stream.  With
-        ``interleave`` (the default) a batch's side work is enqueued in steps during the NEXT batch's encoder: one
-        step (a UNet module, the head, then the lattice + DP + backtrack) right before each layer's FFN2, whose
-        one round of 189 tiles leaves a quarter of the CUs idle -- the side work fills them instead of taking CUs
-        from the multi-round extractor convs it would otherwise share the chip with.  Without it, the whole side
-        pass is enqueued at once behind the encoder (it then overlaps the next batch's extractor).  Leftover steps
-        run when the next encoder is enqueued, or when the handle is assembled.  ``on_device`` (e.g. the RCCL
-        boundary gather) runs on the side stream after the backtrack."""
+        The encoder runs on the caller's current stream and the head + lattice + Viterbi on a side stream that
+        waits for it, so a batch's small-grid tail (UNet GEMMs on a few hundred workgroups, one DP workgroup per
+        utterance) overlaps the next batch's extractor instead of idling most of the chip.  (Enqueuing the side
+        pass in steps at the next encoder's FFN2 launches, whose one round of tiles leaves CUs idle, measured 13 %
+        slower: the steps spill into the full-chip kernels that follow)  ``on_device`` (e.g. the
+        RCCL boundary gather) runs on the side stream after the backtrack."""
         main = torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
-        prev = getattr(self, "_pending", None)
-        gate = prev.gate(main) if (prev is not None and self.interleave) else None
-        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds, gate=gate)
+        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds)
         guard = self._guard({}, (waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds))
-        if prev is not None:
-            prev.finish()
         ready = torch.cuda.Event()
         ready.record(main)
-        work = _SideWork(self, self._side, ready, feats, n_frames, wl, ph_seqs, word_seqs, p2ws, guard, on_device)
-        if self.interleave:
-            self._pending = work
-        else:
-            work.finish()
-            self._pending = None
-        return work.handle
-
-    interleave = False           # (round-4 experiment: hold a batch's side work for the next encoder's gates)
-    gate_points = ("ffn2",)      # where the next encoder takes a step of the held side work (HubertEncoder gates)
-
-    def flush(self):
-        """Enqueue any side work still held for interleaving (the pipeline's last batch)."""
-        prev = getattr(self, "_pending", None)
-        if prev is not None:
-            prev.finish()
-            self._pending = None
-
-
-class _SideWork:
-    """One batch's side-stream pass (decode_steps) enqueued step by step; ``handle`` is the decoder's fetch handle,
-    filled when the last step has been enqueued (``decoder.assemble`` resolves it through its "resolve" entry)."""
-
-    def __init__(self, task, side, ready, feats, n_frames, wl, ph_seqs, word_seqs, p2ws, guard, on_device):
-        self.task, self.side, self.ready, self.feats = task, side, ready, feats
-        self.guard, self.on_device = guard, on_device
-        for p in ph_seqs:    # an out-of-vocabulary phone raises here, for this batch (tools/alignment_decoder.py:35)
-            task.decoder.ph_ids(p)
-        self.gen = task.decode_steps(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
-        self.started = self.done = False
-        self.handle = {"resolve": self.finish}
-
-    def step(self) -> bool:
-        """Enqueue the next step on the side stream; False once the pass is complete."""
-        if self.done:
-            return False
-        with torch.cuda.stream(self.side):
-            if not self.started:
-                self.side.wait_event(self.ready)
-                self.feats.record_stream(self.side)  # the allocator must not recycle it under the side stream
-                self.started = True
-            try:
-                next(self.gen)
-                return True
-            except StopIteration as e:
-                dev_out = e.value
-            if "split_oflow" in self.guard:
-                self.guard["split_oflow"].record_stream(self.side)
-            dev_out.update(self.guard)
-            if self.on_device is not None:
-                self.on_device(dev_out)
-            h = self.task.decoder.fetch(dev_out)
-        self.handle.pop("resolve", None)
-        self.handle.update(h)
-        self.done = True
-        return False
-
-    def gate(self, main):
-        """Callable for the next encoder's FFN2 gates: the side stream waits for the main stream to reach that point,
-        then takes one step."""
-        def g(point):
-            if self.done or point not in self.task.gate_points:
-                return
-            ev = torch.cuda.Event()
-            ev.record(main)
-            self.side.wait_event(ev)
-            self.step()
-        return g
-
-    def finish(self):
-        while self.step():
-            pass
-        return self.handle
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ready)
+            feats.record_stream(self._side)      # the caching allocator must not recycle it under the side stream
+            dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
+            if "split_oflow" in guard:
+                guard["split_oflow"].record_stream(self._side)
+            dev_out.update(guard)
+            if on_device is not None:
+                on_device(dev_out)
+            return self.decoder.fetch(dev_out)
 
 
 def synth_checkpoint(path: str | None = None, *, encoder="cnhubert", model_path="synth:0", seed=1,

@@ -22,15 +22,6 @@ from . import ops
 from .synth import UNetArch
 
 
-def _drain(gen):
-    """Run a step generator to its end and return its result."""
-    while True:
-        try:
-            next(gen)
-        except StopIteration as e:
-            return e.value
-
-
 def _t(x):
     return torch.from_numpy(np.ascontiguousarray(x)) if isinstance(x, np.ndarray) else x.detach().cpu()
 
@@ -227,12 +218,6 @@ class LatticeHead:
         Split path: every producer whose consumer is a split GEMM writes that operand's planes (block GroupNorm and
         LayerNorm, down / up convs with the skip add in their epilogue), so no separate conversion runs beyond the
         input's.  Returns y, or (y, planes) with ``want_split``."""
-        return _drain(self.backbone_steps(x, t_pad, want_split))
-
-    def backbone_steps(self, x: torch.Tensor, t_pad=None, want_split=False):
-        """``backbone`` as a generator that yields after each module's launches (block, down- or up-sampling) and
-        returns its result: the caller may enqueue the steps at points of its choosing (task.submit interleaves
-        them with the next batch's encoder).  The launches and their order are the same as ``backbone``'s."""
         lv = None
         if t_pad is not None and any(int(t) != x.shape[1] for t in t_pad):
             from .hubert import dev_lengths
@@ -245,19 +230,15 @@ class LatticeHead:
             t = h[-1]
             for m in enc:
                 t = m(t[0], L(i), xs=t[1], want_split=True)
-                yield
             h.append(t)
         bd, bb, bu = self.bottleneck
         t = bd(h[-1][0], L(self.arch.times), xs=h[-1][1], want_split=True)
         t = bb(t[0], L(self.arch.times), xs=t[1], want_split=True)
-        yield
         t = bu(t[0], L(self.arch.times), xs=t[1], want_split=True, skip=h[n_enc][0])
-        yield
         for i, dec in enumerate(self.decoders):
             lev = self.arch.times - 1 - i
             last = i + 1 == len(self.decoders)
             t = dec[0](t[0], L(lev), xs=t[1], want_split=want_split if last else True)
-            yield
             if len(dec) > 1:
                 t = dec[1](t[0], L(lev), xs=t[1], want_split=True, skip=h[n_enc - 1 - i][0])
         return t if want_split else t[0]
@@ -267,14 +248,10 @@ class LatticeHead:
         """x [B, T_pad, C_in] -> logits [B, T_pad, V+2] on the chip-wide launches (every GEMM spreads over the whole
         chip; a row's result depends on its own length only).  The one-kernel and per-op-engine forms of round 3
         were parity-green but slower in the pipeline; they are in git history."""
-        return _drain(self.logits_steps(x, t_pad))
-
-    def logits_steps(self, x: torch.Tensor, t_pad=None):
-        """``logits`` as a generator (see backbone_steps); returns the logits."""
         if self.ctx.use_split(self.head_ws):
-            y, ys = yield from self.backbone_steps(x, t_pad, want_split=True)
+            y, ys = self.backbone(x, t_pad, want_split=True)
             return self.ctx.linear(y, ys, self.head_wp, self.head_ws, self.head_bp)[0][:, :, :self.head_w.shape[0]]
-        y = yield from self.backbone_steps(x, t_pad)
+        y = self.backbone(x, t_pad)
         return self.ctx.linear(y, None, self.head_w, None, self.head_b)[0]
 
     @staticmethod

@@ -57,26 +57,10 @@ def setters(task):
                 task._side = plain[key]
         return f
 
-    def combo(*fs):
-        def f():
-            for g in fs:
-                g()
-        return f
-
-    def mode(inter, depth, points=("ffn2",)):
-        return combo(side("plain"), lambda: setattr(task, "interleave", inter), lambda: setattr(task, "gate_points", points),
-                     lambda: setattr(task, "_depth", depth))
     return {
-        "base": mode(False, 1),
+        "base": side("plain"),
         "mask64": side(64),
         "mask32": side(32),
-        # the side-work interleave (a batch's side work enqueued at the next encoder's FFN2 launches) with the host
-        # assembling one batch behind (depth 1) or two (depth 2: the host never waits for the batch it gated)
-        "serial1": mode(False, 1),
-        "serial2": mode(False, 2),
-        "inter1": mode(True, 1),
-        "inter2": mode(True, 2),
-        "interstart2": mode(True, 2, ("extractor", "ffn2")),
     }
 
 
@@ -99,15 +83,13 @@ def main():
     names = args.variants.split(",")
 
     def piped(k):
-        depth = getattr(task, "_depth", 1)
-        pending = []
+        pending = None
         for _ in range(k):
-            pending.append(task.submit(wav, ph, ws, pw, wav_sr=16000))
-            if len(pending) > depth:
-                task.decoder.assemble(pending.pop(0), ph, ws, pw)
-        task.flush()
-        for h in pending:
-            task.decoder.assemble(h, ph, ws, pw)
+            h = task.submit(wav, ph, ws, pw, wav_sr=16000)
+            if pending is not None:
+                task.decoder.assemble(pending, ph, ws, pw)
+            pending = h
+        task.decoder.assemble(pending, ph, ws, pw)
 
     def enc(k):
         for _ in range(k):
@@ -130,7 +112,6 @@ def main():
             if args.encoder_only:
                 res_enc[n].append(clock(enc, args.steps))
             S["base"]()
-            task.flush()
             print(f"round {r} {n}: pipelined {res[n][-1]:.3f} ms/step"
                   + (f", encoder alone {res_enc[n][-1]:.3f}" if args.encoder_only else ""), flush=True)
     for n in names:
