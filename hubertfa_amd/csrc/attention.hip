@@ -277,10 +277,7 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
     constexpr int KST = 2 * SPLANE;                      // halves per K (or V) stage, both planes
     constexpr int NW = SNW, PPW = 8 / SNW;               // 1-KiB DMA pieces (8 keys) per plane per wave
     static_assert(SNW == 4 || SNW == 8, "4 or 8 waves");
-    // K0, K1, V0, V1, V2: V runs two tiles ahead in a 3-stage ring (80 KiB: still 2 workgroups per CU at 4 waves),
-    // so the end-of-tile wait leaves the newest V tile in flight (counted vmcnt) and each V tile gets two
-    // iterations of DMA latency instead of one
-    __shared__ __attribute__((aligned(16))) _Float16 smem[5 * KST];
+    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * KST];   // K0, K1, V0, V1
 
     const int nwg = gridDim.x, orig = blockIdx.x;
     const int xcd = orig & 7, xq = nwg >> 3, xr = nwg & 7;
@@ -402,10 +399,7 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
     const int nkb = (L + SKB - 1) / SKB;
     issueK(0, 0);
     issueV(0, 0);
-    if (nkb > 1) {
-        issueK(1, SKB);
-        issueV(1, SKB);
-    }
+    if (nkb > 1) issueK(1, SKB);
     hfa::wait_vm_barrier<0>();
     f32x16 sA[2], sB[2];
     scores(smem, sA);
@@ -415,8 +409,7 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
     auto step = [&](int t, f32x16 (&s)[2], f32x16 (&nM)[2]) {
         const int st = t & 1;
         if (t + 2 < nkb) issueK(st, (t + 2) * SKB);        // K(t) was read by iteration t - 1's scores
-        const bool vnext = t + 2 < nkb;
-        if (vnext) issueV((t + 2) % 3, (t + 2) * SKB);     // V(t - 1) was read by iteration t - 1's PV
+        if (t + 1 < nkb) issueV(st ^ 1, (t + 1) * SKB);    // V(t - 1) was read by iteration t - 1's PV
         if (t + 1 < nkb) scores(smem + (st ^ 1) * KST, nM);   // tile t + 1, in flight during softmax(t)
         const int key0 = t * SKB;
         if (key0 + SKB > L) {
@@ -455,7 +448,7 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
             }
         ls += __shfl_xor(ls, 32, 64);
         l_run += ls;
-        const _Float16* sV = smem + (2 + __builtin_amdgcn_readfirstlane(t % 3)) * KST;
+        const _Float16* sV = smem + (2 + st) * KST;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -488,11 +481,7 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
                 }
             }
         if (t + 1 < nkb) {
-            // K(t+2), V(t+1) landed (V(t+2), issued last, may stay in flight); K(t+1), V(t) reads done
-            if (vnext)
-                hfa::wait_vm_barrier<2 * PPW>();
-            else
-                hfa::wait_vm_barrier<0>();
+            hfa::wait_vm_barrier<0>();                     // K(t+2), V(t+1) landed; K(t+1), V(t) reads done
         }
     };
     for (int t = 0; t < nkb; t += 2) {
