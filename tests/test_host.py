@@ -463,3 +463,28 @@ def test_bench_config3_batch():
     assert bench.config3_batch(argparse.Namespace(**{**vars(a), "encoder": "large"}), 8) == 0
     assert bench.config3_batch(argparse.Namespace(**{**vars(a), "no_config3": True}), 8) == 0
     assert bench.config_name("base", 8, 64) == "config 3 geometry"
+
+
+def test_bench_thread_cpu_breakdown():
+    """bench.py's per-thread host CPU split (the bench line's host_cpu.threads_cpu_ms_per_step): the launching thread
+    is reported as 'main' and a busy helper thread by its OS name (Python thread names are not OS names)."""
+    import threading
+    import time as _time
+    import bench
+    stop = threading.Event()
+
+    def spin():
+        while not stop.is_set():
+            pass
+    a = bench.thread_cpu()
+    t0 = _time.time()
+    while _time.time() - t0 < 0.2:      # the main thread busy
+        pass
+    th = threading.Thread(target=spin, name="spinner")
+    th.start()
+    _time.sleep(0.3)                     # the helper busy, the main thread asleep
+    b = bench.thread_cpu()
+    stop.set()
+    th.join()
+    rows = bench.thread_cpu_diff(a, b, 1)
+    assert dict(rows).get("main", 0) >= 100 and any(n != "main" and ms >= 100 for n, ms in rows), rows
