@@ -42,7 +42,7 @@ __device__ __forceinline__ float from_lane_below(float v) {
 // refill just issued included) at the top of each group — the prefetch did nothing and each group paid a full
 // memory round trip.  E and nE of a group are one vector load each (lane u holds step t0 + u) broadcast per step
 // with v_readlane, instead of two scalar loads per step whose lgkmcnt(0) waits also catch the refills.
-template <int K, int NW, int G, int R, bool VEC, bool PIPE>
+template <int K, int NW, int G, int R, bool VEC>
 __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
     const int32_t* __restrict__ padv, const float* __restrict__ prob_log,
@@ -50,29 +50,13 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id) {
     static_assert(NW == 1 || K >= 2, "multi-wave DP needs >= 2 states per lane");
     static_assert(G <= 64 && R >= 2, "a group's E / nE fit one wave's lanes; at least two groups in flight");
-    constexpr int NSLOT = 16;                    // PIPE: boundary ring depth (steps a wave may run ahead)
-    __shared__ float xq[PIPE ? NSLOT : 2][NW][2];
-    __shared__ int pub[NW], cons[NW];            // PIPE: last step whose boundary a wave wrote / read
+    __shared__ float xq[2][NW][2];
     const int b = blockIdx.x;
     const int g = threadIdx.x;
     const int lane = g & 63, wave = g >> 6;
     const int T = Tv[b];
     const int S = Sv[b];
     if (T <= 1 || S <= 0) return;
-    // LDS-qualified volatile views (a generic volatile pointer becomes flat accesses, whose vmcnt waits would
-    // also drain the emission prefetch every step)
-    volatile __attribute__((address_space(3))) float* vxq = (__attribute__((address_space(3))) float*)&xq[0][0][0];
-    volatile __attribute__((address_space(3))) int* vpub = (__attribute__((address_space(3))) int*)pub;
-    volatile __attribute__((address_space(3))) int* vcons = (__attribute__((address_space(3))) int*)cons;
-    int pub_seen = 0, cons_seen = 0;             // wave-uniform caches of the neighbours' counters
-    int budget = 1 << 26;                        // spin cap: a wait that never ends still lets the grid drain
-    if (PIPE && NW > 1) {
-        if (lane == 0) {
-            pub[wave] = 0;
-            cons[wave] = 0;
-        }
-        __syncthreads();
-    }
     const int pad = padv ? padv[b] : (S >= 2 ? 2 : 1);
     const size_t ts = (size_t)b * Tmax * Smax;
     const float* pl = prob_log + ts;
@@ -141,38 +125,7 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
         // left neighbour lane's last two q values (states s0-1, s0-2)
         float qm1 = from_lane_below(q[K - 1]);
         float qm2 = (K >= 2) ? from_lane_below(q[K >= 2 ? K - 2 : 0]) : from_lane_below(qm1);
-        if (NW > 1 && PIPE) {
-            // point to point: wave w needs only wave w-1's boundary of this step, written as soon as that wave has
-            // its q, so the waves drift up to NSLOT steps apart instead of meeting at a barrier every step.  LDS
-            // operations of one wave complete in order, so data written before its counter is seen with it.
-            const int slot = t & (NSLOT - 1);
-            if (wave < NW - 1) {
-                if (t - NSLOT > cons_seen) {     // the right neighbour has not read this slot's previous step yet
-                    int c = __builtin_amdgcn_readfirstlane(vcons[wave + 1]);
-                    while (c < t - NSLOT && --budget > 0) c = __builtin_amdgcn_readfirstlane(vcons[wave + 1]);
-                    cons_seen = c;
-                }
-                if (lane == 63) {
-                    vxq[(slot * NW + wave) * 2] = q[K - 1];
-                    vxq[(slot * NW + wave) * 2 + 1] = q[K >= 2 ? K - 2 : 0];
-                }
-                if (lane == 0) vpub[wave] = t;
-            }
-            if (wave > 0) {
-                if (pub_seen < t) {
-                    int c = __builtin_amdgcn_readfirstlane(vpub[wave - 1]);
-                    while (c < t && --budget > 0) c = __builtin_amdgcn_readfirstlane(vpub[wave - 1]);
-                    pub_seen = c;
-                }
-                const float v1 = vxq[(slot * NW + wave - 1) * 2];
-                const float v2 = vxq[(slot * NW + wave - 1) * 2 + 1];
-                if (lane == 0) {
-                    qm1 = v1;
-                    qm2 = v2;
-                    vcons[wave] = t;
-                }
-            }
-        } else if (NW > 1) {
+        if (NW > 1) {
             if (lane == 63) {
                 xq[t & 1][wave][0] = q[K - 1];
                 xq[t & 1][wave][1] = q[K >= 2 ? K - 2 : 0];
@@ -650,7 +603,6 @@ __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
 }
 
 thread_local int g_force_k = 0;   // hfa_viterbi_tuning: states per lane of the multi-wave DP (0 = automatic)
-thread_local bool g_pipe = false;
 
 template <int K, int NW, int G, int R>
 int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const int32_t* pad,
@@ -658,18 +610,12 @@ int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S
                    const int32_t* ids, hipStream_t st) {
     const bool vec = Smax % K == 0 && ((uintptr_t)prob_log % 16 == 0) && ((uintptr_t)dp % 16 == 0) &&
                      ((uintptr_t)bt % 8 == 0);
-    if (vec && g_pipe)
-        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, true, true>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax,
-                           T, S, pad, prob_log, nE, E, curr, dp, bt, ids);
-    else if (vec)
-        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, true, false>), dim3(B), dim3(64 * NW), 0, st, Tmax,
-                           Smax, T, S, pad, prob_log, nE, E, curr, dp, bt, ids);
-    else if (g_pipe)
-        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, false, true>), dim3(B), dim3(64 * NW), 0, st, Tmax,
-                           Smax, T, S, pad, prob_log, nE, E, curr, dp, bt, ids);
+    if (vec)
+        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, true>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
+                           S, pad, prob_log, nE, E, curr, dp, bt, ids);
     else
-        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, false, false>), dim3(B), dim3(64 * NW), 0, st, Tmax,
-                           Smax, T, S, pad, prob_log, nE, E, curr, dp, bt, ids);
+        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, false>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
+                           S, pad, prob_log, nE, E, curr, dp, bt, ids);
     return hfa::check_launch("hfa_viterbi_forward");
 }
 
@@ -733,8 +679,6 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
 }
 
 int hfa_viterbi_tuning(int force_k) {
-    g_pipe = force_k >= 100;
-    if (g_pipe) force_k -= 100;
     if (force_k != 0 && force_k != 2 && force_k != 4 && force_k != 8) {
         hfa::set_error("hfa_viterbi_tuning: states per lane must be 0 (automatic), 2, 4 or 8 (got %d)", force_k);
         return HFA_EINVAL;

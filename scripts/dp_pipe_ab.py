@@ -1,5 +1,6 @@
-"""Multi-wave Viterbi forward A/B (GPU box): the per-step barrier exchange vs the point-to-point boundary ring
-(hfa_viterbi_tuning(100 + k)).  Checks the two give bit-identical dp / bt / curr, then times both, interleaved.
+"""Multi-wave Viterbi forward A/B (GPU box; needs viterbi.hip of commit 6e78506, where hfa_viterbi_tuning(100 + k)
+selects the ring): the per-step barrier exchange vs the point-to-point boundary ring.  Checks the two give
+bit-identical dp / bt / curr, then times both, interleaved (profiles/r04/dp_ring_ab.txt).
     python scripts/dp_pipe_ab.py [--reps 3]"""
 import argparse
 import os
