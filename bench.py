@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--probe", default="auto",
                     help="kernel instantiation to time; auto = the one carrying the most FLOPs in a warmup census")
     ap.add_argument("--serial", action="store_true", help="one stream per step (no head/encoder overlap)")
+    ap.add_argument("--no-held-dp", action="store_true",
+                    help="run a long lattice's DP in one launch behind its head (A/B of task.defer_dp_frames)")
     ap.add_argument("--precision", default="split", choices=["split", "f16"],
                     help="split: f32-class split-f16x3 (the headline); f16: opt-in fast mode, one f16 product per MAC "
                          "in the encoder's split GEMMs (f16-class accuracy, not the reference's f32)")
@@ -392,6 +394,8 @@ def main():
     ckpt = synth_checkpoint(encoder=encoder, model_path="synth:0", seed=1)
     task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
     task.on_predict_start()
+    if args.no_held_dp:
+        task.defer_dp_frames = None
     if args.precision == "f16":
         task.unitsEncoder.model.f16 = True
     B = args.batch
@@ -419,18 +423,23 @@ def main():
         return task.decoder.assemble(handle, *inp[2:])
 
     def run(k, inp=inputs):
-        """k steps, software-pipelined: the host assembles batch i while the GPU runs batch i+1."""
-        pending, res = None, None
+        """k steps, software-pipelined: the host assembles batch i while the GPU runs batch i+1 -- or, when
+        task.submit holds a batch's DP for the next encoder's attention launches (a long lattice), batch i-1: batch
+        i's results land near the end of encoder i+1, and waiting for them there would leave the GPU idle while the
+        host assembles and enqueues the next step."""
+        pending, res = [], None
         for _ in range(k):
             t0, c0, p0 = time.perf_counter(), time.thread_time(), time.process_time()
             h = launch(inp)
             t1, c1 = time.perf_counter(), time.thread_time()
-            if pending is not None:
-                res = finish(pending, inp)
+            pending.append(h)
+            while len(pending) > (2 if "resolve" in h else 1):
+                res = finish(pending.pop(0), inp)
             host_t.append((t1 - t0, time.perf_counter() - t1, c1 - c0, time.thread_time() - c1,
                            time.process_time() - p0))
-            pending = h
-        return finish(pending, inp) if pending is not None else res
+        while pending:
+            res = finish(pending.pop(0), inp)
+        return res
 
     def timed(k, inp=inputs):
         """exactly k steps between barrier + synchronize pairs -> (results, max seconds over ranks)."""

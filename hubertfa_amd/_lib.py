@@ -24,6 +24,7 @@ _SIGS = {
     "hfa_build_arch": [],
     # alignment decoder (viterbi.hip)
     "hfa_viterbi_forward": [I, I, I, P, P, P, P, P, P, P, P, P, P, P],
+    "hfa_viterbi_forward_steps": [I, I, I, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "hfa_viterbi_backtrack": [I, I, I, P, P, P, P, P, P, P, P, P, P],
     "hfa_lattice_prologue": [I, I, I, I, P, P, P, LL, LL, P, LL, LL, P, P, P, P, P, P, P, P, P, P, P],
     "hfa_viterbi_init": [I, I, I, P, P, P, P, P, P, P],

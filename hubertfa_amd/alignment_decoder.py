@@ -10,6 +10,7 @@ only the O(#phones) interval/word assembly, in numpy, with the reference's dtype
 """
 from __future__ import annotations
 
+import functools
 import time
 
 import numpy as np
@@ -75,10 +76,14 @@ class AlignmentDecoder:
 
     # -- batched path ---------------------------------------------------------------------------------------
     def decode_batch(self, frame_logits, edge_logits, wav_lengths, ph_seqs, word_seqs=None, p2ws=None,
-                     keep_frame_probs: bool = False, host: bool = True):
+                     keep_frame_probs: bool = False, host: bool = True, dp_ranges=None):
         """Decode B utterances: frame_logits [B,Tl,V], edge_logits [B,Tl] (GPU tensors, strided views OK).
 
-        Returns one dict per utterance with the reference decode() outputs (+ raw path arrays).
+        Returns one dict per utterance with the reference decode() outputs (+ raw path arrays).  With
+        ``host=False`` the device outputs instead; ``dp_ranges`` (callable (Tmax, Smax) -> n, host=False only):
+        when it returns n > 1 the forward DP is not enqueued here but left as n step-range closures plus the
+        backtrack under ``dev_out["deferred"]``, to be called in order on one stream (task.submit runs them beside
+        the next batch's attention kernels); the outputs are complete when the last one has run.
         """
         dev = _device(frame_logits)
         frame_logits = frame_logits.to(dev).float()
@@ -102,10 +107,24 @@ class AlignmentDecoder:
         lat = ops.lattice_prologue(frame_logits, edge_logits, ids_t, T_t, S_t, want_frame_probs=keep_frame_probs,
                                    init_dp=True)
         dp, bt, curr = lat.pop("dp"), lat.pop("bt"), lat.pop("curr")
-        ops.viterbi_forward(lat["prob_log"], lat["not_edge_log"], lat["edge_log"], curr, dp, bt, ids_t, T_t, S_t)
-        idx, tint, n, fc = ops.viterbi_backtrack(dp, bt, ids_t, T_t, S_t)
-        dev_out = dict(ph_idx_seq=idx, ph_time_int=tint, n=n, frame_confidence=fc, edge_diff=lat["edge_diff"],
-                       T=Ts, lattice=lat)
+        dev_out = dict(edge_diff=lat["edge_diff"], T=Ts, lattice=lat)
+        Tmax = dp.shape[1]
+
+        def forward(t0=None, t1=None):
+            ops.viterbi_forward(lat["prob_log"], lat["not_edge_log"], lat["edge_log"], curr, dp, bt, ids_t, T_t, S_t,
+                                steps=None if t0 is None else (t0, t1))
+
+        def backtrack():
+            idx, tint, n, fc = ops.viterbi_backtrack(dp, bt, ids_t, T_t, S_t)
+            dev_out.update(ph_idx_seq=idx, ph_time_int=tint, n=n, frame_confidence=fc)
+        n_rng = 1 if host or dp_ranges is None or Smax > 8192 else max(1, int(dp_ranges(Tmax, Smax)))
+        if n_rng > 1:
+            cuts = np.linspace(1, Tmax, n_rng + 1).round().astype(int)
+            dev_out["deferred"] = [functools.partial(forward, int(a), int(c)) for a, c in zip(cuts[:-1], cuts[1:])]
+            dev_out["deferred"].append(backtrack)
+            return dev_out
+        forward()
+        backtrack()
         if not host:
             return dev_out
         return self.assemble(dev_out, ph_seqs, word_seqs, p2ws, keep_frame_probs)
@@ -141,6 +160,9 @@ class AlignmentDecoder:
         interval/word assembly.  ``intervals=False`` returns the raw boundary records only (T, ph_idx_seq,
         ph_time_int, frame_confidence, edge_diff), for callers that assemble them elsewhere (``utterance_result``:
         the CLI's export workers, rank 0 after the multi-GPU gather)."""
+        resolve = dev_out.pop("resolve", None)
+        if resolve is not None:              # a pipelined handle whose DP steps are still held (task.submit)
+            resolve()
         if "host" not in dev_out:
             dev_out = self.fetch(dev_out, keep_frame_probs)
         ev = dev_out["event"]

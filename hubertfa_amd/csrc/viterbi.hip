@@ -47,7 +47,7 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
     const int32_t* __restrict__ padv, const float* __restrict__ prob_log,
     const float* __restrict__ not_edge_log, const float* __restrict__ edge_log, double* __restrict__ curr_io,
-    float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id) {
+    float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id, int t_begin, int t_end) {
     static_assert(NW == 1 || K >= 2, "multi-wave DP needs >= 2 states per lane");
     static_assert(G <= 64 && R >= 2, "a group's E / nE fit one wave's lanes; at least two groups in flight");
     __shared__ float xq[2][NW][2];
@@ -56,7 +56,9 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     const int lane = g & 63, wave = g >> 6;
     const int T = Tv[b];
     const int S = Sv[b];
-    if (T <= 1 || S <= 0) return;
+    // time steps [t0, te) of this utterance (a range call continues from dp row t0 - 1 and from curr)
+    const int t0 = max(t_begin, 1), te = min(t_end, T);
+    if (te <= t0 || S <= 0) return;
     const int pad = padv ? padv[b] : (S >= 2 ? 2 : 1);
     const size_t ts = (size_t)b * Tmax * Smax;
     const float* pl = prob_log + ts;
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     for (int k = 0; k < K; ++k) {
         const int s = s0 + k;
         valid[k] = s < S;
-        dprev[k] = valid[k] ? d[s] : neg_inf();
+        dprev[k] = valid[k] ? d[(size_t)(t0 - 1) * Smax + s] : neg_inf();
         curr[k] = valid[k] ? cu[s] : -__builtin_inf();
         zero[k] = valid[k] && ids[s] == 0;
         // prob3 (alignment_decoder.py:191-202): -inf for s < pad, and for s >= pad when
@@ -199,11 +201,11 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     };
 
 #pragma unroll
-    for (int r = 0; r < R; ++r) load(L[r], EV[r], nEV[r], 1 + r * G);
-    int tb = 1;
+    for (int r = 0; r < R; ++r) load(L[r], EV[r], nEV[r], t0 + r * G);
+    int tb = t0;
     // main loop: whole rounds of R groups, straight-line (no early exits: a branch around a refill would again
     // cost the vmcnt tracking); slot r holds steps tb + r G .. + G - 1 on entry
-    for (; tb + R * G <= T; tb += R * G) {
+    for (; tb + R * G <= te; tb += R * G) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
 #pragma unroll
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
 #pragma unroll
         for (int u = 0; u < G; ++u) {
             const int t = tb + r * G + u;
-            if (t < T)   // uniform over the workgroup
+            if (t < te)   // uniform over the workgroup
                 step(L[r][u], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(EV[r]), u)),
                      __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nEV[r]), u)), t);
         }
@@ -607,15 +609,15 @@ thread_local int g_force_k = 0;   // hfa_viterbi_tuning: states per lane of the 
 template <int K, int NW, int G, int R>
 int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const int32_t* pad,
                    const float* prob_log, const float* nE, const float* E, double* curr, float* dp, int8_t* bt,
-                   const int32_t* ids, hipStream_t st) {
+                   const int32_t* ids, int t_begin, int t_end, hipStream_t st) {
     const bool vec = Smax % K == 0 && ((uintptr_t)prob_log % 16 == 0) && ((uintptr_t)dp % 16 == 0) &&
                      ((uintptr_t)bt % 8 == 0);
     if (vec)
         hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, true>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
-                           S, pad, prob_log, nE, E, curr, dp, bt, ids);
+                           S, pad, prob_log, nE, E, curr, dp, bt, ids, t_begin, t_end);
     else
         hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, false>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
-                           S, pad, prob_log, nE, E, curr, dp, bt, ids);
+                           S, pad, prob_log, nE, E, curr, dp, bt, ids, t_begin, t_end);
     return hfa::check_launch("hfa_viterbi_forward");
 }
 
@@ -623,21 +625,25 @@ int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S
 
 extern "C" {
 
-int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S,
-                        const int32_t* prob3_pad_len, const float* prob_log, const float* not_edge_log,
-                        const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,
-                        hipStream_t stream) {
+int hfa_viterbi_forward_steps(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S,
+                              const int32_t* prob3_pad_len, const float* prob_log, const float* not_edge_log,
+                              const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,
+                              int t_begin, int t_end, hipStream_t stream) {
     if (B < 0 || Tmax < 0 || Smax < 0 || (B > 0 && (!T || !S || !prob_log || !not_edge_log || !edge_log ||
                                                      !curr || !dp || !bt || !ph_seq_id))) {
         hfa::set_error("hfa_viterbi_forward: bad arguments");
         return HFA_EINVAL;
     }
-    if (B == 0 || Tmax == 0 || Smax == 0) return HFA_OK;
+    if (t_begin < 1 || t_end < t_begin) {
+        hfa::set_error("hfa_viterbi_forward_steps: bad step range [%d, %d)", t_begin, t_end);
+        return HFA_EINVAL;
+    }
+    if (B == 0 || Tmax == 0 || Smax == 0 || t_begin >= Tmax || t_end == t_begin) return HFA_OK;
     // one wave while a lane holds <= 8 states; beyond that K states per lane over up to 16 waves (K = 8 by
     // default, or forced to 2/4 by hfa_viterbi_tuning: more waves, fewer states each, one barrier per step)
 #define HFA_FWD(K, NW, G, R)                                                                                    \
     return launch_forward<K, NW, G, R>(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log, edge_log, curr, \
-                                       dp, bt, ph_seq_id, stream)
+                                       dp, bt, ph_seq_id, t_begin, t_end, stream)
     // R groups of G steps in flight (K * G * R emission registers per lane, within the VGPR budget of 64 * NW
     // threads: 512 up to 4 waves, 256 at 8, 128 at 16)
     const int per_lane = (Smax + 63) / 64;
@@ -670,12 +676,24 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
     if (waves <= 16) HFA_FWD(8, 16, 2, 3);   // 1024 threads cap VGPRs at 128: shorter groups
 #undef HFA_FWD
     if (Smax <= 4 * kWideSeg) {  // the segmented form, up to 32768 states (the backtrack's 15-bit path entries)
+        if (t_begin != 1 || t_end < Tmax) {
+            hfa::set_error("hfa_viterbi_forward_steps: Smax=%d > 8192 runs whole lattices only", Smax);
+            return HFA_EINVAL;
+        }
         hipLaunchKernelGGL(viterbi_forward_wide_kernel, dim3(B), dim3(64 * kWideNW), 0, stream, Tmax, Smax, T, S,
                            prob3_pad_len, prob_log, not_edge_log, edge_log, curr, dp, bt, ph_seq_id);
         return hfa::check_launch("hfa_viterbi_forward");
     }
     hfa::set_error("hfa_viterbi_forward: Smax=%d exceeds 32768 states per utterance", Smax);
     return HFA_EINVAL;
+}
+
+int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S,
+                        const int32_t* prob3_pad_len, const float* prob_log, const float* not_edge_log,
+                        const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,
+                        hipStream_t stream) {
+    return hfa_viterbi_forward_steps(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log, edge_log, curr, dp,
+                                     bt, ph_seq_id, 1, Tmax > 1 ? Tmax : 1, stream);
 }
 
 int hfa_viterbi_tuning(int force_k) {

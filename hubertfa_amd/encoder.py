@@ -26,6 +26,11 @@ from .hubert import dev_lengths
 from .resample import Resampler, target_length
 
 
+def _g(gate) -> dict:
+    """The encoder's ``gate`` keyword, only when one is set."""
+    return {} if gate is None else {"gate": gate}
+
+
 def _load_tensors(path: str) -> dict:
     if path.endswith(".safetensors"):
         from safetensors.torch import load_file
@@ -124,7 +129,7 @@ class UnitsEncoder:
         return [target_length(int(n), sample_rate, self.encoder_sample_rate) for n in lengths]
 
     @torch.no_grad()
-    def units(self, audio: torch.Tensor, sample_rate: int, lengths=None) -> torch.Tensor:
+    def units(self, audio: torch.Tensor, sample_rate: int, lengths=None, gate=None) -> torch.Tensor:
         """[B, N] -> units [B, L, C].  ``lengths``: per-row sample counts of a zero-padded variable-length batch
         (every row's units then equal what that utterance gives alone)."""
         audio = audio.to(self.device).float()
@@ -134,7 +139,7 @@ class UnitsEncoder:
         if lengths is None:
             if audio_res.size(-1) < 400:   # reference pads the ORIGINAL audio here (encoder.py:51-52)
                 audio_res = torch.nn.functional.pad(audio, (0, 400 - audio_res.size(-1)))
-            return self.model(audio_res)          # rows with a pitch are fine (conv0 / normalise take row strides)
+            return self.model(audio_res, **_g(gate))   # rows with a pitch are fine (conv0 / normalise: row strides)
         lens16 = self.resampled_lengths(lengths, sample_rate)
         if min(lens16) < 400:
             raise ValueError("utterances shorter than 400 encoder samples take the reference's padding quirk "
@@ -142,10 +147,10 @@ class UnitsEncoder:
         audio_res = audio_res.contiguous()
         if any(n != audio_res.shape[-1] for n in lens16):   # the resampler's sinc tails spill past each row's end
             ops.mask_rows(audio_res, dev_lengths(lens16, audio_res.device))
-        return self.model(audio_res, lengths=lens16)
+        return self.model(audio_res, lengths=lens16, **_g(gate))
 
     @torch.no_grad()
-    def units_chunked(self, audio: torch.Tensor, chunk_frames: int, overlap_frames: int) -> torch.Tensor:
+    def units_chunked(self, audio: torch.Tensor, chunk_frames: int, overlap_frames: int, gate=None) -> torch.Tensor:
         """Long-form units of ONE utterance [1, N] at the encoder rate from overlapping windows (BASELINE config 5).
 
         Window k covers global Hubert frames [kC - O, (k+1)C + O) (C = chunk_frames, O = overlap_frames, clipped
@@ -162,7 +167,7 @@ class UnitsEncoder:
         L = m.frame_lengths(N)
         C, O = int(chunk_frames), int(overlap_frames)
         if L <= C + O:
-            return m(x.contiguous())
+            return m(x.contiguous(), **_g(gate))
         if m.arch.do_normalize:          # whole-utterance statistics (Wav2Vec2FeatureExtractor), not per window
             x = ops.wav_normalize(x.contiguous(), 1e-7)
         wins = plan_windows(L, C, O)
@@ -174,7 +179,7 @@ class UnitsEncoder:
             lo, hi = max(0, s0), min(N, s0 + n_win[i])
             if hi > lo:
                 batch[i, lo - s0:hi - s0] = xs[lo:hi]
-        units = m(batch, lengths=n_win, normalized=True)  # [K, Wmax, C]
+        units = m(batch, lengths=n_win, normalized=True, **_g(gate))  # [K, Wmax, C]
         idx = np.concatenate([i * units.shape[1] + np.arange(c0 - a, c1 - a) for i, (c0, c1, a, _) in
                               enumerate(wins)])
         flat = units.reshape(-1, units.shape[-1])
@@ -183,16 +188,17 @@ class UnitsEncoder:
 
     @torch.no_grad()
     def encode_frames(self, audio: torch.Tensor, sample_rate: int, hop_size: int, pad_to: int = 1, lengths=None,
-                      chunk_frames: int | None = None, overlap_frames: int = 100):
+                      chunk_frames: int | None = None, overlap_frames: int = 100, gate=None):
         """[B, N] -> (features [B, T_pad, C] channels-last, n_frames); rows >= n_frames are zero.
 
         With ``lengths`` (per-row sample counts of a zero-padded batch) n_frames is a list (one per row) and
-        rows >= n_frames[b] of row b are zero; T_pad covers the longest row."""
+        rows >= n_frames[b] of row b are zero; T_pad covers the longest row.  ``gate``: called before each
+        attention launch (HubertEncoder.attention_block)."""
         if chunk_frames is not None and lengths is None and audio.shape[0] == 1:
             audio_res = self._resample(audio.to(self.device).float(), sample_rate)
-            units = self.units_chunked(audio_res.contiguous(), chunk_frames, overlap_frames)
+            units = self.units_chunked(audio_res.contiguous(), chunk_frames, overlap_frames, gate=gate)
         else:
-            units = self.units(audio, sample_rate, lengths)
+            units = self.units(audio, sample_rate, lengths, gate=gate)
         if lengths is None:
             n_frames, ratio = self.grid(audio.shape[-1], sample_rate, hop_size)
             T_pad = (n_frames + pad_to - 1) // pad_to * pad_to

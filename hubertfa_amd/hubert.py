@@ -252,9 +252,12 @@ class HubertEncoder:
         return out
 
     def attention_block(self, h_in: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None,
-                        hs: torch.Tensor | None = None) -> torch.Tensor:
+                        hs: torch.Tensor | None = None, gate=None) -> torch.Tensor:
         """softmax(QK^T/sqrt(dh))V over the fused QKV projection.  Split precision: QKV written as split planes,
-        attention on the split kernel, O returned as split planes (the out-projection's A operand)."""
+        attention on the split kernel, O returned as split planes (the out-projection's A operand).  ``gate``
+        (optional callable) is called right before the attention launch: its grid runs several rounds, so work
+        another stream enqueues there (task.submit: a long lattice's DP range) costs it little, where beside a
+        one-round GEMM grid a held CU delays the whole launch."""
         a = self.arch
         B, L, H = (h_in if h_in is not None else hs[0]).shape      # h_in None: the input lives in its planes
         nh = a.heads
@@ -262,9 +265,13 @@ class HubertEncoder:
         if self.precision == "split" and L_.wqkv_s is not None and L_.wo_s is not None and dh == 64:
             qkv_s = self._linear(h_in, L_.wqkv, L_.wqkv_s, L_.bqkv, out_split=True, xs=hs)
             o_s = torch.empty((2, B, L, H), dtype=torch.float16, device=qkv_s.device)
+            if gate is not None:
+                gate()
             return ops.attention_split(qkv_s, o_s, B=B, H=nh, L=L, head_dim=dh, scale=dh ** -0.5, key_len=lens)
         qkv = self._linear(h_in, L_.wqkv, L_.wqkv_s, L_.bqkv)
         o = torch.empty((B, L, H), dtype=torch.float32, device=h_in.device)
+        if gate is not None:
+            gate()
         ops.attention(qkv, qkv[..., H:], qkv[..., 2 * H:], o, B=B, H=nh, L=L, head_dim=dh, scale=dh ** -0.5,
                       q_bs=L * 3 * H, q_ld=3 * H, k_bs=L * 3 * H, k_ld=3 * H, v_bs=L * 3 * H, v_ld=3 * H,
                       o_bs=L * H, o_ld=H, key_len=lens)
@@ -285,14 +292,15 @@ class HubertEncoder:
         return ops.layernorm(x, w, b, eps, out=out), None
 
     def layer(self, h: torch.Tensor, L_: _Layer, lens: torch.Tensor | None = None, hs: torch.Tensor | None = None,
-              want_split: bool = False):
+              want_split: bool = False, gate=None):
         """One encoder layer: (h, hs) -> (h', hs').  ``hs``: h's split planes if its producer wrote them;
-        ``want_split``: also return the output's planes (the next layer's QKV operand), else None."""
+        ``want_split``: also return the output's planes (the next layer's QKV operand), else None.  ``gate``: see
+        attention_block."""
         sp = self.precision == "split" and L_.w1_s is not None and L_.w2_s is not None
         if not self.arch.stable_layer_norm:   # post-LN (HubertEncoderLayer / nn.TransformerEncoderLayer)
             # split path: the residual stream rides in the LayerNorms' split planes (hi + 2^-11 lo, 22 significand
             # bits, the precision every split GEMM operand has): no f32 LayerNorm output is written or read back
-            o = self.attention_block(h, L_, lens, hs)
+            o = self.attention_block(h, L_, lens, hs, gate=gate)
             res = hs if (hs is not None and L_.wo_s is not None and self.precision == "split") else h
             h1 = self._out_proj(o, L_, res)
             h1, h1s = self._ln(h1, L_.ln1_w, L_.ln1_b, out=h1, split=sp, planes_only=sp)
@@ -305,7 +313,7 @@ class HubertEncoder:
         q_planes = (self.precision == "split" and L_.wqkv_s is not None and L_.wo_s is not None and
                     self.arch.hidden // self.arch.heads == 64)
         a_, a_s = self._ln(h, L_.ln1_w, L_.ln1_b, split=L_.wqkv_s is not None, planes_only=q_planes)
-        o = self.attention_block(a_, L_, lens, a_s)
+        o = self.attention_block(a_, L_, lens, a_s, gate=gate)
         h = self._out_proj(o, L_, h)
         a_, a_s = self._ln(h, L_.ln2_w, L_.ln2_b, split=sp, planes_only=sp)
         f = self._linear(a_, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp, xs=a_s)
@@ -315,7 +323,7 @@ class HubertEncoder:
 
     @torch.no_grad()
     def forward(self, wav: torch.Tensor, n_layers: int | None = None, lengths=None,
-                normalized: bool = False) -> torch.Tensor:
+                normalized: bool = False, gate=None) -> torch.Tensor:
         """wav [B, N] -> units [B, L, C].  ``lengths`` (optional, host ints [B]): samples per row of a
         variable-length batch (rows zero-padded to N); row b's units are valid for frame_lengths(lengths[b])
         frames and equal what that utterance gives alone.  ``normalized``: the caller already applied the
@@ -357,7 +365,8 @@ class HubertEncoder:
             h, hs = self._ln(h, self.enc_ln[0], self.enc_ln[1], out=h, split=bool(layers), planes_only=first)
         for i, L_ in enumerate(layers):
             nxt = i + 1 < len(layers)
-            h, hs = self.layer(h, L_, lensL, hs, want_split=nxt and (a.stable_layer_norm or planes_in(layers[i + 1])))
+            h, hs = self.layer(h, L_, lensL, hs, want_split=nxt and (a.stable_layer_norm or planes_in(layers[i + 1])),
+                               gate=gate)
         if a.stable_layer_norm:
             h = ops.layernorm(h, self.enc_ln[0], self.enc_ln[1], a.layer_norm_eps, out=h)
         if self.proj is not None:

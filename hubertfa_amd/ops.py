@@ -37,11 +37,12 @@ def _need(t: torch.Tensor, dtype, name: str, contiguous: bool = True):
 # ------------------------------------------------------------------------------------------------------------
 # Alignment decoder (viterbi.hip)
 # ------------------------------------------------------------------------------------------------------------
-def viterbi_forward(prob_log, not_edge_log, edge_log, curr, dp, bt, ph_seq_id, T, S, pad=None):
+def viterbi_forward(prob_log, not_edge_log, edge_log, curr, dp, bt, ph_seq_id, T, S, pad=None, steps=None):
     """In-place batched forward_pass (alignment_decoder.py:170-230).
 
     prob_log/dp [B,Tmax,Smax] f32 (dp row 0 pre-initialised), bt [B,Tmax,Smax] int8, curr [B,Smax] f64,
-    not_edge_log/edge_log [B,Tmax] f32, ph_seq_id [B,Smax] i32, T/S/pad [B] i32.
+    not_edge_log/edge_log [B,Tmax] f32, ph_seq_id [B,Smax] i32, T/S/pad [B] i32.  ``steps`` (t_begin, t_end):
+    only those time steps, continuing from dp row t_begin - 1 and curr (consecutive ranges = one whole call).
     """
     B, Tmax, Smax = prob_log.shape
     for t, dt, n in ((prob_log, torch.float32, "prob_log"), (not_edge_log, torch.float32, "not_edge_log"),
@@ -55,11 +56,13 @@ def viterbi_forward(prob_log, not_edge_log, edge_log, curr, dp, bt, ph_seq_id, T
     assert curr.shape == (B, Smax) and ph_seq_id.shape == (B, Smax)
     assert not_edge_log.shape == (B, Tmax) and edge_log.shape == (B, Tmax)
 
+    t0, t1 = (1, max(Tmax, 1)) if steps is None else (int(steps[0]), int(steps[1]))
+
     def launch():
-        _lib.call("hfa_viterbi_forward", B, Tmax, Smax, _ptr(T), _ptr(S), _ptr(pad), _ptr(prob_log),
-                  _ptr(not_edge_log), _ptr(edge_log), _ptr(curr), _ptr(dp), _ptr(bt), _ptr(ph_seq_id),
+        _lib.call("hfa_viterbi_forward_steps", B, Tmax, Smax, _ptr(T), _ptr(S), _ptr(pad), _ptr(prob_log),
+                  _ptr(not_edge_log), _ptr(edge_log), _ptr(curr), _ptr(dp), _ptr(bt), _ptr(ph_seq_id), t0, t1,
                   _stream(prob_log.device))
-    if PROBE is None:
+    if PROBE is None or steps is not None:
         return launch()
     # SURVEY §8(d) algorithmic bytes: prob_log in + dp out (4 B each) + bt out (1 B) per cell, 8 B edge terms
     # per frame; counted on the padded planes (exact when every utterance of the batch fills them).

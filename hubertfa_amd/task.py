@@ -124,7 +124,7 @@ class ForcedAlignmentTask:
 
     @torch.no_grad()
     def encode_batch(self, waves: torch.Tensor, wav_sr: int | None = None, lengths=None,
-                     chunk_seconds: float | None = None):
+                     chunk_seconds: float | None = None, gate=None):
         """Device half 1 (current stream): waves [B, N] -> (features [B, T_pad, C], DP frames, wav lengths).
 
         ``lengths`` (optional host ints [B]): samples per row of a variable-length batch, rows zero-padded to N
@@ -147,7 +147,7 @@ class ForcedAlignmentTask:
         n = waves.shape[-1]
         chunk = None if chunk_seconds is None else max(1, int(round(chunk_seconds * 50)))
         feats, n_frames = self.unitsEncoder.encode_frames(waves, sr, hop, pad_to=self.head.divisible,
-                                                          lengths=lengths, chunk_frames=chunk)
+                                                          lengths=lengths, chunk_frames=chunk, gate=gate)
         wl = [n / sr] * waves.shape[0] if lengths is None else [int(m) / sr for m in lengths]
         return feats, n_frames, wl
 
@@ -163,18 +163,20 @@ class ForcedAlignmentTask:
             flag = ops.flag_take(self.head.flag)
         return logits, flag
 
-    def lattice_dp(self, logits, flag, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
-        """Lattice prologue + Viterbi + backtrack (current stream) -> the decoder's device outputs."""
+    def lattice_dp(self, logits, flag, wav_lengths, ph_seqs, word_seqs=None, p2ws=None, dp_ranges=None):
+        """Lattice prologue + Viterbi + backtrack (current stream) -> the decoder's device outputs (with
+        ``dp_ranges``, possibly the DP left as deferred steps: AlignmentDecoder.decode_batch)."""
         frame, edge = logits[:, :, 2:], logits[:, :, 0]      # LatticeHead.split without the unused ctc logits
-        dev_out = self.decoder.decode_batch(frame, edge, wav_lengths, ph_seqs, word_seqs, p2ws, host=False)
+        dev_out = self.decoder.decode_batch(frame, edge, wav_lengths, ph_seqs, word_seqs, p2ws, host=False,
+                                            dp_ranges=dp_ranges)
         if flag is not None:
             dev_out["split_oflow_head"] = flag
         return dev_out
 
-    def decode_device(self, feats, n_frames, wav_lengths, ph_seqs, word_seqs=None, p2ws=None):
+    def decode_device(self, feats, n_frames, wav_lengths, ph_seqs, word_seqs=None, p2ws=None, dp_ranges=None):
         """Device half 2 (current stream): UNet head + lattice + Viterbi -> the decoder's device outputs."""
         logits, flag = self.head_logits(feats, n_frames)
-        return self.lattice_dp(logits, flag, wav_lengths, ph_seqs, word_seqs, p2ws)
+        return self.lattice_dp(logits, flag, wav_lengths, ph_seqs, word_seqs, p2ws, dp_ranges)
 
     def _guard(self, dev_out, redo_args):
         """Split-precision range guard: snapshot (and clear) the split-f16 overflow flag the batch's producers
@@ -233,25 +235,103 @@ class ForcedAlignmentTask:
         waits for it, so a batch's small-grid tail (UNet GEMMs on a few hundred workgroups, one DP workgroup per
         utterance) overlaps the next batch's extractor instead of idling most of the chip.  (Enqueuing the side
         pass in steps at the next encoder's FFN2 launches, whose one round of tiles leaves CUs idle, measured 13 %
-        slower: the steps spill into the full-chip kernels that follow)  ``on_device`` (e.g. the
-        RCCL boundary gather) runs on the side stream after the backtrack."""
+        slower: the steps spill into the full-chip kernels that follow)  A long lattice
+        (``defer_dp_frames``) is the exception: its forward DP holds one CU for milliseconds, and every one-round
+        GEMM grid it overlaps waits for the tile that CU could not start, so its DP is held back and run in step
+        ranges, one right before each attention launch of the NEXT batch's encoder (multi-round grids), the rest
+        when the next encoder has been enqueued or when the handle is assembled (config 5: the DP's cost to the
+        encoder 2.4 -> 0.5 ms, profiles/r04/dp_gate_ab.txt).  ``on_device`` (e.g. the RCCL boundary gather) runs
+        on the side stream after the backtrack."""
         main = torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
-        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds)
+        held, self._held = getattr(self, "_held", None), None
+        feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds,
+                                                gate=held.gate(main) if held is not None else None)
+        if held is not None:
+            held.flush()
         guard = self._guard({}, (waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds))
         ready = torch.cuda.Event()
         ready.record(main)
         with torch.cuda.stream(self._side):
             self._side.wait_event(ready)
             feats.record_stream(self._side)      # the caching allocator must not recycle it under the side stream
-            dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws)
+            dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws,
+                                         dp_ranges=self.dp_ranges if chunk_seconds is None else None)
             if "split_oflow" in guard:
                 guard["split_oflow"].record_stream(self._side)
             dev_out.update(guard)
-            if on_device is not None:
-                on_device(dev_out)
-            return self.decoder.fetch(dev_out)
+            work = _HeldDP(self, dev_out, on_device)
+            if work.steps:
+                self._held = work
+            else:
+                work.complete()
+            return work.handle
+
+    # a lattice of at least this many DP frames (config 5's 300 s: 25 839) runs its forward DP beside the next
+    # batch's attention launches, one step range per encoder layer; None: never.  A range must fit in one
+    # attention launch: the DP's steps grow with the wave's length L, the attention's time with L^2, and at
+    # 16 384 frames (~190 s) a twelfth of the DP (~0.7 ms) is about one unchunked attention launch.  Windowed
+    # long-form (chunk_seconds) never holds: its attention launches are far shorter (profiles/r04/held_dp_ab.txt)
+    defer_dp_frames = 16384
+
+    def dp_ranges(self, Tmax: int, Smax: int) -> int:
+        """How many step ranges submit() cuts a batch's forward DP into (1: one launch, now)."""
+        n_layers = len(getattr(self.unitsEncoder.model, "layers", ()))
+        if self.defer_dp_frames is None or Tmax < self.defer_dp_frames or n_layers < 2:
+            return 1
+        return n_layers
+
+    def flush(self):
+        """Enqueue a held batch's remaining DP steps now (the pipeline's last batch; assemble also does this)."""
+        held, self._held = getattr(self, "_held", None), None
+        if held is not None:
+            held.flush()
+
+
+class _HeldDP:
+    """A batch's deferred forward-DP ranges + backtrack (AlignmentDecoder.decode_batch ``deferred``) and the
+    completion after them: ``on_device``, then the D2H fetch whose handle ``submit`` returned early (its "resolve"
+    entry, which ``decoder.assemble`` calls, runs whatever is still held)."""
+
+    def __init__(self, task, dev_out, on_device):
+        self.task, self.dev_out, self.on_device = task, dev_out, on_device
+        self.steps = dev_out.pop("deferred", [])
+        self.handle = {"resolve": self.flush}
+
+    def complete(self):
+        """(side stream) the batch's outputs are enqueued: run on_device and the fetch; fill the handle."""
+        if self.on_device is not None:
+            self.on_device(self.dev_out)
+        h = self.task.decoder.fetch(self.dev_out)
+        self.handle.pop("resolve", None)
+        self.handle.update(h)
+
+    def _next(self):
+        self.steps.pop(0)()
+        if not self.steps:
+            self.complete()
+
+    def gate(self, main):
+        """The next encoder's attention gate: the side stream waits for the main stream to reach the launch, then
+        takes the next step."""
+        side = self.task._side
+
+        def g():
+            if self.steps:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                with torch.cuda.stream(side):
+                    side.wait_event(ev)
+                    self._next()
+        return g
+
+    def flush(self):
+        with torch.cuda.stream(self.task._side):
+            while self.steps:
+                self._next()
+        if getattr(self.task, "_held", None) is self:
+            self.task._held = None
 
 
 def synth_checkpoint(path: str | None = None, *, encoder="cnhubert", model_path="synth:0", seed=1,

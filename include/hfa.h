@@ -61,6 +61,15 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
                         const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,
                         hipStream_t stream);
 
+/* The same DP over time steps [t_begin, t_end) only (t_begin >= 1; clipped to each utterance's T[b]): it continues
+ * from dp row t_begin - 1 and from curr, and leaves curr for the next range, so consecutive ranges give the bits of
+ * one whole call.  Lets the caller cut a long lattice (config 5: 25 839 steps, 13 ms on one CU) into pieces that
+ * run beside the next batch's attention kernels.  Smax > 8192 (the segmented-state form): whole ranges only. */
+int hfa_viterbi_forward_steps(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S,
+                              const int32_t* prob3_pad_len, const float* prob_log, const float* not_edge_log,
+                              const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,
+                              int t_begin, int t_end, hipStream_t stream);
+
 /* Tuning hook (tests, benchmarks): states per lane of the multi-wave forward DP, 2 / 4 / 8, 0 = automatic (4 up
  * to 4096 states, then 8); the same bits whatever the choice. */
 int hfa_viterbi_tuning(int force_k);

@@ -50,6 +50,12 @@ int main() {
     CHECK(hfa_viterbi_forward(-1, 10, 8, ip, ip, nullptr, fp, fp, fp, dp, fp, bp, ip, st), "viterbi B<0");
     CHECK(hfa_viterbi_forward(2, 10, 9000, ip, ip, nullptr, fp, fp, fp, dp, fp, bp, ip, st), "viterbi Smax");
     CHECK(hfa_viterbi_forward(2, 10, 8, nullptr, ip, nullptr, fp, fp, fp, dp, fp, bp, ip, st), "viterbi NULL T");
+    CHECK(hfa_viterbi_forward_steps(2, 10, 8, ip, ip, nullptr, fp, fp, fp, dp, fp, bp, ip, 0, 5, st),
+          "viterbi steps t_begin 0");
+    CHECK(hfa_viterbi_forward_steps(2, 10, 8, ip, ip, nullptr, fp, fp, fp, dp, fp, bp, ip, 6, 5, st),
+          "viterbi steps reversed");
+    CHECK(hfa_viterbi_forward_steps(2, 10, 9000, ip, ip, nullptr, fp, fp, fp, dp, fp, bp, ip, 2, 5, st),
+          "viterbi steps wide partial");
     g_sentinel[0] = 0;
     expect_err(hfa_viterbi_tuning(3), "viterbi tuning k=3");   // the sentinel call itself
     CHECK(hfa_viterbi_backtrack(2, 70000, 8, ip, ip, fp, bp, ip, nullptr, nullptr, nullptr, fp, st),

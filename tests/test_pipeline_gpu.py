@@ -68,3 +68,38 @@ def test_smoke_entry():
     from hubertfa_amd.smoke import run_smoke
     r = run_smoke()
     assert r["boundary_exact"] == r["utterances"]
+
+
+def test_pipelined_long_lattice_dp_held_for_next_encoder():
+    """task.submit holds a long lattice's forward DP (defer_dp_frames) and runs it in step ranges beside the next
+    batch's attention launches: three 120 s utterances pipelined (the first two held and run under the next
+    encoder, the last one flushed by assemble) give the boundaries, confidences and edge terms of align_batch on
+    each alone, bit for bit.  Also a held handle assembled before any further submit, and windowed long-form
+    (chunk_seconds), which never holds."""
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+    dev = torch.device("cuda")
+    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
+    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
+    task.on_predict_start()
+    task.defer_dp_frames = 8192          # (the shipped 16 384 needs ~190 s utterances; the mechanism is the same)
+    batches = [_inputs(1, 120.0, 240, 900 + i) for i in range(3)]
+    alone = []
+    for wav, ph, ws, pw in batches:
+        alone.append(task.align_batch(torch.from_numpy(wav).to(dev), ph, ws, pw, wav_sr=16000)[0])
+    T = alone[0]["T"]
+    assert T >= task.defer_dp_frames and task.dp_ranges(T + 1, 512) > 1
+    handles = []
+    for wav, ph, ws, pw in batches:
+        handles.append(task.submit(torch.from_numpy(wav).to(dev), ph, ws, pw, wav_sr=16000))
+        assert "resolve" in handles[-1]                     # held: its DP runs under the next submit / assemble
+    got = [task.decoder.assemble(h, *b[1:])[0] for h, b in zip(handles, batches)]
+    h = task.submit(torch.from_numpy(batches[0][0]).to(dev), *batches[0][1:], wav_sr=16000)
+    got.append(task.decoder.assemble(h, *batches[0][1:])[0])
+    for i, (g, a) in enumerate(zip(got, alone + alone[:1])):
+        for k in ("ph_idx_seq", "ph_time_int", "frame_confidence", "edge_diff"):
+            assert np.array_equal(np.asarray(g[k]), np.asarray(a[k])), f"batch {i}: {k}"
+        assert list(g["ph_seq"]) == list(a["ph_seq"])
+        assert np.array_equal(np.asarray(g["ph_intervals"]), np.asarray(a["ph_intervals"])), f"batch {i}"
+    hc = task.submit(torch.from_numpy(batches[1][0]).to(dev), *batches[1][1:], wav_sr=16000, chunk_seconds=20.0)
+    assert "resolve" not in hc
+    task.decoder.assemble(hc, *batches[1][1:])

@@ -72,6 +72,73 @@ def test_forward_batched_bit_exact():
         np.testing.assert_allclose(fc[b, :Ts[b]], z[p + "frame_confidence"], rtol=2e-6, atol=0, equal_nan=True)
 
 
+def test_forward_step_ranges_bit_exact():
+    """hfa_viterbi_forward_steps: the DP cut into consecutive time-step ranges (the pipeline runs a long lattice in
+    pieces beside the next batch's attention kernels) gives the one-call bits.  The 45 reference lattices batched
+    (ragged T: cuts fall past some utterances' ends, one range is a single step), and a multi-wave lattice
+    (S = 1801, 8 waves) in 12 ranges against the pinned C oracle."""
+    from hubertfa_amd import ops
+    from oracle import decode as od
+    z, n = _cases()
+    lats = [_lattice(z, c) for c in range(n)]
+    B = n
+    Tmax = max(l[1][4].shape[0] for l in lats)
+    Smax = max(l[1][4].shape[1] for l in lats)
+    pl = np.zeros((B, Tmax, Smax), np.float32)
+    E = np.zeros((B, Tmax), np.float32)
+    nE = np.zeros((B, Tmax), np.float32)
+    cu = np.full((B, Smax), -np.inf)
+    dp = np.full((B, Tmax, Smax), -np.inf, np.float32)
+    ids = np.zeros((B, Smax), np.int32)
+    Ts, Ss = [], []
+    for b, (i, (p, e, ne, c0, d0, _, _)) in enumerate(lats):
+        T, S = d0.shape
+        Ts.append(T); Ss.append(S)
+        pl[b, :T, :S] = p; E[b, :T] = e; nE[b, :T] = ne; cu[b, :S] = c0; dp[b, :T, :S] = d0; ids[b, :S] = i
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    dp_t, cu_t = t(dp), t(cu)
+    bt_t = torch.full((B, Tmax, Smax), -1, dtype=torch.int8, device=dev)
+    T_t = torch.tensor(Ts, dtype=torch.int32, device=dev)
+    S_t = torch.tensor(Ss, dtype=torch.int32, device=dev)
+    cuts = sorted({1, 37, 200, 201, min(Ts) + 3, Tmax // 2, Tmax})
+    for a, c in zip(cuts[:-1], cuts[1:]):
+        ops.viterbi_forward(t(pl), t(nE), t(E), cu_t, dp_t, bt_t, t(ids), T_t, S_t, steps=(a, c))
+    dp_h, bt_h, cu_h = dp_t.cpu().numpy(), bt_t.cpu().numpy(), cu_t.cpu().numpy()
+    for b in range(B):
+        p = f"c{b}_"
+        T, S = Ts[b], Ss[b]
+        assert np.array_equal(dp_h[b, :T, :S].view(np.int32), z[p + "dp"].view(np.int32)), f"dp case {b}"
+        assert np.array_equal(bt_h[b, 1:T, :S], z[p + "bt"][1:]), f"bt case {b}"
+        assert np.array_equal(cu_h[b, :S].view(np.int64), z[p + "curr"].view(np.int64)), f"curr case {b}"
+
+    T, S, V = 3000, 1801, 63
+    r = np.random.default_rng(5)
+    ids1 = r.integers(1, V, S).astype(np.int64)
+    ids1[::3] = 0
+    ids1[0] = ids1[-1] = 0
+    lp = torch.log_softmax(torch.from_numpy((3 * r.standard_normal((T, V))).astype(np.float32)), -1).numpy()
+    pl1, E1, nE1, cu1, dp1, bt1, pad = od.lattice_inputs(ids1, lp, np.clip(r.uniform(-0.2, 1.2, T), 0, 1))
+    d_ref, b_ref, c_ref = od.forward_pass(T, S, pl1, nE1, E1, cu1.copy(), dp1.copy(), bt1.copy(), ids1, pad)
+    P = -(-S // 8) * 8
+
+    def padded(a, fill):
+        out = np.full(a.shape[:-1] + (P,), fill, dtype=a.dtype)
+        out[..., :S] = a
+        return out
+    t1 = lambda a: t(a)[None]
+    dp_t, cu_t = t1(padded(dp1, -np.inf)), t1(padded(cu1, -np.inf))
+    bt_t = torch.full((1, T, P), -1, dtype=torch.int8, device=dev)
+    Tt, St = (torch.tensor([v], dtype=torch.int32, device=dev) for v in (T, S))
+    edges = np.linspace(1, T, 13).astype(int)
+    for a, c in zip(edges[:-1], edges[1:]):
+        ops.viterbi_forward(t1(padded(pl1, 0.0)), t1(nE1), t1(E1), cu_t, dp_t, bt_t, t1(padded(ids1.astype(np.int32), 0)),
+                            Tt, St, steps=(a, c))
+    assert np.array_equal(dp_t[0, :, :S].cpu().numpy().view(np.int32), d_ref.view(np.int32))
+    assert np.array_equal(bt_t[0, 1:, :S].cpu().numpy().astype(np.int32), b_ref[1:])
+    assert np.array_equal(cu_t[0, :S].cpu().numpy().view(np.int64), c_ref.view(np.int64))
+
+
 @pytest.mark.parametrize("T,S,force_k,pitch8", [(700, 300, 0, False), (1200, 513, 0, False), (3000, 1801, 0, False),
                                                 (2500, 4100, 0, False), (4200, 8000, 0, False),
                                                 (3000, 1801, 0, True), (1200, 513, 2, True), (3000, 1801, 2, True),
