@@ -171,28 +171,30 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
     # zero-padded and aligned with per-row lengths, which keeps every utterance's result identical to aligning it
     # alone (the reference's B=1); files too short for the encoder's 400-sample window are aligned alone.
     # One batch in flight: the host assembles batch i while the GPU runs batch i+1 (task.submit: encoder on the
-    # main stream, head + Viterbi on a side stream).
+    # main stream, head + Viterbi on a side stream).  A batch whose DP task.submit holds for the next encoder's
+    # attention launches (long files) completes only under that encoder, so it stays pending one batch longer
+    # (as in bench.py): waiting for it right after the next submit would idle the GPU.
     plan = plan_batches([(k, it[1], it[2]) for k, it in items.items()], batch_size, sr,
                         task.unitsEncoder.encoder_sample_rate)
-    pending = None
+    pending = []
     for file_sr, ks in plan:
         job, err = None, None
         try:
             job = run(ks, file_sr)
         except recoverable as e:
             err = e
-        if pending is not None:
-            settle(pending)
-            pending = None
+        depth = 2 if job is not None and "resolve" in job[0] else 1
+        while len(pending) >= depth:
+            settle(pending.pop(0))
         if job is not None:
-            pending = job
+            pending.append(job)
         elif len(ks) == 1:
             errors.append([items[ks[0]][0], err])
         else:
             for k in ks:
                 alone(k, file_sr)
-    if pending is not None:
-        settle(pending)
+    while pending:
+        settle(pending.pop(0))
     return out
 
 

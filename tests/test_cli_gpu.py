@@ -87,6 +87,43 @@ def test_pipelined_predict_repeatable(tmp_path):
         assert got == ref, f"rep {rep}: {[n for n in got if got[n] != ref[n]]} differ"
 
 
+def test_predict_long_files_held_dp(tmp_path):
+    """The CLI's loop with long files whose DP task.submit holds for the next encoder (threshold lowered so 50-100 s
+    files qualify), short ones between them (not held: the loop's depth switches 1 <-> 2), one file per batch: the
+    records equal those of the same run with nothing held."""
+    import infer
+    import hubertfa_amd.g2p as g2p_mod
+    import torch
+    from hubertfa_amd import synth
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+    from hubertfa_amd.wav_io import write_wav
+    d = synth.synth_dictionary(n_words=40)
+    dpath = tmp_path / "dict.txt"
+    dpath.write_text("".join(f"{w}\t{' '.join(p)}\n" for w, p in d.items()))
+    seg = tmp_path / "segments"
+    seg.mkdir()
+    for i, secs in enumerate((100.0, 2.0, 60.0, 50.0, 3.0)):
+        write_wav(seg / f"u{i}.wav", synth.synth_audio(int(secs * 16000), seed=i), 16000)
+        (seg / f"u{i}.lab").write_text(synth.synth_lab(max(5, int(secs)), d, seed=i))
+    ck = tmp_path / "m.ckpt"
+    synth_checkpoint(str(ck))
+    g = g2p_mod.DictionaryG2P(dictionary=str(dpath))
+    g.set_in_format("lab")
+    rows = list(g.get_dataset(sorted(seg.rglob("*.wav"))))
+    torch.set_grad_enabled(False)
+    task = ForcedAlignmentTask.load_from_checkpoint(str(ck), device=torch.device("cuda"), hubert_model_path="synth:0")
+
+    def key(records):
+        return {k: (np.asarray(r["ph_time_int"]).tobytes(), np.asarray(r["frame_confidence"]).tobytes(),
+                    np.asarray(r["edge_diff"]).tobytes()) for k, r in records.items()}
+    keys = list(range(len(rows)))
+    task.defer_dp_frames = None
+    ref = key(infer._predict(task, rows, keys, 1, []))
+    task.defer_dp_frames = 4096
+    got = key(infer._predict(task, rows, keys, 1, []))
+    assert len(ref) == len(rows) and got == ref, [n for n in got if got[n] != ref.get(n)]
+
+
 def _mixed_folder(tmp_path):
     """Mixed lengths and two sample rates (16 kHz / 22.05 kHz) -> (segments dir, dictionary, checkpoint)."""
     from hubertfa_amd import synth
