@@ -42,21 +42,18 @@ __device__ __forceinline__ float from_lane_below(float v) {
 // refill just issued included) at the top of each group — the prefetch did nothing and each group paid a full
 // memory round trip.  E and nE of a group are one vector load each (lane u holds step t0 + u) broadcast per step
 // with v_readlane, instead of two scalar loads per step whose lgkmcnt(0) waits also catch the refills.
-template <int K, int NW, int G, int R, bool VEC, int U = 1>
-__global__ __launch_bounds__(64 * NW * U) void viterbi_forward_kernel(
+template <int K, int NW, int G, int R, bool VEC>
+__global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
     const int32_t* __restrict__ padv, const float* __restrict__ prob_log,
     const float* __restrict__ not_edge_log, const float* __restrict__ edge_log, double* __restrict__ curr_io,
-    float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id, int t_begin, int t_end, int nb) {
+    float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id, int t_begin, int t_end) {
     static_assert(NW == 1 || K >= 2, "multi-wave DP needs >= 2 states per lane");
     static_assert(G <= 64 && R >= 2, "a group's E / nE fit one wave's lanes; at least two groups in flight");
     __shared__ float xq[2][NW][2];
-    static_assert(U == 1 || NW == 1, "several utterances per workgroup: one wave each");
-    const int b = blockIdx.x * U + (U > 1 ? (int)(threadIdx.x >> 6) : 0);   // U > 1: wave u runs utterance b
-    const int g = U > 1 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+    const int b = blockIdx.x;
+    const int g = threadIdx.x;
     const int lane = g & 63, wave = g >> 6;
-    if (b >= nb) return;                        // (U > 1: the last workgroup's spare waves)
-
     const int T = Tv[b];
     const int S = Sv[b];
     // time steps [t0, te) of this utterance (a range call continues from dp row t0 - 1 and from curr)
@@ -608,7 +605,6 @@ __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
 }
 
 thread_local int g_force_k = 0;   // hfa_viterbi_tuning: states per lane of the multi-wave DP (0 = automatic)
-thread_local int g_upw = 1;       // A/B: utterances per workgroup of the one-wave DP
 
 template <int K, int NW, int G, int R>
 int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S, const int32_t* pad,
@@ -616,24 +612,12 @@ int launch_forward(int B, int Tmax, int Smax, const int32_t* T, const int32_t* S
                    const int32_t* ids, int t_begin, int t_end, hipStream_t st) {
     const bool vec = Smax % K == 0 && ((uintptr_t)prob_log % 16 == 0) && ((uintptr_t)dp % 16 == 0) &&
                      ((uintptr_t)bt % 8 == 0);
-#define HFA_FWD_U(U)                                                                                             \
-    do {                                                                                                         \
-        const int nwg = (B + (U) - 1) / (U);                                                                     \
-        if (vec)                                                                                                 \
-            hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, true, U>), dim3(nwg), dim3(64 * NW * (U)), 0, \
-                               st, Tmax, Smax, T, S, pad, prob_log, nE, E, curr, dp, bt, ids, t_begin, t_end, B);  \
-        else                                                                                                     \
-            hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, false, U>), dim3(nwg), dim3(64 * NW * (U)), 0, \
-                               st, Tmax, Smax, T, S, pad, prob_log, nE, E, curr, dp, bt, ids, t_begin, t_end, B);  \
-    } while (0)
-    if constexpr (NW == 1) {
-        if (g_upw == 4) HFA_FWD_U(4);
-        else if (g_upw == 2) HFA_FWD_U(2);
-        else HFA_FWD_U(1);
-    } else {
-        HFA_FWD_U(1);
-    }
-#undef HFA_FWD_U
+    if (vec)
+        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, true>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
+                           S, pad, prob_log, nE, E, curr, dp, bt, ids, t_begin, t_end);
+    else
+        hipLaunchKernelGGL((viterbi_forward_kernel<K, NW, G, R, false>), dim3(B), dim3(64 * NW), 0, st, Tmax, Smax, T,
+                           S, pad, prob_log, nE, E, curr, dp, bt, ids, t_begin, t_end);
     return hfa::check_launch("hfa_viterbi_forward");
 }
 
@@ -713,10 +697,6 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
 }
 
 int hfa_viterbi_tuning(int force_k) {
-    if (force_k >= 200) {
-        g_upw = force_k - 200;
-        return HFA_OK;
-    }
     if (force_k != 0 && force_k != 2 && force_k != 4 && force_k != 8) {
         hfa::set_error("hfa_viterbi_tuning: states per lane must be 0 (automatic), 2, 4 or 8 (got %d)", force_k);
         return HFA_EINVAL;

@@ -1,5 +1,5 @@
 """One-wave Viterbi forward with U utterances per workgroup (U waves, one per SIMD; hfa_viterbi_tuning(200 + U) in
-this A/B build): the DP holds B/U CUs instead of B while it runs beside the encoder.  Config-2 geometry by default;
+viterbi.hip of commit c574cbc, reverted): the DP holds B/U CUs instead of B while it runs beside the encoder.  Config-2 geometry by default;
 encoder alone, then encoder + the DP in one launch beside it, for U = 1, 2, 4 (twice), dp / bt / curr checked
 bit-identical to U = 1.
     python scripts/dp_upw_ab.py [--batch 32 --seconds 10 --words 30]"""
