@@ -186,8 +186,9 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
                         long long q_bs, int q_ld, const uint16_t* k, long long k_sp, long long k_bs, int k_ld,
                         const uint16_t* v, long long v_sp, long long v_bs, int v_ld, uint16_t* o, long long o_sp,
                         long long o_bs, int o_ld, const int32_t* key_len, hipStream_t stream);
-/* Waves (x 32 queries) per workgroup of hfa_attention_split: 4 or 8, 0 = automatic (8 for L >= 512).  Results
- * do not depend on it (every query row sees the same tiles in the same order). */
+/* Waves (x 32 queries) per workgroup of hfa_attention_split: 4 or 8, 0 = automatic (the form whose grid gives the
+ * busiest CU fewer query rows; on a tie 8 from 2048 keys).  Results do not depend on it (every query row sees the
+ * same tiles in the same order). */
 int hfa_attention_split_tuning(int waves);
 
 /* ---- normalisation (hubertfa_amd/csrc/norm.hip); act: 0 none, 1 erf-GELU, 2 Hardswish -----------------------

@@ -2,7 +2,7 @@
 so a longer row means fewer, longer query blocks per (batch, head).  What the L = 499 point loses against the long
 rows is the per-block cost (prologue loads, epilogue stores, the padded last tile).  ``--modes``:
 hfa_attention_split_tuning values to compare (0 = automatic, 4 / 8 waves).
-    python scripts/attn_len_sweep.py [--reps 200] [--modes 0,4,8]"""
+    python scripts/attn_len_sweep.py [--reps 200] [--modes 0,4,8] [--lengths 499,14999]"""
 import argparse
 import math
 import os
@@ -20,13 +20,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--modes", default="0")
+    ap.add_argument("--lengths", default="499,704,998,1411,1996,3992,7984",
+                    help="row lengths (B = 32 x 499^2 / L^2, at least 1); 14999 = config 5's 300 s utterance")
+    ap.add_argument("--batch", type=int, default=0, help="fixed batch instead of equal work (0: equal work)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     H, dh = 12, 64
     work = 32 * 499 * 499
     g = torch.Generator(device=dev).manual_seed(0)
-    for L in (499, 704, 998, 1411, 1996, 3992, 7984):
-        B = max(1, round(work / (L * L)))
+    for L in (int(v) for v in a.lengths.split(",")):
+        B = a.batch if a.batch > 0 else max(1, round(work / (L * L)))
         x = torch.randn(B, L, 3 * H * dh, device=dev, generator=g) * 0.5
         qs = ops.split(x)
         o = torch.empty(2, B, L, H * dh, dtype=torch.float16, device=dev)
