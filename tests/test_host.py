@@ -488,3 +488,21 @@ def test_bench_thread_cpu_breakdown():
     th.join()
     rows = bench.thread_cpu_diff(a, b, 1)
     assert dict(rows).get("main", 0) >= 100 and any(n != "main" and ms >= 100 for n, ms in rows), rows
+
+
+def test_held_dp_policy():
+    """task.submit's policy for holding a batch's forward DP (ForcedAlignmentTask.dp_ranges): one range per encoder
+    layer from defer_dp_frames DP frames on (config 5's 300 s: 25 839 frames, 12 layers), one launch below it, for a
+    one-layer encoder, or when holding is switched off."""
+    from types import SimpleNamespace
+    from hubertfa_amd.task import ForcedAlignmentTask
+
+    def task(layers, defer=ForcedAlignmentTask.defer_dp_frames):
+        return SimpleNamespace(defer_dp_frames=defer,
+                               unitsEncoder=SimpleNamespace(model=SimpleNamespace(layers=[None] * layers)))
+    rng = ForcedAlignmentTask.dp_ranges
+    assert ForcedAlignmentTask.defer_dp_frames == 16384
+    assert rng(task(12), 25840, 1808) == 12 and rng(task(24), 25840, 1808) == 24
+    assert rng(task(12), 16384, 96) == 12 and rng(task(12), 16383, 96) == 1
+    assert rng(task(12), 862, 96) == 1                      # config 2
+    assert rng(task(1), 25840, 1808) == 1 and rng(task(12, None), 25840, 1808) == 1
