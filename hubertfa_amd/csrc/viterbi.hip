@@ -16,6 +16,8 @@
 // batch spreads over CUs.  The only cross-lane traffic per step is the two "q" values of the left neighbour
 // lane (DPP/permute via __shfl_up).  Emission rows for t+1.. are prefetched a group ahead so the serial
 // chain never waits on HBM.
+#include <type_traits>
+
 #include "hfa_common.h"
 
 namespace {
@@ -42,12 +44,18 @@ __device__ __forceinline__ float from_lane_below(float v) {
 // refill just issued included) at the top of each group — the prefetch did nothing and each group paid a full
 // memory round trip.  E and nE of a group are one vector load each (lane u holds step t0 + u) broadcast per step
 // with v_readlane, instead of two scalar loads per step whose lgkmcnt(0) waits also catch the refills.
-template <int K, int NW, int G, int R, bool VEC>
-__global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
+//
+// CF: curr held as f32.  Every value the DP writes into curr is an f32 value (L, max(curr, L), 0) and so is the
+// lattice prologue's initialisation, so when every incoming curr is one (checked by the kernel below) the f64
+// max / select updates become f32 ones on one register -- the same bits, ~3 fewer VALU operations per state and
+// step; the f64 form stays for a caller's arbitrary f64 curr.  Only the q term is computed in f64, as before.
+template <int K, int NW, int G, int R, bool VEC, bool CF>
+__device__ __forceinline__ void forward_body(
     int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
     const int32_t* __restrict__ padv, const float* __restrict__ prob_log,
     const float* __restrict__ not_edge_log, const float* __restrict__ edge_log, double* __restrict__ curr_io,
     float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id, int t_begin, int t_end) {
+    using CT = typename std::conditional<CF, float, double>::type;
     static_assert(NW == 1 || K >= 2, "multi-wave DP needs >= 2 states per lane");
     static_assert(G <= 64 && R >= 2, "a group's E / nE fit one wave's lanes; at least two groups in flight");
     __shared__ float xq[2][NW][2];
@@ -73,14 +81,14 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     const int s0 = g * K;
     const int sl = s0 < Smax ? s0 : 0;          // load column of this lane (clamped: lanes past Smax load row start)
     float dprev[K];
-    double curr[K];
+    CT curr[K];
     bool valid[K], zero[K], allow3[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int s = s0 + k;
         valid[k] = s < S;
         dprev[k] = valid[k] ? d[(size_t)(t0 - 1) * Smax + s] : neg_inf();
-        curr[k] = valid[k] ? cu[s] : -__builtin_inf();
+        curr[k] = valid[k] ? (CT)cu[s] : (CT)-__builtin_inf();
         zero[k] = valid[k] && ids[s] == 0;
         // prob3 (alignment_decoder.py:191-202): -inf for s < pad, and for s >= pad when
         // (s - pad + 1 < S - 1 and ph_seq_id[s - pad + 1] != 0).
@@ -122,7 +130,7 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
         for (int k = 0; k < K; ++k) {
             a[k] = __fadd_rn(dprev[k], Lu[k]);                                       // dp + L     (f32)
             const float a2 = __fadd_rn(a[k], E);                                     //  + E       (f32)
-            q[k] = (float)__dadd_rn((double)a2, __dmul_rn(curr[k], ratio));          //  + C*T/S   (f64)
+            q[k] = (float)__dadd_rn((double)a2, __dmul_rn((double)curr[k], ratio));  //  + C*T/S   (f64)
         }
         // left neighbour lane's last two q values (states s0-1, s0-2)
         float qm1 = from_lane_below(q[K - 1]);
@@ -147,7 +155,8 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
             const float p1 = __fadd_rn(a[k], nE);
             const float src1 = (k >= 1) ? q[k >= 1 ? k - 1 : 0] : qm1;
             const float src2 = (k >= 2) ? q[k >= 2 ? k - 2 : 0] : (k == 1 ? qm1 : qm2);
-            const float p2 = (s == 0) ? neg_inf() : src1;
+            // (state 0: src1 is the -inf lane 0 of wave 0 gets from below, so p2 = -inf as the reference's)
+            const float p2 = src1;
             const float p3 = allow3[k] ? (pad == 1 ? src1 : src2) : neg_inf();
             float best = p1;
             int idx = 0;
@@ -160,10 +169,10 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
                 d[row + s] = best;
                 bb[row + s] = (int8_t)idx;
             }
-            const double Ld = (double)Lu[k];
-            if (idx == 0) curr[k] = (Ld > curr[k]) ? Ld : curr[k];  // max(curr, L) (:222)
-            else curr[k] = Ld;                                       // (:224)
-            if (zero[k]) curr[k] = 0.0;                              // (:226-228)
+            // max(curr, L) on a stay (:222), L on an advance or skip (:224), 0 on a zero-id state (:226-228)
+            const CT Lc = (CT)Lu[k];
+            curr[k] = (idx != 0 || Lc > curr[k]) ? Lc : curr[k];
+            if (zero[k]) curr[k] = (CT)0;
             dprev[k] = best;
         }
         if (VEC) {     // states past S inside the Smax pitch get don't-care values
@@ -228,7 +237,32 @@ __global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
     }
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        if (valid[k]) cu[s0 + k] = curr[k];
+        if (valid[k]) cu[s0 + k] = (double)curr[k];
+}
+
+template <int K, int NW, int G, int R, bool VEC>
+__global__ __launch_bounds__(64 * NW) void viterbi_forward_kernel(
+    int Tmax, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
+    const int32_t* __restrict__ padv, const float* __restrict__ prob_log,
+    const float* __restrict__ not_edge_log, const float* __restrict__ edge_log, double* __restrict__ curr_io,
+    float* __restrict__ dp, int8_t* __restrict__ bt, const int32_t* __restrict__ ph_seq_id, int t_begin, int t_end) {
+    // f32 curr (CF) when every incoming curr of the utterance is an f32 value (NaN, or f64-only values: the f64 form)
+    const int b = blockIdx.x, S = Sv[b];
+    bool f32 = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int s = (int)threadIdx.x * K + k;
+        if (s < S) {
+            const double c = curr_io[(size_t)b * Smax + s];
+            f32 = f32 && (double)(float)c == c;
+        }
+    }
+    if (__syncthreads_and(f32))
+        forward_body<K, NW, G, R, VEC, true>(Tmax, Smax, Tv, Sv, padv, prob_log, not_edge_log, edge_log, curr_io, dp,
+                                             bt, ph_seq_id, t_begin, t_end);
+    else
+        forward_body<K, NW, G, R, VEC, false>(Tmax, Smax, Tv, Sv, padv, prob_log, not_edge_log, edge_log, curr_io, dp,
+                                              bt, ph_seq_id, t_begin, t_end);
 }
 
 // S > 8192 (up to 32768 states, the backtrack's 15-bit path entries; the reference takes any S): the

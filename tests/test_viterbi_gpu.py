@@ -139,6 +139,41 @@ def test_forward_step_ranges_bit_exact():
     assert np.array_equal(cu_t[0, :S].cpu().numpy().view(np.int64), c_ref.view(np.int64))
 
 
+@pytest.mark.parametrize("T,S", [(300, 200), (900, 1801)])
+def test_forward_f64_curr_bit_exact(T, S):
+    """The DP runs curr in f32 when every incoming value is an f32 one (the lattice prologue's, and everything the DP
+    itself writes); a caller's curr with f64-only values (forward_pass takes any float64 array) takes the f64 form:
+    both bit-exact with the pinned C oracle, on a one-wave and a multi-wave lattice."""
+    from hubertfa_amd import ops
+    from oracle import decode as od
+    r = np.random.default_rng(T + S)
+    V = 63
+    ids = r.integers(1, V, S).astype(np.int64)
+    ids[::3] = 0
+    ids[0] = ids[-1] = 0
+    lp = torch.log_softmax(torch.from_numpy((3 * r.standard_normal((T, V))).astype(np.float32)), -1).numpy()
+    pl, E, nE, cu, dp, bt, pad = od.lattice_inputs(ids, lp, np.clip(r.uniform(-0.2, 1.2, T), 0, 1))
+    P = -(-S // 8) * 8
+
+    def padded(a, fill):
+        out = np.full(a.shape[:-1] + (P,), fill, dtype=a.dtype)
+        out[..., :S] = a
+        return out
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))[None].to(dev)
+    for label, c0 in (("f32 values", cu), ("f64 values", -5.0 * r.random(S) - 1e-9 * r.random(S))):
+        assert (label == "f32 values") == bool(np.all(c0.astype(np.float32).astype(np.float64) == c0))
+        d_ref, b_ref, c_ref = od.forward_pass(T, S, pl, nE, E, c0.copy(), dp.copy(), bt.copy(), ids, pad)
+        dp_t, cu_t = t(padded(dp, -np.inf)), t(padded(c0, -np.inf))
+        bt_t = torch.full((1, T, P), -1, dtype=torch.int8, device=dev)
+        Tt, St = (torch.tensor([v], dtype=torch.int32, device=dev) for v in (T, S))
+        ops.viterbi_forward(t(padded(pl, 0.0)), t(nE), t(E), cu_t, dp_t, bt_t, t(padded(ids.astype(np.int32), 0)),
+                            Tt, St)
+        assert np.array_equal(dp_t[0, :, :S].cpu().numpy().view(np.int32), d_ref.view(np.int32)), label
+        assert np.array_equal(bt_t[0, 1:, :S].cpu().numpy().astype(np.int32), b_ref[1:]), label
+        assert np.array_equal(cu_t[0, :S].cpu().numpy().view(np.int64), c_ref.view(np.int64)), label
+
+
 @pytest.mark.parametrize("T,S,force_k,pitch8", [(700, 300, 0, False), (1200, 513, 0, False), (3000, 1801, 0, False),
                                                 (2500, 4100, 0, False), (4200, 8000, 0, False),
                                                 (3000, 1801, 0, True), (1200, 513, 2, True), (3000, 1801, 2, True),
