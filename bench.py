@@ -78,6 +78,8 @@ def parse():
                     help="long-form: encode overlapping windows of this length (config 5 chunked; B=1 only)")
     ap.add_argument("--no-config3", action="store_true",
                     help="N > 1: skip the extra BASELINE config-3 measurement (global batch 512) after the timed steps")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="N = 1 headline runs: skip the config4 / config5 blocks measured after the timed steps")
     ap.add_argument("--host-input", action="store_true",
                     help="waves start in host memory and are uploaded inside every step (task.upload, as infer.py) (PCIe-inclusive "
                          "rate; the headline value keeps inputs resident in HBM)")
@@ -325,7 +327,7 @@ def secondary_rooflines(iso, pipe, T, S):
                  "achieved": rate / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": rate / 1e9 / HBM_PEAK_GBPS,
                  "bytes_per_launch": ps["avg_work"]}
             if name == "viterbi_forward_kernel":
-                e["us_per_time_step"] = ps["avg_ms"] * 1e3 / T
+                e["us_per_time_step"] = ps["total_ms"] * 1e3 / ps["units"] if ps["units"] else ps["avg_ms"] * 1e3 / T
                 e["states"] = S
         pp = pipe.summary(name)
         if name in SECONDARY_NOTE:
@@ -370,8 +372,83 @@ def thread_cpu_diff(a, b, steps, top=5):
     return rows[:top]
 
 
+def launcher_cmd(gpus: int, argv, port: int):
+    """The torch.distributed.run command that starts ``gpus`` ranks of this script with the same arguments."""
+    return [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def check_world(args, env=None):
+    """``--gpus N`` against the launch: None when this process is a rank of the right world (or a one-GPU run), else
+    "launch" (no WORLD_SIZE and N > 1: start N ranks) or an error message (a rank count other than N, too few
+    visible devices).  Reads no device state beyond the count (torch.cuda.device_count() does not initialise HIP)."""
+    env = os.environ if env is None else env
+    if args.gpus < 1:
+        return f"--gpus {args.gpus}: at least one GPU"
+    if "WORLD_SIZE" in env:
+        w = int(env["WORLD_SIZE"])
+        if w != args.gpus:
+            return f"--gpus {args.gpus} but this launch has WORLD_SIZE={w} ranks"
+        return None
+    if args.gpus == 1:
+        return None
+    if args.device is None:
+        import torch
+        n = torch.cuda.device_count()
+        if n < args.gpus:
+            return (f"--gpus {args.gpus}: only {n} GPU(s) visible (HIP_VISIBLE_DEVICES / the node); pass --device D to "
+                    f"rehearse {args.gpus} ranks on one GPU")
+    return "launch"
+
+
+def launch_ranks(args) -> int:
+    """Start ``--gpus`` ranks of this script under torch.distributed.run as a CHILD process (never exec: nothing here
+    has touched the GPU, and the ranks do it themselves), relay its output (rank 0 prints the one JSON line) and
+    return its exit code.  SIGTERM / SIGINT are passed on to the child's process group."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    p = subprocess.Popen(launcher_cmd(args.gpus, sys.argv[1:], port), start_new_session=True)
+
+    def relay(sig, _frame):
+        try:
+            os.killpg(p.pid, sig)
+        except ProcessLookupError:
+            pass
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, relay)
+    return p.wait()
+
+
+def device_census(dev, world):
+    """What the collective layer saw: the process group's world size and every rank's device and PCI address,
+    gathered to every rank (outside the timed region)."""
+    import torch
+    import torch.distributed as dist
+    pr = torch.cuda.get_device_properties(dev)
+    mine = {"rank": dist.get_rank() if world > 1 else 0, "device": int(dev.index), "name": pr.name,
+            "pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}",
+            "visible": os.environ.get("HIP_VISIBLE_DEVICES", os.environ.get("CUDA_VISIBLE_DEVICES"))}
+    if world == 1:
+        return {"world_size": 1, "backend": None, "ranks": [mine]}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    return {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "ranks": allr,
+            "distinct_devices": len({r["pci"] for r in allr})}
+
+
 def main():
     args = parse()
+    verdict = check_world(args)
+    if verdict == "launch":
+        sys.exit(launch_ranks(args))
+    if verdict is not None:
+        print(f"bench.py: {verdict}", file=sys.stderr, flush=True)
+        sys.exit(2)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -404,25 +481,25 @@ def main():
     wav_host = torch.from_numpy(wav_np).pin_memory() if args.host_input else None
     inputs = (wav_dev, wav_host, ph_seqs, word_seqs, p2ws)
 
-    def launch(inp):
+    def launch(inp, tk):
         """GPU half of one step (+ the boundary gather) and the async D2H of its results: the encoder on the main
         stream, head + DP on a side stream overlapping the next step's encoder (task.submit).  With --host-input the
         step starts with task.upload of its waves (the CLI's pinned non-blocking H2D)."""
         wav_d, wav_h, ph, ws, pw = inp
-        wav = task.upload(wav_h) if wav_h is not None else wav_d
+        wav = tk.upload(wav_h) if wav_h is not None else wav_d
         if args.serial:
-            dev_out = task.align_batch(wav, ph, ws, pw, wav_sr=16000, host=False, chunk_seconds=args.chunk_seconds)
+            dev_out = tk.align_batch(wav, ph, ws, pw, wav_sr=16000, host=False, chunk_seconds=args.chunk_seconds)
             if world > 1:
                 gather_boundaries(dev_out, uniform=True)
-            return task.decoder.fetch(dev_out)
-        return task.submit(wav, ph, ws, pw, wav_sr=16000,
+            return tk.decoder.fetch(dev_out)
+        return tk.submit(wav, ph, ws, pw, wav_sr=16000,
                            on_device=(lambda d: gather_boundaries(d, uniform=True)) if world > 1 else None,
                            chunk_seconds=args.chunk_seconds)
 
-    def finish(handle, inp):
-        return task.decoder.assemble(handle, *inp[2:])
+    def finish(handle, inp, tk):
+        return tk.decoder.assemble(handle, *inp[2:])
 
-    def run(k, inp=inputs):
+    def run(k, inp=inputs, tk=task):
         """k steps, software-pipelined: the host assembles batch i while the GPU runs batch i+1 -- or, when
         task.submit holds a batch's DP for the next encoder's attention launches (a long lattice), batch i-1: batch
         i's results land near the end of encoder i+1, and waiting for them there would leave the GPU idle while the
@@ -430,24 +507,24 @@ def main():
         pending, res = [], None
         for _ in range(k):
             t0, c0, p0 = time.perf_counter(), time.thread_time(), time.process_time()
-            h = launch(inp)
+            h = launch(inp, tk)
             t1, c1 = time.perf_counter(), time.thread_time()
             pending.append(h)
             while len(pending) > (2 if "resolve" in h else 1):
-                res = finish(pending.pop(0), inp)
+                res = finish(pending.pop(0), inp, tk)
             host_t.append((t1 - t0, time.perf_counter() - t1, c1 - c0, time.thread_time() - c1,
                            time.process_time() - p0))
         while pending:
-            res = finish(pending.pop(0), inp)
+            res = finish(pending.pop(0), inp, tk)
         return res
 
-    def timed(k, inp=inputs):
+    def timed(k, inp=inputs, tk=task):
         """exactly k steps between barrier + synchronize pairs -> (results, max seconds over ranks)."""
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        r = run(k, inp)
+        r = run(k, inp, tk)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -473,6 +550,7 @@ def main():
     thr1 = thread_cpu()
     ops.PROBE = None
 
+    devices = device_census(dev, world)
     n_frames = res[0]["T"]
     audio_s = world * B * args.seconds * args.steps
     value = audio_s / el
@@ -519,6 +597,7 @@ def main():
                    "global_batch": world * B, "seconds_per_utterance": args.seconds, "dp_frames": n_frames,
                    "states": len(ph_seqs[0]), "parallelism": f"utterance-dp{world}", "precision": args.precision},
         "frames_per_s": frames_ps,
+        "ranks": devices,
         "hubert_frames_per_s": world * B * task.unitsEncoder.model.frame_lengths(int(round(args.seconds * 16000)))
                                * args.steps / el,
         "realtime_factor": value,
@@ -555,6 +634,52 @@ def main():
                           "global_batch": world * c3, "steps": args.steps, "ms_per_step": el3 / args.steps * 1e3,
                           "value": world * c3 * args.seconds * args.steps / el3, "unit": "audio_s/s",
                           "frames_per_s": world * c3 * n_frames * args.steps / el3}
+    def extra_block(workload, tk, b, seconds, words, steps, warmup):
+        """Another BASELINE config on this GPU after the headline's timed region, with the same path and protocol
+        (warmup census of the MFMA kernels, then exactly ``steps`` timed steps between synchronises): its rate, DP
+        frames/s, the dominant GEMM's and the attention's fractions of the split ceiling (HIP events)."""
+        n0 = len(host_t)
+        x = make_inputs(b, seconds, words, seed0=5000)
+        inp = (torch.from_numpy(x[0]).to(dev), None) + x[1:]
+        cen = ops.KernelProbe(None)
+        ops.PROBE = cen
+        run(warmup, inp, tk)
+        ops.PROBE = None
+        torch.cuda.synchronize()
+        name = cen.dominant()
+        pr = ops.KernelProbe(name, extra=("attn_fwd_split_kernel",))
+        ops.PROBE = pr
+        r, e = timed(steps, inp, tk)
+        ops.PROBE = None
+        del host_t[n0:]
+        blk = {"workload": workload, "per_gpu_batch": b, "seconds_per_utterance": seconds, "states": len(x[1][0]),
+               "steps": steps, "warmup": warmup, "ms_per_step": e / steps * 1e3,
+               "value": b * seconds * steps / e, "unit": "audio_s/s",
+               "frames_per_s": b * r[0]["T"] * steps / e, "dp_frames": r[0]["T"]}
+        for key, kname in (("dominant_kernel", name), ("attention", "attn_fwd_split_kernel")):
+            s = pr.summary(kname)
+            if s["launches"]:
+                ach = s["avg_flops"] / (s["avg_ms"] * 1e-3) / 1e12
+                blk[key] = {"kernel": kname, "achieved": ach, "peak": mfma_peak(kname), "unit": "TFLOP/s",
+                            "frac": ach / mfma_peak(kname), "avg_launch_ms": s["avg_ms"], "launches": s["launches"]}
+        torch.cuda.synchronize()
+        return blk
+
+    if (world == 1 and not args.no_extra_configs and args.encoder == "base" and args.seconds == 10.0 and B == 32
+            and args.chunk_seconds is None and not args.serial and args.precision == "split" and not args.host_input):
+        # BASELINE configs 4 and 5 on this GPU, driver-observed in the same line (verdict r04 item 4): config 4's
+        # per-GPU shard (Hubert-large 24L, 32 x 10 s) and config 5 unchunked (one 300 s utterance, the reference's
+        # whole-wave encoding, tools/encoder.py:36-60; its DP held for the next encoder's attention launches)
+        ck4 = synth_checkpoint(encoder="cnhubert-large", model_path="synth:0", seed=1)
+        t4 = ForcedAlignmentTask(**ck4["hyper_parameters"], state_dict=ck4["state_dict"], device=dev)
+        t4.on_predict_start()
+        xs = max(3, min(args.steps, 10))
+        out["config4"] = extra_block("config 4 geometry: Hubert-large (cnhubert-large arch, 24 layers) + UNet head + "
+                                     "Viterbi, 32 x 10 s per GPU (config 4 is 256 over 8 GPUs)", t4, 32, 10.0,
+                                     args.words, xs, 2)
+        del t4
+        out["config5"] = extra_block("config 5: one 300 s utterance, unchunked (whole-wave encoding), Hubert-base, "
+                                     "600 two-phone words (S = 1801), 1 GPU", task, 1, 300.0, 600, 10, 2)
     if args.chunk_seconds is not None:
         out["chunk_agreement"] = chunk_agreement(task, wav_dev, ph_seqs, word_seqs, p2ws, args.chunk_seconds)
     if world == 1 and args.chunk_seconds is None and not args.serial:

@@ -29,6 +29,7 @@ _SIGS = {
     "hfa_lattice_prologue": [I, I, I, I, P, P, P, LL, LL, P, LL, LL, P, P, P, P, P, P, P, P, P, P, P],
     "hfa_viterbi_init": [I, I, I, P, P, P, P, P, P, P],
     "hfa_viterbi_tuning": [I],
+    "hfa_viterbi_range_max_states": [],
     # WAV front end (wav.cpp, host memory)
     "hfa_wav_info": [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32),
                      ctypes.POINTER(ctypes.c_int32)],
@@ -39,6 +40,7 @@ _RESTYPE = {"hfa_last_error": ctypes.c_char_p, "hfa_build_arch": ctypes.c_char_p
 
 
 HFA_EINVAL = -1000
+ABI_VERSION = 2          # include/hfa.h HFA_ABI_VERSION: the argument lists _SIGS and the kernel modules declare
 
 
 class HFALibraryError(RuntimeError):
@@ -95,6 +97,10 @@ def lib():
             raise HFALibraryError(f"failed to load {LIB_PATH}: {e}") from e
         for name in _SIGS:
             _bind(L, name)
+        got = L.hfa_abi_version()
+        if got != ABI_VERSION:       # an older / newer build: its argument lists differ
+            raise HFALibraryError(f"{LIB_PATH} has C-ABI version {got}, this binding is written for {ABI_VERSION}: "
+                                  f"rebuild it (make -C hubertfa_amd/csrc)")
         _lib = L
     return _lib
 

@@ -16,7 +16,7 @@ import time
 import numpy as np
 import torch
 
-from . import ops
+from . import _lib, ops
 from .intervals import assemble_intervals, total_confidence, utterance_result  # noqa: F401 (public names)
 
 
@@ -117,7 +117,9 @@ class AlignmentDecoder:
         def backtrack():
             idx, tint, n, fc = ops.viterbi_backtrack(dp, bt, ids_t, T_t, S_t)
             dev_out.update(ph_idx_seq=idx, ph_time_int=tint, n=n, frame_confidence=fc)
-        n_rng = 1 if host or dp_ranges is None or Smax > 8192 else max(1, int(dp_ranges(Tmax, Smax)))
+        # past the library's range limit (the segmented-state form) the DP runs whole lattices only
+        n_rng = 1 if host or dp_ranges is None or Smax > _lib.lib().hfa_viterbi_range_max_states() \
+            else max(1, int(dp_ranges(Tmax, Smax)))
         if n_rng > 1:
             cuts = np.linspace(1, Tmax, n_rng + 1).round().astype(int)
             dev_out["deferred"] = [functools.partial(forward, int(a), int(c)) for a, c in zip(cuts[:-1], cuts[1:])]

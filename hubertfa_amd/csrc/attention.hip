@@ -528,16 +528,17 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
 namespace {
 thread_local int g_attn_waves = 0;   // hfa_attention_split_tuning override (0: automatic)
 // Waves (x 32 queries) per workgroup of the split attention, by the busiest CU's share of the grid: the B*H*ceil(L /
-// 32w) query blocks of w waves spread over the 256 CUs, so that CU runs ceil(blocks / 256) * w waves' worth of query
-// rows.  The smaller share wins; on a tie 8 waves for long rows (>= 2048 keys: half the K/V staging per query), 4 for
+// 32w) query blocks of w waves spread over the device's CUs (256 on a whole MI355X), so that CU runs ceil(blocks /
+// CUs) * w waves' worth of query rows.  The smaller share wins; on a tie 8 waves for long rows (>= 2048 keys: half the K/V staging per query), 4 for
 // short ones (per-block prologue and epilogue).  Measured (profiles/r04/attn_waves_rule.txt): at one utterance,
 // L = 1 000 ... 18 000, it picks the faster form at every length, where the old rule (8 from L >= 512) was 9-17 %
 // slower at L = 6 000-8 000, 11 000-13 000 and 18 000; 4 x 3 000 -8 %; configs 2, 4 and 5 keep their forms.
 inline int split_attn_waves(int B, int H, int L) {
     if (g_attn_waves == 4 || g_attn_waves == 8) return g_attn_waves;
+    const long long cus = hfa::device_cus();
     auto share = [&](int w) {
         const long long blocks = (long long)B * H * ((L + QW * w - 1) / (QW * w));
-        return (blocks + 255) / 256 * w;
+        return (blocks + cus - 1) / cus * w;
     };
     const long long s4 = share(4), s8 = share(8);
     return (s8 < s4 || (s8 == s4 && L >= 2048)) ? 8 : 4;

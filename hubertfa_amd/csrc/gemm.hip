@@ -584,45 +584,32 @@ __global__ __launch_bounds__(256, 4) void gemm_dma_n48_kernel(const GemmP p) {
 // ds_read_b128 brings 8 consecutive k of its row = one MFMA operand (lane l: row l&31, k 8(l>>5)..+7 of a 16-k
 // sub-step; the same mapping on both operands).
 template <int MF> struct AccT;
-template <> struct AccT<32> { typedef f32x16 type; };
 template <> struct AccT<16> { typedef f32x4 type; };
 
-// The 32x32 output block (i, j) of a wave's tile (units of 32 rows / columns) -> the wave's [32][36] LDS slab, with
-// bias and GELU applied, from either accumulator layout: MF 32 = one 32x32x16 accumulator (col lane&31, row (e&3) +
-// 8(e>>2) + 4(lane>>5)), MF 16 = 2 x 2 16x16x32 accumulators (col lane&15, row 4(lane>>4) + e).  Returns true when
-// an accumulator is not finite.
+// The 32x32 output block (i, j) of a wave's tile (units of 32 rows / columns) -> the wave's [32][S] LDS slab, with
+// bias and GELU applied, from the 2 x 2 16x16x32 accumulators that cover it (col lane&15, row 4(lane>>4) + e).
+// Returns true when an accumulator is not finite.
 template <int MF, int NI, int NJ, int S = 36>
 __device__ __forceinline__ bool fill_slab(const typename AccT<MF>::type (&acc)[NI][NJ], int i, int j, int epi,
                                           const float* biasb, int col0, int N, int lane, float* slab,
                                           float scale = 1.0f) {
+    static_assert(MF == 16, "16x16x32 accumulators");
     bool bad = false;
-    if constexpr (MF == 32) {
-        const int r32 = lane & 31, h = lane >> 5;
-        const float bv = (biasb && col0 + r32 < N) ? biasb[col0 + r32] : 0.0f;
+    const int c16 = lane & 15, g = lane >> 4;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            bad |= !__builtin_isfinite(acc[i][j][e]);
-            float v = acc[i][j][e] + bv;
-            if (epi == EPI_GELU) v = hfa::gelu_fast(v);
-            slab[((e & 3) + 8 * (e >> 2) + 4 * h) * S + r32] = v;
-        }
-    } else {
-        const int c16 = lane & 15, g = lane >> 4;
+    for (int jj = 0; jj < 2; ++jj) {
+        const int col = 16 * jj + c16;
+        const float bv = (biasb && col0 + col < N) ? biasb[col0 + col] : 0.0f;
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            const int col = 16 * jj + c16;
-            const float bv = (biasb && col0 + col < N) ? biasb[col0 + col] : 0.0f;
+        for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-            for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float a = acc[2 * i + ii][2 * j + jj][e];
-                    bad |= !__builtin_isfinite(a);
-                    float v = __builtin_fmaf(a, scale, bv);   // scale: the single accumulator's 2^-11 (exact)
-                    if (epi == EPI_GELU) v = hfa::gelu_fast(v);
-                    slab[(16 * ii + 4 * g + e) * S + col] = v;
-                }
-        }
+            for (int e = 0; e < 4; ++e) {
+                const float a = acc[2 * i + ii][2 * j + jj][e];
+                bad |= !__builtin_isfinite(a);
+                float v = __builtin_fmaf(a, scale, bv);   // scale: the single accumulator's 2^-11 (exact)
+                if (epi == EPI_GELU) v = hfa::gelu_fast(v);
+                slab[(16 * ii + 4 * g + e) * S + col] = v;
+            }
     }
     return bad;
 }
@@ -852,27 +839,22 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
 // output, which the epilogue flags) -- and the result is scaled by 2^-11 at the end.  Half the accumulator
 // registers, so a wave can own a 128 x 64 tile: 0.5 LDS fragment reads per MFMA instead of 0.67 (the LDS, shared
 // by the DMA fills and the fragment reads, is what bounds the 64 x 64-per-wave kernel: scripts/gpu_split_abl.sh).
-// BK (halves per row per K-step) 32: [row][4 x 16 B] images, chunk c of row r at c ^ ((r >> 2) & 3); BK 16: [row][2 x
-// 16 B], chunk c at c ^ (((r >> 2) ^ (r >> 3)) & 1).  Both keep the 32x32x16 operand reads (lane: row lane&31, chunk
-// 2 kk + lane/32) conflict-free; BK 16 halves the stage so more stages fit (DMA latency hidden behind more steps).
-// MF 16 (every automatic tile): v_mfma_f32_16x16x32_f16 instead of 32x32x16 (single accumulator, BK 32 only): the
-// same LDS operand bytes per MFMA FLOP for the same wave tile, one MFMA per 32-deep K-step per 16 x 16 block; the image
-// swizzle is then chunk c of row r at c ^ {0, 2, 3, 1}[(r >> 2) & 3] (conflict-free for the lane map row lane&15,
-// chunk lane>>4).  Measured on the workload's shapes (profiles/r02/split_mf16.txt): 4-9 % faster than the 32x32x16
-// form; the chip holds a higher clock under it (1.96-2.04 vs 1.73-1.85 GHz, same MFMA busy).  The next stage's DMA
-// pieces go out two per A block over the first blocks of a K-step instead of all at its top (+2-6 %), so the
-// two waves of a SIMD do not both stall on DMA issue while the matrix pipe idles.
+// BK (halves per row per K-step) 32: [row][4 x 16 B] images.  MF 16: v_mfma_f32_16x16x32_f16, one MFMA per 32-deep
+// K-step per 16 x 16 block; chunk c of row r sits at c ^ {0, 2, 3, 1}[(r >> 2) & 3] (conflict-free for the lane map
+// row lane&15, chunk lane>>4).  Measured on the workload's shapes (profiles/r02/split_mf16.txt): 4-9 % faster than
+// the 32x32x16 form (retired in round 5 with the two-accumulator and 16-deep-K-step tuning tiles); the chip holds a
+// higher clock under it (1.96-2.04 vs 1.73-1.85 GHz, same MFMA busy).  The next stage's DMA pieces go out two per A
+// block over the first blocks of a K-step instead of all at its top (+2-6 %), so the two waves of a SIMD do not both
+// stall on DMA issue while the matrix pipe idles.
 // F16 (opt-in fast mode, MF 16 tiles only): the operands' high planes alone, one product a1 w1 per MAC -- f16-class
 // accuracy (inputs rounded to 11 significand bits, f32 accumulation); the low planes are neither fetched nor read.
 template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT, bool GT, bool ONE, int BK,
           int MF = 32, bool F16 = false>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const GemmP p) {
-    static_assert(BK == 16 || BK == 32, "BK 16 or 32");
-    static_assert(MF == 32 || (MF == 16 && ONE && BK == 32), "16x16x32 tiles: single accumulator, BK 32");
+    static_assert(MF == 16 && ONE && BK == 32, "the built tiles: 16x16x32 MFMA, single accumulator, BK 32");
     static_assert(!F16 || (MF == 16 && NS == 2 && !GT), "the one-product mode runs on the 2-stage 16x16x32 tiles");
     constexpr int CPR = BK / 8, NW = WM * WN;                // 16-B chunks per row per plane
-    constexpr int RPP = 64 / CPR, KK = BK / 16;               // rows per 1-KiB DMA piece, MFMA k-steps per K-step
-    constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
+    constexpr int RPP = 64 / CPR;                             // rows per 1-KiB DMA piece
     constexpr int IA = BM / RPP, IW = BN / RPP;               // 1-KiB DMA pieces per plane per K-step
     constexpr int DA = (IA + NW - 1) / NW, DB = (IW + NW - 1) / NW;   // uneven shares: wave + d*NW < IA only
     static_assert(NS == 2 || (IA % NW == 0 && IW % NW == 0), "counted vmcnt waits need even DMA shares");
@@ -898,10 +880,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     const __amdgpu_buffer_rsrc_t rW2 = hfa::make_rsrc(Wb + p.sWp, w_bytes);
 
     // DMA d of this wave fills rows (wave + d*NW)*RPP + lane/CPR of each plane, chunk slot lane%CPR (swizzled source)
-    auto swz = [](int r) {
-        if constexpr (MF == 16) return (0x78 >> (2 * ((r >> 2) & 3))) & 3;      // {0, 2, 3, 1}[(r >> 2) & 3]
-        return CPR == 4 ? ((r >> 2) & 3) : (((r >> 2) ^ (r >> 3)) & 1);
-    };
+    auto swz = [](int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; };      // {0, 2, 3, 1}[(r >> 2) & 3]
     int a_t0[DA], a_c[DA], a_tap[DA];
     unsigned voffA[DA], voffW[DB];
 #pragma unroll
@@ -1016,7 +995,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     };
 
     const int wm = wave / WN, wn = wave % WN;
-    if constexpr (MF == 16) {
+    {
         constexpr int NI = BM / WM / 16, NJ = BN / WN / 16;       // 16 x 16 blocks per wave
 
         const int r16 = lane & 15, c = lane >> 4;
@@ -1096,106 +1075,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         else
             store_f32_lds<16, EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
                                            slab, true, kScale);
-        return;
-    } else {
-    const int r32 = lane & 31, h = lane >> 5;
-    int rdA[KK], rdB[KK];                                    // f16x8 (16-B) units within a stage
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-        const int c = kk * 2 + h;
-        rdA[kk] = (wm * (BM / WM) + r32) * CPR + (c ^ swz(r32));
-        rdB[kk] = 2 * PA / 8 + (wn * (BN / WN) + r32) * CPR + (c ^ swz(r32));
-    }
-    f32x16 accM[TI][TJ], accC[ONE ? 1 : TI][ONE ? 1 : TJ];
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) accM[i][j][e] = 0.0f;
-    if constexpr (!ONE) {
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-            for (int j = 0; j < TJ; ++j)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) accC[i][j][e] = 0.0f;
-    }
-
-    const int nk = p.K / BK;
-#pragma unroll
-    for (int s = 0; s < NS - 1; ++s)
-        if (s < nk) issue(s);
-    if (nk >= NS - 1) hfa::wait_vm_barrier<(NS - 2) * DN>();
-    else hfa::wait_vm_barrier<0>();
-
-    const f16x8* s8 = reinterpret_cast<const f16x8*>(smem);
-    int stage = 0;
-    for (int kt = 0; kt < nk; ++kt) {
-        const bool more = kt + NS - 1 < nk;
-        const int nstage = stage == 0 ? NS - 1 : stage - 1;
-        if (more) issue(nstage);
-        const f16x8* st = s8 + stage * (STAGE / 8);
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-            f16x8 a1[TI], a2[TI], w1[TJ], w2[TJ];
-#pragma unroll
-            for (int i = 0; i < TI; ++i) {
-                a1[i] = st[rdA[kk] + i * 32 * CPR];
-                a2[i] = st[rdA[kk] + PA / 8 + i * 32 * CPR];
-            }
-#pragma unroll
-            for (int j = 0; j < TJ; ++j) {
-                w1[j] = st[rdB[kk] + j * 32 * CPR];
-                w2[j] = st[rdB[kk] + PW / 8 + j * 32 * CPR];
-            }
-            if constexpr (ONE) {
-                f16x8 w1s[TJ];
-#pragma unroll
-                for (int j = 0; j < TJ; ++j) w1s[j] = w1[j] * (_Float16)2048.0f;
-#pragma unroll
-                for (int i = 0; i < TI; ++i)
-#pragma unroll
-                    for (int j = 0; j < TJ; ++j) {
-                        accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w1s[j], accM[i][j], 0, 0, 0);
-                        accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w2[j], accM[i][j], 0, 0, 0);
-                        accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accM[i][j], 0, 0, 0);
-                    }
-            } else {
-#pragma unroll
-                for (int i = 0; i < TI; ++i)
-#pragma unroll
-                    for (int j = 0; j < TJ; ++j) {
-                        accM[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w1[j], accM[i][j], 0, 0, 0);
-                        accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[i], w2[j], accC[i][j], 0, 0, 0);
-                        accC[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2[i], w1[j], accC[i][j], 0, 0, 0);
-                    }
-            }
-        }
-        if (kt + 1 < nk) {
-            if (more) hfa::wait_vm_barrier<(NS - 2) * DN>();
-            else hfa::wait_vm_barrier<0>();
-        }
-        stage = stage + 1 == NS ? 0 : stage + 1;
-    }
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                if constexpr (ONE) accM[i][j][e] *= 1.0f / 2048.0f;
-                else accM[i][j][e] = __builtin_fmaf(accC[i][j][e], 1.0f / 2048.0f, accM[i][j][e]);
-            }
-    static_assert(NW * 32 * 36 * 4 <= NS * STAGE * 2, "epilogue slabs exceed the staging LDS");
-    __syncthreads();
-    float* slab = reinterpret_cast<float*>(smem) + wave * (32 * 36);
-    if constexpr (OUT_SPLIT)
-        store_split_lds<32, TI, TJ>(p, accM, EPI, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
-                                    slab);
-    else
-        store_f32_lds<32, EPI, TI, TJ>(p, accM, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane, slab,
-                                       ONE);
     }
 }
 
@@ -1613,27 +1492,33 @@ __global__ __launch_bounds__(512, 1) void posconv_split_kernel(const GemmP p) {
 }
 
 // ---- split-f16 dispatch --------------------------------------------------------------------------------------
-enum { SCFG_AUTO = 0, SCFG_128x128 = 1, SCFG_128x64 = 2, SCFG_256x128 = 3, SCFG_128x128_NS3 = 4, SCFG_128x128_NS4 = 5,
-       SCFG_256x128_NS3 = 6, SCFG_256x256_1 = 7, SCFG_256x128_1 = 8, SCFG_128x128_1 = 9, SCFG_128x64_1 = 10,
-       SCFG_256x256_1_K16S4 = 11, SCFG_256x256_1_K16S3 = 12, SCFG_128x128_1_K16S4 = 13, SCFG_256x64_1 = 14,
-       SCFG_N48 = 15, SCFG_WIN = 16, SCFG_256x256_M16 = 17, SCFG_128x128_M16 = 18, SCFG_128x64_M16 = 19,
-       SCFG_256x64_M16 = 20, SCFG_256x128_M16_S3 = 21, SCFG_128x256_M16_S3 = 22, SCFG_256x192_M16 = 23,
-       SCFG_192x256_M16 = 24, SCFG_128x192_M16 = 25, SCFG_192x128_M16 = 26, SCFG_COUNT = 27 };
-struct SplitGeom { int BM, BN, WM, WN, NS, OCC; bool ONE; int BK; int MF; };
-constexpr SplitGeom kSplitGeom[SCFG_COUNT] = {
-    {128, 128, 2, 2, 2, 2, false, 32}, {128, 128, 2, 2, 2, 2, false, 32}, {128, 64, 2, 2, 2, 2, false, 32},
-    {256, 128, 4, 2, 2, 1, false, 32}, {128, 128, 2, 2, 3, 1, false, 32}, {128, 128, 2, 2, 4, 1, false, 32},
-    {256, 128, 4, 2, 3, 1, false, 32}, {256, 256, 2, 4, 2, 1, true, 32},  {256, 128, 2, 2, 2, 1, true, 32},
-    {128, 128, 2, 2, 2, 2, true, 32},  {128, 64, 2, 2, 2, 2, true, 32},   {256, 256, 2, 4, 4, 1, true, 16},
-    {256, 256, 2, 4, 3, 1, true, 16},  {128, 128, 2, 2, 4, 2, true, 16},  {256, 64, 4, 1, 2, 2, true, 32},
-    {128, 48, 4, 1, 2, 2, true, 32},       // SCFG_N48: gemm_split48_kernel (16x16x32 MFMA), not gemm_split_kernel
-    {256, 48, 8, 1, 3, 1, true, 32},       // SCFG_WIN: posconv_split_kernel (LDS-resident input window)
-    {256, 256, 2, 4, 2, 1, true, 32, 16}, {128, 128, 2, 2, 2, 2, true, 32, 16}, {128, 64, 2, 2, 2, 2, true, 32, 16},
-    {256, 64, 4, 1, 2, 2, true, 32, 16}, {256, 128, 4, 2, 3, 1, true, 32, 16}, {128, 256, 2, 4, 3, 1, true, 32, 16},
-    {256, 192, 4, 2, 2, 1, true, 32, 16}, {192, 256, 2, 4, 2, 1, true, 32, 16},
-    // two workgroups per CU (2 x 80 KiB of LDS): 500 / 504 tiles fill the 512 slots of an N = 768 grid at
-    // B*L = 15968 rows in one balanced round (the 256 x 256 tile: 189 tiles on 256 CUs)
-    {128, 192, 2, 2, 2, 2, true, 32, 16}, {192, 128, 2, 2, 2, 2, true, 32, 16}};
+// Tile ids (hfa_gemm_split_tuning): only the tiles the automatic choice can return are built.  The ids are the ones
+// earlier rounds' measurements name (profiles/r0*/): 1-14, 21, 22 and 26 were tuning-only tiles (the 32x32x16
+// two-accumulator forms, 16-deep K-steps, 3/4-stage rings, 192 x 128) and are retired (git history keeps them).
+enum { SCFG_AUTO = 0, SCFG_N48 = 15, SCFG_WIN = 16, SCFG_256x256_M16 = 17, SCFG_128x128_M16 = 18,
+       SCFG_128x64_M16 = 19, SCFG_256x64_M16 = 20, SCFG_256x192_M16 = 23, SCFG_192x256_M16 = 24,
+       SCFG_128x192_M16 = 25 };
+struct SplitGeom { int BM, BN, WM, WN, NS, OCC; };
+inline bool split_cfg_valid(int cfg) {
+    return cfg == SCFG_AUTO || (cfg >= SCFG_N48 && cfg <= SCFG_256x64_M16) || (cfg >= SCFG_256x192_M16 &&
+                                                                                  cfg <= SCFG_128x192_M16);
+}
+// every gemm_split_kernel tile: single accumulator, v_mfma_f32_16x16x32_f16, 32-deep K-steps
+constexpr SplitGeom split_geom(int cfg) {
+    switch (cfg) {
+        case SCFG_N48: return {128, 48, 4, 1, 2, 2};    // gemm_split48_kernel (16x16x32 MFMA), not gemm_split_kernel
+        case SCFG_WIN: return {256, 48, 8, 1, 3, 1};    // posconv_split_kernel (LDS-resident input window)
+        case SCFG_256x256_M16: return {256, 256, 2, 4, 2, 1};
+        case SCFG_128x64_M16: return {128, 64, 2, 2, 2, 2};
+        case SCFG_256x64_M16: return {256, 64, 4, 1, 2, 2};
+        case SCFG_256x192_M16: return {256, 192, 4, 2, 2, 1};
+        case SCFG_192x256_M16: return {192, 256, 2, 4, 2, 1};
+        // two workgroups per CU (2 x 80 KiB of LDS): 500 tiles fill the 512 slots of an N = 768 grid at B*L = 15968
+        // rows in one balanced round (the 256 x 256 tile: 189 tiles on 256 CUs)
+        case SCFG_128x192_M16: return {128, 192, 2, 2, 2, 2};
+        default: return {128, 128, 2, 2, 2, 2};         // SCFG_128x128_M16
+    }
+}
 thread_local int g_split_cfg = 0;   // tuning override (hfa_gemm_split_tuning)
 thread_local int g_win_nb = 3;   // column blocks of the window kernel the name query reports (N / 16)
 thread_local int g_win_rb = 2;   // and its row blocks per wave
@@ -1641,10 +1526,10 @@ thread_local int g_win_rb = 2;   // and its row blocks per wave
 // Measured on the workload's shapes (scripts/split_gemm_bench.py, profiles/r01/split_gemm_cfgs.txt): the 256 x 256
 // single-accumulator tile is 7-15 % faster than 128 x 128 on the extractor convs, FFN and out-projection (even at
 // 189 tiles for N = 768) and within 3 % on the QKV projection; small grids keep the narrower tiles.  Every
-// automatic choice is a single-accumulator tile: each output element then sees the same MFMA sequence (same
-// k-blocks, same three products in the same order) whatever the tile, so a row's result does not depend on the
-// batch it is in (variable-length batches stay bit-identical to the reference's B = 1 runs).  Since round 2 every
-// automatic tile is a 16x16x32 (MF 16) tile; the 32x32x16 tiles stay as tuning choices.
+// tile is a single-accumulator tile: each output element then sees the same MFMA sequence (same k-blocks, same three
+// products in the same order) whatever the tile, so a row's result does not depend on the batch it is in
+// (variable-length batches stay bit-identical to the reference's B = 1 runs).  Since round 2 every tile is a
+// 16x16x32 (MF 16) tile (4-9 % over the 32x32x16 form, profiles/r02/split_mf16.txt).
 inline bool win_ok(const GemmP& p) {   // posconv_split_kernel: stride 1, N 48 or 64, Cg % 8, Cg <= 64, window fits
     return (p.N == 48 || p.N == 64) && p.Ch == nullptr && p.stride == 1 && p.Cg % 8 == 0 && p.Cg >= 32 &&
            p.Cg <= 2 * (p.N / 16) * 8 && p.K % p.Cg == 0 && 256 + p.K / p.Cg - 1 <= win_rows(2);
@@ -1654,7 +1539,7 @@ inline bool win_rb4(const GemmP& p) { return p.N == 48 && p.M > 256 && 512 + p.K
 
 inline int split_cfg(const GemmP& p, int Z) {
     const bool n48 = p.N == 48 && p.Ch == nullptr && p.Cg % 8 == 0 && p.Cg >= 32;
-    if (g_split_cfg > 0 && g_split_cfg < SCFG_COUNT) {
+    if (g_split_cfg != SCFG_AUTO) {
         if (g_split_cfg == SCFG_N48 && !n48) return SCFG_128x64_M16;
         if (g_split_cfg == SCFG_WIN && !win_ok(p)) return SCFG_128x64_M16;
         return g_split_cfg;
@@ -1704,8 +1589,8 @@ inline int split_cfg(const GemmP& p, int Z) {
 
 // general taps (Cg % 32 != 0, the grouped positional conv off the window kernel): the tiles with a GT instantiation
 inline int gt_cfg(int cfg) {
-    if (cfg == SCFG_256x64_1 || cfg == SCFG_256x64_M16) return SCFG_256x64_M16;
-    return kSplitGeom[cfg].BN == 64 ? SCFG_128x64_M16 : SCFG_128x128_M16;
+    if (cfg == SCFG_256x64_M16) return SCFG_256x64_M16;
+    return split_geom(cfg).BN == 64 ? SCFG_128x64_M16 : SCFG_128x128_M16;
 }
 
 inline void split_name(int cfg, int epi, bool outs, bool gt, bool f16, char* buf, int len) {
@@ -1719,31 +1604,29 @@ inline void split_name(int cfg, int epi, bool outs, bool gt, bool f16, char* buf
         return;
     }
     if (gt) cfg = gt_cfg(cfg);
-    const SplitGeom& g = kSplitGeom[cfg];
-    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, %s, %d, %d, %s>", epi, g.BM, g.BN,
-             g.WM, g.WN, g.NS, g.OCC, outs ? "true" : "false", gt ? "true" : "false", g.ONE ? "true" : "false", g.BK,
-             g.MF ? g.MF : 32, f16 ? "true" : "false");
+    const SplitGeom g = split_geom(cfg);
+    snprintf(buf, len, "gemm_split_kernel<%d, %d, %d, %d, %d, %d, %d, %s, %s, true, 32, 16, %s>", epi, g.BM, g.BN,
+             g.WM, g.WN, g.NS, g.OCC, outs ? "true" : "false", gt ? "true" : "false", f16 ? "true" : "false");
 }
 
 template <int EPI, bool OUTS, int CFG, bool GT = false, bool F16 = false>
 int launch_split_cfg(GemmP p, int Z, hipStream_t st) {
-    constexpr SplitGeom g = kSplitGeom[CFG];
+    constexpr SplitGeom g = split_geom(CFG);
     dim3 grid;
     if (int rc = set_grid(p, g.BM, g.BN, grid, Z)) return rc;
-    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, g.ONE, g.BK,
-                                          g.MF ? g.MF : 32, F16>),
+    hipLaunchKernelGGL((gemm_split_kernel<EPI, g.BM, g.BN, g.WM, g.WN, g.NS, g.OCC, OUTS, GT, true, 32, 16, F16>),
                        grid, dim3(64 * g.WM * g.WN), 0, st, p);
     return hfa::check_launch("hfa_conv_gemm_split");
 }
 
-// the one-product fast mode (HFA_GEMM_F16): the automatic 2-stage 16x16x32 tiles; other choices map to them
+// the one-product fast mode (HFA_GEMM_F16): the 256 x 256 / 256 x 192 / 128 x 128 / 128 x 64 / 256 x 64 tiles; the
+// 192-row tiles map to 256 x 256
 inline int f16_cfg(int cfg) {
     switch (cfg) {
         case SCFG_256x256_M16: case SCFG_128x128_M16: case SCFG_128x64_M16: case SCFG_256x64_M16:
         case SCFG_256x192_M16: return cfg;
-        case SCFG_256x256_1: case SCFG_256x128_M16_S3: case SCFG_128x256_M16_S3: case SCFG_192x256_M16:
-            return SCFG_256x256_M16;
-        default: return kSplitGeom[cfg].BN == 64 ? SCFG_128x64_M16 : SCFG_128x128_M16;
+        case SCFG_192x256_M16: return SCFG_256x256_M16;
+        default: return split_geom(cfg).BN == 64 ? SCFG_128x64_M16 : SCFG_128x128_M16;
     }
 }
 
@@ -1774,30 +1657,13 @@ int launch_split(GemmP p, int Z, int cfg, hipStream_t st, bool f16) {
         }
     }
     switch (cfg) {
-        case SCFG_128x64: return launch_split_cfg<EPI, OUTS, SCFG_128x64>(p, Z, st);
-        case SCFG_256x128: return launch_split_cfg<EPI, OUTS, SCFG_256x128>(p, Z, st);
-        case SCFG_128x128_NS3: return launch_split_cfg<EPI, OUTS, SCFG_128x128_NS3>(p, Z, st);
-        case SCFG_128x128_NS4: return launch_split_cfg<EPI, OUTS, SCFG_128x128_NS4>(p, Z, st);
-        case SCFG_256x128_NS3: return launch_split_cfg<EPI, OUTS, SCFG_256x128_NS3>(p, Z, st);
-        case SCFG_256x256_1: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1>(p, Z, st);
-        case SCFG_256x128_1: return launch_split_cfg<EPI, OUTS, SCFG_256x128_1>(p, Z, st);
-        case SCFG_128x128_1: return launch_split_cfg<EPI, OUTS, SCFG_128x128_1>(p, Z, st);
-        case SCFG_128x64_1: return launch_split_cfg<EPI, OUTS, SCFG_128x64_1>(p, Z, st);
-        case SCFG_256x256_1_K16S4: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1_K16S4>(p, Z, st);
-        case SCFG_256x256_1_K16S3: return launch_split_cfg<EPI, OUTS, SCFG_256x256_1_K16S3>(p, Z, st);
-        case SCFG_128x128_1_K16S4: return launch_split_cfg<EPI, OUTS, SCFG_128x128_1_K16S4>(p, Z, st);
-        case SCFG_256x64_1: return launch_split_cfg<EPI, OUTS, SCFG_256x64_1>(p, Z, st);
         case SCFG_256x256_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x256_M16>(p, Z, st);
-        case SCFG_128x128_M16: return launch_split_cfg<EPI, OUTS, SCFG_128x128_M16>(p, Z, st);
         case SCFG_128x64_M16: return launch_split_cfg<EPI, OUTS, SCFG_128x64_M16>(p, Z, st);
         case SCFG_256x64_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x64_M16>(p, Z, st);
-        case SCFG_256x128_M16_S3: return launch_split_cfg<EPI, OUTS, SCFG_256x128_M16_S3>(p, Z, st);
-        case SCFG_128x256_M16_S3: return launch_split_cfg<EPI, OUTS, SCFG_128x256_M16_S3>(p, Z, st);
         case SCFG_256x192_M16: return launch_split_cfg<EPI, OUTS, SCFG_256x192_M16>(p, Z, st);
         case SCFG_192x256_M16: return launch_split_cfg<EPI, OUTS, SCFG_192x256_M16>(p, Z, st);
         case SCFG_128x192_M16: return launch_split_cfg<EPI, OUTS, SCFG_128x192_M16>(p, Z, st);
-        case SCFG_192x128_M16: return launch_split_cfg<EPI, OUTS, SCFG_192x128_M16>(p, Z, st);
-        default: return launch_split_cfg<EPI, OUTS, SCFG_128x128>(p, Z, st);
+        default: return launch_split_cfg<EPI, OUTS, SCFG_128x128_M16>(p, Z, st);
     }
 }
 
@@ -2074,6 +1940,10 @@ const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split
 }
 
 int hfa_gemm_split_tuning(int cfg) {
+    if (!split_cfg_valid(cfg)) {
+        hfa::set_error("hfa_gemm_split_tuning: tile %d is not built (0 auto, 15-20, 23-25)", cfg);
+        return HFA_EINVAL;
+    }
     g_split_cfg = cfg;
     return HFA_OK;
 }

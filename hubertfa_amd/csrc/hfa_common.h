@@ -18,6 +18,9 @@
 namespace hfa {
 
 void set_error(const char* fmt, ...);
+// Compute units of the calling thread's current device (hipDeviceProp_t::multiProcessorCount, cached per device);
+// 256 on a whole MI355X, fewer on a partitioned one.  Grid-shape rules use it instead of a constant.
+int device_cus();
 
 inline int check_launch(const char* what) {
     hipError_t e = hipGetLastError();

@@ -711,7 +711,7 @@ int hfa_viterbi_forward_steps(int B, int Tmax, int Smax, const int32_t* T, const
 #undef HFA_FWD
     if (Smax <= 4 * kWideSeg) {  // the segmented form, up to 32768 states (the backtrack's 15-bit path entries)
         if (t_begin != 1 || t_end < Tmax) {
-            hfa::set_error("hfa_viterbi_forward_steps: Smax=%d > 8192 runs whole lattices only", Smax);
+            hfa::set_error("hfa_viterbi_forward_steps: Smax=%d > %d runs whole lattices only", Smax, kWideSeg);
             return HFA_EINVAL;
         }
         hipLaunchKernelGGL(viterbi_forward_wide_kernel, dim3(B), dim3(64 * kWideNW), 0, stream, Tmax, Smax, T, S,
@@ -729,6 +729,8 @@ int hfa_viterbi_forward(int B, int Tmax, int Smax, const int32_t* T, const int32
     return hfa_viterbi_forward_steps(B, Tmax, Smax, T, S, prob3_pad_len, prob_log, not_edge_log, edge_log, curr, dp,
                                      bt, ph_seq_id, 1, Tmax > 1 ? Tmax : 1, stream);
 }
+
+int hfa_viterbi_range_max_states(void) { return kWideSeg; }
 
 int hfa_viterbi_tuning(int force_k) {
     if (force_k != 0 && force_k != 2 && force_k != 4 && force_k != 8) {

@@ -62,11 +62,13 @@ def viterbi_forward(prob_log, not_edge_log, edge_log, curr, dp, bt, ph_seq_id, T
         _lib.call("hfa_viterbi_forward_steps", B, Tmax, Smax, _ptr(T), _ptr(S), _ptr(pad), _ptr(prob_log),
                   _ptr(not_edge_log), _ptr(edge_log), _ptr(curr), _ptr(dp), _ptr(bt), _ptr(ph_seq_id), t0, t1,
                   _stream(prob_log.device))
-    if PROBE is None or steps is not None:
+    if PROBE is None:
         return launch()
     # SURVEY §8(d) algorithmic bytes: prob_log in + dp out (4 B each) + bt out (1 B) per cell, 8 B edge terms
-    # per frame; counted on the padded planes (exact when every utterance of the batch fills them).
-    PROBE("viterbi_forward_kernel", B * (9.0 * Tmax * Smax + 8.0 * Tmax), launch, kind="bytes")
+    # per frame; counted on the padded planes (exact when every utterance of the batch fills them).  A step range
+    # (a held DP, task.submit) counts its own time steps: ``units`` carries them, so the per-step figures hold.
+    n = max(t1 - t0, 0) if steps is not None else Tmax
+    PROBE("viterbi_forward_kernel", B * (9.0 * n * Smax + 8.0 * n), launch, kind="bytes", units=n)
 
 
 def viterbi_backtrack(dp, bt, ph_seq_id, T, S):
@@ -212,7 +214,7 @@ class KernelProbe:
     def dominant(self) -> str:
         return max(self.census, key=self.census.get)
 
-    def __call__(self, name: str, work: float, launch, kind: str = "flops", shape=None):
+    def __call__(self, name: str, work: float, launch, kind: str = "flops", shape=None, units=None):
         if self.name is None:
             if kind == "flops":
                 self.census[name] = self.census.get(name, 0.0) + work
@@ -223,16 +225,19 @@ class KernelProbe:
         s.record()
         launch()
         e.record()
-        self.records.setdefault(name, []).append((s, e, work))
+        self.records.setdefault(name, []).append((s, e, work, units))
 
     def summary(self, name: str | None = None):
+        """launches, total / average ms, work; ``units`` = the launches' own units (the DP's time steps) when
+        every launch reported them, else None."""
         torch.cuda.synchronize()
         recs = self.records.get(name or self.name, [])
         n = len(recs)
-        ms = sum(s.elapsed_time(e) for s, e, _ in recs)
-        w = sum(f for _, _, f in recs)
+        ms = sum(s.elapsed_time(e) for s, e, _, _ in recs)
+        w = sum(f for _, _, f, _ in recs)
+        u = sum(x for *_, x in recs) if recs and all(x is not None for *_, x in recs) else None
         return {"launches": n, "total_ms": ms, "avg_ms": ms / max(n, 1), "work": w, "avg_work": w / max(n, 1),
-                "flops": w, "avg_flops": w / max(n, 1)}
+                "flops": w, "avg_flops": w / max(n, 1), "units": u}
 
 
 PROBE = None

@@ -249,7 +249,7 @@ class ForcedAlignmentTask:
         feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds,
                                                 gate=held.gate(main) if held is not None else None)
         if held is not None:
-            held.flush()
+            held.drain()        # a failure there belongs to the held batch: its handle's resolve() re-raises it
         guard = self._guard({}, (waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds))
         ready = torch.cuda.Event()
         ready.record(main)
@@ -283,20 +283,26 @@ class ForcedAlignmentTask:
         return n_layers
 
     def flush(self):
-        """Enqueue a held batch's remaining DP steps now (the pipeline's last batch; assemble also does this)."""
+        """Enqueue a held batch's remaining DP steps now (the pipeline's last batch; assemble also does this).  An
+        error in them stays with that batch: its handle's resolve() (decoder.assemble) raises it."""
         held, self._held = getattr(self, "_held", None), None
         if held is not None:
-            held.flush()
+            held.drain()
 
 
 class _HeldDP:
     """A batch's deferred forward-DP ranges + backtrack (AlignmentDecoder.decode_batch ``deferred``) and the
     completion after them: ``on_device``, then the D2H fetch whose handle ``submit`` returned early (its "resolve"
-    entry, which ``decoder.assemble`` calls, runs whatever is still held)."""
+    entry, which ``decoder.assemble`` calls, runs whatever is still held).
+
+    Failures stay with this batch: a step is dropped only after it ran, the first error stops the rest
+    (a DP missing a time range must never reach the backtrack) and is kept, and ``resolve`` -- this batch's
+    assemble -- raises it; the next batch's encoder, whose attention launches gate the steps, never sees it."""
 
     def __init__(self, task, dev_out, on_device):
         self.task, self.dev_out, self.on_device = task, dev_out, on_device
         self.steps = dev_out.pop("deferred", [])
+        self.error = None
         self.handle = {"resolve": self.flush}
 
     def complete(self):
@@ -308,9 +314,18 @@ class _HeldDP:
         self.handle.update(h)
 
     def _next(self):
-        self.steps.pop(0)()
-        if not self.steps:
-            self.complete()
+        if self.error is not None or not self.steps:
+            return
+        try:
+            self.steps[0]()
+            self.steps.pop(0)
+            if not self.steps:
+                self.complete()
+        except Exception as e:  # noqa: BLE001 — kept for this batch's resolve(); see the class note
+            self.error = e
+            self.steps = []
+            if getattr(self.task, "_held", None) is self:
+                self.task._held = None
 
     def gate(self, main):
         """The next encoder's attention gate: the side stream waits for the main stream to reach the launch, then
@@ -318,7 +333,7 @@ class _HeldDP:
         side = self.task._side
 
         def g():
-            if self.steps:
+            if self.steps and self.error is None:
                 ev = torch.cuda.Event()
                 ev.record(main)
                 with torch.cuda.stream(side):
@@ -326,12 +341,19 @@ class _HeldDP:
                     self._next()
         return g
 
-    def flush(self):
+    def drain(self):
+        """Enqueue every remaining step (on the side stream); errors are kept, not raised."""
         with torch.cuda.stream(self.task._side):
-            while self.steps:
+            while self.steps and self.error is None:
                 self._next()
         if getattr(self.task, "_held", None) is self:
             self.task._held = None
+
+    def flush(self):
+        """The handle's resolve(): drain, then raise this batch's error if one of its steps failed."""
+        self.drain()
+        if self.error is not None:
+            raise self.error
 
 
 def synth_checkpoint(path: str | None = None, *, encoder="cnhubert", model_path="synth:0", seed=1,

@@ -31,6 +31,9 @@ extern "C" {
 
 /* ---- library ------------------------------------------------------------------------------------------- */
 const char* hfa_last_error(void);
+/* HFA_ABI_VERSION: bumped on every incompatible change of an entry point's arguments or of the set of entry points
+ * (INTEGRATION.md §4 lists the changes); bindings check hfa_abi_version() == the version they were written for. */
+#define HFA_ABI_VERSION 2
 int hfa_abi_version(void);
 const char* hfa_build_arch(void);
 
@@ -69,6 +72,9 @@ int hfa_viterbi_forward_steps(int B, int Tmax, int Smax, const int32_t* T, const
                               const int32_t* prob3_pad_len, const float* prob_log, const float* not_edge_log,
                               const float* edge_log, double* curr, float* dp, int8_t* bt, const int32_t* ph_seq_id,
                               int t_begin, int t_end, hipStream_t stream);
+/* The largest Smax for which hfa_viterbi_forward_steps takes partial step ranges (8192: past it the segmented-state
+ * form runs whole lattices only); callers that cut a DP into ranges ask the library instead of repeating it. */
+int hfa_viterbi_range_max_states(void);
 
 /* Tuning hook (tests, benchmarks): states per lane of the multi-wave forward DP, 2 / 4 / 8, 0 = automatic (4 up
  * to 4096 states, then 8); the same bits whatever the choice. */
@@ -154,16 +160,12 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
 /* rocprof symbol stem of the split instantiation for an M x N x K contraction over Z = Zb*G (out_split: planes out;
  * stride 1 assumed, as the grouped positional conv's window kernel needs). */
 const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split, int epilogue, int Cg);
-/* Tile override for the split GEMM: 0 auto, 1 128x128, 2 128x64, 3 256x128 (8 waves), 4/5 128x128 with 3/4
- * stages (one workgroup per CU), 6 256x128 with 3 stages, 7 256x256 single accumulator (8 waves of 128x64),
- * 8 256x128 single accumulator (4 waves), 9 128x128 single accumulator, 10 128x64 single accumulator, 11/12
- * 256x256 single accumulator with 16-deep K-steps and 4/3 stages, 13 128x128 likewise with 4 stages, 14 256x64
- * single accumulator (4 waves of 64x64), 15 the N = 48 kernel (16x16x32 MFMA; chosen automatically for N = 48
- * with f32 output, e.g. the grouped positional conv at Cg = 48), 16 the LDS-window positional conv kernel, 17-20
- * the 256x256 / 128x128 / 128x64 / 256x64 single-accumulator tiles on v_mfma_f32_16x16x32_f16, 21/22 256x128 /
- * 128x256 likewise with 3 stages, 23/24 256x192 / 192x256 likewise (one round of 252 tiles for N = 768 at
- * B*T = 15968 rows), 25/26 128x192 / 192x128 with two workgroups per CU.  The automatic choice uses single-accumulator tiles only: results then do not depend on the
- * tile. */
+/* Tile override for the split GEMM (tests, benchmarks): 0 auto; 15 the N = 48 kernel (16x16x32 MFMA; chosen
+ * automatically for N = 48 with f32 output, e.g. the grouped positional conv at Cg = 48); 16 the LDS-window
+ * positional conv kernel; 17 / 18 / 19 / 20 the 256x256 / 128x128 / 128x64 / 256x64 tiles; 23 / 24 256x192 /
+ * 192x256 (one round of 252 tiles for N = 768 at B*T = 15968 rows); 25 128x192 with two workgroups per CU.  Every
+ * tile is a single-accumulator v_mfma_f32_16x16x32_f16 tile, so results do not depend on the tile.  Other values
+ * (the retired tuning-only tiles 1-14, 21, 22, 26) return HFA_EINVAL and leave the override unchanged. */
 int hfa_gemm_split_tuning(int cfg);
 /* x [rows, cols] f32 (row stride ldx) -> split planes y (row stride ldy, plane 1 at +sp); raises *oflow (if
  * non-NULL) for |x| >= 65504 or a non-finite x. */

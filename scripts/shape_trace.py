@@ -26,7 +26,7 @@ class LaunchLog:
         self.name = "-"
         self.entries = []
 
-    def __call__(self, name, work, launch, kind="flops", shape=None):
+    def __call__(self, name, work, launch, kind="flops", shape=None, units=None):
         self.entries.append({"name": name, "work": work, "kind": kind, "shape": list(shape) if shape else None})
         return launch()
 

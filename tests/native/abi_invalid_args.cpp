@@ -168,8 +168,10 @@ int main() {
         }
     }
     // host queries and tuning hooks (thread-local state; name strings stay valid, bounded)
-    for (int cfg = 0; cfg < 25; ++cfg) {
-        hfa_gemm_split_tuning(cfg);
+    for (int cfg = -1; cfg < 28; ++cfg) {
+        const bool built = cfg == 0 || (cfg >= 15 && cfg <= 20) || (cfg >= 23 && cfg <= 25);
+        const int rc = hfa_gemm_split_tuning(cfg);   // retired / unknown tiles are refused, the override unchanged
+        if ((rc == 0) != built) { std::printf("FAIL split tuning cfg %d rc %d\n", cfg, rc); ++g_fail; }
         const char* n = hfa_gemm_split_kernel_name(15968, 3072, 768, 1, 1, 1, 768);
         if (!n || std::strlen(n) == 0 || std::strlen(n) >= 128) { std::printf("FAIL split name cfg %d\n", cfg); ++g_fail; }
     }

@@ -94,3 +94,24 @@ def test_split_gemm_tile_choice():
     assert ops._split_name(499, 48, 6144, 512, False, 1, 48) == "posconv_split_kernel<1, 3, 4>"   # 512-row tiles
     assert ops._split_name(200, 48, 6144, 512, False, 1, 48) == "posconv_split_kernel<1, 3, 2>"
     assert ops._split_name(499, 64, 8192, 512, False, 1, 64) == "posconv_split_kernel<1, 4, 2>"   # Hubert-large
+
+
+def test_abi_version_and_host_queries():
+    """The library reports the C-ABI version the binding is written for (hfa_lattice_prologue gained dp /
+    curr, hfa_gemm_split_kernel_name gained K, the UNet exports went: version 2), the DP's range limit comes from the
+    library (alignment_decoder asks it), and the split tile override refuses the retired tuning-only tiles."""
+    from hubertfa_amd import _lib, ops  # noqa: F401
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libhfa.so not built")
+    L = _lib.lib()
+    assert L.hfa_abi_version() == _lib.ABI_VERSION == 2
+    hdr = open(os.path.join(REPO, "include", "hfa.h")).read()
+    assert re.search(r"#define HFA_ABI_VERSION 2\b", hdr)
+    assert L.hfa_viterbi_range_max_states() == 8192
+    for cfg in (1, 7, 11, 14, 21, 22, 26, 27, -1):
+        assert L.hfa_gemm_split_tuning(cfg) == _lib.HFA_EINVAL, cfg
+    for cfg in (15, 16, 17, 18, 19, 20, 23, 24, 25, 0):
+        assert L.hfa_gemm_split_tuning(cfg) == 0, cfg
+    # the name query answers from the built tiles only (every one a single-accumulator 16x16x32 tile)
+    for M, N in ((15968, 2304), (15968, 768), (499, 512), (864, 192), (15968, 3072)):
+        assert ops._split_name(M, N, 768, 1, True, 1, 768).endswith(", true, 32, 16, false>")

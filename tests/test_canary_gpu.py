@@ -145,7 +145,7 @@ def _untouched(raw, full, cols):
             and bool((pad == CANARY).all()))
 
 
-@pytest.mark.parametrize("cfg", [0, 17, 18, 19, 20, 7, 9, 10])
+@pytest.mark.parametrize("cfg", [0, 17, 18, 19, 20, 23, 24, 25])
 @pytest.mark.parametrize("M,N,K", [(1, 68, 64), (257, 200, 96), (300, 516, 512), (1000, 772, 768)])
 def test_split_gemm_epilogue_bounds(cfg, M, N, K):
     """Split GEMM epilogues (f32 + residual, planes-only, dual) on ragged M / N into strided outputs whose row

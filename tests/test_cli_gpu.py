@@ -186,13 +186,19 @@ def test_infer_two_ranks_match_one_rank(tmp_path):
 
 
 def test_bench_contract_two_ranks():
-    """The driver's N > 1 bench launch (torchrun, one process per rank, barrier + synchronize around the timed
-    steps, max over ranks), rehearsed with 2 ranks on GPU 0 over gloo: rank 0 alone prints one JSON line whose
-    value is the whole-job rate (global batch = world x per-rank batch) and whose metric is BASELINE.json's."""
+    """The N > 1 bench launch, rehearsed with 2 ranks on GPU 0 over gloo and started the way a plain
+    `python bench.py --gpus 2` is (no outer torchrun: bench.py starts torch.distributed.run itself as a child,
+    verdict r04 item 1): one process per rank, barrier + synchronize around the timed steps, max over ranks; rank 0
+    alone prints one JSON line whose value is the whole-job rate (global batch = world x per-rank batch), whose
+    metric is BASELINE.json's, and whose `ranks` block shows the process group's two distinct ranks."""
     import json
+    import subprocess
+    import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    p = _torchrun(["--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "4", "--seconds", "2",
-                   "--no-cpu-baseline", "--dist-backend", "gloo", "--device", "0"], script="bench.py", timeout=300)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "-u", os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1", "--batch", "4", "--seconds", "2", "--no-cpu-baseline", "--dist-backend", "gloo",
+                        "--device", "0"], env=env, cwd=repo, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
@@ -203,6 +209,9 @@ def test_bench_contract_two_ranks():
     assert d["config"]["global_batch"] == 8 and d["higher_is_better"] is True
     assert d["value"] > 0 and abs(d["value"] - 2 * 4 * 2.0 * 2 / (2 * d["ms_per_step"] * 1e-3)) < 1e-6 * d["value"]
     assert d["roofline"]["bound"] == "mfma" and 0 < d["roofline"]["frac"] < 1
+    rk = d["ranks"]
+    assert rk["world_size"] == 2 and rk["backend"] == "gloo"
+    assert sorted(r["rank"] for r in rk["ranks"]) == [0, 1] and all(r["device"] == 0 for r in rk["ranks"])
 
 
 @pytest.mark.timeout(600)
@@ -216,7 +225,7 @@ def test_bench_two_ranks_config3_block():
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["config"]["global_batch"] == 8
+    assert d["config"]["global_batch"] == 8 and d["ranks"]["world_size"] == 2
     c3 = d["config3"]
     assert c3["per_gpu_batch"] == 256 and c3["global_batch"] == 512 and c3["steps"] == 1
     assert c3["value"] > 0 and abs(c3["value"] - 512 * 10.0 / (c3["ms_per_step"] * 1e-3)) < 1e-6 * c3["value"]

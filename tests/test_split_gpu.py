@@ -42,7 +42,7 @@ def test_split_planes_and_flag():
     flag.zero_()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13, 14, 15, 17, 18, 19, 20, 23, 24, 25, 26])
+@pytest.mark.parametrize("cfg", [0, 15, 17, 18, 19, 20, 23, 24, 25])
 @pytest.mark.parametrize("M,N,K,epi,res,outs", [(300, 200, 128, 0, False, False), (1000, 768, 768, 1, False, False),
                                                 (257, 72, 192, 0, True, False), (4096, 3072, 768, 1, False, True),
                                                 (130, 2304, 768, 0, False, True), (64, 768, 3072, 0, True, False)])
@@ -69,7 +69,7 @@ def test_split_linear(cfg, M, N, K, epi, res, outs):
         _close(got, ref, 2e-5, 2e-5)
 
 
-@pytest.mark.parametrize("cfg", [0, 9, 17, 18, 19])
+@pytest.mark.parametrize("cfg", [0, 17, 18, 19, 20])
 @pytest.mark.parametrize("Cin,Cout,k,s,pad,T", [(512, 512, 3, 2, 0, 301), (512, 512, 2, 2, 0, 100),
                                                 (192, 192, 3, 1, 1, 64), (192, 384, 2, 2, 0, 40),
                                                 (512, 512, 3, 2, 0, 1301)])
@@ -94,8 +94,8 @@ def test_split_conv_vs_conv1d(Cin, Cout, k, s, pad, T, cfg):
     _close(y, ref, 2e-5, 2e-5)
 
 
-@pytest.mark.parametrize("H,G,k,L,cfg", [(768, 16, 128, 499, 0), (768, 16, 128, 77, 1), (96, 2, 8, 40, 0),
-                                         (640, 16, 16, 130, 0), (768, 16, 128, 300, 14), (1024, 16, 32, 260, 14),
+@pytest.mark.parametrize("H,G,k,L,cfg", [(768, 16, 128, 499, 0), (768, 16, 128, 77, 18), (96, 2, 8, 40, 0),
+                                         (640, 16, 16, 130, 0), (768, 16, 128, 300, 20), (1024, 16, 32, 260, 20),
                                          (1024, 16, 128, 499, 0), (768, 16, 128, 499, 15), (768, 16, 64, 1000, 15),
                                          (768, 16, 128, 5, 15), (96, 2, 8, 40, 15), (1024, 16, 32, 100, 15),
                                          (768, 16, 128, 499, 16), (768, 16, 128, 300, 16), (768, 16, 128, 3, 16),
@@ -152,11 +152,11 @@ def test_posconv_window_tiles_bit_identical():
 
 
 @pytest.mark.parametrize("outs", [False, True])
-@pytest.mark.parametrize("cfgs", [(0, 17, 18, 19, 20, 23, 24, 25, 26), (7, 9, 10, 8, 11, 12, 13, 14)])
+@pytest.mark.parametrize("cfgs", [(0, 17, 18, 19, 20, 23, 24, 25)])
 def test_split_single_acc_tiles_bit_identical(outs, cfgs):
-    """Every automatic tile (17 = 256x256, 18 = 128x128, 19 = 128x64, 20 = 256x64, 23 = 256x192, 24 = 192x256,
-    25 = 128x192, 26 = 192x128: single-accumulator 16x16x32 tiles) gives the same bits, so a row's result does not depend on the batch (and so the grid) it runs in; the
-    32x32x16 tiles (tuning only) agree among themselves the same way."""
+    """Every built tile (17 = 256x256, 18 = 128x128, 19 = 128x64, 20 = 256x64, 23 = 256x192, 24 = 192x256,
+    25 = 128x192: single-accumulator 16x16x32 tiles) gives the same bits, so a row's result does not depend on the
+    batch (and so the grid) it runs in."""
     from hubertfa_amd import ops, _lib
     d = torch.device("cuda")
     M, N, K = 700, 768, 1536
@@ -173,8 +173,8 @@ def test_split_single_acc_tiles_bit_identical(outs, cfgs):
         assert torch.equal(o, outs_[0])
 
 
-@pytest.mark.parametrize("cfg,outs", [(7, False), (8, False), (9, True), (10, False), (17, False), (18, True),
-                                      (19, False), (20, True), (23, True), (24, False), (25, True), (26, False)])
+@pytest.mark.parametrize("cfg,outs", [(17, False), (17, True), (18, True), (19, False), (20, True), (23, True),
+                                      (24, False), (25, True), (25, False)])
 def test_split_single_acc_weight_range_flag(cfg, outs):
     """Single-accumulator tiles form 2^11 * hi(w) in f16: a weight with |w| >= 32 overflows there, and the
     non-finite result raises the split flag (the caller re-runs on the f32 GEMM) instead of passing silently."""
