@@ -69,8 +69,6 @@ def parse():
     ap.add_argument("--probe", default="auto",
                     help="kernel instantiation to time; auto = the one carrying the most FLOPs in a warmup census")
     ap.add_argument("--serial", action="store_true", help="one stream per step (no head/encoder overlap)")
-    ap.add_argument("--pair", choices=["auto", "on", "off"], default="auto",
-                    help="task.pair_batches (one side pass per two batches): auto = the task's default")
     ap.add_argument("--no-held-dp", action="store_true",
                     help="run a long lattice's DP in one launch behind its head (A/B of task.defer_dp_frames)")
     ap.add_argument("--precision", default="split", choices=["split", "f16"],
@@ -475,8 +473,6 @@ def main():
     task.on_predict_start()
     if args.no_held_dp:
         task.defer_dp_frames = None
-    if args.pair != "auto":
-        task.pair_batches = args.pair == "on"
     if args.precision == "f16":
         task.unitsEncoder.model.f16 = True
     B = args.batch
@@ -514,7 +510,7 @@ def main():
             h = launch(inp, tk)
             t1, c1 = time.perf_counter(), time.thread_time()
             pending.append(h)
-            while len(pending) > h.get("depth", 2 if "resolve" in h else 1):
+            while len(pending) > (2 if "resolve" in h else 1):
                 res = finish(pending.pop(0), inp, tk)
             host_t.append((t1 - t0, time.perf_counter() - t1, c1 - c0, time.thread_time() - c1,
                            time.process_time() - p0))

@@ -188,13 +188,12 @@ class UnitsEncoder:
 
     @torch.no_grad()
     def encode_frames(self, audio: torch.Tensor, sample_rate: int, hop_size: int, pad_to: int = 1, lengths=None,
-                      chunk_frames: int | None = None, overlap_frames: int = 100, gate=None, out=None):
+                      chunk_frames: int | None = None, overlap_frames: int = 100, gate=None):
         """[B, N] -> (features [B, T_pad, C] channels-last, n_frames); rows >= n_frames are zero.
 
         With ``lengths`` (per-row sample counts of a zero-padded batch) n_frames is a list (one per row) and
         rows >= n_frames[b] of row b are zero; T_pad covers the longest row.  ``gate``: called before each
-        attention launch (HubertEncoder.attention_block).  ``out`` ([B, T_pad, C] f32, e.g. rows of a larger
-        buffer): the features are gathered into it."""
+        attention launch (HubertEncoder.attention_block)."""
         if chunk_frames is not None and lengths is None and audio.shape[0] == 1:
             audio_res = self._resample(audio.to(self.device).float(), sample_rate)
             units = self.units_chunked(audio_res.contiguous(), chunk_frames, overlap_frames, gate=gate)
@@ -203,14 +202,14 @@ class UnitsEncoder:
         if lengths is None:
             n_frames, ratio = self.grid(audio.shape[-1], sample_rate, hop_size)
             T_pad = (n_frames + pad_to - 1) // pad_to * pad_to
-            return ops.units_gather(units.contiguous(), n_frames, T_pad, ratio, out=out), n_frames
+            return ops.units_gather(units.contiguous(), n_frames, T_pad, ratio), n_frames
         nfs = [self.grid(int(n), sample_rate, hop_size)[0] for n in lengths]
         _, ratio = self.grid(int(lengths[0]), sample_rate, hop_size)
         Ls = [self.model.frame_lengths(n) for n in self.resampled_lengths(lengths, sample_rate)]
         T_pad = (max(nfs) + pad_to - 1) // pad_to * pad_to
         dev = units.device
         feats = ops.units_gather(units.contiguous(), max(nfs), T_pad, ratio, n_frames_b=dev_lengths(nfs, dev),
-                                 U_b=dev_lengths(Ls, dev), out=out)
+                                 U_b=dev_lengths(Ls, dev))
         return feats, nfs
 
     def encode(self, audio, sample_rate, hop_size):

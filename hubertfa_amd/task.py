@@ -124,14 +124,13 @@ class ForcedAlignmentTask:
 
     @torch.no_grad()
     def encode_batch(self, waves: torch.Tensor, wav_sr: int | None = None, lengths=None,
-                     chunk_seconds: float | None = None, gate=None, out=None):
+                     chunk_seconds: float | None = None, gate=None):
         """Device half 1 (current stream): waves [B, N] -> (features [B, T_pad, C], DP frames, wav lengths).
 
         ``lengths`` (optional host ints [B]): samples per row of a variable-length batch, rows zero-padded to N
         at ``wav_sr``; then DP frames is a per-row list and every row aligns exactly as it would alone.
         ``chunk_seconds`` (one long utterance): encode overlapping windows of that length as one batch
-        (UnitsEncoder.units_chunked) — long-form speed at the cost of per-window attention context.  ``out``
-        ([B, T_pad, C] f32): gather the features into it (rows of a paired side-pass buffer, ``submit``)."""
+        (UnitsEncoder.units_chunked) — long-form speed at the cost of per-window attention context."""
         self.on_predict_start()
         sr = self.melspec_config["sample_rate"]
         hop = self.melspec_config["hop_length"]
@@ -148,21 +147,9 @@ class ForcedAlignmentTask:
         n = waves.shape[-1]
         chunk = None if chunk_seconds is None else max(1, int(round(chunk_seconds * 50)))
         feats, n_frames = self.unitsEncoder.encode_frames(waves, sr, hop, pad_to=self.head.divisible,
-                                                          lengths=lengths, chunk_frames=chunk, gate=gate, out=out)
+                                                          lengths=lengths, chunk_frames=chunk, gate=gate)
         wl = [n / sr] * waves.shape[0] if lengths is None else [int(m) / sr for m in lengths]
         return feats, n_frames, wl
-
-    def frame_plan(self, n_samples: int, wav_sr: int | None, lengths=None):
-        """(DP frames of the longest row, T_pad) that encode_batch will produce for waves of ``n_samples`` columns
-        (``lengths``: per-row sample counts) at ``wav_sr``, without running anything."""
-        self.on_predict_start()
-        sr = self.melspec_config["sample_rate"]
-        hop = self.melspec_config["hop_length"]
-        rows = [int(n) for n in lengths] if lengths is not None else [int(n_samples)]
-        if wav_sr is not None and wav_sr != sr:
-            rows = [target_length(n, wav_sr, sr) for n in rows]
-        t = max(self.unitsEncoder.grid(n, sr, hop)[0] for n in rows)
-        return t, self.head.padded_len(t)
 
     def head_logits(self, feats, n_frames):
         """UNet head (current stream): features -> (logits [B, T, V+2], the head's range-flag snapshot or None)."""
@@ -254,49 +241,18 @@ class ForcedAlignmentTask:
         ranges, one right before each attention launch of the NEXT batch's encoder (multi-round grids), the rest
         when the next encoder has been enqueued or when the handle is assembled (config 5: the DP's cost to the
         encoder 2.4 -> 0.5 ms, profiles/r04/dp_gate_ab.txt).  ``on_device`` (e.g. the RCCL boundary gather) runs
-        on the side stream after the backtrack.
-
-        ``pair_batches``: a batch's features are held for one step and the next batch's encoder writes the rows
-        after them in the same buffer, so ONE side pass (UNet, head, lattice, DP) serves both batches: half the
-        UNet launches, each over twice the rows (the UNet's CU-time, not its FLOPs, is what the encoder pays for:
-        0.875 ms per 32 utterances alone, 1.40 ms per 64, profiles/r04/unet_batch_scaling.txt).  Every row's result
-        is the one it gets alone (the UNet, lattice and DP are row-independent).  A batch whose shape does not fit
-        the held one's buffer sends the held batch through alone first.  Handles of paired batches carry
-        ``"depth": 2``: the caller should assemble two batches behind (bench.py, infer.py)."""
+        on the side stream after the backtrack."""
         main = torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
         held, self._held = getattr(self, "_held", None), None
-        pend, self._pair = getattr(self, "_pair", None), None
-        pairable = self.pair_batches and chunk_seconds is None
-        t_max = t_pad = None
-        if pairable or pend is not None:
-            t_max, t_pad = self.frame_plan(waves.shape[-1], wav_sr, lengths)
-            pairable = pairable and (self.defer_dp_frames is None or t_max < self.defer_dp_frames)
-        B = waves.shape[0]
-        join = pend is not None and pairable and pend.fits(B, t_pad)
-        if pend is not None and not join:
-            pend.run_alone()
-        out = buf = None
-        if join:
-            out = pend.buf[pend.B:pend.B + B]
-        elif pairable:
-            buf = torch.empty((2 * B, t_pad, int(self.hubert_config["channel"])), dtype=torch.float32,
-                              device=self.device)
-            out = buf[:B]
         feats, n_frames, wl = self.encode_batch(waves, wav_sr, lengths, chunk_seconds,
-                                                gate=held.gate(main) if held is not None else None, out=out)
+                                                gate=held.gate(main) if held is not None else None)
         if held is not None:
             held.drain()        # a failure there belongs to the held batch: its handle's resolve() re-raises it
         guard = self._guard({}, (waves, ph_seqs, word_seqs, p2ws, wav_sr, lengths, chunk_seconds))
         ready = torch.cuda.Event()
         ready.record(main)
-        if pairable and not join:                   # hold these features for the next batch's rows
-            self._pair = _PairedBatch(self, buf, B, t_pad, n_frames, wl, ph_seqs, word_seqs, p2ws, guard, on_device,
-                                      ready)
-            return self._pair.handle
-        if join:
-            return pend.join(B, n_frames, wl, ph_seqs, word_seqs, p2ws, guard, on_device, ready)
         with torch.cuda.stream(self._side):
             self._side.wait_event(ready)
             feats.record_stream(self._side)      # the caching allocator must not recycle it under the side stream
@@ -311,9 +267,6 @@ class ForcedAlignmentTask:
             else:
                 work.complete()
             return work.handle
-
-    # pair consecutive batches into one side pass (submit); set False for one side pass per batch
-    pair_batches = False
 
     # a lattice of at least this many DP frames (config 5's 300 s: 25 839) runs its forward DP beside the next
     # batch's attention launches, one step range per encoder layer; None: never.  A range must fit in one
@@ -330,117 +283,11 @@ class ForcedAlignmentTask:
         return n_layers
 
     def flush(self):
-        """Enqueue a held batch's remaining DP steps, or a held paired batch's side pass alone, now (the pipeline's
-        last batch; assemble also does this).  An error in them stays with that batch: its handle's resolve()
-        (decoder.assemble) raises it."""
-        pend, self._pair = getattr(self, "_pair", None), None
-        if pend is not None:
-            pend.run_alone()
+        """Enqueue a held batch's remaining DP steps now (the pipeline's last batch; assemble also does this).  An
+        error in them stays with that batch: its handle's resolve() (decoder.assemble) raises it."""
         held, self._held = getattr(self, "_held", None), None
         if held is not None:
             held.drain()
-
-
-def _rows(dev_out: dict, a: int, b: int) -> dict:
-    """Rows [a, b) of a batch's device outputs (views; host lists sliced)."""
-    out = {}
-    for k, v in dev_out.items():
-        if k == "split_oflow_head":                 # the head's flag snapshot: one per side pass, shared
-            out[k] = v
-        elif isinstance(v, torch.Tensor):
-            out[k] = v[a:b]
-        elif isinstance(v, dict):
-            out[k] = {kk: (vv[a:b] if isinstance(vv, torch.Tensor) else vv) for kk, vv in v.items()}
-        elif isinstance(v, list):
-            out[k] = v[a:b]
-        else:
-            out[k] = v
-    return out
-
-
-class _PairedBatch:
-    """A batch whose features wait in the first rows of a two-batch buffer for the next batch (task.submit
-    ``pair_batches``).  ``join`` runs ONE side pass over both batches' rows and completes both handles;
-    ``run_alone`` (a next batch that does not fit, the pipeline's end, or this batch's own assemble) runs it over
-    this batch's rows only."""
-
-    def __init__(self, task, buf, B, t_pad, n_frames, wl, ph_seqs, word_seqs, p2ws, guard, on_device, ready):
-        self.task, self.buf, self.B, self.t_pad = task, buf, B, t_pad
-        self.n_frames, self.wl, self.guard, self.on_device, self.ready = n_frames, wl, guard, on_device, ready
-        self.meta = (list(ph_seqs), _opt(word_seqs, len(ph_seqs)), _opt(p2ws, len(ph_seqs)))
-        self.done, self.error = False, None
-        self.handle = {"resolve": self.resolve, "depth": 2}
-
-    def fits(self, B: int, t_pad: int) -> bool:
-        return not self.done and t_pad == self.t_pad and self.B + B <= self.buf.shape[0]
-
-    def _fill(self, handle, dev_out, guard, on_device):
-        dev_out.update(guard)
-        if on_device is not None:
-            on_device(dev_out)
-        h = self.task.decoder.fetch(dev_out)
-        handle.pop("resolve", None)
-        handle.update(h)
-
-    def run_alone(self):
-        """This batch's side pass over its own rows; an error is kept for its resolve() (a failure
-        belongs to the batch it came from, not to the submit that happened to enqueue it)."""
-        if self.done:
-            return
-        self.done = True
-        t = self.task
-        try:
-            with torch.cuda.stream(t._side):
-                t._side.wait_event(self.ready)
-                feats = self.buf[:self.B]
-                self.buf.record_stream(t._side)
-                dev_out = t.decode_device(feats, self.n_frames, self.wl, *self.meta)
-                if "split_oflow" in self.guard:
-                    self.guard["split_oflow"].record_stream(t._side)
-                self._fill(self.handle, dev_out, self.guard, self.on_device)
-        except Exception as e:  # noqa: BLE001 — raised by this batch's resolve()
-            self.error = e
-
-    def resolve(self):
-        if getattr(self.task, "_pair", None) is self:
-            self.task._pair = None
-        self.run_alone()
-        if self.error is not None:
-            raise self.error
-
-    def join(self, B, n_frames, wl, ph_seqs, word_seqs, p2ws, guard, on_device, ready):
-        """The next batch's rows are in buf[self.B:self.B + B] (its encoder recorded ``ready``): one side pass."""
-        self.done = True
-        t = self.task
-        B1 = self.B
-        if isinstance(self.n_frames, int) and isinstance(n_frames, int) and self.n_frames == n_frames:
-            nf = n_frames
-        else:
-            one = lambda n, k: list(n) if isinstance(n, (list, tuple)) else [n] * k  # noqa: E731
-            nf = one(self.n_frames, B1) + one(n_frames, B)
-        ph = self.meta[0] + list(ph_seqs)
-        ws = self.meta[1] + _opt(word_seqs, B)
-        pw = self.meta[2] + _opt(p2ws, B)
-        handle = {"depth": 2}
-        try:
-            with torch.cuda.stream(t._side):
-                t._side.wait_event(ready)            # (after the held batch's own event on the same main stream)
-                feats = self.buf[:B1 + B]
-                self.buf.record_stream(t._side)
-                dev_out = t.decode_device(feats, nf, list(self.wl) + list(wl), ph, ws, pw)
-                for g in (self.guard, guard):
-                    if "split_oflow" in g:
-                        g["split_oflow"].record_stream(t._side)
-                self._fill(self.handle, _rows(dev_out, 0, B1), self.guard, self.on_device)
-                self._fill(handle, _rows(dev_out, B1, B1 + B), guard, on_device)
-        except Exception as e:  # noqa: BLE001 — the shared pass failed: both batches fail (this one raises now)
-            self.error = e
-            raise
-        return handle
-
-
-def _opt(seq, n):
-    return list(seq) if seq is not None else [None] * n
 
 
 class _HeldDP:

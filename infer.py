@@ -183,7 +183,7 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
             job = run(ks, file_sr)
         except recoverable as e:
             err = e
-        depth = 1 if job is None else job[0].get("depth", 2 if "resolve" in job[0] else 1)
+        depth = 2 if job is not None and "resolve" in job[0] else 1
         while len(pending) >= depth:
             settle(pending.pop(0))
         if job is not None:

@@ -103,48 +103,3 @@ def test_pipelined_long_lattice_dp_held_for_next_encoder():
     hc = task.submit(torch.from_numpy(batches[1][0]).to(dev), *batches[1][1:], wav_sr=16000, chunk_seconds=20.0)
     assert "resolve" not in hc
     task.decoder.assemble(hc, *batches[1][1:])
-
-
-def test_paired_side_pass_rows_equal_alone():
-    """task.submit with pair_batches: consecutive batches share ONE side pass (UNet, head, lattice, DP) over a
-    two-batch feature buffer.  Every row equals its own align_batch run bit for bit: uniform pairs, a pair of
-    different batch sizes, a batch whose frame count differs from the held one (the held batch runs alone, the new
-    one is held), variable-length batches, an odd last batch flushed by assemble, and a held handle assembled before
-    any further submit."""
-    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
-    dev = torch.device("cuda")
-    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
-    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
-    task.on_predict_start()
-    # held / joins / held / mismatched frames (held runs alone, new held) / joins / held / too many rows for the
-    # held buffer (held runs alone) / joined by the varlen batch below / the last varlen batch flushed by assemble
-    specs = [(3, 4.0, 8, 11), (3, 4.0, 8, 12), (2, 4.0, 8, 13), (2, 3.0, 6, 15), (2, 3.0, 6, 16), (1, 4.0, 8, 14),
-             (3, 4.0, 8, 17)]
-    batches = [_inputs(*s) for s in specs]
-    lens = [None] * len(batches)
-    # a variable-length pair: rows shorter than the batch's width
-    vb = [_inputs(2, 4.0, 8, 30 + i) for i in range(2)]
-    for wav, *_ in vb:
-        wav[1, 40000:] = 0.0
-    batches += vb
-    lens += [[64000, 40000], [64000, 40000]]
-
-    def key(r):
-        return tuple(np.asarray(r[k]).tobytes() for k in ("ph_idx_seq", "ph_time_int", "frame_confidence",
-                                                           "edge_diff"))
-    alone = [[key(r) for r in task.align_batch(torch.from_numpy(w).to(dev), ph, ws, pw, wav_sr=16000, lengths=ln)]
-             for (w, ph, ws, pw), ln in zip(batches, lens)]
-    task.pair_batches = True
-    try:
-        handles = [task.submit(torch.from_numpy(w).to(dev), ph, ws, pw, wav_sr=16000, lengths=ln)
-                   for (w, ph, ws, pw), ln in zip(batches, lens)]
-        assert all(h.get("depth") == 2 for h in handles)
-        got = [[key(r) for r in task.decoder.assemble(h, *b[1:])] for h, b in zip(handles, batches)]
-        for i, (g, a) in enumerate(zip(got, alone)):
-            assert g == a, f"batch {i} ({specs[i] if i < len(specs) else 'varlen'}): rows differ from align_batch"
-        w, ph, ws, pw = batches[0]
-        h = task.submit(torch.from_numpy(w).to(dev), ph, ws, pw, wav_sr=16000)
-        assert "resolve" in h                               # held for a partner
-        assert [key(r) for r in task.decoder.assemble(h, ph, ws, pw)] == alone[0]
-    finally:
-        task.pair_batches = False
