@@ -69,8 +69,6 @@ def parse():
     ap.add_argument("--probe", default="auto",
                     help="kernel instantiation to time; auto = the one carrying the most FLOPs in a warmup census")
     ap.add_argument("--serial", action="store_true", help="one stream per step (no head/encoder overlap)")
-    ap.add_argument("--no-fuse-ln", action="store_true",
-                    help="the encoder's residual GEMM + LayerNorm as two launches (A/B of HubertEncoder.fuse_ln)")
     ap.add_argument("--no-held-dp", action="store_true",
                     help="run a long lattice's DP in one launch behind its head (A/B of task.defer_dp_frames)")
     ap.add_argument("--precision", default="split", choices=["split", "f16"],
@@ -477,8 +475,6 @@ def main():
         task.defer_dp_frames = None
     if args.precision == "f16":
         task.unitsEncoder.model.f16 = True
-    if args.no_fuse_ln:
-        task.unitsEncoder.model.fuse_ln = False
     B = args.batch
     wav_np, ph_seqs, word_seqs, p2ws = make_inputs(B, args.seconds, args.words, seed0=1000 * (rank + 1))
     wav = wav_dev = torch.from_numpy(wav_np).to(dev)

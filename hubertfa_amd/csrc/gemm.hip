@@ -46,14 +46,6 @@ struct GemmP {
     int* oflow;
     int cvec;      // split f32 output: 16-B row pieces (C rows 16-B aligned); 0: scalar stores (no R, no planes)
     const _Float16* Rh; long long sRp;   // split f32 output: the residual as split planes (strides of R, in halves)
-    // fused row LayerNorm (hfa_linear_split_ln; f32 C, Z = 1): after storing its tile every workgroup arrives at its
-    // row block's counter ln_cnt[tm]; the last of the row block's n_tiles arrivals normalises the block's complete
-    // rows of C into ln_ys planes (and / or f32 ln_y) and resets the counter
-    int* ln_cnt;
-    const float* ln_g; const float* ln_b; float ln_eps;
-    float* ln_y; long long ln_ldy;
-    _Float16* ln_ys; long long ln_ldys, ln_sps;
-    int ln_T; const int32_t* ln_tlen;
 };
 
 enum { EPI_NONE = 0, EPI_GELU = 1 };
@@ -839,114 +831,6 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
     if ((bad || hfa::range_bad(nanacc)) && p.oflow) *p.oflow = 1;
 }
 
-// Fused row LayerNorm of a finished row block (hfa_linear_split_ln).  Arrival (every workgroup; the guide's producer
-// recipe for a hand-off through memory, MI355X_MICROARCH.md §Workgroup dispatch ... inter-workgroup visibility): each
-// wave's tile stores drained (vmcnt(0)), a workgroup barrier, then one lane: an agent-scope release (buffer_wbl2 sc1:
-// the XCD L2's dirty lines reach memory), vmcnt(0) again (the compiler may drop its own wait after the write-back),
-// and an agent-scope atomic add on the row block's counter, whose returned value tells the last of the n_tiles
-// arrivals.  That workgroup alone continues (consumer recipe): one agent-scope acquire (buffer_inv sc1), vmcnt(0), a
-// barrier, then plain loads of the block's complete rows of C; it resets the counter (the next launch sees it through
-// the kernel boundary).  No workgroup ever waits for another, so nothing assumes co-residency.  The row arithmetic
-// is norm.hip layernorm_kernel's, one wave per row (every output bit equal to the separate LayerNorm launch), four
-// rows per wave in flight.  N <= 1024, N % 4 == 0.
-template <int NW>
-__device__ __forceinline__ void ln_tail(const GemmP& p, int tm, int BM, int* flag) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(p.ln_cnt + tm, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == p.n_tiles - 1;
-        if (last) __hip_atomic_store(p.ln_cnt + tm, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = last;
-    }
-    __syncthreads();
-    if (!*flag) return;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    constexpr int VPL = 4, RW = 4;                        // 16-B pieces per lane per row, rows per wave in flight
-    const int N = p.N, r0 = tm * BM, r1 = (tm + 1) * BM < p.M ? (tm + 1) * BM : p.M;
-    hfa::h2v nanacc = {(_Float16)0.0f, (_Float16)0.0f};
-    const float c2048 = 2048.0f;
-    for (int rb = r0 + wave * RW; rb < r1; rb += NW * RW) {
-        f32x4 v[RW][VPL];
-#pragma unroll
-        for (int q = 0; q < RW; ++q) {
-            const int r = rb + q < r1 ? rb + q : r0;
-            const float* xr = p.C + (long long)r * p.ldc;
-#pragma unroll
-            for (int i = 0; i < VPL; ++i) {
-                const int c = (lane + i * 64) * 4;
-                v[q][i] = c < N ? *reinterpret_cast<const f32x4*>(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < RW; ++q) {
-            const int r = rb + q;
-            if (r >= r1) break;
-            float* yr = p.ln_y ? p.ln_y + (long long)r * p.ln_ldy : nullptr;
-            _Float16* hr = p.ln_ys ? p.ln_ys + (long long)r * p.ln_ldys : nullptr;
-            if (p.ln_tlen && r % p.ln_T >= p.ln_tlen[r / p.ln_T]) {   // padding row of a varlen batch: zeros
-#pragma unroll
-                for (int i = 0; i < VPL; ++i) {
-                    const int c = (lane + i * 64) * 4;
-                    if (c < N) {
-                        if (yr) *reinterpret_cast<f32x4*>(yr + c) = f32x4{0.f, 0.f, 0.f, 0.f};
-                        if (hr) {
-                            *reinterpret_cast<uint2*>(hr + c) = make_uint2(0u, 0u);
-                            *reinterpret_cast<uint2*>(hr + p.ln_sps + c) = make_uint2(0u, 0u);
-                        }
-                    }
-                }
-                continue;
-            }
-            float s = 0.f;
-#pragma unroll
-            for (int i = 0; i < VPL; ++i) s += (v[q][i][0] + v[q][i][1]) + (v[q][i][2] + v[q][i][3]);
-            const float mean = hfa::wave_sum(s) / (float)N;
-            float ss = 0.f;
-#pragma unroll
-            for (int i = 0; i < VPL; ++i) {
-                const int c = (lane + i * 64) * 4;
-                if (c < N) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float d = v[q][i][e] - mean;
-                        ss += d * d;
-                    }
-                }
-            }
-            const float var = hfa::wave_sum(ss) / (float)N;
-            const float rstd = 1.0f / sqrtf(var + p.ln_eps);
-#pragma unroll
-            for (int i = 0; i < VPL; ++i) {
-                const int c = (lane + i * 64) * 4;
-                if (c < N) {
-                    const f32x4 g = *reinterpret_cast<const f32x4*>(p.ln_g + c);
-                    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.ln_b + c);
-                    f32x4 o;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) o[e] = (v[q][i][e] - mean) * rstd * g[e] + bb[e];
-                    if (yr) *reinterpret_cast<f32x4*>(yr + c) = o;
-                    if (hr) {
-                        uint2 h1, h2;
-                        hfa::split_pair(o[0], o[1], h1.x, h2.x, nanacc, c2048);
-                        hfa::split_pair(o[2], o[3], h1.y, h2.y, nanacc, c2048);
-                        *reinterpret_cast<uint2*>(hr + c) = h1;
-                        *reinterpret_cast<uint2*>(hr + p.ln_sps + c) = h2;
-                    }
-                }
-            }
-        }
-    }
-    if (hfa::range_bad(nanacc) && p.oflow) *p.oflow = 1;
-}
-
 // GT (general taps): Cg a multiple of 8 but not of 32 (the grouped positional conv, Cg = 48): a K-step's four
 // 16-B chunks can straddle a tap boundary, so every lane tracks its own chunk's (tap, channel) instead of the
 // workgroup-uniform tap + scalar channel offset.
@@ -1188,11 +1072,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
         else if constexpr (OUT_SPLIT)
             store_split_lds<16, TI, TJ>(p, acc, EPI, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
                                         slab, kScale);
-        else {
+        else
             store_f32_lds<16, EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
                                            slab, true, kScale);
-            if (p.ln_cnt) ln_tail<NW>(p, tm, BM, reinterpret_cast<int*>(smem));
-        }
     }
 }
 
@@ -1889,8 +1771,6 @@ GemmP make_params(int M, int N, int K, int G, const float* A, long long sAb, lon
     p.Ah = nullptr; p.sAp = 0; p.Wh = nullptr; p.sWp = 0; p.Ch = nullptr; p.sCp = 0; p.oflow = nullptr;
     p.cvec = 1;
     p.Rh = nullptr; p.sRp = 0;
-    p.ln_cnt = nullptr; p.ln_g = p.ln_b = nullptr; p.ln_eps = 0.0f; p.ln_y = nullptr; p.ln_ldy = 0;
-    p.ln_ys = nullptr; p.ln_ldys = p.ln_sps = 0; p.ln_T = 0; p.ln_tlen = nullptr;
     return p;
 }
 
@@ -1946,63 +1826,12 @@ int hfa_gemm_f32(int M, int N, int K, const float* A, int lda, const float* W, i
 
 // Split-f16 implicit GEMM (gemm_split_kernel): A, W as f16 plane pairs (plane 1 at +sAp / +sWp halves), element
 // strides in halves; output either f32 C (+R) or, with Cs, f16 planes (plane 1 at +sCp; bias/GELU only, no R).
-}  // extern "C"
-
-namespace {
-struct LnArgs {                     // hfa_linear_split_ln's LayerNorm (GemmP ln_* fields)
-    const float *g, *b; float eps; int T; const int32_t* t_len;
-    float* y; long long ldy; uint16_t* ys; long long ldys, sps; int* counters;
-};
-
-int conv_gemm_split_impl(int M, int N, int K, int Zb, int G, const uint16_t* A, long long sAp, long long sAb,
-                         long long sAg, int ldx, int stride, int pad, int Cg, int Tin, const uint16_t* W,
-                         long long sWp, long long sWg, int ldw, const float* bias, long long sBg, const float* R,
-                         long long sRb, long long sRg, int ldr, const uint16_t* Rs, long long sRp, float* C,
-                         uint16_t* Cs, long long sCp, long long sCb, long long sCg, int ldc, int epilogue, int* oflow,
-                         hipStream_t stream, const LnArgs* ln);
-}  // namespace
-
-extern "C" {
-
 int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, long long sAp, long long sAb,
                         long long sAg, int ldx, int stride, int pad, int Cg, int Tin, const uint16_t* W,
                         long long sWp, long long sWg, int ldw, const float* bias, long long sBg, const float* R,
                         long long sRb, long long sRg, int ldr, const uint16_t* Rs, long long sRp, float* C,
                         uint16_t* Cs, long long sCp, long long sCb, long long sCg, int ldc, int epilogue, int* oflow,
                         hipStream_t stream) {
-    return conv_gemm_split_impl(M, N, K, Zb, G, A, sAp, sAb, sAg, ldx, stride, pad, Cg, Tin, W, sWp, sWg, ldw, bias,
-                                sBg, R, sRb, sRg, ldr, Rs, sRp, C, Cs, sCp, sCb, sCg, ldc, epilogue, oflow, stream,
-                                nullptr);
-}
-
-long long hfa_linear_split_ln_workspace_bytes(int M) { return ((long long)(M + 63) / 64 + 1) * (long long)sizeof(int); }
-
-int hfa_linear_split_ln(int M, int N, int K, const uint16_t* A, long long sAp, int lda, const uint16_t* W,
-                        long long sWp, int ldw, const float* bias, const float* R, int ldr, const uint16_t* Rs,
-                        long long sRp, float* C, int ldc, const float* gamma, const float* beta, float eps, int T,
-                        const int32_t* t_len, float* y, long long ldy, uint16_t* ys, long long ldys, long long sps,
-                        int* counters, int* oflow, hipStream_t stream) {
-    if (N <= 0 || N % 4 || N > 1024 || !C || !gamma || !beta || !counters || (!y && !ys) ||
-        (((uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)y) & 15) || (y && ldy % 4) ||
-        (ys && ((((uintptr_t)ys) & 7) || ldys % 4 || sps % 4)) || (t_len && (T <= 0 || M % T))) {
-        hfa::set_error("hfa_linear_split_ln: N %% 4 == 0 and N <= 1024, C, gamma, beta, counters and y and / or ys "
-                       "required (16-B y rows, 8-B plane rows), t_len needs M = B * T");
-        return HFA_EINVAL;
-    }
-    const LnArgs ln{gamma, beta, eps, T, t_len, y, ldy, ys, ldys, sps, counters};
-    return conv_gemm_split_impl(M, N, K, 1, 1, A, sAp, 0, 0, lda, 1, 0, K, M, W, sWp, 0, ldw, bias, 0, R, 0, 0, ldr,
-                                Rs, sRp, C, nullptr, 0, 0, 0, ldc, EPI_NONE, oflow, stream, &ln);
-}
-
-}  // extern "C"
-
-namespace {
-int conv_gemm_split_impl(int M, int N, int K, int Zb, int G, const uint16_t* A, long long sAp, long long sAb,
-                         long long sAg, int ldx, int stride, int pad, int Cg, int Tin, const uint16_t* W,
-                         long long sWp, long long sWg, int ldw, const float* bias, long long sBg, const float* R,
-                         long long sRb, long long sRg, int ldr, const uint16_t* Rs, long long sRp, float* C,
-                         uint16_t* Cs, long long sCp, long long sCb, long long sCg, int ldc, int epilogue, int* oflow,
-                         hipStream_t stream, const LnArgs* ln) {
     if (M < 0 || N < 0 || K < 0 || Zb < 0 || G < 1 || stride < 1 || Cg < 1 || Tin < 1) {
         hfa::set_error("hfa_conv_gemm_split: bad sizes M=%d N=%d K=%d Zb=%d G=%d", M, N, K, Zb, G);
         return HFA_EINVAL;
@@ -2063,16 +1892,7 @@ int conv_gemm_split_impl(int M, int N, int K, int Zb, int G, const uint16_t* A, 
         hfa::set_error("hfa_conv_gemm_split: a split-plane residual needs 16-B aligned C rows");
         return HFA_EINVAL;
     }
-    if (ln) {
-        p.ln_cnt = ln->counters; p.ln_g = ln->g; p.ln_b = ln->b; p.ln_eps = ln->eps; p.ln_T = ln->T;
-        p.ln_tlen = ln->t_len; p.ln_y = ln->y; p.ln_ldy = ln->ldy; p.ln_ys = reinterpret_cast<_Float16*>(ln->ys);
-        p.ln_ldys = ln->ldys; p.ln_sps = ln->sps;
-    }
     const int Z = Zb * G, cfg = split_cfg(p, Z);
-    if (ln && (cfg == SCFG_WIN || cfg == SCFG_N48 || !p.cvec || split_geom(cfg).BM < 64)) {
-        hfa::set_error("hfa_linear_split_ln: needs 16-B aligned C rows and a gemm_split_kernel tile");
-        return HFA_EINVAL;
-    }
     if ((cfg == SCFG_WIN || cfg == SCFG_N48) && (!p.cvec || Rs)) {
         hfa::set_error("hfa_conv_gemm_split: the grouped positional conv kernels need 16-B aligned C rows and an f32 "
                        "residual");
@@ -2106,9 +1926,6 @@ int conv_gemm_split_impl(int M, int N, int K, int Zb, int G, const uint16_t* A, 
     return epilogue == EPI_GELU ? launch_split<EPI_GELU, false>(p, Z, cfg, stream, f16)
                                 : launch_split<EPI_NONE, false>(p, Z, cfg, stream, f16);
 }
-}  // namespace
-
-extern "C" {
 
 const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split, int epilogue, int Cg) {
     GemmP p = make_params(M, N, K, 1, nullptr, 0, 0, 0, 1, 0, Cg, 1, nullptr, 0, 0);

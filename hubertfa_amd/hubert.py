@@ -91,9 +91,6 @@ class HubertEncoder:
         self.f16 = precision == "f16"           # a flag beside precision: the f32 re-run of the range guard
         precision = "split" if self.f16 else precision      # switches precision only
         self.precision = precision
-        # the residual GEMMs (out-projection, FFN2) and the LayerNorm after them as one launch on the split path
-        # (ops.linear_split_ln: the same values as the two launches); False: two launches
-        self.fuse_ln = True
         self.device = torch.device(device)
         sd = _strip(state_dict)
         dev = self.device
@@ -285,15 +282,6 @@ class HubertEncoder:
             return self._linear(None, L_.wo, L_.wo_s, L_.bo, residual=residual, xs=o)
         return self._linear(o, L_.wo, L_.wo_s, L_.bo, residual=residual)
 
-    def _linear_ln(self, xs, w, ws, bias, residual, ln, planes=True, f32=False):
-        """LayerNorm(x @ W^T + bias + residual) in one launch when the fused form applies (split path with split
-        weights, xs given as planes, hidden <= 1024, not the f16 mode), else None: (y f32 or None, planes or None)."""
-        if not (self.fuse_ln and self.precision == "split" and not self.f16 and ws is not None and xs is not None
-                and xs.dtype == torch.float16 and ws.shape[1] <= 1024):
-            return None
-        return ops.linear_split_ln(xs, ws, bias, residual, ln[0], ln[1], self.arch.layer_norm_eps, out_f32=f32,
-                                   out_split=planes)
-
     def _ln(self, x, w, b, out=None, split=False, planes_only=False):
         """LayerNorm; with ``split`` (a split GEMM consumes the result) also the split planes, from the same
         kernel: returns (y, planes) — planes None when not requested.  ``planes_only`` (split path): no f32 output
@@ -314,18 +302,9 @@ class HubertEncoder:
             # bits, the precision every split GEMM operand has): no f32 LayerNorm output is written or read back
             o = self.attention_block(h, L_, lens, hs, gate=gate)
             res = hs if (hs is not None and L_.wo_s is not None and self.precision == "split") else h
-            fused = self._linear_ln(o, L_.wo, L_.wo_s, L_.bo, res, (L_.ln1_w, L_.ln1_b)) if sp else None
-            if fused is not None:                # out-projection + residual + norm1 in one launch (planes only)
-                h1, h1s = fused
-            else:
-                h1 = self._out_proj(o, L_, res)
-                h1, h1s = self._ln(h1, L_.ln1_w, L_.ln1_b, out=h1, split=sp, planes_only=sp)
+            h1 = self._out_proj(o, L_, res)
+            h1, h1s = self._ln(h1, L_.ln1_w, L_.ln1_b, out=h1, split=sp, planes_only=sp)
             f = self._linear(h1, L_.w1, L_.w1_s, L_.b1, epilogue=ops.EPI_GELU, out_split=sp, xs=h1s)
-            if sp:                               # FFN2 + residual + norm2 in one launch where it applies
-                fused = self._linear_ln(f, L_.w2, L_.w2_s, L_.b2, h1s, (L_.ln2_w, L_.ln2_b), planes=want_split,
-                                        f32=not want_split)
-                if fused is not None:
-                    return fused
             h2 = self._linear(None, L_.w2, L_.w2_s, L_.b2, residual=h1s, xs=f) if sp else \
                 ops.linear(f, L_.w2, L_.b2, residual=h1)
             return self._ln(h2, L_.ln2_w, L_.ln2_b, out=h2, split=want_split, planes_only=want_split)

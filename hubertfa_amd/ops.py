@@ -388,63 +388,6 @@ def linear_split(xs, Ws, bias=None, residual=None, out=None, epilogue=EPI_NONE, 
     return (out, hs) if dual else out
 
 
-_lib.register("hfa_linear_split_ln", [_I_, _I_, _I_, _P_, _LL_, _I_, _P_, _LL_, _I_, _P_, _P_, _I_, _P_, _LL_, _P_, _I_,
-                                      _P_, _P_, _F_, _I_, _P_, _P_, _LL_, _P_, _LL_, _LL_, _P_, _P_, _P_])
-_lib.register("hfa_linear_split_ln_workspace_bytes", [_I_], ctypes.c_longlong)
-_LN_CNT = {}
-
-
-def _ln_counters(device, M: int) -> torch.Tensor:
-    """The fused LayerNorm's row-block arrival counters for ``device`` (zeroed once; every launch leaves them zero),
-    grown to cover M rows."""
-    need = int(_lib.lib().hfa_linear_split_ln_workspace_bytes(M)) // 4
-    c = _LN_CNT.get(device)
-    if c is None or c.numel() < need:
-        c = torch.zeros(max(need, 4096), dtype=torch.int32, device=device)
-        _LN_CNT[device] = c
-    return c
-
-
-def linear_split_ln(xs, Ws, bias, residual, gamma, beta, eps, out_f32=True, out_split=True, flag=None):
-    """LayerNorm(x @ W^T + bias + residual) * gamma + beta in ONE launch (gemm.hip hfa_linear_split_ln: the split
-    GEMM's last workgroup per row block normalises the block's rows; the values are those of linear_split followed
-    by layernorm).  xs / Ws: split planes [2, ..., K] / [2, N, K]; residual f32 [..., N] or planes [2, ..., N].
-    Returns (y f32 or None, planes [2, ..., N] or None): ``out_f32`` keeps the f32 LayerNorm output (written over the
-    GEMM's own f32 result), ``out_split`` its split planes."""
-    K = xs.shape[-1]
-    N = Ws.shape[1]
-    lead = xs.shape[1:-1]
-    M = 1
-    for d in lead:
-        M *= d
-    dev = xs.device
-    _need(xs, torch.float16, "xs", contiguous=False)
-    _need(Ws, torch.float16, "Ws")
-    C = torch.empty((*lead, N), dtype=torch.float32, device=dev)
-    ys = torch.empty((2, *lead, N), dtype=torch.float16, device=dev) if out_split else None
-    R = Rs = None
-    if residual is not None:
-        if residual.dtype == torch.float16:
-            Rs = residual.reshape(2, -1, N)
-        else:
-            R = residual.reshape(-1, N)
-    c2, y2 = C.view(-1, N), (ys.view(2, -1, N) if ys is not None else None)
-    ldx = xs.stride(-2) if xs.dim() > 2 else K
-
-    def launch():
-        _lib.call("hfa_linear_split_ln", M, N, K, _ptr(xs), xs.stride(0), ldx, _ptr(Ws), Ws.stride(0), Ws.stride(1),
-                  _ptr(bias), _ptr(R), R.stride(0) if R is not None else (Rs.stride(1) if Rs is not None else 0),
-                  _ptr(Rs), Rs.stride(0) if Rs is not None else 0, _ptr(c2), N, _ptr(gamma), _ptr(beta), float(eps), 0,
-                  None, _ptr(c2 if out_f32 else None), N if out_f32 else 0, _ptr(y2),
-                  y2.stride(1) if y2 is not None else 0, y2.stride(0) if y2 is not None else 0,
-                  _ptr(_ln_counters(dev, M)), _ptr(split_flag(dev) if flag is None else flag), _stream(dev))
-    if PROBE is None:
-        launch()
-    else:
-        PROBE(_split_name(M, N, K, 1, False, EPI_NONE, K), 2.0 * M * N * K, launch, shape=(M, N, K, 1))
-    return (C if out_f32 else None), ys
-
-
 def _lens(lens):
     """Optional per-row lengths of a variable-length batch: None or an int32 device tensor [B]."""
     if lens is None:

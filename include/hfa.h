@@ -157,21 +157,6 @@ int hfa_conv_gemm_split(int M, int N, int K, int Zb, int G, const uint16_t* A, l
                         long long sRb, long long sRg, int ldr, const uint16_t* Rs, long long sRp, float* C,
                         uint16_t* Cs, long long sCp, long long sCb, long long sCg, int ldc, int epilogue, int* oflow,
                         hipStream_t stream);
-/* hfa_conv_gemm_split as a plain Linear (Z = 1, f32 C + R or Rs, no activation) followed by a row LayerNorm of C
- * in the same launch: y / ys = LayerNorm(C) * gamma + beta over each row's N <= 1024 columns (N % 4 == 0), rows
- * t >= t_len[b] of a [B, T] batch (M = B * T) as zeros, exactly the values hfa_layernorm_split gives on C.  Replaces
- * the out-projection / FFN2 + residual + LayerNorm of the post-LN encoder layer (nn.TransformerEncoderLayer
- * norm1/norm2, transformers HubertEncoderLayer.layer_norm / final_layer_norm; networks/hubert/model.py:27-32) and the
- * pre-LN layer's residual sum + next LayerNorm (HubertEncoderLayerStableLayerNorm).  C (f32 [M, ldc]) receives
- * A.W + bias + R as hfa_conv_gemm_split writes it; the last workgroup of each row block (an agent-scope counter in
- * `counters`, hfa_linear_split_ln_workspace_bytes(M) bytes of device memory, zero before the first call and left
- * zero by every call) normalises the block's rows.  One stream at a time per counters buffer. */
-long long hfa_linear_split_ln_workspace_bytes(int M);
-int hfa_linear_split_ln(int M, int N, int K, const uint16_t* A, long long sAp, int lda, const uint16_t* W,
-                        long long sWp, int ldw, const float* bias, const float* R, int ldr, const uint16_t* Rs,
-                        long long sRp, float* C, int ldc, const float* gamma, const float* beta, float eps, int T,
-                        const int32_t* t_len, float* y, long long ldy, uint16_t* ys, long long ldys, long long sps,
-                        int* counters, int* oflow, hipStream_t stream);
 /* rocprof symbol stem of the split instantiation for an M x N x K contraction over Z = Zb*G (out_split: planes out;
  * stride 1 assumed, as the grouped positional conv's window kernel needs). */
 const char* hfa_gemm_split_kernel_name(int M, int N, int K, int Z, int out_split, int epilogue, int Cg);
