@@ -189,9 +189,11 @@ class HubertEncoder:
                           out_split=n > 1 and self._split_conv(1))
         else:
             h = ops.conv0(x, self.conv_w[0], bias=self.conv_b[0])
-            h = ops.layernorm(h, ln0[0], ln0[1], a.layer_norm_eps, act=ops.ACT_GELU, out=h)
-            if n > 1 and self._split_conv(1):
-                h = ops.split(h)
+            if n > 1 and self._split_conv(1):      # LayerNorm + GELU straight to the next conv's split planes
+                h = ops.layernorm(h, ln0[0], ln0[1], a.layer_norm_eps, act=ops.ACT_GELU, out=False,
+                                  out_split=True)[1]
+            else:
+                h = ops.layernorm(h, ln0[0], ln0[1], a.layer_norm_eps, act=ops.ACT_GELU, out=h)
         for i in range(1, n):
             k, s = a.conv_kernel[i], a.conv_stride[i]
             split_in = h.dtype == torch.float16
@@ -211,10 +213,15 @@ class HubertEncoder:
             else:
                 ops.conv_gemm(h, self.conv_w[i], out, **kw)
             if layer_norm:
-                out = ops.layernorm(out, self.conv_ln[i][0], self.conv_ln[i][1], a.layer_norm_eps,
-                                    act=ops.ACT_GELU, out=out)
+                # (HubertLayerNormConvLayer, Hubert-large) the planes of LayerNorm + GELU written by the LayerNorm
+                # itself when a split conv follows -- the same values as splitting its f32 output, without the f32
+                # write and the conversion pass (2.1 GB each way at conv0's 32 x 32 000 frames)
                 if i + 1 < n and self._split_conv(i + 1):
-                    out = ops.split(out)
+                    out = ops.layernorm(out, self.conv_ln[i][0], self.conv_ln[i][1], a.layer_norm_eps,
+                                        act=ops.ACT_GELU, out=False, out_split=True)[1]
+                else:
+                    out = ops.layernorm(out, self.conv_ln[i][0], self.conv_ln[i][1], a.layer_norm_eps,
+                                        act=ops.ACT_GELU, out=out)
             h = out
         return h
 

@@ -1,0 +1,65 @@
+"""Split-GEMM microbenchmark for library A/Bs (HFA_LIB selects the build): us per launch and f32-equivalent TF/s on
+config 2's dominant shapes with the automatic tile, median of 5 x --reps launches (run on the GPU box)."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from hubertfa_amd import ops  # noqa: E402
+
+# name, M, N, K, Zb, conv (k, stride, Tin, Cin) or None, epilogue, planes out, residual planes
+SHAPES = [("conv1", 15999, 512, 1536, 32, (3, 2, 31999, 512), 1, True, False),
+          ("ffn1", 15968, 3072, 768, 1, None, 1, True, False),
+          ("qkv", 15968, 2304, 768, 1, None, 0, True, False),
+          ("ffn2", 15968, 768, 3072, 1, None, 0, False, True),
+          ("outproj", 15968, 768, 768, 1, None, 0, False, True)]
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    ts = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / reps * 1e3)
+    return sorted(ts)[2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tag", default=os.path.basename(os.path.dirname(os.environ.get("HFA_LIB", "cur/x"))))
+    args = ap.parse_args()
+    d = torch.device("cuda")
+    for name, M, N, K, Zb, conv, epi, outs, res in SHAPES:
+        W = ops.split(torch.randn(N, K, device=d) * K ** -0.5)
+        b = torch.randn(N, device=d)
+        if conv:
+            k, s, Tin, Cin = conv
+            A = ops.split(torch.randn(Zb, Tin, Cin, device=d))
+            C = torch.empty(2, Zb, M, N, dtype=torch.float16, device=d)
+
+            def go():
+                ops.conv_gemm_split(A, W, Cs=C, M=M, N=N, K=K, Zb=Zb, sAb=Tin * Cin, ldx=Cin, stride=s, Cg=Cin,
+                                    Tin=Tin, bias=b, sCb=M * N, ldc=N, epilogue=epi)
+        else:
+            A = ops.split(torch.randn(M, K, device=d))
+            R = ops.split(torch.randn(M, N, device=d)) if res else None
+
+            def go():
+                ops.linear_split(A, W, b, residual=R, epilogue=epi, out_split=outs)
+        us = timeit(go, args.reps // (4 if conv else 1) or 1)
+        print(f"{args.tag:12s} {name:8s} {us:8.1f} us {2.0 * M * N * K * Zb / us / 1e6:7.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
