@@ -268,12 +268,54 @@ __global__ __launch_bounds__(256) void gn_rows_partial_kernel(int T, int C, int 
     }
 }
 
+// (b, g) statistics from S = sum x, SS = sum x^2 over the row's Tb * Cg values
+__device__ __forceinline__ void gn_stat(double S, double SS, int Tb, int Cg, float eps, float* out) {
+    const double n = (double)Tb * Cg;
+    const double mean_d = Tb > 0 ? S / n : 0.0;
+    double var_d = Tb > 0 ? SS / n - mean_d * mean_d : 0.0;
+    if (var_d < 0) var_d = 0;
+    out[0] = (float)mean_d;
+    out[1] = (float)(1.0 / sqrt(var_d + (double)eps));
+}
+
+// Long rows (more than kGnStatParts parts, e.g. config 5's UNet level 0 at T = 25 840: 808 parts): the statistics once
+// per batch row, before pass 2.  The parts are summed in part order exactly as pass 2 does in-block (the same bits),
+// but staged through LDS in coalesced chunks: pass 2's per-block loop reads one dependent f64 pair per part and took
+// ~125 us per call there, in every one of its 808 blocks at once.
+constexpr int kGnStatParts = 64;
+
+__global__ __launch_bounds__(256) void gn_rows_stats_kernel(int T, int Cg, int G, const int32_t* __restrict__ t_len,
+                                                            const double* __restrict__ part, int P, float eps,
+                                                            float* __restrict__ stats) {
+    const int b = blockIdx.x;
+    const int Tb = t_len ? t_len[b] : T;
+    const int pb = (Tb + kGnRows - 1) / kGnRows;
+    __shared__ double buf[kGnStatParts * 64 * 2];      // kGnStatParts parts x G <= 64 groups x (S, SS): 64 KiB
+    double S = 0.0, SS = 0.0;
+    for (int k0 = 0; k0 < pb; k0 += kGnStatParts) {
+        const int n = (pb - k0 < kGnStatParts ? pb - k0 : kGnStatParts) * G * 2;
+        const double* src = part + ((size_t)b * P + k0) * G * 2;
+        for (int i = threadIdx.x; i < n; i += 256) buf[i] = src[i];
+        __syncthreads();
+        if (threadIdx.x < G) {
+            const int g = threadIdx.x;
+            for (int i = 2 * g; i < n; i += 2 * G) {
+                S += buf[i];
+                SS += buf[i + 1];
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < G) gn_stat(S, SS, Tb, Cg, eps, stats + ((size_t)b * G + threadIdx.x) * 2);
+}
+
 __global__ __launch_bounds__(256) void gn_rows_apply_kernel(int T, int C, int G, const float* __restrict__ x,
                                                             long long x_bs, int ldx, const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, float eps, int act,
                                                             float* __restrict__ y, long long y_bs, int ldy,
                                                             const int32_t* __restrict__ t_len,
                                                             const double* __restrict__ part,
+                                                            const float* __restrict__ stats,
                                                             _Float16* __restrict__ ys, long long ys_bs, int ldys,
                                                             long long sps, int* __restrict__ oflow) {
     const int pi = blockIdx.x, b = blockIdx.y, P = gridDim.x;
@@ -281,19 +323,20 @@ __global__ __launch_bounds__(256) void gn_rows_apply_kernel(int T, int C, int G,
     const int Tb = t_len ? t_len[b] : T;
     __shared__ float stat[64][2];                       // G <= 64: mean, rstd per group
     if (threadIdx.x < G) {
-        const int g = threadIdx.x, pb = (Tb + kGnRows - 1) / kGnRows;   // this row's own parts, in order
-        double S = 0.0, SS = 0.0;
-        for (int k = 0; k < pb; ++k) {
-            const double* pp = part + (((size_t)b * P + k) * G + g) * 2;
-            S += pp[0];
-            SS += pp[1];
+        const int g = threadIdx.x;
+        if (stats) {                                    // long rows: gn_rows_stats_kernel summed the parts
+            stat[g][0] = stats[((size_t)b * G + g) * 2];
+            stat[g][1] = stats[((size_t)b * G + g) * 2 + 1];
+        } else {
+            const int pb = (Tb + kGnRows - 1) / kGnRows;   // this row's own parts, in order
+            double S = 0.0, SS = 0.0;
+            for (int k = 0; k < pb; ++k) {
+                const double* pp = part + (((size_t)b * P + k) * G + g) * 2;
+                S += pp[0];
+                SS += pp[1];
+            }
+            gn_stat(S, SS, Tb, Cg, eps, &stat[g][0]);
         }
-        const double n = (double)Tb * Cg;
-        const double mean_d = Tb > 0 ? S / n : 0.0;
-        double var_d = Tb > 0 ? SS / n - mean_d * mean_d : 0.0;
-        if (var_d < 0) var_d = 0;
-        stat[g][0] = (float)mean_d;
-        stat[g][1] = (float)(1.0 / sqrt(var_d + (double)eps));
     }
     __syncthreads();
     const int col = threadIdx.x % C4, r0 = threadIdx.x / C4;
@@ -378,7 +421,8 @@ int hfa_layernorm_split(int rows, int C, const float* x, long long ldx, const fl
 long long hfa_groupnorm_workspace_bytes(int B, int T, int C, int G) {
     (void)C;
     const long long a = (long long)B * G * 64 * 2 * sizeof(double) + 64;                      // split-T path
-    const long long r = (long long)B * ((T + kGnRows - 1) / kGnRows) * G * 2 * sizeof(double);   // row-parallel path
+    const long long r = (long long)B * ((T + kGnRows - 1) / kGnRows) * G * 2 * sizeof(double)   // row-parallel path
+                        + (long long)B * G * 2 * sizeof(float);                                 // its long-row stats
     return a > r ? a : r;
 }
 
@@ -402,10 +446,13 @@ int hfa_groupnorm_split(int B, int T, int C, int G, const float* x, long long x_
     }
     const int P = (T + kGnRows - 1) / kGnRows;
     double* part = reinterpret_cast<double*>(workspace);
+    float* stats = P > kGnStatParts ? reinterpret_cast<float*>(part + (size_t)B * P * G * 2) : nullptr;
     hipLaunchKernelGGL(gn_rows_partial_kernel, dim3(P, B), dim3(256), 0, stream, T, C, G, x, x_bs, ldx, t_len, part);
+    if (stats)
+        hipLaunchKernelGGL(gn_rows_stats_kernel, dim3(B), dim3(256), 0, stream, T, C / G, G, t_len, part, P, eps, stats);
     // (the apply pass may write y in place of x: every partial of the batch row is complete at this launch boundary)
     hipLaunchKernelGGL(gn_rows_apply_kernel, dim3(P, B), dim3(256), 0, stream, T, C, G, x, x_bs, ldx, gamma, beta,
-                       eps, act, y, y_bs, ldy, t_len, part, ys, ys_bs, ldys, sps, oflow);
+                       eps, act, y, y_bs, ldy, t_len, part, stats, ys, ys_bs, ldys, sps, oflow);
     return hfa::check_launch("hfa_groupnorm_split");
 }
 

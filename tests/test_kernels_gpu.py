@@ -245,6 +245,26 @@ def test_groupnorm_split_planes(B, T, C):
     assert torch.equal(pl, ops.split(yl))
 
 
+def test_groupnorm_long_row_stats_pass_bits():
+    """Rows of more than 64 parts (2 048 frames) get their statistics from gn_rows_stats_kernel, which sums the parts in
+    the order the apply pass uses in-block for shorter rows: a 1 500-frame row inside a batch padded to 3 000 frames
+    (stats pass) gives the bits it gets alone (in-block sums), and a 30 000-frame row matches f64 GroupNorm."""
+    from hubertfa_amd import ops
+    d = torch.device("cuda")
+    C = 192
+    x = (_r(2, 3000, C, seed=18, scale=2.0) + 0.3).to(d)
+    g, b = (_r(C, seed=19) * 0.1 + 1).to(d), (_r(C, seed=20) * 0.1).to(d)
+    lens = torch.tensor([3000, 1500], dtype=torch.int32, device=d)
+    yl, pl = ops.groupnorm(x, 16, g, b, 1e-5, act=ops.ACT_HARDSWISH, t_len=lens, out_split=True)
+    alone, pa = ops.groupnorm(x[1:2, :1500].contiguous(), 16, g, b, 1e-5, act=ops.ACT_HARDSWISH, out_split=True)
+    assert torch.equal(yl[1, :1500], alone[0]) and torch.equal(pl[:, 1, :1500], pa[:, 0])
+    xl = (_r(1, 30000, C, seed=21, scale=2.0) + 0.3)
+    ref = F.hardswish(F.group_norm(xl.double().transpose(1, 2), 16, g.cpu().double(), b.cpu().double(),
+                                   1e-5)).transpose(1, 2)
+    y, _ = ops.groupnorm(xl.to(d), 16, g, b, 1e-5, act=ops.ACT_HARDSWISH, out_split=True)
+    _close(y, ref, 1e-5, 2e-5)
+
+
 def test_split_gemm_dual_output():
     """Dual epilogue: the f32 output (+bias, +residual) and the planes of that same value in one launch."""
     from hubertfa_amd import ops
