@@ -37,28 +37,36 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--data", default="randn", choices=["randn", "zeros", "hionly"],
+                    help="operand data: randn, all zeros, or f16-exact values (zero low planes)")
     ap.add_argument("--tag", default=os.path.basename(os.path.dirname(os.environ.get("HFA_LIB", "cur/x"))))
     args = ap.parse_args()
     d = torch.device("cuda")
+
+    def rnd(*shape):
+        x = torch.randn(*shape, device=d)
+        if args.data == "zeros":
+            return torch.zeros_like(x)
+        return x.half().float() if args.data == "hionly" else x
     for name, M, N, K, Zb, conv, epi, outs, res in SHAPES:
-        W = ops.split(torch.randn(N, K, device=d) * K ** -0.5)
+        W = ops.split((rnd(N, K) * K ** -0.5).half().float() if args.data == "hionly" else rnd(N, K) * K ** -0.5)
         b = torch.randn(N, device=d)
         if conv:
             k, s, Tin, Cin = conv
-            A = ops.split(torch.randn(Zb, Tin, Cin, device=d))
+            A = ops.split(rnd(Zb, Tin, Cin))
             C = torch.empty(2, Zb, M, N, dtype=torch.float16, device=d)
 
             def go():
                 ops.conv_gemm_split(A, W, Cs=C, M=M, N=N, K=K, Zb=Zb, sAb=Tin * Cin, ldx=Cin, stride=s, Cg=Cin,
                                     Tin=Tin, bias=b, sCb=M * N, ldc=N, epilogue=epi)
         else:
-            A = ops.split(torch.randn(M, K, device=d))
+            A = ops.split(rnd(M, K))
             R = ops.split(torch.randn(M, N, device=d)) if res else None
 
             def go():
                 ops.linear_split(A, W, b, residual=R, epilogue=epi, out_split=outs)
         us = timeit(go, args.reps // (4 if conv else 1) or 1)
-        print(f"{args.tag:12s} {name:8s} {us:8.1f} us {2.0 * M * N * K * Zb / us / 1e6:7.1f} TF/s", flush=True)
+        print(f"{args.tag + '/' + args.data:18s} {name:8s} {us:8.1f} us {2.0 * M * N * K * Zb / us / 1e6:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
