@@ -85,9 +85,9 @@ def parse():
     ap.add_argument("--host-input", action="store_true",
                     help="waves start in host memory and are uploaded inside every step (task.upload, as infer.py) (PCIe-inclusive "
                          "rate; the headline value keeps inputs resident in HBM)")
-    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r04", "traffic_r04.json"),
+    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r05", "traffic_r05.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by scripts/pmc_traffic.py)")
-    ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "r04", "pmc_r04.json"),
+    ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "r05", "pmc_r05.json"),
                     help="PMC-derived MFMA busy and clock per kernel (written by scripts/pmc_kernels.py)")
     return ap.parse_args()
 
