@@ -37,8 +37,9 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--data", default="randn", choices=["randn", "zeros", "hionly"],
-                    help="operand data: randn, all zeros, or f16-exact values (zero low planes)")
+    ap.add_argument("--data", default="randn", choices=["randn", "zeros", "hionly", "wrows", "arows"],
+                    help="operand data: randn, all zeros, f16-exact values (zero low planes), every W row equal (wrows) or every "
+                         "A row equal (arows)")
     ap.add_argument("--tag", default=os.path.basename(os.path.dirname(os.environ.get("HFA_LIB", "cur/x"))))
     args = ap.parse_args()
     d = torch.device("cuda")
@@ -47,20 +48,29 @@ def main():
         x = torch.randn(*shape, device=d)
         if args.data == "zeros":
             return torch.zeros_like(x)
-        return x.half().float() if args.data == "hionly" else x
+        return x
+
+    def rows_equal(x, which):                  # hionly rounding; every row (last dim) a copy of row 0 for `which`
+        if args.data == "hionly":
+            return x.half().float()
+        if args.data != which:
+            return x
+        x2 = x.reshape(-1, x.shape[-1])
+        return x2[:1].expand_as(x2).contiguous().reshape(x.shape)
+
     for name, M, N, K, Zb, conv, epi, outs, res in SHAPES:
-        W = ops.split((rnd(N, K) * K ** -0.5).half().float() if args.data == "hionly" else rnd(N, K) * K ** -0.5)
+        W = ops.split(rows_equal(rnd(N, K) * K ** -0.5, "wrows"))
         b = torch.randn(N, device=d)
         if conv:
             k, s, Tin, Cin = conv
-            A = ops.split(rnd(Zb, Tin, Cin))
+            A = ops.split(rows_equal(rnd(Zb, Tin, Cin), "arows"))
             C = torch.empty(2, Zb, M, N, dtype=torch.float16, device=d)
 
             def go():
                 ops.conv_gemm_split(A, W, Cs=C, M=M, N=N, K=K, Zb=Zb, sAb=Tin * Cin, ldx=Cin, stride=s, Cg=Cin,
                                     Tin=Tin, bias=b, sCb=M * N, ldc=N, epilogue=epi)
         else:
-            A = ops.split(rnd(M, K))
+            A = ops.split(rows_equal(rnd(M, K), "arows"))
             R = ops.split(torch.randn(M, N, device=d)) if res else None
 
             def go():
