@@ -69,8 +69,6 @@ def parse():
     ap.add_argument("--probe", default="auto",
                     help="kernel instantiation to time; auto = the one carrying the most FLOPs in a warmup census")
     ap.add_argument("--serial", action="store_true", help="one stream per step (no head/encoder overlap)")
-    ap.add_argument("--gate-backtrack", action="store_true",
-                    help="a held DP's backtrack takes the last attention gate (A/B of task.gate_backtrack)")
     ap.add_argument("--no-held-dp", action="store_true",
                     help="run a long lattice's DP in one launch behind its head (A/B of task.defer_dp_frames)")
     ap.add_argument("--precision", default="split", choices=["split", "f16"],
@@ -475,8 +473,6 @@ def main():
     task.on_predict_start()
     if args.no_held_dp:
         task.defer_dp_frames = None
-    if args.gate_backtrack:
-        task.gate_backtrack = True
     if args.precision == "f16":
         task.unitsEncoder.model.f16 = True
     B = args.batch

@@ -275,16 +275,12 @@ class ForcedAlignmentTask:
     # long-form (chunk_seconds) never holds: its attention launches are far shorter (profiles/r04/held_dp_ab.txt)
     defer_dp_frames = 16384
 
-    # True: the held DP takes one range fewer than the encoder has layers, so its backtrack (one workgroup, 1.6 ms at
-    # config 5) is gated at the last attention launch too instead of running beside the one-round GEMMs after it
-    gate_backtrack = False
-
     def dp_ranges(self, Tmax: int, Smax: int) -> int:
         """How many step ranges submit() cuts a batch's forward DP into (1: one launch, now)."""
         n_layers = len(getattr(self.unitsEncoder.model, "layers", ()))
         if self.defer_dp_frames is None or Tmax < self.defer_dp_frames or n_layers < 2:
             return 1
-        return n_layers - 1 if getattr(self, "gate_backtrack", False) and n_layers > 2 else n_layers
+        return n_layers
 
     def flush(self):
         """Enqueue a held batch's remaining DP steps now (the pipeline's last batch; assemble also does this).  An
