@@ -8,7 +8,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-from hubertfa_amd import ops  # noqa: E402
+from hubertfa_amd import _lib, ops  # noqa: E402
 
 # name, M, N, K, Zb, conv (k, stride, Tin, Cin) or None, epilogue, planes out, residual planes
 SHAPES = [("conv1", 15999, 512, 1536, 32, (3, 2, 31999, 512), 1, True, False),
@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--chain", action="store_true",
                     help="with --convs: conv1..conv4 back to back (each reading the previous output), each timed "
                          "with events, after the isolated loops")
+    ap.add_argument("--cfg", type=int, default=0, help="split tile (hfa_gemm_split_tuning); outputs are checked "
+                    "bit for bit against the automatic tile's")
     ap.add_argument("--tag", default=os.path.basename(os.path.dirname(os.environ.get("HFA_LIB", "cur/x"))))
     args = ap.parse_args()
     d = torch.device("cuda")
@@ -89,14 +91,23 @@ def main():
             def go():
                 ops.conv_gemm_split(A, W, Cs=C, M=M, N=N, K=K, Zb=Zb, sAb=Tin * Cin, ldx=Cin, stride=s, Cg=Cin,
                                     Tin=Tin, bias=b, sCb=M * N, ldc=N, epilogue=epi)
+                return C
         else:
             A = ops.split(act(rows_equal(rnd(M, K), "arows")))
             R = ops.split(torch.randn(M, N, device=d)) if res else None
 
             def go():
-                ops.linear_split(A, W, b, residual=R, epilogue=epi, out_split=outs)
+                return ops.linear_split(A, W, b, residual=R, epilogue=epi, out_split=outs)
+        tag = args.tag
+        if args.cfg:
+            ref = go().clone()
+            _lib.lib().hfa_gemm_split_tuning(args.cfg)
+            same = torch.equal(go(), ref)
+            tag = f"{args.tag}/cfg{args.cfg}{'' if same else '/MISMATCH'}"
         us = timeit(go, args.reps // (4 if conv else 1) or 1)
-        print(f"{args.tag + '/' + args.data:18s} {name:8s} {us:8.1f} us {2.0 * M * N * K * Zb / us / 1e6:7.1f} TF/s", flush=True)
+        if args.cfg:
+            _lib.lib().hfa_gemm_split_tuning(0)
+        print(f"{tag + '/' + args.data:18s} {name:8s} {us:8.1f} us {2.0 * M * N * K * Zb / us / 1e6:7.1f} TF/s", flush=True)
     if args.convs and args.chain:
         chain_convs(d)
 
