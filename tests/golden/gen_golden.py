@@ -15,6 +15,7 @@ Reference call sites exercised:
   * tools/alignment_decoder.py:26-143   AlignmentDecoder.decode         -> decode_cases.npz
   * networks/g2p/*.py                   G2P plugins                     -> g2p.json
   * networks/g2p/dictionary_g2p.py over dictionary/*.txt (the CLI's default -d)  -> g2p_dicts.json
+  * networks/g2p/*.py + alignment_decoder.py:35 on edge inputs (error types)   -> g2p_edges.json
   * tools/post_processing.py:68-105     post_processing                 -> postproc.json
   * tools/encoder.py:56-59              grid gather index (torch expr)  -> gather_index.npz
   * networks/hubert/model.py            HubertSoft.units                -> hubert_soft.npz
@@ -217,6 +218,46 @@ def gen_g2p():
     with open(os.path.join(HERE, "g2p.json"), "w") as f:
         json.dump(res, f, indent=1)
     print("g2p done")
+
+
+def gen_g2p_edges():
+    """Edge inputs through the reference's G2P plugins and the decoder's phone lookup: empty and blank texts, SP-only
+    texts, repeated / leading / trailing spaces, dictionaries with no known word; the exception type when one is
+    raised (base_g2p.py:37-40 AssertionError, alignment_decoder.py:35 KeyError), else the outputs."""
+    import torch
+    from networks.g2p import DictionaryG2P, NoneG2P, PhonemeG2P
+    from tools.alignment_decoder import AlignmentDecoder
+
+    g_dict = DictionaryG2P(dictionary=os.path.join(HERE, "synth_dict.txt"))
+    texts = ["", " ", "SP", "SP SP", "a", " a", "a ", "a  b", "SP a SP", "AP a", "a\tb", "oov_only", "w000  ",
+             "  w000 w001", "w000 oov w001 oov"]
+    res = {"dictionary": "synth_dict.txt", "cases": []}
+
+    def run(g, t):
+        try:
+            ph, w, m = g(t)
+            return {"ph_seq": list(ph), "word_seq": list(w), "map": [int(x) for x in m]}
+        except Exception as e:  # noqa: BLE001
+            return {"error": type(e).__name__}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for t in texts:
+            res["cases"].append({"text": t, "dict": run(g_dict, t), "none": run(NoneG2P(), t),
+                                 "phoneme": run(PhonemeG2P(), t)})
+    vocab = {"vocab": {"SP": 0, "AP": 0, "a": 1, "b": 2}, "vocab_size": 3}
+    dec = AlignmentDecoder(vocab, {"sample_rate": 44100, "hop_length": 512})
+    lg = torch.zeros(1, 8, 3)
+    oov = []
+    for ph_seq in (["SP", "a", "SP"], ["SP", "zz", "SP"], ["SP", "", "SP"]):
+        try:
+            dec.decode(lg, torch.zeros(1, 8), lg, None, ph_seq)
+            oov.append({"ph_seq": ph_seq, "error": None})
+        except Exception as e:  # noqa: BLE001
+            oov.append({"ph_seq": ph_seq, "error": type(e).__name__})
+    res["decode_lookup"] = {"vocab": vocab, "cases": oov}
+    with open(os.path.join(HERE, "g2p_edges.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print("g2p edges done")
 
 
 def gen_g2p_dicts():
@@ -621,6 +662,7 @@ def main():
     which = sys.argv[1:] or ["dp", "decode", "g2p", "postproc", "gather", "hubert", "unet", "e2e10s", "loaders"]
     for w in which:
         {"dp": gen_dp_cases, "decode": gen_decode_cases, "g2p": gen_g2p, "g2p_dicts": gen_g2p_dicts,
+         "g2p_edges": gen_g2p_edges,
          "postproc": gen_postproc,
          "gather": gen_gather_index, "hubert": gen_hubert, "unet": gen_unet, "e2e10s": gen_e2e10s,
          "loaders": gen_loaders}[w]()

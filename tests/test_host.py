@@ -34,6 +34,43 @@ def test_g2p_plugins_match_reference():
                 assert [int(x) for x in m] == case["map"]
 
 
+def test_g2p_edge_inputs_and_lookup_errors_match_reference():
+    """Edge texts (empty, blank, SP-only, repeated / leading / trailing spaces, tabs, unknown words) through the
+    three G2P plugins give the reference's outputs, and the decoder's phone lookup raises the reference's KeyError
+    on an unknown phone (alignment_decoder.py:35) before any device work (tests/golden/g2p_edges.json, made by the
+    reference's own classes)."""
+    import builtins
+
+    import torch
+    from hubertfa_amd.alignment_decoder import AlignmentDecoder
+    from hubertfa_amd.g2p import DictionaryG2P, NoneG2P, PhonemeG2P
+    gold = json.load(open(os.path.join(GOLDEN, "g2p_edges.json")))
+    gs = {"dict": DictionaryG2P(dictionary=os.path.join(GOLDEN, gold["dictionary"])), "none": NoneG2P(),
+          "phoneme": PhonemeG2P()}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for case in gold["cases"]:
+            for name, g in gs.items():
+                want = case[name]
+                if "error" in want:
+                    with pytest.raises(getattr(builtins, want["error"])):
+                        g(case["text"])
+                    continue
+                ph, w, m = g(case["text"])
+                assert (list(ph), list(w), [int(x) for x in m]) == (want["ph_seq"], want["word_seq"], want["map"]), \
+                    (name, case["text"])
+    lk = gold["decode_lookup"]
+    dec = AlignmentDecoder(lk["vocab"], {"sample_rate": 44100, "hop_length": 512})
+    lg = torch.zeros(1, 8, 3)
+    for case in lk["cases"]:
+        if case["error"] is None:
+            assert list(dec.ph_ids(case["ph_seq"])) == [lk["vocab"]["vocab"][p] for p in case["ph_seq"]]
+        else:
+            assert case["error"] == "KeyError"
+            with pytest.raises(KeyError):
+                dec.decode(lg, torch.zeros(1, 8), lg, None, case["ph_seq"])
+
+
 @pytest.mark.parametrize("name", ["opencpop-extension", "jyutping_dict", "japanese_dict_full"])
 def test_g2p_reference_dictionaries(name, tmp_path):
     """DictionaryG2P over the reference's shipped dictionaries (the CLI's default -d opencpop-extension.txt,
