@@ -1,0 +1,13 @@
+# Round-5 re-validation of the committed tree: every GPU test, smoke, and the default bench line (config 2 + the
+# config 4 / config 5 blocks + CPU baseline), as the driver runs them.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r05_check
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputests.log 2>&1 || { echo "GPU TESTS FAIL"; tail -40 $O/gputests.log; exit 1; }
+tail -1 $O/gputests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "SMOKE FAIL"; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo "BENCH FAIL"; tail -20 $O/bench.err; exit 1; }
+python -c "import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['value'], d['roofline']['frac'], d['config4']['value'], d['config5']['value'], d['cpu_baseline']['value'])"
+echo ALLOK
