@@ -239,9 +239,7 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int SKB = 64;              // keys per tile
-constexpr int SNS = 2;               // LDS stages
 constexpr int SPLANE = SKB * DH;     // halves per plane image (8 KiB)
-constexpr int SSTAGE = 4 * SPLANE;   // K1, K2, V1, V2
 constexpr float kLo = 1.0f / 2048.0f;
 
 struct AttnSP {
