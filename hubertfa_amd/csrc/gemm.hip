@@ -1553,7 +1553,14 @@ inline int split_cfg(const GemmP& p, int Z) {
     if (p.N <= 64 || blocks128 < 256) return SCFG_128x64_M16;
     // (a half-filled single round of big tiles loses to 128 x 128: extractor conv6, 128 big tiles, 227 vs 288 TF/s;
     // at 189 big tiles -- the N = 768 projections -- 256 x 256 still wins, 300 vs 275, profiles/r03/conv6_tiles.txt)
-    if (blocks256 <= 128 || p.N < 512) return SCFG_128x128_M16;
+    if (blocks256 <= 128 || p.N < 512) {
+        // narrow N that 128-wide column tiles would pad (profiles/r05/side_tiles.txt): N = 192 at K <= 1152 (the
+        // UNet's 192-channel convs and linears) on exact 64-wide tiles, 5-20 % faster; 128 < N < 192 (the
+        // 44.1 k -> 16 k resampler, N = 160) on one 192-wide column tile, 14 % faster
+        if (p.N % 128 && p.N % 64 == 0 && p.K <= 1152) return SCFG_128x64_M16;
+        if (p.N > 128 && p.N < 192) return SCFG_128x192_M16;
+        return SCFG_128x128_M16;
+    }
     // Large grids: the 256 x 256 tile unless a 192-wide tile fills the last round of CUs much better.  Score =
     // fill of the rounds (tiles / (rounds x 256 CUs)) x the tile's per-FLOP speed (192-wide tiles 0.92 of 256 x 256),
     // ties to 256 x 256.  Measured (scripts/split_gemm_bench.py, profiles/r03/split_tiles_c5.txt): QKV at M = 15 968
