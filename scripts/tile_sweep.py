@@ -16,7 +16,11 @@ SHAPES = [("unet k3 864 192->192", 864, 192, 192, 3, 1), ("unet k3 432 192->192"
           ("unet k3 216 192->192", 216, 192, 192, 3, 1), ("unet k3 108 384->384", 108, 384, 384, 3, 1),
           ("unet k3 864 768->192", 864, 768, 192, 3, 1), ("unet lin 432 192->384", 432, 192, 384, 1, 1),
           ("unet k2s2 864 192->192", 864, 192, 192, 2, 2), ("head lin 864 192->68", 864, 192, 68, 1, 1)]
-CFGS = (0, 17, 18, 19, 25)
+# --encoder: the encoder's smaller main-stream shapes (feature projection; extractor conv6 = k2 s2 over 999 frames,
+# and two off-path probes: k2 s2 over 499 frames, k3 s2 over 1999 frames)
+ENC_SHAPES = [("feature proj 512->768", 15968, 512, 768, 1, 1), ("conv6 k2s2 Tin=999", 999, 512, 512, 2, 2),
+              ("k2s2 Tin=499", 499, 512, 512, 2, 2), ("k3s2 Tin=1999", 1999, 512, 512, 3, 2)]
+CFGS = (0, 17, 18, 19, 20, 23, 24, 25)
 
 
 def timeit(fn, reps=20):
@@ -37,14 +41,15 @@ def timeit(fn, reps=20):
 
 def main():
     d = torch.device("cuda")
-    B = 32
-    for name, T, Cin, N, k, s in SHAPES:
+    enc = "--encoder" in sys.argv
+    for name, T, Cin, N, k, s in (ENC_SHAPES if enc else SHAPES):
+        B = 1 if (enc and k == 1) else 32
         K = k * Cin
         W = ops.split(torch.randn(N, K, device=d) * K ** -0.5)
         bias = torch.randn(N, device=d)
         A = ops.split(torch.randn(B, T, Cin, device=d))
-        M = (T + 2 * (k // 2) - k) // s + 1 if k == 3 else (T - k) // s + 1
-        pad = k // 2 if k == 3 else 0
+        pad = k // 2 if (k == 3 and not enc) else 0     # the UNet's k3 convs pad 1; the extractor's do not
+        M = (T + 2 * pad - k) // s + 1
         C = torch.empty(B, M, N, device=d)
 
         def go():
