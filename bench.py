@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--words", type=int, default=30)
     ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="CPU baseline time budget (seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sustained-s", type=float, default=10.0,
+                    help="N = 1: after the timed steps, run this many seconds of continuous steps and report the first "
+                         "and last 2 s (0: skip)")
     ap.add_argument("--encoder", default="base", choices=["base", "large", "soft"],
                     help="base = cnhubert (config 2/3), large = cnhubert-large 24L/1024 (config 4), soft = hubertsoft")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo only for rehearsals")
@@ -127,7 +130,9 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s, encoder="cnhubert"):
-    """CPU oracle on a bounded sample (whole utterances until the budget is spent)."""
+    """CPU oracle on a bounded sample (whole utterances until the budget is spent), with the per-stage split SURVEY
+    §8(d) asks for (resample, Hubert, gather + UNet + head, decode) and the C Viterbi alone on one core per
+    utterance (the numba-equivalent: forward_pass + backtrack, alignment_decoder.py:170-230, 269-288)."""
     import numpy as np
     import torch
     from hubertfa_amd import synth
@@ -141,26 +146,56 @@ def cpu_baseline(wav, ph_seqs, word_seqs, p2ws, ckpt, budget_s, encoder="cnhuber
     ua = synth.UNetArch(input_dims=arch.out_channels, vocab_size=vocab["vocab_size"])
     usd = {k: v.numpy() for k, v in ckpt["state_dict"].items()}
     threads = torch.get_num_threads()
+    stages = {"resample": 0.0, "hubert": 0.0, "unet_head": 0.0, "decode": 0.0}
     done, t0 = 0, time.perf_counter()
+    last = None
     while time.perf_counter() - t0 < budget_s:   # cycle over the batch until the budget is spent
         i = done % len(wav)
+        ta = time.perf_counter()
         x16 = torch.from_numpy(wav[i:i + 1])
         x44 = ores.resample(x16, 16000, 44100, 6)
         xr = ores.resample(x44, 44100, 16000, 128)
+        tb = time.perf_counter()
         units = hubert_cpu.hubert_forward(arch, sd, xr)
+        tc = time.perf_counter()
         n44 = x44.shape[-1]
         n_frames = n44 // 512 + 1
         ratio = (512 / 44100) / (320 / 16000)
         idx = torch.clamp(torch.round(ratio * torch.arange(n_frames)).long(), max=units.shape[1] - 1)
         feats = units[:, idx]
         logits = hubert_cpu.unet_head_forward(ua, usd, feats)
-        odec.decode(vocab, logits[:, :, 2:], logits[:, :, 0], n44 / 44100, ph_seqs[i], word_seqs[i], p2ws[i])
+        td = time.perf_counter()
+        r = odec.decode(vocab, logits[:, :, 2:], logits[:, :, 0], n44 / 44100, ph_seqs[i], word_seqs[i], p2ws[i])
+        te = time.perf_counter()
+        for k, dt in zip(stages, (tb - ta, tc - tb, td - tc, te - td)):
+            stages[k] += dt
+        last = (np.array([vocab["vocab"][p] for p in ph_seqs[i]]), r[5]["ph_prob_log"], r[5]["edge_prob"])
         done += 1
     el = time.perf_counter() - t0
+    # the C Viterbi alone (single-threaded C, -O2 -ffp-contract=off): lattice prep + forward_pass + backtrack of one
+    # utterance, repeated for >= 1 s
+    ids, ppl, ep = last
+    n_v, tv = 0, time.perf_counter()
+    while n_v < 3 or time.perf_counter() - tv < 1.0:
+        odec._decode(ids, ppl, ep)
+        n_v += 1
+    v_ms = 1e3 * (time.perf_counter() - tv) / n_v
     secs = done * wav.shape[1] / 16000
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {"value": secs / el, "unit": "audio_s/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "os_cpu_count": os.cpu_count(), "affinity_cpus": affinity, "torch_threads": threads,
+            "stages_ms_per_utterance": {k: 1e3 * v / max(done, 1) for k, v in stages.items()},
+            "viterbi_1core_ms_per_utterance": v_ms, "viterbi_T": int(ppl.shape[0]), "viterbi_S": int(len(ids)),
+            "viterbi_1core_us_per_time_step": 1e3 * v_ms / max(int(ppl.shape[0]), 1),
             "sample": f"{done} x {wav.shape[1] / 16000:.0f} s utterances of the same workload, sequential B=1 "
-                      f"(oracle: torch-CPU fp32 resample + {encoder} + UNet, C Viterbi), {el:.1f} s wall"}
+                      f"(oracle: torch-CPU fp32 resample + {encoder} + UNet on {threads} torch threads, C Viterbi "
+                      f"on 1 core), {el:.1f} s wall",
+            "note": "cores = torch intra-op threads used (torch.get_num_threads(); the box's share of a larger node: "
+                    "os_cpu_count is the whole machine, affinity_cpus what this process may run on); the C Viterbi "
+                    "is single-threaded like the reference's numba forward_pass"}
 
 
 def config_name(encoder: str, world: int, B: int, seconds: float = 10.0) -> str:
@@ -263,6 +298,51 @@ def config3_batch(args, world: int) -> int:
     if world * args.batch == 512 or 512 % world or args.no_config3:
         return 0
     return 512 // world
+
+
+def sustained(run, seconds, audio_per_step, headline_ms, window_s=2.0):
+    """Sustained throughput (verdict r05 item 2): ``seconds`` of continuous pipelined steps right after the timed
+    region, one HIP event on the launching stream at the start of every step.  The interval between two steps'
+    events is that step's share of the device's time (the host keeps the stream fed), so the first and the last
+    ``window_s`` seconds of intervals show whether the 20-step headline rate holds as the chip heats; ``wall`` is the
+    whole run's wall clock.  Outside the timed region."""
+    import torch
+    evs = []
+
+    def mark():
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        evs.append(ev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(10 ** 9, on_step=mark, until=t0 + seconds)
+    end = torch.cuda.Event(enable_timing=True)
+    end.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    evs.append(end)
+    step_events = [evs[i].elapsed_time(evs[i + 1]) for i in range(len(evs) - 1)]      # ms
+
+    def window(ms_list):
+        acc, out = 0.0, []
+        for m in ms_list:
+            if acc >= window_s * 1e3:
+                break
+            out.append(m)
+            acc += m
+        return out
+    first, last = window(step_events), window(step_events[::-1])
+    mean = lambda x: sum(x) / len(x)  # noqa: E731
+    f_ms, l_ms = mean(first), mean(last)
+    return {"seconds": wall, "steps": len(step_events), "ms_per_step": 1e3 * wall / len(step_events),
+            "value": audio_per_step * len(step_events) / wall, "unit": "audio_s/s",
+            "first_window_ms_per_step": f_ms, "last_window_ms_per_step": l_ms,
+            "first_window_value": audio_per_step / f_ms * 1e3, "last_window_value": audio_per_step / l_ms * 1e3,
+            "window_s": window_s, "min_step_ms": min(step_events), "max_step_ms": max(step_events),
+            "last_vs_headline": headline_ms / l_ms,
+            "note": "continuous pipelined config-2 steps (bench's own loop) right after the timed region; per-step "
+                    "times are the intervals between HIP events recorded on the launching stream at each step's start, "
+                    "the last one ends at the drained pipeline; wall includes the final drain"}
 
 
 def host_io(wav_np, res, seconds, budget_s=3.0):
@@ -499,13 +579,18 @@ def main():
     def finish(handle, inp, tk):
         return tk.decoder.assemble(handle, *inp[2:])
 
-    def run(k, inp=inputs, tk=task):
+    def run(k, inp=inputs, tk=task, on_step=None, until=None):
         """k steps, software-pipelined: the host assembles batch i while the GPU runs batch i+1 -- or, when
         task.submit holds a batch's DP for the next encoder's attention launches (a long lattice), batch i-1: batch
         i's results land near the end of encoder i+1, and waiting for them there would leave the GPU idle while the
-        host assembles and enqueues the next step."""
+        host assembles and enqueues the next step.  ``on_step`` runs before each step's launch; ``until`` (a
+        perf_counter time) ends the loop early (the sustained block)."""
         pending, res = [], None
         for _ in range(k):
+            if until is not None and time.perf_counter() >= until:
+                break
+            if on_step is not None:
+                on_step()
             t0, c0, p0 = time.perf_counter(), time.thread_time(), time.process_time()
             h = launch(inp, tk)
             t1, c1 = time.perf_counter(), time.thread_time()
@@ -621,6 +706,10 @@ def main():
         rd = RANDOM_DATA_F16_TFLOPS / (1 if probe_name.endswith(", true>") else 3)
         out["roofline"]["random_data_mfma_rate"] = rd
         out["roofline"]["frac_of_random_data_rate"] = achieved / rd
+    if world == 1 and args.sustained_s > 0 and args.chunk_seconds is None:
+        n0 = len(host_t)
+        out["sustained"] = sustained(run, args.sustained_s, B * args.seconds, out["ms_per_step"])
+        del host_t[n0:]
     c3 = config3_batch(args, world)
     if c3:
         # BASELINE config 3 (512 x 10 s over the node) measured after the weak-scaling region, whose per-GPU batch

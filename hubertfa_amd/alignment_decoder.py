@@ -162,9 +162,10 @@ class AlignmentDecoder:
         interval/word assembly.  ``intervals=False`` returns the raw boundary records only (T, ph_idx_seq,
         ph_time_int, frame_confidence, edge_diff), for callers that assemble them elsewhere (``utterance_result``:
         the CLI's export workers, rank 0 after the multi-GPU gather)."""
-        resolve = dev_out.pop("resolve", None)
+        resolve = dev_out.get("resolve")
         if resolve is not None:              # a pipelined handle whose DP steps are still held (task.submit)
-            resolve()
+            resolve()                        # (raises a held step's error, again on every retry: ADVICE r05)
+            dev_out.pop("resolve", None)
         if "host" not in dev_out:
             dev_out = self.fetch(dev_out, keep_frame_probs)
         ev = dev_out["event"]

@@ -1546,18 +1546,21 @@ inline int split_cfg(const GemmP& p, int Z) {
     }
     if (win_ok(p)) return SCFG_WIN;
     if (n48) return SCFG_N48;
+    // the rules below were measured on a whole MI355X (256 CUs); a partitioned device scales them with its CU count
+    const long long cus = hfa::device_cus();
     const long long blocks128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128) * Z;
     const long long blocks256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256) * Z;
-    if (p.N == 64 && p.Cg % 32 == 0 && (long long)((p.M + 255) / 256) * Z >= 256)
+    if (p.N == 64 && p.Cg % 32 == 0 && (long long)((p.M + 255) / 256) * Z >= cus)
         return SCFG_256x64_M16;            // grouped positional conv at Cg = 64 (Hubert-large): 1.26x the 128x64 tile
-    if (p.N <= 64 || blocks128 < 256) return SCFG_128x64_M16;
+    if (p.N <= 64 || blocks128 < cus) return SCFG_128x64_M16;
     // (a half-filled single round of big tiles loses to 128 x 128: extractor conv6, 128 big tiles, 227 vs 288 TF/s;
     // at 189 big tiles -- the N = 768 projections -- 256 x 256 still wins, 300 vs 275, profiles/r03/conv6_tiles.txt)
-    if (blocks256 <= 128 || p.N < 512) {
+    if (2 * blocks256 <= cus || p.N < 512) {
         // narrow N that 128-wide column tiles would pad (profiles/r05/side_tiles.txt): N = 192 at K <= 1152 (the
         // UNet's 192-channel convs and linears) on exact 64-wide tiles, 5-20 % faster; 128 < N < 192 (the
-        // 44.1 k -> 16 k resampler, N = 160) on one 192-wide column tile, 14 % faster
-        if (p.N % 128 && p.N % 64 == 0 && p.K <= 1152) return SCFG_128x64_M16;
+        // 44.1 k -> 16 k resampler, N = 160) on one 192-wide column tile, 14 % faster.  Only the measured widths:
+        // other N % 128 != 0 shapes (320, 448, ...) keep 128 x 128 until measured.
+        if (p.N == 192 && p.K <= 1152) return SCFG_128x64_M16;
         if (p.N > 128 && p.N < 192) return SCFG_128x192_M16;
         return SCFG_128x128_M16;
     }
@@ -1568,7 +1571,7 @@ inline int split_cfg(const GemmP& p, int Z) {
     // M = 17 924 (config 5 windows: 639 tiles = 2.5 rounds) 256 x 256 340 / 128 x 128 318; FFN1 at M = 17 924 (852
     // tiles = 3.3 rounds) 256 x 256 308 / 192 x 256 304 / 128 x 128 276 — a thin last round costs less than its
     // share (fewer busy CUs hold a higher clock), so the 128 x 128 tile is never the better large-grid choice.
-    auto fill = [](long long b) { return (double)b / (double)(((b + 255) / 256) * 256); };
+    auto fill = [cus](long long b) { return (double)b / (double)(((b + cus - 1) / cus) * cus); };
     const long long blocks192n = (long long)((p.M + 255) / 256) * ((p.N + 191) / 192) * Z;   // 256 x 192
     const long long blocks192m = (long long)((p.M + 191) / 192) * ((p.N + 255) / 256) * Z;   // 192 x 256
     // One-round grids: the 192 x 256 tile when it still makes one round and busies more CUs -- the N = 768 family
@@ -1577,14 +1580,14 @@ inline int split_cfg(const GemmP& p, int Z) {
     // microbenchmark had not shown it).
     double best = fill(blocks256);
     int cfg = SCFG_256x256_M16;
-    if (blocks256 <= 256) {
+    if (blocks256 <= cus) {
         // Short K (the out-projection and the feature projection, K <= 1024): two 128 x 192 workgroups per CU when
         // they still make one round of the 512 slots, so one tile's epilogue runs beside the other's main loop
         // (out-projection 70-72 -> 69-70 us, three interleaved pairs, profiles/r04/attn_persistent_ab.txt; FFN2's
         // K = 3072 stays on 192 x 256: 208 vs 219 us, profiles/r04/layer_tiles.txt)
         const long long blocks128x192 = (long long)((p.M + 127) / 128) * ((p.N + 191) / 192) * Z;
-        if (p.K <= 1024 && blocks128x192 <= 512 && blocks128x192 > 2 * blocks256) return SCFG_128x192_M16;
-        return (blocks192m <= 256 && blocks192m > blocks256) ? SCFG_192x256_M16 : cfg;
+        if (p.K <= 1024 && blocks128x192 <= 2 * cus && blocks128x192 > 2 * blocks256) return SCFG_128x192_M16;
+        return (blocks192m <= cus && blocks192m > blocks256) ? SCFG_192x256_M16 : cfg;
     }
     if (0.92 * fill(blocks192m) > best + 0.05) {
         best = 0.92 * fill(blocks192m);

@@ -297,7 +297,9 @@ class _HeldDP:
 
     Failures stay with this batch: a step is dropped only after it ran, the first error stops the rest
     (a DP missing a time range must never reach the backtrack) and is kept, and ``resolve`` -- this batch's
-    assemble -- raises it; the next batch's encoder, whose attention launches gate the steps, never sees it."""
+    assemble -- raises it (on every call); the next batch's encoder, whose attention launches gate the steps, never
+    sees it.  Exception: in a multi-rank run whose ``on_device`` is a collective, the error is raised at once
+    (ADVICE r05): the peers would otherwise wait in the gather this rank never reaches."""
 
     def __init__(self, task, dev_out, on_device):
         self.task, self.dev_out, self.on_device = task, dev_out, on_device
@@ -326,6 +328,11 @@ class _HeldDP:
             self.steps = []
             if getattr(self.task, "_held", None) is self:
                 self.task._held = None
+            if self.on_device is not None and _dist_world() > 1:
+                # on_device is this batch's collective (the boundary gather): deferring the error would leave the
+                # peer ranks blocked in it until the process-group timeout and hide the cause.  Raise now, so this
+                # rank exits and the launcher (torch.distributed.run) tears the job down with this error in its log
+                raise
 
     def gate(self, main):
         """The next encoder's attention gate: the side stream waits for the main stream to reach the launch, then
@@ -354,6 +361,11 @@ class _HeldDP:
         self.drain()
         if self.error is not None:
             raise self.error
+
+
+def _dist_world() -> int:
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
 def synth_checkpoint(path: str | None = None, *, encoder="cnhubert", model_path="synth:0", seed=1,

@@ -89,7 +89,13 @@ def test_split_gemm_tile_choice():
     assert tile(17924, 768) == [" 256", " 256"]           # config 5 windows: 192 x 256 would take a second round
     assert tile(15999, 512, Z=32, epi=1) == [" 256", " 256"]   # extractor conv1
     assert tile(499, 512, Z=32, epi=1) == [" 128", " 128"]     # extractor conv6: 128 big tiles, half a round
-    assert tile(864, 192, Z=32) == [" 128", " 128"]       # UNet level 0: small grid
+    # narrow N (profiles/r05/side_tiles.txt, gemm.hip split_cfg): the UNet's 192-channel convs / linears at K <= 1152
+    # on exact 64-wide tiles; wider K keeps 128 x 128; the 44.1 k -> 16 k resampler's N = 160 on one 192-wide column
+    # tile; unmeasured widths (N = 320) keep 128 x 128
+    assert tile(864, 192, Z=32) == [" 128", " 64"]        # UNet level 0 (K = 768)
+    assert tile(864, 192, Z=32, K=1536) == [" 128", " 128"]
+    assert tile(1000, 160, Z=256, K=1184) == [" 128", " 192"]   # resampler 44.1 k -> 16 k: 8 groups x 32 rows
+    assert tile(864, 320, Z=32) == [" 128", " 128"]
     # the grouped positional conv (Cg = 48, k = 128): the LDS-window kernel, named as launched (the K argument)
     assert ops._split_name(499, 48, 6144, 512, False, 1, 48) == "posconv_split_kernel<1, 3, 4>"   # 512-row tiles
     assert ops._split_name(200, 48, 6144, 512, False, 1, 48) == "posconv_split_kernel<1, 3, 2>"

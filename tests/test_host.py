@@ -624,3 +624,34 @@ def test_held_dp_failure_stays_with_its_batch():
     h.drain()
     with pytest.raises(ValueError, match="gather failed"):
         h.flush()
+
+
+def test_held_dp_failure_reraised_on_retry_and_prompt_under_distributed(monkeypatch):
+    """decoder.assemble keeps a held handle's resolve until it succeeds, so a caller that catches the
+    held batch's error and assembles again gets the same error (not a KeyError); and in a multi-rank run whose
+    on_device is the boundary collective, the failing step raises at once instead of leaving the peers in it."""
+    from types import SimpleNamespace
+    from hubertfa_amd import task as task_mod
+    from hubertfa_amd.alignment_decoder import AlignmentDecoder
+    from hubertfa_amd.task import _HeldDP
+
+    def bad():
+        raise RuntimeError("dp range failed")
+    tk = SimpleNamespace(_side=None, decoder=SimpleNamespace(fetch=lambda d: {"n": 1}))
+    h = _HeldDP(tk, {"deferred": [bad]}, None)
+    h.drain()
+    dec = AlignmentDecoder({"vocab": {"SP": 0, "a": 1}, "vocab_size": 2}, {"sample_rate": 44100, "hop_length": 512})
+    for _ in range(2):
+        with pytest.raises(RuntimeError, match="dp range failed"):
+            dec.assemble(h.handle, [["SP", "a", "SP"]])
+    assert "resolve" in h.handle
+    # distributed with a collective completion: the gate's step raises immediately
+    monkeypatch.setattr(task_mod, "_dist_world", lambda: 2)
+    h = _HeldDP(tk, {"deferred": [bad]}, lambda d: None)
+    with pytest.raises(RuntimeError, match="dp range failed"):
+        h._next()
+    assert h.error is not None and not h.steps
+    # without a collective completion it stays deferred even at world 2
+    h = _HeldDP(tk, {"deferred": [bad]}, None)
+    h._next()
+    assert h.error is not None
