@@ -1,5 +1,5 @@
 """The config-2 split attention alone (B=32, L=499, 12 heads of 64), 20 launches: a short program for rocprofv3 PMC
-passes (scripts/gpu_r04p.sh).   python scripts/attn_pmc_driver.py"""
+passes (scripts/archive/gpu_r04p.sh).   python scripts/attn_pmc_driver.py"""
 import os
 import sys
 

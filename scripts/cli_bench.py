@@ -16,6 +16,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--profile", action="store_true", help="cProfile the second run (host time by function)")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--seconds", type=float, nargs=2, default=(8.0, 12.0), help="utterance length range (s)")
+    ap.add_argument("--metrics", default=None, help="infer.py --metrics: append each run's JSON line to this file")
     args = ap.parse_args()
     import numpy as np
     from click.testing import CliRunner
@@ -31,8 +33,8 @@ def main():
         seg = os.path.join(td, "segments")
         os.makedirs(seg)
         rng = np.random.default_rng(0)
-        secs = rng.uniform(8.0, 12.0, args.n)
-        base = synth.synth_audio(int(12.0 * 16000), seed=1)
+        secs = rng.uniform(args.seconds[0], args.seconds[1], args.n)
+        base = synth.synth_audio(int(args.seconds[1] * 16000), seed=1)
         for i, s in enumerate(secs):
             write_wav(os.path.join(seg, f"u{i:05d}.wav"), base[: int(s * 16000)], 16000)
             with open(os.path.join(seg, f"u{i:05d}.lab"), "w") as f:
@@ -40,6 +42,8 @@ def main():
         ck = os.path.join(td, "m.ckpt")
         synth_checkpoint(ck)
         argv0 = ["-c", ck, "-f", seg, "-d", dpath, "-sc", "--hubert_path", "synth:0", "--batch_size", str(args.batch)]
+        if args.metrics:
+            argv0 += ["--metrics", os.path.abspath(args.metrics)]
         for rep in range(args.reps):              # the first run also pays kernel loading and warm-up
             argv = argv0
             prof = None

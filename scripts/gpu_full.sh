@@ -6,4 +6,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -3 gpurun_out/gputests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "SMOKE FAIL"; tail -20 gpurun_out/smoke.log; exit 1; }
 tail -2 gpurun_out/smoke.log
-bash scripts/gpu_prof.sh
+bash scripts/archive/gpu_prof.sh

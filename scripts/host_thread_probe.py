@@ -33,6 +33,75 @@ def _read(path):
         return ""
 
 
+def _maps():
+    """[(lo, hi, perms, offset, path)] of this process's mappings."""
+    out = []
+    for ln in _read(f"/proc/{os.getpid()}/maps").splitlines():
+        f = ln.split(None, 5)
+        lo, hi = (int(x, 16) for x in f[0].split("-"))
+        out.append((lo, hi, f[1], int(f[2], 16), f[5] if len(f) > 5 else ""))
+    return out
+
+
+def stack_scan(sp, pc, maps, depth=32768):
+    """Poor man's backtrace of a thread parked in a syscall (no ptrace, no gdb on the box): the syscall's user pc,
+    then every 8-byte word in [sp, sp + depth) of the thread's own stack mapping that points into an executable
+    file mapping of this process, as (library, file offset) -- return addresses, plus some stale words."""
+    import ctypes
+    out = []
+
+    def where(a):
+        for lo, hi, perms, off, path in maps:
+            if lo <= a < hi and "x" in perms and path.startswith("/"):
+                return os.path.basename(path), a - lo + off
+        return None
+    w = where(pc)
+    if w:
+        out.append(w)
+    top = next((hi for lo, hi, perms, _o, _p in maps if lo <= sp < hi), None)
+    if top is None:
+        return out
+    n = min(depth, top - sp) // 8
+    raw = ctypes.string_at(sp, n * 8)
+    for i in range(n):
+        a = int.from_bytes(raw[8 * i:8 * i + 8], "little")
+        w = where(a)
+        if w:
+            out.append(w)
+    return out
+
+
+def symbolize(frames):
+    """(library, offset) -> 'library!symbol+0x..' from the library's dynamic and static symbol tables (nm)."""
+    import bisect
+    import subprocess
+    tables = {}
+    libs = {}
+    for lo, hi, perms, off, path in _maps():
+        if path.startswith("/"):
+            libs.setdefault(os.path.basename(path), path)
+    res = []
+    for lib, off in frames:
+        if lib not in tables:
+            syms = []
+            for extra in (["-D"], []):
+                try:
+                    txt = subprocess.run(["nm", "-C", "--defined-only", *extra, libs[lib]], capture_output=True,
+                                         text=True, timeout=60).stdout
+                except Exception:  # noqa: BLE001
+                    txt = ""
+                for ln in txt.splitlines():
+                    f = ln.split(" ", 2)
+                    if len(f) == 3 and f[1] in "tTwW":
+                        syms.append((int(f[0], 16), f[2]))
+            syms.sort()
+            tables[lib] = ([a for a, _ in syms], [n for _, n in syms])
+        addrs, names = tables[lib]
+        i = bisect.bisect_right(addrs, off) - 1
+        res.append(f"{lib}!{names[i][:90]}+{off - addrs[i]:#x}" if i >= 0 else f"{lib}+{off:#x}")
+    return res
+
+
 class Sampler(threading.Thread):
     def __init__(self, period=0.002):
         super().__init__(daemon=True)
@@ -41,6 +110,8 @@ class Sampler(threading.Thread):
         self.sysc = collections.defaultdict(collections.Counter)
         self.wchan = collections.defaultdict(collections.Counter)
         self.n = 0
+        self.stacks = collections.defaultdict(list)      # tid -> [(sp, pc, frames)] of samples parked in a syscall
+        self.maps = _maps()
 
     def run(self):
         self.me = threading.get_native_id()
@@ -58,6 +129,12 @@ class Sampler(threading.Thread):
                 sc = _read(f"{base}/{t}/syscall").split()
                 key = "running" if sc[:1] == ["running"] else (SYSCALLS.get(int(sc[0]), sc[0]) if sc and sc[0].lstrip("-").isdigit() else "?")
                 self.sysc[tid][key] += 1
+                if key not in ("running", "?") and len(sc) >= 3 and len(self.stacks[tid]) < 6:
+                    try:
+                        sp, pc = int(sc[-2], 16), int(sc[-1], 16)
+                        self.stacks[tid].append(stack_scan(sp, pc, self.maps))
+                    except Exception:  # noqa: BLE001 — a diagnostic: a torn read just drops the sample
+                        pass
                 w = _read(f"{base}/{t}/wchan").strip() or "0"
                 self.wchan[tid][w] += 1
             self.n += 1
@@ -68,7 +145,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--device-flags", default="default", choices=sorted(FLAGS))
     ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--env", action="append", default=[], help="K=V set before the HIP runtime starts")
     a = ap.parse_args()
+    for kv in a.env:
+        k, _, v = kv.partition("=")
+        os.environ[k] = v
     import torch
     if FLAGS[a.device_flags] is not None:
         hip = ctypes.CDLL("libamdhip64.so.7")          # the runtime torch loaded (same soname: one instance)
@@ -113,12 +194,23 @@ def main():
         if ms <= 0.05 or tid == smp.me:
             continue
         tot = sum(smp.state[tid].values()) or 1
+        st = _read(f"/proc/{os.getpid()}/task/{tid}/status")
+        vcs = next((int(ln.split()[1]) for ln in st.splitlines() if ln.startswith("voluntary_ctxt_switches")), None)
         rows.append({"tid": tid, "name": "main" if tid == main_id else name, "cpu_ms_per_step": round(ms, 2),
+                     "voluntary_ctxt_switches_total": vcs,
                      "share_R": round(smp.state[tid]["R"] / tot, 3),
                      "syscalls": {k: round(v / tot, 3) for k, v in smp.sysc[tid].most_common(4)},
                      "wchan": {k: round(v / tot, 3) for k, v in smp.wchan[tid].most_common(3)}})
     rows.sort(key=lambda r: -r["cpu_ms_per_step"])
-    print(json.dumps({"device_flags": a.device_flags, "steps": a.steps, "ms_per_step": 1e3 * el / a.steps,
+    for r in rows[:3]:              # the busiest threads' parked stacks, deduplicated frames in first-seen order
+        seen, frames = set(), []
+        for fr in smp.stacks.get(r["tid"], []):
+            for f in fr[:40]:
+                if f not in seen:
+                    seen.add(f)
+                    frames.append(f)
+        r["stack_frames"] = symbolize(frames[:40])
+    print(json.dumps({"device_flags": a.device_flags, "env": a.env, "steps": a.steps, "ms_per_step": 1e3 * el / a.steps,
                       "process_cpu_ms_per_step": sum(r["cpu_ms_per_step"] for r in rows), "samples": smp.n,
                       "threads": rows[:8], "n_threads": len(a1)}), flush=True)
 

@@ -1,7 +1,7 @@
 """LayerNorm microbenchmark (GPU box): the encoder's post-LN shape [32 x 499, 768] f32 -> split planes only (the
 pipelined step's layernorm_kernel<3>), and -> f32 + planes, against a plain f32 device copy of the same bytes;
 HIP events over 200 launches.  Bit-identity of the outputs against HFA_LIB's reference build is checked by the
-caller (scripts/gpu_r04ae.sh saves them).    python scripts/ln_bench.py [--save out.pt]"""
+caller (scripts/archive/gpu_r04ae.sh saves them).    python scripts/ln_bench.py [--save out.pt]"""
 import argparse
 import os
 import sys

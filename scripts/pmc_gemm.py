@@ -1,4 +1,4 @@
-"""Summarise the PMC passes of scripts/gpu_pmc_gemm.sh per GEMM dispatch shape.
+"""Summarise the PMC passes of scripts/archive/gpu_pmc_gemm.sh per GEMM dispatch shape.
 
 MFMA-pipe utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs) (BUSY counts 64 cycles per
 32x32x2 f32 MFMA summed over SIMDs; GRBM_GUI_ACTIVE is summed over the 8 XCDs); effective clock =

@@ -231,6 +231,33 @@ def test_bench_two_ranks_config3_block():
     assert c3["value"] > 0 and abs(c3["value"] - 512 * 10.0 / (c3["ms_per_step"] * 1e-3)) < 1e-6 * c3["value"]
 
 
+@pytest.mark.timeout(600)
+def test_bench_eight_ranks_rehearsal():
+    """Verdict r05 item 4: the 8-rank launch the driver's N = 8 run makes, rehearsed on one GPU (gloo, every rank on
+    GPU 0, a plain `python bench.py --gpus 8` that starts torch.distributed.run itself): the census has 8 distinct
+    ranks in one process group of world size 8, the weak-scaling line is the 8-rank aggregate, and the config-3 block
+    runs BASELINE config 3's 64 utterances per GPU (512 over the node) with 8 processes sharing the host."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "-u", os.path.join(repo, "bench.py"), "--gpus", "8", "--steps", "2",
+                        "--warmup", "1", "--batch", "2", "--seconds", "10", "--no-cpu-baseline", "--dist-backend",
+                        "gloo", "--device", "0"], env=env, cwd=repo, capture_output=True, text=True, timeout=580)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 16 and d["config"]["parallelism"] == "utterance-dp8"
+    rk = d["ranks"]
+    assert rk["world_size"] == 8 and rk["backend"] == "gloo" and len(rk["ranks"]) == 8
+    assert sorted(r["rank"] for r in rk["ranks"]) == list(range(8))
+    c3 = d["config3"]
+    assert c3["per_gpu_batch"] == 64 and c3["global_batch"] == 512 and c3["steps"] == 2
+    assert c3["value"] > 0 and abs(c3["value"] - 512 * 10.0 / (c3["ms_per_step"] * 1e-3)) < 1e-6 * c3["value"]
+
+
 def test_predict_isolates_failing_file(tmp_path):
     """A batch that raises a recoverable error is re-run file by file; the file that fails alone is logged and
     skipped, every other file gets exactly its normal result."""

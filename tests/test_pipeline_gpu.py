@@ -103,3 +103,21 @@ def test_pipelined_long_lattice_dp_held_for_next_encoder():
     hc = task.submit(torch.from_numpy(batches[1][0]).to(dev), *batches[1][1:], wav_sr=16000, chunk_seconds=20.0)
     assert "resolve" not in hc
     task.decoder.assemble(hc, *batches[1][1:])
+
+
+def test_pipelined_submit_matches_align_batch():
+    """Four config-2-geometry batches through task.submit (the encoder of batch i+1 beside batch i's head + DP on the
+    side stream) give align_batch's boundaries, confidences and edge terms bit for bit, batch by batch."""
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+    dev = torch.device("cuda")
+    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
+    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
+    task.on_predict_start()
+    batches = [_inputs(8, 10.0, 30, 300 + 10 * i) for i in range(4)]
+    alone = [task.align_batch(torch.from_numpy(w).to(dev), ph, ws, pw, wav_sr=16000) for w, ph, ws, pw in batches]
+    handles = [task.submit(torch.from_numpy(w).to(dev), ph, ws, pw, wav_sr=16000) for w, ph, ws, pw in batches]
+    for i, (h, b, a) in enumerate(zip(handles, batches, alone)):
+        got = task.decoder.assemble(h, *b[1:])
+        for u, (g, r) in enumerate(zip(got, a)):
+            for k in ("ph_idx_seq", "ph_time_int", "frame_confidence", "edge_diff"):
+                assert np.array_equal(np.asarray(g[k]), np.asarray(r[k])), f"batch {i} utt {u}: {k}"
