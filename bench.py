@@ -47,7 +47,7 @@ RANDOM_DATA_F16_TFLOPS = 1247.0    # MI355X_MICROARCH.md 'DVFS give-back' (1): b
 def mfma_peak(kernel: str) -> float:
     if kernel.startswith("gemm_split_kernel") and kernel.endswith(", true>"):
         return F16_MFMA_PEAK_TFLOPS
-    split = kernel.startswith("gemm_split_kernel") or kernel.startswith("attn_fwd_split_kernel")
+    split = kernel.startswith("gemm_split_kernel") or kernel.startswith("attn_fwd_split")
     return SPLIT_F32EQ_PEAK_TFLOPS if split else F32_MFMA_PEAK_TFLOPS
 HBM_PEAK_GBPS = 8000.0             # MI355X HBM3E, MI355X_MICROARCH.md
 
@@ -381,7 +381,8 @@ def host_io(wav_np, res, seconds, budget_s=3.0):
                                           "writes each batch's TextGrids, while the GPU runs the neighbouring batch)"}
 
 
-SECONDARY = ("viterbi_forward_kernel", "hfa_conv0_split", "hfa_conv0_f32", "attn_fwd_split_kernel", "attn_fwd_f32_kernel")
+SECONDARY = ("viterbi_forward_kernel", "hfa_conv0_split", "hfa_conv0_f32", "attn_fwd_split16_kernel", "attn_fwd_split_kernel",
+             "attn_fwd_f32_kernel")
 SECONDARY_NOTE = {"hfa_conv0_split": "one hfa_conv0_split call: conv0_gram_kernel + conv0_gram_stats_kernel + "
                                      "conv0_packed_kernel (statistics and the apply pass)",
                   "hfa_conv0_f32": "one hfa_conv0_f32 call (the f32 path: statistics + the VALU apply pass)"}
@@ -736,7 +737,8 @@ def main():
         ops.PROBE = None
         torch.cuda.synchronize()
         name = cen.dominant()
-        pr = ops.KernelProbe(name, extra=("attn_fwd_split_kernel",))
+        attn = ops.attention_split_probe_name()
+        pr = ops.KernelProbe(name, extra=(attn,))
         ops.PROBE = pr
         r, e = timed(steps, inp, tk)
         ops.PROBE = None
@@ -745,7 +747,7 @@ def main():
                "steps": steps, "warmup": warmup, "ms_per_step": e / steps * 1e3,
                "value": b * seconds * steps / e, "unit": "audio_s/s",
                "frames_per_s": b * r[0]["T"] * steps / e, "dp_frames": r[0]["T"]}
-        for key, kname in (("dominant_kernel", name), ("attention", "attn_fwd_split_kernel")):
+        for key, kname in (("dominant_kernel", name), ("attention", attn)):
             s = pr.summary(kname)
             if s["launches"]:
                 ach = s["avg_flops"] / (s["avg_ms"] * 1e-3) / 1e12

@@ -521,10 +521,308 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split_kernel(const AttnS
     }
 }
 
+
+// ---- split-f16 flash attention on v_mfma_f32_16x16x32_f16 (round 6) --------------------------------------------
+// The same arithmetic as attn_fwd_split_kernel (one score accumulator k1 q1 + k1 (2^-11 q2) + k2 (2^-11 q1), stale-max
+// online softmax in the exp2 domain, P = 2^11 exp2(...) split in registers, O^T += V1 (2^11 P1) + V1 P2 + V2 P1 on one
+// accumulator at scale 2^11, software-pipelined K/V rings) with every contraction on the 16x16x32 MFMA: the same
+// cycles per FLOP as 32x32x16, but the chip holds a higher clock under it (MI355X_MICROARCH.md: 1.12-1.15x the
+// FLOP/s in bare loops; the split GEMMs gained 4-9 %, profiles/r02/split_mf16.txt).
+//   * scores S^T[key][q]: 4 key blocks x 2 query blocks of 16 per wave and 64-key tile; lane (g = lane >> 4, i =
+//     lane & 15) holds query 16 qb + i, keys 16 kb + 4 g + e -- two queries per lane, each query's 64 keys over the
+//     4 lane groups (row max / sum: in-lane, then xor 16 and xor 32);
+//   * P^T as the B operand of a 32-key step j straight from the score registers: lane group g supplies keys
+//     32 j + 4 g + (0..3) and 32 j + 16 + 4 g + (0..3); the V^T A operand is read in the same key order with two
+//     ds_read_b64_tr_b16 per plane (4 keys x 16 d each, rows 32 j + 4 g and 32 j + 16 + 4 g);
+//   * K image as the 32x32 kernel's (chunk c of row r at c ^ ((r >> 1) & 7): conflict-free for the 16x16x32 row
+//     reads too); V image with chunk c of row r at c ^ (((r >> 1) & 3) << 1): the four 4-row blocks a 32-lane half
+//     reads in one transposed read (rows R .. R + 7) take four different chunk pairs, conflict-free.
+template <int SNW>
+__global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split16_kernel(const AttnSP p) {
+    constexpr int KST = 2 * SPLANE;                      // halves per K (or V) stage, both planes
+    constexpr int NW = SNW, PPW = 8 / SNW;               // 1-KiB DMA pieces (8 keys) per plane per wave
+    static_assert(SNW == 4 || SNW == 8, "4 or 8 waves");
+    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * KST];   // K0, K1, V0, V1
+
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, xq = nwg >> 3, xr = nwg & 7;
+    const int wgid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (orig >> 3);
+    const int nqb = (p.L + QW * NW - 1) / (QW * NW);
+    const int bh = wgid / nqb, qblk = wgid - bh * nqb;
+    const int b = bh / p.H, hd = bh - b * p.H;
+    const int L = p.key_len ? p.key_len[b] : p.L;
+    if (qblk * (QW * NW) >= L) {                         // whole workgroup is padding: zero its O rows, exit
+        for (int i = threadIdx.x; i < QW * NW * (DH / 4); i += NW * 64) {
+            const int qq = qblk * (QW * NW) + i / (DH / 4), c4 = (i % (DH / 4)) * 4;
+            if (qq < p.L) {
+                _Float16* dst = p.o + b * p.o_bs + (long long)qq * p.o_ld + hd * DH + c4;
+                const f16x4 z{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+                *reinterpret_cast<f16x4*>(dst) = z;
+                *reinterpret_cast<f16x4*>(dst + p.o_sp) = z;
+            }
+        }
+        return;
+    }
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, i16 = lane & 15;
+    const int q0 = qblk * (QW * NW) + wave * QW;
+
+    const _Float16* Q = p.q + b * p.q_bs + hd * DH;
+    const _Float16* Kp = p.k + b * p.k_bs + hd * DH;
+    const _Float16* Vp = p.v + b * p.v_bs + hd * DH;
+    const long long kbytes = ((long long)(L - 1) * p.k_ld + DH) * 2, vbytes = ((long long)(L - 1) * p.v_ld + DH) * 2;
+    const __amdgpu_buffer_rsrc_t rK1 = hfa::make_rsrc(Kp, kbytes), rK2 = hfa::make_rsrc(Kp + p.k_sp, kbytes);
+    const __amdgpu_buffer_rsrc_t rV1 = hfa::make_rsrc(Vp, vbytes), rV2 = hfa::make_rsrc(Vp + p.v_sp, vbytes);
+
+    // Q^T B operands: lane (g, i) holds query q0 + 16 qb + i, d = 32 s + 8 g .. + 7
+    f16x8 q1[2][2], q1s[2][2], q2s[2][2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+        const int qi = q0 + 16 * qb + i16;
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+            f16x8 h1, h2;
+            if (qi < L) {
+                const _Float16* src = Q + (long long)qi * p.q_ld + 32 * sd + 8 * g;
+                h1 = *reinterpret_cast<const f16x8*>(src);
+                h2 = *reinterpret_cast<const f16x8*>(src + p.q_sp);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) h1[j] = h2[j] = (_Float16)0.0f;
+            }
+            q1[qb][sd] = h1;
+            q1s[qb][sd] = h1 * (_Float16)kLo;
+            q2s[qb][sd] = h2 * (_Float16)kLo;
+        }
+    }
+
+    int rowd[PPW], kch[PPW], vch[PPW];
+#pragma unroll
+    for (int d = 0; d < PPW; ++d) {
+        rowd[d] = (wave * PPW + d) * 8 + (lane >> 3);
+        kch[d] = (lane & 7) ^ ((rowd[d] >> 1) & 7);
+        vch[d] = (lane & 7) ^ (((rowd[d] >> 1) & 3) << 1);
+    }
+    const unsigned lds0 = hfa::lds_addr(smem);
+    auto issueK = [&](int stage, int key0) {
+        const unsigned base = lds0 + stage * KST * 2 + wave * PPW * 1024;
+#pragma unroll
+        for (int d = 0; d < PPW; ++d) {
+            const int key = key0 + rowd[d];
+            const unsigned ko = key < L ? (unsigned)((key * p.k_ld + kch[d] * 8) * 2) : hfa::DMA_OOB;
+            hfa::dma16(ko, rK1, 0u, base + d * 1024);
+            hfa::dma16(ko, rK2, 0u, base + SPLANE * 2 + d * 1024);
+        }
+    };
+    auto issueV = [&](int stage, int key0) {
+        const unsigned base = lds0 + (2 + stage) * KST * 2 + wave * PPW * 1024;
+#pragma unroll
+        for (int d = 0; d < PPW; ++d) {
+            const int key = key0 + rowd[d];
+            const unsigned vo = key < L ? (unsigned)((key * p.v_ld + vch[d] * 8) * 2) : hfa::DMA_OOB;
+            hfa::dma16(vo, rV1, 0u, base + d * 1024);
+            hfa::dma16(vo, rV2, 0u, base + SPLANE * 2 + d * 1024);
+        }
+    };
+
+    // K row reads: row 16 kb + i, chunk 4 sd + g (halves offset within a plane image)
+    int kofs[2];
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) kofs[sd] = i16 * DH + (((4 * sd + g) ^ ((i16 >> 1) & 7)) << 3);
+    // (row 16 kb + i has the swizzle of i: 16 kb only adds multiples of 8 to r >> 1)
+    // V transposed reads: lane 4qq + pp of the group supplies row R + qq, d columns 16 dblk + 4 pp .. + 3, i.e.
+    // chunk 2 dblk + (pp >> 1), byte 8 (pp & 1); R = 32 j + 4 g (+ 16): R + qq has (R + qq) >> 1 & 3 = (2 g + (qq >> 1)) & 3
+    // for R = 32 j + 4 g, and the same for R + 16
+    const int qq = i16 >> 2, pp = i16 & 3;
+    const int vfx = ((((4 * g + qq) >> 1) & 3) << 1);
+    int vofs[4];                                          // per dblk, bytes from the row R + qq's start
+#pragma unroll
+    for (int db = 0; db < 4; ++db) vofs[db] = (((2 * db + (pp >> 1)) ^ vfx) << 4) + 8 * (pp & 1);
+    const int vrow0 = (4 * g + qq) * (DH * 2);            // bytes: row 4 g + qq of the step
+
+    const float qscale = p.scale * 1.44269504088896340736f;
+    auto scores = [&](const _Float16* sK, f32x4 (&sM)[4][2]) {
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) sM[kb][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int sd = 0; sd < 2; ++sd) {
+                const f16x8 k1 = *reinterpret_cast<const f16x8*>(sK + kb * 16 * DH + kofs[sd]);
+                const f16x8 k2 = *reinterpret_cast<const f16x8*>(sK + SPLANE + kb * 16 * DH + kofs[sd]);
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb) {
+                    sM[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1, q1[qb][sd], sM[kb][qb], 0, 0, 0);
+                    sM[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1, q2s[qb][sd], sM[kb][qb], 0, 0, 0);
+                    sM[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k2, q1s[qb][sd], sM[kb][qb], 0, 0, 0);
+                }
+            }
+    };
+    f32x4 o[4][2];
+#pragma unroll
+    for (int db = 0; db < 4; ++db) o[db][0] = o[db][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run[2] = {-__builtin_inff(), -__builtin_inff()}, l_run[2] = {0.0f, 0.0f};
+
+    const int nkb = (L + SKB - 1) / SKB;
+    issueK(0, 0);
+    issueV(0, 0);
+    if (nkb > 1) issueK(1, SKB);
+    hfa::wait_vm_barrier<0>();
+    f32x4 sA[4][2], sB[4][2];
+    scores(smem, sA);
+    __syncthreads();                                       // every wave's K(0) reads done before K(2) lands there
+    const float one = 1.0f;
+    auto step = [&](int t, f32x4 (&s)[4][2], f32x4 (&nM)[4][2]) {
+        const int st = t & 1;
+        if (t + 2 < nkb) issueK(st, (t + 2) * SKB);
+        if (t + 1 < nkb) issueV(st ^ 1, (t + 1) * SKB);
+        if (t + 1 < nkb) scores(smem + (st ^ 1) * KST, nM);
+        const int key0 = t * SKB;
+        if (key0 + SKB > L) {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (key0 + 16 * kb + 4 * g + e >= L) s[kb][0][e] = s[kb][1][e] = -__builtin_inff();
+        }
+        bool move_any = false;
+        float m_new[2];
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            float bq[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bq[e] = fmaxf(fmaxf(s[0][qb][e], s[1][qb][e]), fmaxf(s[2][qb][e], s[3][qb][e]));
+            float bm = fmaxf(fmaxf(bq[0], bq[1]), fmaxf(bq[2], bq[3]));
+            bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+            bm = fmaxf(bm, __shfl_xor(bm, 32, 64)) * qscale;
+            const float m_cand = fmaxf(m_run[qb], bm);
+            const bool move = m_cand > m_run[qb] + kSlack;
+            m_new[qb] = move ? m_cand : m_run[qb];
+            move_any |= move;
+        }
+        if (__builtin_amdgcn_ballot_w64(move_any)) {
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                const float alpha = __builtin_amdgcn_exp2f(m_run[qb] - m_new[qb]);
+                l_run[qb] *= alpha;
+#pragma unroll
+                for (int db = 0; db < 4; ++db) o[db][qb] *= alpha;
+                m_run[qb] = m_new[qb];
+            }
+        }
+        float ls[2] = {0.0f, 0.0f};
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            const float nref = 11.0f - (m_run[qb] + kSlack);
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    s[kb][qb][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][qb][e], qscale, nref));
+                    ls[qb] += s[kb][qb][e];
+                }
+        }
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            float v = ls[qb];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            l_run[qb] += v;
+        }
+        const char* sV = reinterpret_cast<const char*>(smem + (2 + st) * KST);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            // P^T B operands of step j: keys 32 j + 4 g + (0..3) (score block 2 j) then 32 j + 16 + 4 g + (0..3) (2 j + 1)
+            f16x8 p1s[2], p1[2], p2[2];
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                unsigned w1[4], w2[4];
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj) {
+                        const float x0 = s[2 * j + h][qb][2 * jj], x1 = s[2 * j + h][qb][2 * jj + 1];
+                        w1[2 * h + jj] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x0, x1}, f16x2));
+                        w2[2 * h + jj] = hfa::split_lo_pair(w1[2 * h + jj], x0, x1, one);
+                    }
+                p1s[qb] = __builtin_bit_cast(f16x8, make_uint4(w1[0], w1[1], w1[2], w1[3]));
+                p2[qb] = __builtin_bit_cast(f16x8, make_uint4(w2[0], w2[1], w2[2], w2[3]));
+                p1[qb] = p1s[qb] * (_Float16)kLo;
+            }
+            const int rb = 32 * j * (DH * 2) + vrow0;
+#pragma unroll
+            for (int db = 0; db < 4; ++db) {
+                const f16x4 a0 = lds_tr(reinterpret_cast<const _Float16*>(sV), rb + vofs[db]);
+                const f16x4 a1 = lds_tr(reinterpret_cast<const _Float16*>(sV), rb + 16 * DH * 2 + vofs[db]);
+                const f16x4 b0 = lds_tr(reinterpret_cast<const _Float16*>(sV) + SPLANE, rb + vofs[db]);
+                const f16x4 b1 = lds_tr(reinterpret_cast<const _Float16*>(sV) + SPLANE, rb + 16 * DH * 2 + vofs[db]);
+                const f16x8 v1 = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                const f16x8 v2 = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+                for (int qb = 0; qb < 2; ++qb) {
+                    o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(v1, p1s[qb], o[db][qb], 0, 0, 0);
+                    o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(v1, p2[qb], o[db][qb], 0, 0, 0);
+                    o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(v2, p1[qb], o[db][qb], 0, 0, 0);
+                }
+            }
+        }
+        if (t + 1 < nkb) {
+            hfa::wait_vm_barrier<0>();                     // K(t+2), V(t+1) landed; K(t+1), V(t) reads done
+        }
+    };
+    for (int t = 0; t < nkb; t += 2) {
+        step(t, sA, sB);
+        if (t + 1 < nkb) step(t + 1, sB, sA);
+    }
+
+    // O[q][d] = o[db][qb][e] / l at q = 16 qb + i, d = 16 db + 4 g + e; staged per 32-column half through a
+    // [32 q][36] f32 slab per wave, then written as split planes with row-contiguous stores
+    __syncthreads();
+    float inv[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) inv[qb] = 1.0f / l_run[qb];            // o and l both carry the 2^11 scale
+    float* slab = reinterpret_cast<float*>(smem) + wave * (QW * 36);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb)
+                *reinterpret_cast<f32x4*>(slab + (16 * qb + i16) * 36 + 16 * dd + 4 * g) = o[2 * hh + dd][qb] * inv[qb];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int idx = lane + it * 64;
+            const int row = idx >> 3, c4 = (idx & 7) * 4;
+            const int qq2 = q0 + row;
+            if (qq2 < p.L) {
+                const f32x4 x4 = *reinterpret_cast<const f32x4*>(slab + row * 36 + c4);
+                f16x4 h1, h2;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float x = qq2 < L ? x4[t] : 0.0f;
+                    h1[t] = (_Float16)x;
+                    h2[t] = (_Float16)((x - (float)h1[t]) * 2048.0f);
+                }
+                _Float16* dst = p.o + b * p.o_bs + (long long)qq2 * p.o_ld + hd * DH + hh * 32 + c4;
+                *reinterpret_cast<f16x4*>(dst) = h1;
+                *reinterpret_cast<f16x4*>(dst + p.o_sp) = h2;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 }  // namespace
 
 namespace {
 thread_local int g_attn_waves = 0;   // hfa_attention_split_tuning override (0: automatic)
+thread_local int g_attn_form = 0;    // hfa_attention_split_form override (0: automatic, 32: 32x32x16, 16: 16x16x32)
+constexpr int kAttnFormDefault = 16; // the form the automatic choice takes
 // Waves (x 32 queries) per workgroup of the split attention, by the busiest CU's share of the grid: the B*H*ceil(L /
 // 32w) query blocks of w waves spread over the device's CUs (256 on a whole MI355X), so that CU runs ceil(blocks /
 // CUs) * w waves' worth of query rows.  The smaller share wins; on a tie 8 waves for long rows (>= 2048 keys: half the K/V staging per query), 4 for
@@ -607,10 +905,17 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
         hfa::set_error("hfa_attention_split: grid too large");
         return HFA_EINVAL;
     }
-    if (nw == 8)
+    const int form = g_attn_form ? g_attn_form : kAttnFormDefault;
+    if (form == 16) {
+        if (nw == 8)
+            hipLaunchKernelGGL((attn_fwd_split16_kernel<8>), dim3((unsigned)nblk), dim3(8 * 64), 0, stream, p);
+        else
+            hipLaunchKernelGGL((attn_fwd_split16_kernel<4>), dim3((unsigned)nblk), dim3(4 * 64), 0, stream, p);
+    } else if (nw == 8) {
         hipLaunchKernelGGL((attn_fwd_split_kernel<8>), dim3((unsigned)nblk), dim3(8 * 64), 0, stream, p);
-    else
+    } else {
         hipLaunchKernelGGL((attn_fwd_split_kernel<4>), dim3((unsigned)nblk), dim3(4 * 64), 0, stream, p);
+    }
     return hfa::check_launch("hfa_attention_split");
 }
 
@@ -622,6 +927,25 @@ int hfa_attention_split_tuning(int waves) {
     }
     g_attn_waves = waves;
     return HFA_OK;
+}
+
+// MFMA form of hfa_attention_split: 16 (v_mfma_f32_16x16x32_f16), 32 (v_mfma_f32_32x32x16_f16), 0 = automatic.
+int hfa_attention_split_form(int form) {
+    if (form != 0 && form != 16 && form != 32) {
+        hfa::set_error("hfa_attention_split_form: form must be 0, 16 or 32");
+        return HFA_EINVAL;
+    }
+    g_attn_form = form;
+    return HFA_OK;
+}
+
+// The kernel instantiation hfa_attention_split launches for (B, H, L) under the current tuning (probe / profiler
+// labels): "attn_fwd_split16_kernel<4>" etc.
+const char* hfa_attention_split_kernel_name(int B, int H, int L) {
+    static thread_local char buf[64];
+    const int nw = split_attn_waves(B, H, L), form = g_attn_form ? g_attn_form : kAttnFormDefault;
+    snprintf(buf, sizeof(buf), "%s<%d>", form == 16 ? "attn_fwd_split16_kernel" : "attn_fwd_split_kernel", nw);
+    return buf;
 }
 
 }  // extern "C"

@@ -172,6 +172,8 @@ _lib.register("hfa_attention_f32", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_
 _lib.register("hfa_attention_split", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _LL_,
                                       _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _P_])
 _lib.register("hfa_attention_split_tuning", [_I_])
+_lib.register("hfa_attention_split_form", [_I_])
+_lib.register("hfa_attention_split_kernel_name", [_I_, _I_, _I_], ctypes.c_char_p)
 _lib.register("hfa_layernorm_split", [_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_,
                                       _LL_, _P_, _P_])
 _lib.register("hfa_layernorm_f32",[_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_])
@@ -412,8 +414,9 @@ def attention(q, k, v, out, *, B, H, L, head_dim, scale, q_bs, q_ld, k_bs, k_ld,
 
 
 def attention_split(qkv_s, out_s, *, B, H, L, head_dim, scale, key_len=None):
-    """Flash attention on split planes (attention.hip attn_fwd_split_kernel): ``qkv_s`` [2, B, L, 3*H*head_dim]
-    f16 planes of the fused QKV projection (Q | K | V column blocks), ``out_s`` [2, B, L, H*head_dim] planes."""
+    """Flash attention on split planes (attention.hip attn_fwd_split16_kernel / attn_fwd_split_kernel): ``qkv_s``
+    [2, B, L, 3*H*head_dim] f16 planes of the fused QKV projection (Q | K | V column blocks), ``out_s``
+    [2, B, L, H*head_dim] planes."""
     _need(qkv_s, torch.float16, "qkv_s")
     _need(out_s, torch.float16, "out_s")
     D = H * head_dim
@@ -431,9 +434,15 @@ def attention_split(qkv_s, out_s, *, B, H, L, head_dim, scale, key_len=None):
     if PROBE is None:
         launch()
     else:
-        PROBE("attn_fwd_split_kernel", 4.0 * B * H * L * L * head_dim, launch, kind="flops_aux",
+        PROBE(attention_split_probe_name(), 4.0 * B * H * L * L * head_dim, launch, kind="flops_aux",
               shape=(B, H, L, head_dim))
     return out_s
+
+
+def attention_split_probe_name() -> str:
+    """rocprof symbol stem of the split attention the library launches under the current MFMA form
+    (hfa_attention_split_form): "attn_fwd_split16_kernel" (16x16x32, the default) or "attn_fwd_split_kernel"."""
+    return _lib.lib().hfa_attention_split_kernel_name(1, 1, 1).decode().split("<")[0]
 
 
 def layernorm(x, gamma, beta, eps=1e-5, act=ACT_NONE, out=None, residual=None, t_len=None, out_split=None,

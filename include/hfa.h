@@ -192,6 +192,12 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
  * busiest CU fewer query rows; on a tie 8 from 2048 keys).  Results do not depend on it (every query row sees the
  * same tiles in the same order). */
 int hfa_attention_split_tuning(int waves);
+/* MFMA form of hfa_attention_split (tuning / A-B; 0 = automatic = 16): 16 = v_mfma_f32_16x16x32_f16, 32 =
+ * v_mfma_f32_32x32x16_f16 (the round-2..5 kernel).  The same products in the same key-tile order; outputs agree to
+ * f32 rounding.  HFA_EINVAL for any other value. */
+int hfa_attention_split_form(int form);
+/* Name of the instantiation hfa_attention_split launches for (B, H, L) under the current tuning (profiler labels). */
+const char* hfa_attention_split_kernel_name(int B, int H, int L);
 
 /* ---- normalisation (hubertfa_amd/csrc/norm.hip); act: 0 none, 1 erf-GELU, 2 Hardswish -----------------------
  * y = act(LayerNorm(x (+ res)) * gamma + beta) over rows of C <= 4096 (C % 4 == 0).

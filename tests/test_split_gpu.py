@@ -4,6 +4,8 @@ The split operand x = x1 + 2^-11 x2 keeps 22 significand bits; the product adds 
 products in f32.  Bars: the same tolerances as the f32 MFMA GEMM tests (2e-5 relative + 2e-5 absolute on unit-scale
 data) — the split path is measured at or below the f32 path's own error (scripts/split_gemm_bench.py).
 """
+import contextlib
+
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -364,9 +366,25 @@ def _attn_ref(qkv, B, L, H, D, lens=None):
     return (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B, L, H * D)
 
 
+@contextlib.contextmanager
+def _attn_form(form):
+    """hfa_attention_split's MFMA form for the block: 16 (16x16x32, the default), 32 (32x32x16)."""
+    from hubertfa_amd import _lib
+    _lib.call("hfa_attention_split_form", form)
+    try:
+        yield
+    finally:
+        _lib.call("hfa_attention_split_form", 0)
+
+
+ATTN_FORMS = [16, 32]
+
+
+@pytest.mark.parametrize("form", ATTN_FORMS)
 @pytest.mark.parametrize("B,H,L", [(2, 12, 499), (1, 3, 64), (3, 2, 1), (1, 16, 200), (1, 1, 1500)])
-def test_attention_split(B, H, L):
-    """Split attention vs f64, at the f32 kernel's own tolerance (tests/test_kernels_gpu.py::test_attention)."""
+def test_attention_split(B, H, L, form):
+    """Split attention vs f64, at the f32 kernel's own tolerance (tests/test_kernels_gpu.py::test_attention), in
+    both MFMA forms."""
     from hubertfa_amd import ops
     D = 64
     qkv = _r(B, L, 3 * H * D, seed=8, scale=1.5)
@@ -374,12 +392,39 @@ def test_attention_split(B, H, L):
     d = torch.device("cuda")
     qs = ops.split(qkv.to(d))
     out = torch.empty(2, B, L, H * D, dtype=torch.float16, device=d)
-    ops.attention_split(qs, out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5)
+    with _attn_form(form):
+        ops.attention_split(qs, out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5)
     got = out[0].float() + out[1].float() / 2048.0
     _close(got, ref, 1e-4, 2e-5)
 
 
-def test_attention_split_varlen():
+@pytest.mark.parametrize("L", [499, 4999])
+def test_attention_split_forms_agree(L):
+    """The 16x16x32 and 32x32x16 forms compute the same products in the same K/V tile order and differ only in the
+    MFMA's internal summation: against f64, the 16x16x32 form's largest error is within 1.25x the 32x32x16 form's
+    (and both meet the split tolerance), at config 2's length and a long row; and the launched instantiation's name
+    follows the form."""
+    from hubertfa_amd import ops, _lib
+    B, H, D = (4, 12, 64) if L < 1000 else (1, 2, 64)
+    qkv = _r(B, L, 3 * H * D, seed=21, scale=2.0)
+    ref = _attn_ref(qkv, B, L, H, D)
+    d = torch.device("cuda")
+    qs = ops.split(qkv.to(d))
+    errs = []
+    for form in (16, 32):
+        with _attn_form(form):
+            o = torch.empty(2, B, L, H * D, dtype=torch.float16, device=d)
+            ops.attention_split(qs, o, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5)
+            got = (o[0].double() + o[1].double() / 2048.0).cpu()
+            name = _lib.lib().hfa_attention_split_kernel_name(B, H, L).decode()
+            assert name.startswith("attn_fwd_split16_kernel<" if form == 16 else "attn_fwd_split_kernel<"), name
+        _close(got.float(), ref, 1e-4, 2e-5)
+        errs.append(float((got - ref).abs().max()))
+    assert errs[0] <= 1.25 * errs[1] + 1e-7, errs
+
+
+@pytest.mark.parametrize("form", ATTN_FORMS)
+def test_attention_split_varlen(form):
     """Per-row key lengths: each row equals its own un-padded attention (rows past the length untouched)."""
     from hubertfa_amd import ops
     from hubertfa_amd.hubert import dev_lengths
@@ -390,7 +435,8 @@ def test_attention_split_varlen():
     d = torch.device("cuda")
     qs = ops.split(qkv.to(d))
     out = torch.full((2, B, L, H * D), float("nan"), dtype=torch.float16, device=d)   # padding rows must be written
-    ops.attention_split(qs, out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5, key_len=dev_lengths(lens, d))
+    with _attn_form(form):
+        ops.attention_split(qs, out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5, key_len=dev_lengths(lens, d))
     got = (out[0].float() + out[1].float() / 2048.0).cpu()
     for b, n in enumerate(lens):
         _close(got[b, :n], ref[b, :n], 1e-4, 2e-5)
@@ -431,10 +477,11 @@ def test_attention_split_repeatable():
         assert torch.equal(one[:, 0], first[:, b, :n])
 
 
+@pytest.mark.parametrize("form", ATTN_FORMS)
 @pytest.mark.parametrize("L", [499, 700])
-def test_attention_split_waves_bit_identical(L):
+def test_attention_split_waves_bit_identical(L, form):
     """4- and 8-wave workgroups give bit-identical planes (each query row sees the same key tiles in the same
-    order), with and without per-row key lengths."""
+    order), with and without per-row key lengths, in both MFMA forms."""
     from hubertfa_amd import ops, _lib
     from hubertfa_amd.hubert import dev_lengths
     B, H, D = 3, 4, 64
@@ -445,15 +492,17 @@ def test_attention_split_waves_bit_identical(L):
         for nw in (4, 8):
             _lib.call("hfa_attention_split_tuning", nw)
             try:
-                o = torch.full((2, B, L, H * D), float("nan"), dtype=torch.float16, device=d)
-                ops.attention_split(qs, o, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5, key_len=kl)
+                with _attn_form(form):
+                    o = torch.full((2, B, L, H * D), float("nan"), dtype=torch.float16, device=d)
+                    ops.attention_split(qs, o, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5, key_len=kl)
                 outs.append(o)
             finally:
                 _lib.call("hfa_attention_split_tuning", 0)
         assert torch.equal(outs[0], outs[1])
 
 
-def test_attention_split_large_scores():
+@pytest.mark.parametrize("form", ATTN_FORMS)
+def test_attention_split_large_scores(form):
     """Peaked softmax (scores ~ +-60): the score's own f32-level rounding dominates both kernels' error; the split
     kernel stays within 2x the f32 MFMA kernel's error against f64."""
     from hubertfa_amd import ops
@@ -463,7 +512,8 @@ def test_attention_split_large_scores():
     ref = _attn_ref(qkv, B, L, H, D)
     d = torch.device("cuda")
     out = torch.empty(2, B, L, H * D, dtype=torch.float16, device=d)
-    ops.attention_split(ops.split(qkv.to(d)), out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5)
+    with _attn_form(form):
+        ops.attention_split(ops.split(qkv.to(d)), out, B=B, H=H, L=L, head_dim=D, scale=D ** -0.5)
     qd = qkv.to(d)
     o32 = torch.empty(B, L, H * D, device=d)
     ld = 3 * H * D
