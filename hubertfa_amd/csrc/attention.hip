@@ -250,7 +250,6 @@ struct AttnSP {
     const _Float16* v; long long v_sp, v_bs; int v_ld;
     _Float16* o; long long o_sp, o_bs; int o_ld;
     const int32_t* key_len;
-    int sched;                  // 16x16x32 kernel, 8 waves: bit 0 = stagger waves 4-7, bit 1 = s_setprio 1 for them
 };
 
 __device__ __forceinline__ f16x4 lds_tr(const _Float16* base, int byte_off) {
@@ -676,18 +675,11 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split16_kernel(const Att
     scores(smem, sA);
     __syncthreads();                                       // every wave's K(0) reads done before K(2) lands there
     const float one = 1.0f;
-    // 8 waves: a SIMD's two waves are wave w and w + 4 of this workgroup, kept in step by the per-tile barrier.  In
-    // lockstep both run their score MFMAs, then both their softmax (the matrix pipe idle), then both their PV MFMAs.
-    // Staggered (sched bit 0), waves 4-7 take the tile's phases in the order softmax(t), PV(t), scores(t + 1): their
-    // softmax runs beside waves 0-3's score MFMAs and their PV beside waves 0-3's softmax (MI355X_MICROARCH.md,
-    // "Two waves per SIMD" item 9).  Same products in the same order per query: results are bit-identical.
-    const bool late = SNW == 8 && (p.sched & 1) && wave >= 4;
-    if (SNW == 8 && (p.sched & 2) && wave >= 4) __builtin_amdgcn_s_setprio(1);
     auto step = [&](int t, f32x4 (&s)[4][2], f32x4 (&nM)[4][2]) {
         const int st = t & 1;
         if (t + 2 < nkb) issueK(st, (t + 2) * SKB);
         if (t + 1 < nkb) issueV(st ^ 1, (t + 1) * SKB);
-        if (!late && t + 1 < nkb) scores(smem + (st ^ 1) * KST, nM);
+        if (t + 1 < nkb) scores(smem + (st ^ 1) * KST, nM);
         const int key0 = t * SKB;
         if (key0 + SKB > L) {
 #pragma unroll
@@ -777,7 +769,6 @@ __global__ __launch_bounds__(SNW * 64, 2) void attn_fwd_split16_kernel(const Att
                 }
             }
         }
-        if (late && t + 1 < nkb) scores(smem + (st ^ 1) * KST, nM);
         if (t + 1 < nkb) {
             hfa::wait_vm_barrier<0>();                     // K(t+2), V(t+1) landed; K(t+1), V(t) reads done
         }
@@ -832,7 +823,6 @@ namespace {
 thread_local int g_attn_waves = 0;   // hfa_attention_split_tuning override (0: automatic)
 thread_local int g_attn_form = 0;    // hfa_attention_split_form override (0: automatic, 32: 32x32x16, 16: 16x16x32)
 constexpr int kAttnFormDefault = 16; // the form the automatic choice takes
-thread_local int g_attn_sched = 0;   // hfa_attention_split_sched: AttnSP::sched of the 16x16x32 kernel
 // Waves (x 32 queries) per workgroup of the split attention, by the busiest CU's share of the grid: the B*H*ceil(L /
 // 32w) query blocks of w waves spread over the device's CUs (256 on a whole MI355X), so that CU runs ceil(blocks /
 // CUs) * w waves' worth of query rows.  The smaller share wins; on a tie 8 waves for long rows (>= 2048 keys: half the K/V staging per query), 4 for
@@ -908,7 +898,7 @@ int hfa_attention_split(int B, int H, int L, int head_dim, float scale, const ui
         return HFA_EINVAL;
     }
     AttnSP p{B, H, L, scale, (const _Float16*)q, q_sp, q_bs, q_ld, (const _Float16*)k, k_sp, k_bs, k_ld,
-             (const _Float16*)v, v_sp, v_bs, v_ld, (_Float16*)o, o_sp, o_bs, o_ld, key_len, g_attn_sched};
+             (const _Float16*)v, v_sp, v_bs, v_ld, (_Float16*)o, o_sp, o_bs, o_ld, key_len};
     const int nw = split_attn_waves(B, H, L);
     const long long nblk = (long long)((L + QW * nw - 1) / (QW * nw)) * B * H;
     if (nblk > 0x7fffffffLL) {
@@ -946,17 +936,6 @@ int hfa_attention_split_form(int form) {
         return HFA_EINVAL;
     }
     g_attn_form = form;
-    return HFA_OK;
-}
-
-// Wave schedule of the 16x16x32 kernel's 8-wave workgroups (A/B): bit 0 staggers waves 4-7, bit 1 gives them issue
-// priority 1; 0 = lockstep.
-int hfa_attention_split_sched(int sched) {
-    if (sched < 0 || sched > 3) {
-        hfa::set_error("hfa_attention_split_sched: 0..3");
-        return HFA_EINVAL;
-    }
-    g_attn_sched = sched;
     return HFA_OK;
 }
 

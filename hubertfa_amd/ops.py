@@ -173,7 +173,6 @@ _lib.register("hfa_attention_split", [_I_, _I_, _I_, _I_, _F_, _P_, _LL_, _LL_, 
                                       _LL_, _I_, _P_, _LL_, _LL_, _I_, _P_, _P_])
 _lib.register("hfa_attention_split_tuning", [_I_])
 _lib.register("hfa_attention_split_form", [_I_])
-_lib.register("hfa_attention_split_sched", [_I_])
 _lib.register("hfa_attention_split_kernel_name", [_I_, _I_, _I_], ctypes.c_char_p)
 _lib.register("hfa_layernorm_split", [_I_, _I_, _P_, _LL_, _P_, _LL_, _P_, _P_, _F_, _I_, _P_, _LL_, _I_, _P_, _P_, _LL_,
                                       _LL_, _P_, _P_])

@@ -196,10 +196,6 @@ int hfa_attention_split_tuning(int waves);
  * v_mfma_f32_32x32x16_f16 (the round-2..5 kernel).  The same products in the same key-tile order; outputs agree to
  * f32 rounding.  HFA_EINVAL for any other value. */
 int hfa_attention_split_form(int form);
-/* Wave schedule of the 16x16x32 form's 8-wave workgroups (A/B; results bit-identical): bit 0 staggers waves 4-7
- * (softmax, PV, then the next scores, beside waves 0-3's scores, softmax, PV), bit 1 gives waves 4-7 issue priority 1;
- * 0 = lockstep.  HFA_EINVAL outside 0..3. */
-int hfa_attention_split_sched(int sched);
 /* Name of the instantiation hfa_attention_split launches for (B, H, L) under the current tuning (profiler labels). */
 const char* hfa_attention_split_kernel_name(int B, int H, int L);
 

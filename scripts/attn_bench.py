@@ -37,15 +37,13 @@ def main():
             ops.attention(qkv, qkv[..., H * D:], qkv[..., 2 * H * D:], out, B=B, H=H, L=L, head_dim=D,
                           scale=D ** -0.5, q_bs=L * 3 * H * D, q_ld=3 * H * D, k_bs=L * 3 * H * D, k_ld=3 * H * D,
                           v_bs=L * 3 * H * D, v_ld=3 * H * D, o_bs=L * H * D, o_ld=H * D)
-        arms = [("f32", go, 0, 0, 0)] + [(f"mf{form}-{'auto' if nw == 0 else f'{nw}w'}", go_split, nw, form, 0)
-                                          for form in (32, 16) for nw in (0, 4, 8)]
-        arms += [(f"mf16-8w-s{sc}", go_split, 8, 16, sc) for sc in (1, 2, 3)]
+        arms = [("f32", go, 0, 0)] + [(f"mf{form}-{'auto' if nw == 0 else f'{nw}w'}", go_split, nw, form)
+                                       for form in (32, 16) for nw in (0, 4, 8)]
         res = {a[0]: [] for a in arms}
         for _ in range(args.rounds):                  # interleaved rounds: clock drift hits every arm alike
-            for tag, fn, nw, form, sched in arms:
+            for tag, fn, nw, form in arms:
                 _lib.call("hfa_attention_split_tuning", nw)
                 _lib.call("hfa_attention_split_form", form)
-                _lib.call("hfa_attention_split_sched", sched)
                 for _ in range(3):
                     fn()
                 torch.cuda.synchronize()
@@ -58,7 +56,6 @@ def main():
                 res[tag].append(e0.elapsed_time(e1) / args.reps)
                 _lib.call("hfa_attention_split_tuning", 0)
                 _lib.call("hfa_attention_split_form", 0)
-                _lib.call("hfa_attention_split_sched", 0)
         for tag, v in res.items():
             ms = sorted(v)[len(v) // 2]
             tf = 4.0 * B * H * L * L * D / ms / 1e9
