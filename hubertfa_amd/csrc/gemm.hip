@@ -1079,34 +1079,36 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
 }
 
 // f32 -> (hi, lo * 2^11) f16 planes, row-wise with 4-element vectors where aligned; raises *oflow for |x| >= 65504
-// or a non-finite x.
+// or a non-finite x.  Rows blockIdx.y, + gridDim.y, ... (a capped grid, hfa::grid_cap).
 __global__ __launch_bounds__(256) void split_f16_kernel(int rows, int cols, const float* __restrict__ x, long long ldx,
                                                         _Float16* __restrict__ y, long long ldy, long long sp,
                                                         int* __restrict__ oflow) {
     const int c4 = (blockIdx.x * 256 + threadIdx.x) * 4;
-    const int r = blockIdx.y;
-    if (r >= rows || c4 >= cols) return;
-    const float* src = x + (long long)r * ldx + c4;
-    _Float16* dst = y + (long long)r * ldy + c4;
+    if (c4 >= cols) return;
+    const bool vec = c4 + 3 < cols && ((ldx | ldy | sp) & 3) == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0;
     bool bad = false;
-    if (c4 + 3 < cols && ((ldx | ldy | sp) & 3) == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(src);
-        f16x4 v1, v2;
+    for (int r = blockIdx.y; r < rows; r += gridDim.y) {
+        const float* src = x + (long long)r * ldx + c4;
+        _Float16* dst = y + (long long)r * ldy + c4;
+        if (vec) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(src);
+            f16x4 v1, v2;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            bad |= !(__builtin_fabsf(v[t]) < 65504.0f);
-            v1[t] = (_Float16)v[t];
-            v2[t] = (_Float16)((v[t] - (float)v1[t]) * 2048.0f);
-        }
-        *reinterpret_cast<f16x4*>(dst) = v1;
-        *reinterpret_cast<f16x4*>(dst + sp) = v2;
-    } else {
-        for (int t = 0; t < 4 && c4 + t < cols; ++t) {
-            const float v = src[t];
-            bad |= !(__builtin_fabsf(v) < 65504.0f);
-            const _Float16 v1 = (_Float16)v;
-            dst[t] = v1;
-            dst[t + sp] = (_Float16)((v - (float)v1) * 2048.0f);
+            for (int t = 0; t < 4; ++t) {
+                bad |= !(__builtin_fabsf(v[t]) < 65504.0f);
+                v1[t] = (_Float16)v[t];
+                v2[t] = (_Float16)((v[t] - (float)v1[t]) * 2048.0f);
+            }
+            *reinterpret_cast<f16x4*>(dst) = v1;
+            *reinterpret_cast<f16x4*>(dst + sp) = v2;
+        } else {
+            for (int t = 0; t < 4 && c4 + t < cols; ++t) {
+                const float v = src[t];
+                bad |= !(__builtin_fabsf(v) < 65504.0f);
+                const _Float16 v1 = (_Float16)v;
+                dst[t] = v1;
+                dst[t + sp] = (_Float16)((v - (float)v1) * 2048.0f);
+            }
         }
     }
     if (bad && oflow) *oflow = 1;
@@ -1971,7 +1973,9 @@ int hfa_split_f16(int rows, int cols, const float* x, long long ldx, uint16_t* y
         hfa::set_error("hfa_split_f16: too many rows");
         return HFA_EINVAL;
     }
-    dim3 grid((cols + 1023) / 1024, rows);
+    const int cb = (cols + 1023) / 1024;
+    const int gy = hfa::capped((long long)rows * cb) / cb;
+    dim3 grid(cb, gy > 0 ? gy : 1);
     hipLaunchKernelGGL(split_f16_kernel, grid, dim3(256), 0, stream, rows, cols, x, ldx,
                        reinterpret_cast<_Float16*>(y), ldy, sp, oflow);
     return hfa::check_launch("hfa_split_f16");

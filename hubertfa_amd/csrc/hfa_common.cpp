@@ -7,6 +7,7 @@
 
 namespace {
 thread_local char g_last_error[512] = "";
+thread_local int g_grid_cap = 0;
 }
 
 namespace hfa {
@@ -16,6 +17,8 @@ void set_error(const char* fmt, ...) {
     vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
     va_end(ap);
 }
+
+int grid_cap() { return g_grid_cap; }
 
 int device_cus() {
     static std::atomic<int> cache[64];            // 0 = not asked yet
@@ -33,4 +36,13 @@ extern "C" {
 const char* hfa_last_error(void) { return g_last_error; }
 int hfa_abi_version(void) { return HFA_ABI_VERSION; }
 const char* hfa_build_arch(void) { return "gfx950"; }
+
+int hfa_set_grid_cap(int wgs) {
+    if (wgs < 0) {
+        hfa::set_error("hfa_set_grid_cap: wgs must be >= 0");
+        return HFA_EINVAL;
+    }
+    g_grid_cap = wgs;
+    return HFA_OK;
+}
 }

@@ -21,6 +21,15 @@ void set_error(const char* fmt, ...);
 // Compute units of the calling thread's current device (hipDeviceProp_t::multiProcessorCount, cached per device);
 // 256 on a whole MI355X, fewer on a partitioned one.  Grid-shape rules use it instead of a constant.
 int device_cus();
+// Workgroup cap for the row-streaming kernels (split_f16, LayerNorm, lattice prologue) on this host thread
+// (hfa_set_grid_cap; 0 = none): a capped launch runs its rows in a grid-stride loop over at most this many
+// workgroups.  task.submit caps the side pass's launches, whose tens of thousands of one-row workgroups otherwise
+// cost the encoder beside them more than their work (profiles/r06/side_cost_decomposition.txt).
+int grid_cap();
+inline int capped(long long want) {
+    const int cap = grid_cap();
+    return (int)(cap > 0 && want > cap ? cap : want);
+}
 
 inline int check_launch(const char* what) {
     hipError_t e = hipGetLastError();

@@ -24,9 +24,9 @@ __device__ __forceinline__ float act_apply(float v, int act) {
     return v;
 }
 
-// Row-per-wave LayerNorm; C % 4 == 0, C <= 64*4*VPL
+// Row-per-wave LayerNorm; C % 4 == 0, C <= 64*4*VPL.  One row (wave index `wave`) per call.
 template <int VPL>
-__global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const float* __restrict__ x, long long ldx,
+__device__ __forceinline__ void layernorm_row(int wave, int lane, int C, const float* __restrict__ x, long long ldx,
                                                         const float* __restrict__ res, long long ldr,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps, int act,
@@ -36,9 +36,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
                                                         int* __restrict__ oflow) {
     // ys (optional): the output also as split-f16 planes (gemm.hip's split operand: hi, (x - hi) * 2^11), so the
     // next split GEMM reads it without a separate conversion pass; *oflow raised for |y| >= 65504 / non-finite
-    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    if (wave >= rows) return;
     if (t_len && wave % T >= t_len[wave / T]) {     // padding row of a variable-length batch: zeros
         float* yr = y ? y + wave * ldy : nullptr;
         for (int c = lane * 4; c < C; c += 256) {
@@ -104,6 +101,22 @@ __global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const f
         }
     }
     if (hfa::range_bad(nanacc) && oflow) *oflow = 1;
+}
+
+// Rows wave, wave + 4 gridDim.x, ... (a capped grid, hfa::grid_cap)
+template <int VPL>
+__global__ __launch_bounds__(256) void layernorm_kernel(int rows, int C, const float* __restrict__ x, long long ldx,
+                                                        const float* __restrict__ res, long long ldr,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps, int act,
+                                                        float* __restrict__ y, long long ldy, int T,
+                                                        const int32_t* __restrict__ t_len,
+                                                        _Float16* __restrict__ ys, long long ldys, long long sps,
+                                                        int* __restrict__ oflow) {
+    const int lane = threadIdx.x & 63;
+    for (int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wave < rows; wave += gridDim.x * (blockDim.x >> 6))
+        layernorm_row<VPL>(wave, lane, C, x, ldx, res, ldr, gamma, beta, eps, act, y, ldy, T, t_len, ys, ldys, sps,
+                           oflow);
 }
 
 // GroupNorm over a channels-last [T, C] slab per batch item: group g = channels [g*Cg, (g+1)*Cg) over all T.
@@ -403,7 +416,7 @@ int hfa_layernorm_split(int rows, int C, const float* x, long long ldx, const fl
                        "strides multiple of 4");
         return HFA_EINVAL;
     }
-    const int blocks = (rows + 3) / 4;
+    const int blocks = hfa::capped((rows + 3) / 4);
     const int vpl = (C + 255) / 256;
 #define HFA_LN(V)                                                                                               \
     hipLaunchKernelGGL(layernorm_kernel<V>, dim3(blocks), dim3(256), 0, stream, rows, C, x, ldx, res, ldr, gamma, \

@@ -563,6 +563,63 @@ __global__ __launch_bounds__(256) void viterbi_init_kernel(int Tmax, int Smax, c
     dp_row0(b, Tmax, Smax, S, ph_seq_id + (size_t)b * Smax, Tv[b] > 0 ? row0 : nullptr, threadIdx.x, 256, dp, curr);
 }
 
+// One frame t of batch b (one wave): masked log-softmax over V into lsm, the lattice row, edge terms, dp row 0.
+__device__ __forceinline__ void lattice_frame(
+    int t, int b, int T, int S, int V, int Tmax, int Smax, const int32_t* __restrict__ ids,
+    const unsigned char* allowed, float* lsm_w, int lane, const float* __restrict__ frame_logits, long long f_ld,
+    long long f_bs, const float* __restrict__ edge_logits, long long e_ld, long long e_bs,
+    float* __restrict__ ph_prob_log, float* __restrict__ ph_frame_pred, float* __restrict__ prob_log,
+    float* __restrict__ edge_log, float* __restrict__ not_edge_log, float* __restrict__ edge_diff,
+    double* __restrict__ edge_prob_out, float* __restrict__ dp, double* __restrict__ curr) {
+    const float* xr = frame_logits + b * f_bs + t * f_ld;
+    float m = neg_inf();
+    for (int v = lane; v < V; v += 64) {
+        const float x = xr[v] - (allowed[v] ? 0.0f : 1e9f);
+        lsm_w[v] = x;
+        m = fmaxf(m, x);
+    }
+    m = hfa::wave_max(m);
+    float sum = 0.0f;
+    for (int v = lane; v < V; v += 64) sum += expf(lsm_w[v] - m);
+    sum = hfa::wave_sum(sum);
+    const float lse = logf(sum);
+    const float inv = 1.0f / sum;
+    for (int v = lane; v < V; v += 64) {
+        const float xm = lsm_w[v] - m;
+        const float lp = xm - lse;
+        if (ph_prob_log) ph_prob_log[((size_t)b * Tmax + t) * V + v] = lp;
+        if (ph_frame_pred) ph_frame_pred[((size_t)b * Tmax + t) * V + v] = expf(xm) * inv;
+        lsm_w[v] = lp;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int s = lane; s < S; s += 64) {
+        const int v = ids[s];
+        prob_log[((size_t)b * Tmax + t) * Smax + s] = lsm_w[v];
+    }
+    if (t == 0 && dp) {          // _decode's dp / curr initialisation from this frame's lattice row (no extra launch)
+        const float l0 = lsm_w[ids[0]], l1 = S > 1 ? lsm_w[ids[1]] : 0.0f;
+        const float row0[2] = {l0, l1};
+        dp_row0(b, Tmax, Smax, S, ids, row0, lane, 64, dp, curr);
+    }
+    if (lane == 0) {
+        const float* er = edge_logits + b * e_bs;
+        auto edge_pred = [&](int tt) {
+            const float x = er[tt * e_ld];
+            const float sg = 1.0f / (1.0f + expf(-x));
+            return fminf(fmaxf((sg - 0.1f) / 0.8f, 0.0f), 1.0f);
+        };
+        const float e = edge_pred(t);
+        const float en = (t + 1 < T) ? edge_pred(t + 1) : 0.0f;
+        const float ep = (t > 0) ? edge_pred(t - 1) : 0.0f;
+        edge_diff[(size_t)b * Tmax + t] = (t + 1 < T) ? (en - e) : 0.0f;
+        double pr = (double)e + (double)ep;
+        pr = pr < 0.0 ? 0.0 : (pr > 1.0 ? 1.0 : pr);
+        if (edge_prob_out) edge_prob_out[(size_t)b * Tmax + t] = pr;
+        edge_log[(size_t)b * Tmax + t] = (float)log(pr + 1e-6);
+        not_edge_log[(size_t)b * Tmax + t] = (float)log(1.0 - pr + 1e-6);
+    }
+}
+
 __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
     int Tmax, int V, int Smax, const int32_t* __restrict__ Tv, const int32_t* __restrict__ Sv,
     const float* __restrict__ frame_logits, long long f_ld, long long f_bs, const float* __restrict__ edge_logits,
@@ -584,57 +641,15 @@ __global__ __launch_bounds__(kProThreads) void lattice_prologue_kernel(
     }
     __syncthreads();
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int t = blockIdx.x * (kProThreads / 64) + w;
-    if (t >= T) {
-        if (t == 0 && dp) dp_row0(b, Tmax, Smax, 0, ids, nullptr, lane, 64, dp, curr);   // T = 0: an all -inf row
-        return;
-    }
-    const float* xr = frame_logits + b * f_bs + t * f_ld;
-    float m = neg_inf();
-    for (int v = lane; v < V; v += 64) {
-        const float x = xr[v] - (allowed[v] ? 0.0f : 1e9f);
-        lsm[w][v] = x;
-        m = fmaxf(m, x);
-    }
-    m = hfa::wave_max(m);
-    float sum = 0.0f;
-    for (int v = lane; v < V; v += 64) sum += expf(lsm[w][v] - m);
-    sum = hfa::wave_sum(sum);
-    const float lse = logf(sum);
-    const float inv = 1.0f / sum;
-    for (int v = lane; v < V; v += 64) {
-        const float xm = lsm[w][v] - m;
-        const float lp = xm - lse;
-        if (ph_prob_log) ph_prob_log[((size_t)b * Tmax + t) * V + v] = lp;
-        if (ph_frame_pred) ph_frame_pred[((size_t)b * Tmax + t) * V + v] = expf(xm) * inv;
-        lsm[w][v] = lp;
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (int s = lane; s < S; s += 64) {
-        const int v = ids[s];
-        prob_log[((size_t)b * Tmax + t) * Smax + s] = lsm[w][v];
-    }
-    if (t == 0 && dp) {          // _decode's dp / curr initialisation from this frame's lattice row (no extra launch)
-        const float l0 = lsm[w][ids[0]], l1 = S > 1 ? lsm[w][ids[1]] : 0.0f;
-        const float row0[2] = {l0, l1};
-        dp_row0(b, Tmax, Smax, S, ids, row0, lane, 64, dp, curr);
-    }
-    if (lane == 0) {
-        const float* er = edge_logits + b * e_bs;
-        auto edge_pred = [&](int tt) {
-            const float x = er[tt * e_ld];
-            const float sg = 1.0f / (1.0f + expf(-x));
-            return fminf(fmaxf((sg - 0.1f) / 0.8f, 0.0f), 1.0f);
-        };
-        const float e = edge_pred(t);
-        const float en = (t + 1 < T) ? edge_pred(t + 1) : 0.0f;
-        const float ep = (t > 0) ? edge_pred(t - 1) : 0.0f;
-        edge_diff[(size_t)b * Tmax + t] = (t + 1 < T) ? (en - e) : 0.0f;
-        double pr = (double)e + (double)ep;
-        pr = pr < 0.0 ? 0.0 : (pr > 1.0 ? 1.0 : pr);
-        if (edge_prob_out) edge_prob_out[(size_t)b * Tmax + t] = pr;
-        edge_log[(size_t)b * Tmax + t] = (float)log(pr + 1e-6);
-        not_edge_log[(size_t)b * Tmax + t] = (float)log(1.0 - pr + 1e-6);
+    // frames t = blockIdx.x * 4 + w, + 4 gridDim.x, ... (a capped grid, hfa::grid_cap); a wave's lsm row is reused
+    const int tstride = gridDim.x * (kProThreads / 64);
+    const int tfirst = blockIdx.x * (kProThreads / 64) + w;
+    if (tfirst == 0 && T <= 0 && dp) dp_row0(b, Tmax, Smax, 0, ids, nullptr, lane, 64, dp, curr);   // T = 0: -inf row
+    for (int t = tfirst; t < T; t += tstride) {
+        lattice_frame(t, b, T, S, V, Tmax, Smax, ids, allowed, lsm[w], lane, frame_logits, f_ld, f_bs, edge_logits,
+                      e_ld, e_bs, ph_prob_log, ph_frame_pred, prob_log, edge_log, not_edge_log, edge_diff,
+                      edge_prob_out, dp, curr);
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -788,7 +803,9 @@ int hfa_lattice_prologue(int B, int Tmax, int V, int Smax, const int32_t* T, con
         hfa::set_error("hfa_lattice_prologue: null pointer (dp and curr go together)");
         return HFA_EINVAL;
     }
-    dim3 grid((Tmax + kProThreads / 64 - 1) / (kProThreads / 64), B);
+    const int tb = (Tmax + kProThreads / 64 - 1) / (kProThreads / 64);
+    const int gx = hfa::capped((long long)tb * B) / B;
+    dim3 grid(gx > 0 ? gx : 1, B);
     hipLaunchKernelGGL(lattice_prologue_kernel, grid, dim3(kProThreads), 0, stream, Tmax, V, Smax, T, S,
                        frame_logits, frame_ld, frame_bs, edge_logits, edge_ld, edge_bs, ph_seq_id, ph_prob_log,
                        ph_frame_pred, prob_log, edge_log, not_edge_log, edge_diff, edge_prob, dp, curr);

@@ -5,6 +5,7 @@ libhfa.so.  Inputs must already be on the GPU — there is no CPU path and no si
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import torch
@@ -590,6 +591,20 @@ def flag_take(flag: torch.Tensor) -> torch.Tensor:
     snap = torch.empty_like(flag)
     _lib.call("hfa_flag_take", flag.numel(), _ptr(flag), _ptr(snap), _stream(flag.device))
     return snap
+
+
+_lib.register("hfa_set_grid_cap", [_I_])
+
+
+@contextlib.contextmanager
+def grid_cap(wgs: int):
+    """Launches of the row-streaming kernels (split_f16, LayerNorm, lattice prologue) made by this thread inside the
+    block use at most ``wgs`` workgroups (hfa_set_grid_cap; results identical)."""
+    _lib.call("hfa_set_grid_cap", int(wgs))
+    try:
+        yield
+    finally:
+        _lib.call("hfa_set_grid_cap", 0)
 
 
 def add(a, b, out=None):

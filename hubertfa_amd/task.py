@@ -256,8 +256,9 @@ class ForcedAlignmentTask:
         with torch.cuda.stream(self._side):
             self._side.wait_event(ready)
             feats.record_stream(self._side)      # the caching allocator must not recycle it under the side stream
-            dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws,
-                                         dp_ranges=self.dp_ranges if chunk_seconds is None else None)
+            with ops.grid_cap(self.side_grid_cap):
+                dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws,
+                                             dp_ranges=self.dp_ranges if chunk_seconds is None else None)
             if "split_oflow" in guard:
                 guard["split_oflow"].record_stream(self._side)
             dev_out.update(guard)
@@ -267,6 +268,10 @@ class ForcedAlignmentTask:
             else:
                 work.complete()
             return work.handle
+
+    # workgroups at most per launch of the side pass's row-streaming kernels (ops.grid_cap; 0: uncapped): beside the
+    # next batch's encoder, their one-row workgroups cost the encoder more than their work
+    side_grid_cap = 512
 
     # a lattice of at least this many DP frames (config 5's 300 s: 25 839) runs its forward DP beside the next
     # batch's attention launches, one step range per encoder layer; None: never.  A range must fit in one

@@ -271,6 +271,12 @@ int hfa_selftest_gelu(long long n, const float* x, float* y, hipStream_t stream)
 /* Range-guard bookkeeping (no reference counterpart: the split-f16 arithmetic's per-batch overflow flags): snap[i] =
  * flags[i], then flags[i] = 0, for i < n, stream-ordered (the batch's snapshot travels with its outputs). */
 int hfa_flag_take(int n, int* flags, int* snap, hipStream_t stream);
+/* Workgroup cap (no reference counterpart; 0 = none, the default) for this host thread's later launches of the
+ * row-streaming kernels -- hfa_split_f16, hfa_layernorm_f32 / _split, hfa_lattice_prologue: a capped launch runs its
+ * rows in a grid-stride loop over at most `wgs` workgroups (results identical).  The pipelined step enqueues its side
+ * pass (UNet head + lattice, beside the next batch's encoder) under a cap: its tens of thousands of one-row
+ * workgroups otherwise cost the encoder more than their work. */
+int hfa_set_grid_cap(int wgs);
 /* out = a + b (UNet skip connection, networks/layer/backbone/unet.py:114). */
 int hfa_add_f32(long long n, const float* a, const float* b, float* out, hipStream_t stream);
 /* torchaudio.transforms.Resample (sinc_interp_hann) as pad + MFMA GEMM (tools/load_wav.py:7,

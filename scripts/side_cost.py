@@ -92,6 +92,7 @@ def mode_build(a):
 
 def mode_ab(a):
     torch, d, task, zt, wav, ph, ws, pw = setup(zero=True)
+    from hubertfa_amd import ops
     rep = json.load(open(a.replay))["sequence"]
     occ = ctypes.CDLL(OCC_LIB)
     occ.occ_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
@@ -106,6 +107,12 @@ def mode_ab(a):
     def real(f2):
         task.decoder.fetch(task.decode_device(f2, n_frames, wl, ph, ws, pw))
 
+    def real_cap(cap):
+        def run(f2):
+            with ops.grid_cap(cap):
+                task.decoder.fetch(task.decode_device(f2, n_frames, wl, ph, ws, pw))
+        return run
+
     def zero(_f2):
         zt.decoder.fetch(zt.decode_device(zfeats, n_frames, wl, ph, ws, pw))
 
@@ -116,6 +123,15 @@ def mode_ab(a):
             rc = occ.occ_launch(k["wgs"], k["block"], k["lds"], k["vgprs"], k["us"] * scale,
                                 slots[i:i + 1].data_ptr(), s)
             assert rc == 0, rc
+
+    def replay_cap(cap):
+        def run(_f2):
+            s = torch.cuda.current_stream().cuda_stream
+            slots.zero_()
+            for i, k in enumerate(rep):
+                occ.occ_launch(min(k["wgs"], cap), k["block"], k["lds"], k["vgprs"], k["us"],
+                               slots[i:i + 1].data_ptr(), s)
+        return run
 
     def replay_nolds(_f2):
         s = torch.cuda.current_stream().cuda_stream
@@ -148,10 +164,15 @@ def mode_ab(a):
             with torch.cuda.stream(side):
                 side_work(feats)
         return run
-    arms = {"E": lambda: task.encode_batch(wav, 16000), "E+S": piped(real), "E+Z": piped(zero),
+    arms = {"E": lambda: task.encode_batch(wav, 16000), "E+S": piped(real),
+            "E+S(cap 256)": piped(real_cap(256)), "E+S(cap 512)": piped(real_cap(512)),
+            "E+S(cap 1024)": piped(real_cap(1024)), "E+Z": piped(zero),
             "E+R": piped(replay), "E+R x1.5": piped(lambda f2: replay(f2, 1.5)),
             "E+R(no LDS, 64 VGPR)": piped(replay_nolds),
-            "S alone": alone(real), "Z alone": alone(zero), "R alone": alone(replay)}
+            "E+R(wgs<=1024)": piped(replay_cap(1024)), "E+R(wgs<=256)": piped(replay_cap(256)),
+            "S alone": alone(real), "S(cap 256) alone": alone(real_cap(256)), "S(cap 512) alone": alone(real_cap(512)),
+            "Z alone": alone(zero), "R alone": alone(replay),
+            "R(wgs<=256) alone": alone(replay_cap(256))}
     res = {k: [] for k in arms}
     for _ in range(a.rounds):
         for name, fn in arms.items():
@@ -159,7 +180,7 @@ def mode_ab(a):
     med = {k: statistics.median(v) for k, v in res.items()}
     e = med["E"]
     out = {"steps": a.steps, "rounds": a.rounds, "median_ms": med, "all_ms": res,
-           "cost_ms": {k: med[k] - e for k in ("E+S", "E+Z", "E+R", "E+R x1.5", "E+R(no LDS, 64 VGPR)")}}
+           "cost_ms": {k: med[k] - e for k in arms if k.startswith("E+")}}
     c = out["cost_ms"]
     out["share_of_side_cost"] = {"zero_operands (same work, no switching)": c["E+Z"] / c["E+S"] if c["E+S"] else None,
                                  "occupancy replay (no work)": c["E+R"] / c["E+S"] if c["E+S"] else None}

@@ -98,6 +98,7 @@ int main() {
                                    nullptr, st), "attention_split head_dim");
     CHECK(hfa_attention_split_tuning(3), "attention tuning waves=3");
     CHECK(hfa_attention_split_form(8), "attention form 8");
+    CHECK(hfa_set_grid_cap(-1), "grid cap -1");
     // norms
     CHECK(hfa_layernorm_f32(10, 6, fp, 8, nullptr, 0, fp, fp, 1e-5f, 0, fp, 8, 0, nullptr, st), "LN C%4");
     CHECK(hfa_layernorm_f32(10, 8, fmis, 8, nullptr, 0, fp, fp, 1e-5f, 0, fp, 8, 0, nullptr, st),

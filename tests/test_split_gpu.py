@@ -522,3 +522,47 @@ def test_attention_split_large_scores(form):
     e_split = float(((out[0].double() + out[1].double() / 2048.0).cpu() - ref).abs().max())
     e_f32 = float((o32.double().cpu() - ref).abs().max())
     assert e_split <= max(2.0 * e_f32, 2e-5), (e_split, e_f32)
+
+
+@pytest.mark.parametrize("cap", [1, 7, 256])
+def test_grid_cap_bit_identical(cap):
+    """hfa_set_grid_cap (ops.grid_cap): the row-streaming kernels in a grid-stride loop over at most `cap`
+    workgroups give the uncapped launches' outputs bit for bit -- split_f16 (and its range flag), LayerNorm at several
+    row widths with residual, activation, split planes and varlen padding rows, and the lattice prologue."""
+    from hubertfa_amd import ops
+    from hubertfa_amd.hubert import dev_lengths
+    d = torch.device("cuda")
+    g = torch.Generator().manual_seed(cap)
+
+    def both(fn):
+        a = fn()
+        with ops.grid_cap(cap):
+            b = fn()
+        torch.cuda.synchronize()
+        return a, b
+    x = torch.randn(3000, 768, generator=g).to(d)
+    x[17, 5] = 70000.0                                          # out of f16 range: raises the flag
+    for xa in (x, x[:, :700]):
+        (pa, fa), (pb, fb) = both(lambda: (lambda f: (ops.split(xa, flag=f), f))(torch.zeros(1, dtype=torch.int32,
+                                                                                             device=d)))
+        assert torch.equal(pa, pb) and int(fa.item()) == int(fb.item()) == 1
+    for C in (192, 384, 768, 1024):
+        xb = torch.randn(4, 300, C, generator=g).to(d)
+        res = torch.randn(4, 300, C, generator=g).to(d)
+        gam, bet = torch.randn(C, generator=g).to(d), torch.randn(C, generator=g).to(d)
+        tl = dev_lengths([300, 211, 5, 160], d)
+        (oa, sa), (ob, sb) = both(lambda: ops.layernorm(xb, gam, bet, act=ops.ACT_GELU, residual=res, t_len=tl,
+                                                        out_split=True))
+        assert torch.equal(oa, ob) and torch.equal(sa, sb), C
+    B, Tl, V, Smax = 5, 861, 65, 96
+    fl = torch.randn(B, Tl, V, generator=g).to(d)
+    el = torch.randn(B, Tl, generator=g).to(d)
+    ids = torch.randint(0, V, (B, Smax), generator=g, dtype=torch.int32).to(d)
+    Tv = torch.tensor([861, 430, 1, 0, 700], dtype=torch.int32, device=d)
+    Sv = torch.tensor([91, 46, 3, 2, 96], dtype=torch.int32, device=d)
+    la, lb = both(lambda: ops.lattice_prologue(fl, el, ids, Tv, Sv, want_frame_probs=True, init_dp=True))
+    for b, (T, S) in enumerate(zip(Tv.tolist(), Sv.tolist())):      # what the prologue writes (the rest is empty())
+        for k in ("edge_log", "not_edge_log", "edge_diff", "edge_prob", "ph_prob_log", "ph_frame_pred"):
+            assert torch.equal(la[k][b, :T], lb[k][b, :T]), (k, b)
+        assert torch.equal(la["prob_log"][b, :T, :S], lb["prob_log"][b, :T, :S]), b
+        assert torch.equal(la["dp"][b, 0], lb["dp"][b, 0]) and torch.equal(la["curr"][b], lb["curr"][b]), b
