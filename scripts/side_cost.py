@@ -124,12 +124,17 @@ def mode_ab(a):
                                 slots[i:i + 1].data_ptr(), s)
             assert rc == 0, rc
 
-    def replay_cap(cap):
+    def replay_cap(cap, gemm_cap=None):
+        """every kernel's grid capped at `cap` workgroups; `gemm_cap`: the GEMM and GroupNorm kernels' at that
+        instead (what a persistent UNet GEMM / capped GroupNorm would hold)"""
         def run(_f2):
             s = torch.cuda.current_stream().cuda_stream
             slots.zero_()
             for i, k in enumerate(rep):
-                occ.occ_launch(min(k["wgs"], cap), k["block"], k["lds"], k["vgprs"], k["us"],
+                c = cap
+                if gemm_cap is not None and ("gemm_split" in k["name"] or "gn_rows" in k["name"]):
+                    c = gemm_cap
+                occ.occ_launch(min(k["wgs"], c), k["block"], k["lds"], k["vgprs"], k["us"],
                                slots[i:i + 1].data_ptr(), s)
         return run
 
@@ -166,10 +171,14 @@ def mode_ab(a):
         return run
     arms = {"E": lambda: task.encode_batch(wav, 16000), "E+S": piped(real),
             "E+S(cap 256)": piped(real_cap(256)), "E+S(cap 512)": piped(real_cap(512)),
-            "E+S(cap 1024)": piped(real_cap(1024)), "E+Z": piped(zero),
+            "E+S(cap 1024)": piped(real_cap(1024)),
+            "E+Z": piped(zero),
             "E+R": piped(replay), "E+R x1.5": piped(lambda f2: replay(f2, 1.5)),
             "E+R(no LDS, 64 VGPR)": piped(replay_nolds),
             "E+R(wgs<=1024)": piped(replay_cap(1024)), "E+R(wgs<=256)": piped(replay_cap(256)),
+            "E+R(rows<=512)": piped(replay_cap(512, 10 ** 9)),
+            "E+R(rows<=512, gemm/gn<=256)": piped(replay_cap(512, 256)),
+            "E+R(rows<=512, gemm/gn<=128)": piped(replay_cap(512, 128)),
             "S alone": alone(real), "S(cap 256) alone": alone(real_cap(256)), "S(cap 512) alone": alone(real_cap(512)),
             "Z alone": alone(zero), "R alone": alone(replay),
             "R(wgs<=256) alone": alone(replay_cap(256))}

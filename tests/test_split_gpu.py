@@ -528,7 +528,8 @@ def test_attention_split_large_scores(form):
 def test_grid_cap_bit_identical(cap):
     """hfa_set_grid_cap (ops.grid_cap): the row-streaming kernels in a grid-stride loop over at most `cap`
     workgroups give the uncapped launches' outputs bit for bit -- split_f16 (and its range flag), LayerNorm at several
-    row widths with residual, activation, split planes and varlen padding rows, and the lattice prologue."""
+    row widths with residual, activation, split planes and varlen padding rows, and the lattice prologue; and the
+    whole UNet head (its LayerNorms and conversions capped) on a variable-length batch."""
     from hubertfa_amd import ops
     from hubertfa_amd.hubert import dev_lengths
     d = torch.device("cuda")
@@ -560,6 +561,15 @@ def test_grid_cap_bit_identical(cap):
     ids = torch.randint(0, V, (B, Smax), generator=g, dtype=torch.int32).to(d)
     Tv = torch.tensor([861, 430, 1, 0, 700], dtype=torch.int32, device=d)
     Sv = torch.tensor([91, 46, 3, 2, 96], dtype=torch.int32, device=d)
+    from hubertfa_amd import synth
+    from hubertfa_amd.unet import LatticeHead
+    ua = synth.UNetArch(input_dims=768, vocab_size=63)
+    sd = {k: torch.from_numpy(v) for k, v in synth.synth_unet_state_dict(ua, seed=3).items()}
+    head = LatticeHead(ua, sd, d)
+    feats = torch.randn(6, 864, 768, generator=g).to(d)
+    for t_pad in (None, [864, 432, 96, 864, 800, 8]):
+        ha, hb = both(lambda: head.logits(feats, t_pad) if t_pad else head.logits(feats))
+        assert torch.equal(ha, hb), t_pad
     la, lb = both(lambda: ops.lattice_prologue(fl, el, ids, Tv, Sv, want_frame_probs=True, init_dp=True))
     for b, (T, S) in enumerate(zip(Tv.tolist(), Sv.tolist())):      # what the prologue writes (the rest is empty())
         for k in ("edge_log", "not_edge_log", "edge_diff", "edge_prob", "ph_prob_log", "ph_frame_pred"):
