@@ -848,9 +848,12 @@ __device__ __forceinline__ void store_f32_lds(const GemmP& p, const typename Acc
 // stall on DMA issue while the matrix pipe idles.
 // F16 (opt-in fast mode, MF 16 tiles only): the operands' high planes alone, one product a1 w1 per MAC -- f16-class
 // accuracy (inputs rounded to 11 significand bits, f32 accumulation); the low planes are neither fetched nor read.
+// One output tile of gemm_split_kernel (wgid: the tile, z: the launch's blockIdx.z); smem: the kernel's NS * STAGE
+// halves of LDS.  (A function of its own since round 6: the same arithmetic, and 2 % off FFN2's 192 x 256 tile in
+// the layer microbenchmark, profiles/r06/gemm_tile_fn_ab.txt.)
 template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT, bool GT, bool ONE, int BK,
-          int MF = 32, bool F16 = false>
-__global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const GemmP p) {
+          int MF, bool F16>
+__device__ __forceinline__ void gemm_split_tile(const GemmP p, int wgid, int z, _Float16* smem) {
     static_assert(MF == 16 && ONE && BK == 32, "the built tiles: 16x16x32 MFMA, single accumulator, BK 32");
     static_assert(!F16 || (MF == 16 && NS == 2 && !GT), "the one-product mode runs on the 2-stage 16x16x32 tiles");
     constexpr int CPR = BK / 8, NW = WM * WN;                // 16-B chunks per row per plane
@@ -860,13 +863,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
     static_assert(NS == 2 || (IA % NW == 0 && IW % NW == 0), "counted vmcnt waits need even DMA shares");
     constexpr int PA = BM * BK, PW = BN * BK;                 // halves per plane image
     constexpr int STAGE = 2 * PA + 2 * PW;                    // halves per stage: A1, A2, W1, W2
-    __shared__ __attribute__((aligned(16))) _Float16 smem[NS * STAGE];
 
-    const int nwg = gridDim.x, orig = blockIdx.x;
-    const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
-    const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
     const int tm = wgid / p.n_tiles, tn = wgid - tm * p.n_tiles;
-    const int zb = blockIdx.z / p.G, zg = blockIdx.z - zb * p.G;
+    const int zb = z / p.G, zg = z - zb * p.G;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -1076,6 +1075,17 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const Gem
             store_f32_lds<16, EPI, TI, TJ>(p, acc, zb, zg, tm * BM + wm * (BM / WM), tn * BN + wn * (BN / WN), lane,
                                            slab, true, kScale);
     }
+}
+
+template <int EPI, int BM, int BN, int WM, int WN, int NS, int OCC, bool OUT_SPLIT, bool GT, bool ONE, int BK,
+          int MF = 32, bool F16 = false>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_split_kernel(const GemmP p) {
+    __shared__ __attribute__((aligned(16))) _Float16 smem[NS * (2 * BM * BK + 2 * BN * BK)];
+    // XCD-aware bijective remap: consecutive tile ids (the column tiles of one row panel) share an XCD's L2
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+    gemm_split_tile<EPI, BM, BN, WM, WN, NS, OCC, OUT_SPLIT, GT, ONE, BK, MF, F16>(p, wgid, blockIdx.z, smem);
 }
 
 // f32 -> (hi, lo * 2^11) f16 planes, row-wise with 4-element vectors where aligned; raises *oflow for |x| >= 65504

@@ -50,10 +50,13 @@ __device__ __forceinline__ unsigned lds_addr(const void* ptr) {
 }
 
 __device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned soff, unsigned lds) {
-    unsigned keep;   // M0 is compiler-reserved: set and restore it inside the statement that uses it
+    // M0 is compiler-reserved: set and restore it inside the statement that uses it.  soff / lds are wave-uniform;
+    // readfirstlane states it where the divergence analysis cannot prove it
+    unsigned keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
                  "s_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds) : "memory");
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(soff)),
+                   "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
 }
 
 template <int N>
