@@ -86,9 +86,13 @@ def parse():
     ap.add_argument("--host-input", action="store_true",
                     help="waves start in host memory and are uploaded inside every step (task.upload, as infer.py) (PCIe-inclusive "
                          "rate; the headline value keeps inputs resident in HBM)")
-    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r05", "traffic_r05.json"),
+    ap.add_argument("--probe-every", type=int, default=1,
+                    help="time the dominant kernel's launches (HIP events) in every N-th timed step only")
+    ap.add_argument("--probe-secondary", action="store_true",
+                    help="also time the secondary kernels inside the timed region (else in an untimed pipelined pass)")
+    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "r06", "traffic_r06.json"),
                     help="PMC-derived HBM bytes per launch of the probed kernel (written by scripts/pmc_traffic.py)")
-    ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "r05", "pmc_r05.json"),
+    ap.add_argument("--pmc-file", default=os.path.join(REPO, "profiles", "r06", "pmc_r06.json"),
                     help="PMC-derived MFMA busy and clock per kernel (written by scripts/pmc_kernels.py)")
     return ap.parse_args()
 
@@ -604,13 +608,13 @@ def main():
             res = finish(pending.pop(0), inp, tk)
         return res
 
-    def timed(k, inp=inputs, tk=task):
+    def timed(k, inp=inputs, tk=task, on_step=None):
         """exactly k steps between barrier + synchronize pairs -> (results, max seconds over ranks)."""
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        r = run(k, inp, tk)
+        r = run(k, inp, tk, on_step=on_step)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -629,12 +633,32 @@ def main():
     ops.PROBE = None
     torch.cuda.synchronize()
     probe_name = census.dominant() if args.probe == "auto" else args.probe
-    probe = ops.KernelProbe(probe_name, extra=SECONDARY)
+    # the dominant kernel is timed live in the timed steps (every --probe-every-th step); each timed launch adds two
+    # event records to the stream, so the secondary kernels are timed in a separate untimed pipelined pass below
+    probe = ops.KernelProbe(probe_name, extra=SECONDARY if args.probe_secondary else ())
     ops.PROBE = probe
     thr0 = thread_cpu()
-    res, el = timed(args.steps)
+    step_i = [0]
+
+    step_ev = []                      # one event per timed step at its start (the launching stream)
+
+    def sample_step():
+        probe.active = step_i[0] % max(args.probe_every, 1) == 0
+        step_i[0] += 1
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        step_ev.append(ev)
+    res, el = timed(args.steps, on_step=sample_step)
     thr1 = thread_cpu()
     ops.PROBE = None
+    probe.active = True
+    pipe = probe
+    if not args.probe_secondary:       # the secondary kernels' in-pipeline durations: the same loop, untimed
+        pipe = ops.KernelProbe("-", extra=SECONDARY)
+        ops.PROBE = pipe
+        run(min(args.steps, 5))
+        torch.cuda.synchronize()
+        ops.PROBE = None
 
     devices = device_census(dev, world)
     n_frames = res[0]["T"]
@@ -695,6 +719,7 @@ def main():
                                     "MAC, 2516.6 TF f16 dense / 3" if probe_name.startswith("gemm_split_kernel")
                                     else "f32 MFMA dense peak"),
                      "traffic": traffic, "launches": ps["launches"], "avg_launch_ms": ps["avg_ms"],
+                     "timed_steps_probed": len(range(0, args.steps, max(args.probe_every, 1))),
                      "flops_per_launch": ps["avg_flops"],
                      "mfma_busy": pmc.get("mfma_busy") if pmc else None,
                      "clock_ghz": pmc.get("clock_ghz") if pmc else None,
@@ -707,6 +732,16 @@ def main():
         rd = RANDOM_DATA_F16_TFLOPS / (1 if probe_name.endswith(", true>") else 3)
         out["roofline"]["random_data_mfma_rate"] = rd
         out["roofline"]["frac_of_random_data_rate"] = achieved / rd
+    if len(step_ev) > 2:
+        # where the timed region's time goes: step-start to step-start intervals on the device, and what the wall clock
+        # holds beyond them (the drain: the last batch's side pass + assembly after the last step's start)
+        iv = [step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(len(step_ev) - 1)]
+        srt = sorted(iv)
+        out["timed_step_profile"] = {
+            "first_interval_ms": iv[0], "median_interval_ms": srt[len(srt) // 2], "max_interval_ms": srt[-1],
+            "sum_intervals_ms": sum(iv), "wall_ms": el * 1e3, "wall_minus_intervals_ms": el * 1e3 - sum(iv),
+            "note": "device time between consecutive timed steps' starts; wall_minus_intervals = the last step, its "
+                    "drain and the host work around the timed region"}
     if world == 1 and args.sustained_s > 0 and args.chunk_seconds is None:
         n0 = len(host_t)
         out["sustained"] = sustained(run, args.sustained_s, B * args.seconds, out["ms_per_step"])
@@ -783,7 +818,7 @@ def main():
                                                chunk_seconds=args.chunk_seconds), ph_seqs, word_seqs, p2ws)
     torch.cuda.synchronize()
     ops.PROBE = None
-    out["secondary"] = secondary_rooflines(iso, probe, n_frames, len(ph_seqs[0]))
+    out["secondary"] = secondary_rooflines(iso, pipe, n_frames, len(ph_seqs[0]))
     ht = host_t[max(args.warmup, 1):max(args.warmup, 1) + args.steps]      # the timed steps
     avg = lambda i: 1e3 * sum(h[i] for h in ht) / max(len(ht), 1)  # noqa: E731
     out["host_cpu"] = {

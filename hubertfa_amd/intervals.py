@@ -10,12 +10,49 @@ import numpy as np
 
 
 def assemble_intervals(ph_idx_seq, ph_time_int, edge_diff, T, frame_length, ph_seq, word_seq, ph_idx_to_word_idx):
-    """Fractional boundaries and word grouping (alignment_decoder.py:103-138), numpy f64 as the reference."""
+    """Fractional boundaries and word grouping (alignment_decoder.py:103-138), numpy f64 as the reference.
+
+    The phone / word loop of the reference runs as array operations (the host assembles every batch of the pipelined
+    step while the GPU runs the next one, and the last batch's assembly is exposed): SP phones dropped by a mask, a
+    word opened wherever the word index changes between kept phones, closed at its last phone.  The loop form
+    (assemble_intervals_loop, the reference's statement order) is the fallback where the two could differ: a kept
+    phone without a word (index -1, where the reference's first merge would index an empty list)."""
     ph_time_int = np.asarray(ph_time_int)
     edge_diff = np.asarray(edge_diff, dtype=np.float64)
     ph_time_fractional = (edge_diff[ph_time_int] / 2).clip(-0.5, 0.5)
     ph_time_pred = frame_length * np.concatenate([ph_time_int.astype("float32") + ph_time_fractional, [T]])
     ph_intervals = np.stack([ph_time_pred[:-1], ph_time_pred[1:]], axis=1)
+    idx = np.asarray(ph_idx_seq, dtype=np.int64)
+    keep = np.fromiter((ph_seq[i] != "SP" for i in idx.tolist()), dtype=bool, count=len(idx))
+    sel = np.flatnonzero(keep)
+    if len(sel) == 0:
+        return np.array([]), np.array([]), np.array([]), np.array([])
+    kept = idx[sel].tolist()
+    p2w = ph_idx_to_word_idx
+    w = np.fromiter((p2w[i] for i in kept), dtype=np.int64, count=len(kept))
+    if (w < 0).any():
+        return _assemble_loop(ph_intervals, ph_idx_seq, ph_seq, word_seq, ph_idx_to_word_idx)
+    ph_iv = ph_intervals[sel]
+    first = np.flatnonzero(np.concatenate([[True], w[1:] != w[:-1]]))
+    last = np.concatenate([first[1:] - 1, [len(w) - 1]])
+    word_iv = np.stack([ph_iv[first, 0], ph_iv[last, 1]], axis=1)
+    return (np.array([ph_seq[i] for i in kept]), ph_iv.clip(min=0, max=None),
+            np.array([word_seq[k] for k in w[first].tolist()]), word_iv.clip(min=0, max=None))
+
+
+def assemble_intervals_loop(ph_idx_seq, ph_time_int, edge_diff, T, frame_length, ph_seq, word_seq,
+                            ph_idx_to_word_idx):
+    """assemble_intervals in the reference's own statement order (alignment_decoder.py:103-138): the fallback and the
+    check (tests/test_host.py) of the array form."""
+    ph_time_int = np.asarray(ph_time_int)
+    edge_diff = np.asarray(edge_diff, dtype=np.float64)
+    ph_time_fractional = (edge_diff[ph_time_int] / 2).clip(-0.5, 0.5)
+    ph_time_pred = frame_length * np.concatenate([ph_time_int.astype("float32") + ph_time_fractional, [T]])
+    ph_intervals = np.stack([ph_time_pred[:-1], ph_time_pred[1:]], axis=1)
+    return _assemble_loop(ph_intervals, ph_idx_seq, ph_seq, word_seq, ph_idx_to_word_idx)
+
+
+def _assemble_loop(ph_intervals, ph_idx_seq, ph_seq, word_seq, ph_idx_to_word_idx):
     ph_seq_pred, ph_intervals_pred, word_seq_pred, word_intervals_pred = [], [], [], []
     word_idx_last = -1
     for i, ph_idx in enumerate(ph_idx_seq):

@@ -213,6 +213,7 @@ class KernelProbe:
         self.watch = set(extra) | ({name} if name else set())
         self.records = {}
         self.census = {}
+        self.active = True           # False: launches pass through untimed (bench.py samples the timed steps)
 
     def dominant(self) -> str:
         return max(self.census, key=self.census.get)
@@ -222,7 +223,7 @@ class KernelProbe:
             if kind == "flops":
                 self.census[name] = self.census.get(name, 0.0) + work
             return launch()
-        if name not in self.watch:
+        if name not in self.watch or not self.active:
             return launch()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()

@@ -655,3 +655,35 @@ def test_held_dp_failure_reraised_on_retry_and_prompt_under_distributed(monkeypa
     h = _HeldDP(tk, {"deferred": [bad]}, None)
     h._next()
     assert h.error is not None
+
+
+def test_interval_assembly_array_form_matches_loop():
+    """intervals.assemble_intervals (array form) against the reference-order loop (assemble_intervals_loop,
+    alignment_decoder.py:103-138) on random paths: SP-heavy and SP-free sequences, repeated word indices, a single
+    phone, an all-SP path, an empty path, AP-like id-0 phones inside words; values and dtypes equal."""
+    from hubertfa_amd.intervals import assemble_intervals, assemble_intervals_loop
+    rng = np.random.default_rng(5)
+    phones = ["a", "b", "cc", "ddd", "SP", "AP", "e"]
+    for case in range(300):
+        S = int(rng.integers(1, 60))
+        ph_seq = [phones[int(k)] for k in rng.integers(0, len(phones), S)]
+        if case % 7 == 0:
+            ph_seq = ["SP"] * S
+        words, p2w, w = [], [], -1
+        for p in ph_seq:
+            if p == "SP":
+                p2w.append(-1)
+                continue
+            if w < 0 or rng.random() < 0.5:
+                w += 1
+                words.append(f"w{w}")
+            p2w.append(w if rng.random() > 0.1 or w == 0 else w - 1)      # sometimes back to an earlier word
+        T = int(rng.integers(max(S, 1), 300))
+        n = int(rng.integers(0, S + 1)) if case % 11 else 0
+        idx = np.sort(rng.choice(S, n, replace=False))
+        tint = np.sort(rng.choice(T, n, replace=False))
+        ed = rng.standard_normal(T)
+        a = assemble_intervals(idx, tint, ed, T, 512 / 44100, ph_seq, words, p2w)
+        b = assemble_intervals_loop(idx, tint, ed, T, 512 / 44100, ph_seq, words, p2w)
+        for x, y in zip(a, b):
+            assert x.dtype == y.dtype and x.shape == y.shape and np.array_equal(x, y), case
