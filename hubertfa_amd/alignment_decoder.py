@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from .intervals import assemble_intervals, total_confidence, utterance_result  # noqa: F401 (public names)
+from .intervals import assemble_intervals, batch_results, total_confidence, utterance_result  # noqa: F401 (public names)
 
 
 def _device(t: torch.Tensor) -> torch.device:
@@ -179,20 +179,19 @@ class AlignmentDecoder:
         idx_h, tint_h, n_h, fc_h, ed_h = (hd[k] for k in self._FETCH_KEYS)
         ep_h = hd.get("edge_prob") if keep_frame_probs else None
         fp_h = hd.get("ph_frame_pred") if keep_frame_probs else None
-        out = []
-        for b in range(len(ph_seqs)):
-            T = Ts[b]
-            ph_seq = ph_seqs[b]
-            ws = word_seqs[b] if word_seqs is not None and word_seqs[b] is not None else ph_seq
-            pw = p2ws[b] if p2ws is not None and p2ws[b] is not None else np.arange(len(ph_seq))
-            k = int(n_h[b])
-            rec = dict(T=T, ph_idx_seq=idx_h[b, :k].astype(np.int64), ph_time_int=tint_h[b, :k].astype(np.int64),
-                       frame_confidence=fc_h[b, :T].copy(), edge_diff=ed_h[b, :T].copy())
-            r = utterance_result(rec, ph_seq, ws, pw, self.frame_length) if intervals else rec
-            if keep_frame_probs:
-                r["edge_prob"] = ep_h[b, :T].copy()
-                r["ph_frame_pred"] = fp_h[b, :T].copy()
-            out.append(r)
+        if intervals:        # the batch's fractional boundaries in one set of array operations (intervals.py)
+            out = batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, self.frame_length)
+        else:
+            out = []
+            for b in range(len(ph_seqs)):
+                T, k = Ts[b], int(n_h[b])
+                out.append(dict(T=T, ph_idx_seq=idx_h[b, :k].astype(np.int64),
+                                ph_time_int=tint_h[b, :k].astype(np.int64), frame_confidence=fc_h[b, :T].copy(),
+                                edge_diff=ed_h[b, :T].copy()))
+        if keep_frame_probs:
+            for b, r in enumerate(out):
+                r["edge_prob"] = ep_h[b, :Ts[b]].copy()
+                r["ph_frame_pred"] = fp_h[b, :Ts[b]].copy()
         return out
 
     # -- reference static/numpy API on the GPU --------------------------------------------------------------

@@ -22,22 +22,7 @@ def assemble_intervals(ph_idx_seq, ph_time_int, edge_diff, T, frame_length, ph_s
     ph_time_fractional = (edge_diff[ph_time_int] / 2).clip(-0.5, 0.5)
     ph_time_pred = frame_length * np.concatenate([ph_time_int.astype("float32") + ph_time_fractional, [T]])
     ph_intervals = np.stack([ph_time_pred[:-1], ph_time_pred[1:]], axis=1)
-    idx = np.asarray(ph_idx_seq, dtype=np.int64)
-    keep = np.fromiter((ph_seq[i] != "SP" for i in idx.tolist()), dtype=bool, count=len(idx))
-    sel = np.flatnonzero(keep)
-    if len(sel) == 0:
-        return np.array([]), np.array([]), np.array([]), np.array([])
-    kept = idx[sel].tolist()
-    p2w = ph_idx_to_word_idx
-    w = np.fromiter((p2w[i] for i in kept), dtype=np.int64, count=len(kept))
-    if (w < 0).any():
-        return _assemble_loop(ph_intervals, ph_idx_seq, ph_seq, word_seq, ph_idx_to_word_idx)
-    ph_iv = ph_intervals[sel]
-    first = np.flatnonzero(np.concatenate([[True], w[1:] != w[:-1]]))
-    last = np.concatenate([first[1:] - 1, [len(w) - 1]])
-    word_iv = np.stack([ph_iv[first, 0], ph_iv[last, 1]], axis=1)
-    return (np.array([ph_seq[i] for i in kept]), ph_iv.clip(min=0, max=None),
-            np.array([word_seq[k] for k in w[first].tolist()]), word_iv.clip(min=0, max=None))
+    return _phones_words(ph_intervals, np.asarray(ph_idx_seq, dtype=np.int64), ph_seq, word_seq, ph_idx_to_word_idx)
 
 
 def assemble_intervals_loop(ph_idx_seq, ph_time_int, edge_diff, T, frame_length, ph_seq, word_seq,
@@ -69,6 +54,56 @@ def _assemble_loop(ph_intervals, ph_idx_seq, ph_seq, word_seq, ph_idx_to_word_id
             word_idx_last = word_idx
     return (np.array(ph_seq_pred), np.array(ph_intervals_pred).clip(min=0, max=None), np.array(word_seq_pred),
             np.array(word_intervals_pred).clip(min=0, max=None))
+
+
+def _phones_words(ph_intervals, idx, ph_seq, word_seq, ph_idx_to_word_idx):
+    """assemble_intervals' phone / word selection from the [n, 2] phone intervals (array form; loop fallback)."""
+    keep = np.fromiter((ph_seq[i] != "SP" for i in idx.tolist()), dtype=bool, count=len(idx))
+    sel = np.flatnonzero(keep)
+    if len(sel) == 0:
+        return np.array([]), np.array([]), np.array([]), np.array([])
+    kept = idx[sel].tolist()
+    w = np.fromiter((ph_idx_to_word_idx[i] for i in kept), dtype=np.int64, count=len(kept))
+    if (w < 0).any():
+        return _assemble_loop(ph_intervals, idx, ph_seq, word_seq, ph_idx_to_word_idx)
+    ph_iv = ph_intervals[sel]
+    first = np.flatnonzero(np.concatenate([[True], w[1:] != w[:-1]]))
+    last = np.concatenate([first[1:] - 1, [len(w) - 1]])
+    word_iv = np.stack([ph_iv[first, 0], ph_iv[last, 1]], axis=1)
+    return (np.array([ph_seq[i] for i in kept]), ph_iv.clip(min=0, max=None),
+            np.array([word_seq[k] for k in w[first].tolist()]), word_iv.clip(min=0, max=None))
+
+
+def batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, frame_length: float) -> list:
+    """utterance_result for a whole batch of raw boundary arrays as they leave the GPU (idx / tint [B, >= n], n [B],
+    frame_confidence / edge_diff [B, >= T] f32): the fractional boundaries of every utterance in one set of array
+    operations (elementwise, so each value is the per-utterance form's, bit for bit), the phone / word selection and
+    the confidence per utterance.  Returns the records utterance_result returns."""
+    B = len(ph_seqs)
+    T = np.asarray(list(Ts[:B]), dtype=np.int64)
+    n = np.asarray(n_h[:B], dtype=np.int64)
+    cols = np.arange(idx_h.shape[1])[None, :]
+    valid = cols < n[:, None]
+    tint = np.where(valid, tint_h[:B], 0).astype(np.int64)
+    ed = np.take_along_axis(ed_h[:B], tint, axis=1).astype(np.float64)
+    ed = np.where(tint == (T - 1)[:, None], 0.0, ed)          # edge_diff's last frame is 0 (alignment_decoder.py:83)
+    body = frame_length * (tint.astype("float32") + (ed / 2).clip(-0.5, 0.5))
+    ends = frame_length * T.astype(np.float64)
+    out = []
+    for b in range(B):
+        k, Tb = int(n[b]), int(T[b])
+        ph_seq = ph_seqs[b]
+        ws = word_seqs[b] if word_seqs is not None and word_seqs[b] is not None else ph_seq
+        pw = p2ws[b] if p2ws is not None and p2ws[b] is not None else np.arange(len(ph_seq))
+        tp = np.concatenate([body[b, :k], ends[b:b + 1]])
+        iv = np.stack([tp[:-1], tp[1:]], axis=1)
+        idx = idx_h[b, :k].astype(np.int64)
+        rec = dict(T=Ts[b], ph_idx_seq=idx, ph_time_int=tint_h[b, :k].astype(np.int64),
+                   frame_confidence=fc_h[b, :Tb].copy(), edge_diff=ed_h[b, :Tb].copy())
+        ph_p, ph_iv, w_p, w_iv = _phones_words(iv, idx, ph_seq, ws, pw)
+        out.append(dict(rec, ph_seq=ph_p, ph_intervals=ph_iv, word_seq=w_p, word_intervals=w_iv,
+                        confidence=total_confidence(rec["frame_confidence"])))
+    return out
 
 
 def total_confidence(frame_confidence: np.ndarray):

@@ -687,3 +687,57 @@ def test_interval_assembly_array_form_matches_loop():
         b = assemble_intervals_loop(idx, tint, ed, T, 512 / 44100, ph_seq, words, p2w)
         for x, y in zip(a, b):
             assert x.dtype == y.dtype and x.shape == y.shape and np.array_equal(x, y), case
+
+
+def test_batch_results_match_per_utterance():
+    """intervals.batch_results (decoder.assemble's batched host assembly) gives every utterance exactly what
+    utterance_result gives it from its own raw record: ragged n and T, a path ending on the last frame (its edge_diff
+    entry replaced by 0), garbage past n and T in the padded buffers, default word sequences."""
+    from hubertfa_amd.intervals import batch_results, utterance_result
+    rng = np.random.default_rng(9)
+    phones = ["SP", "a", "b", "AP", "cc"]
+    for trial in range(20):
+        B = int(rng.integers(1, 9))
+        Tmax, maxn = 300, 120
+        Ts = [int(rng.integers(1, Tmax + 1)) for _ in range(B)]
+        ph_seqs, word_seqs, p2ws, recs = [], [], [], []
+        idx_h = rng.integers(-5, 99, (B, maxn)).astype(np.int32)          # garbage beyond n
+        tint_h = rng.integers(-9, 10 ** 6, (B, maxn)).astype(np.int32)
+        fc_h = rng.random((B, Tmax)).astype(np.float32)
+        ed_h = rng.standard_normal((B, Tmax)).astype(np.float32)
+        n_h = np.zeros(B, np.int32)
+        for b in range(B):
+            S = int(rng.integers(1, 40))
+            ph = ["SP"] + [phones[int(k)] for k in rng.integers(0, len(phones), S)]
+            words, p2w, w = [], [], -1
+            for p in ph:
+                if p == "SP":
+                    p2w.append(-1)
+                    continue
+                if w < 0 or rng.random() < 0.6:
+                    w += 1
+                    words.append(f"w{w}")
+                p2w.append(w)
+            n = int(rng.integers(0, min(len(ph), Ts[b]) + 1))
+            n_h[b] = n
+            idx_h[b, :n] = np.sort(rng.choice(len(ph), n, replace=False))
+            t = np.sort(rng.choice(Ts[b], n, replace=False))
+            if n and trial % 2:
+                t[-1] = Ts[b] - 1
+            tint_h[b, :n] = t
+            default = trial % 5 == 0
+            ph_seqs.append(ph)
+            word_seqs.append(None if default else words)
+            p2ws.append(None if default else p2w)
+        got = batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, 512 / 44100)
+        for b in range(B):
+            k, T = int(n_h[b]), Ts[b]
+            rec = dict(T=T, ph_idx_seq=idx_h[b, :k].astype(np.int64), ph_time_int=tint_h[b, :k].astype(np.int64),
+                       frame_confidence=fc_h[b, :T].copy(), edge_diff=ed_h[b, :T].copy())
+            ws = word_seqs[b] if word_seqs[b] is not None else ph_seqs[b]
+            pw = p2ws[b] if p2ws[b] is not None else np.arange(len(ph_seqs[b]))
+            ref = utterance_result(rec, ph_seqs[b], ws, pw, 512 / 44100)
+            assert got[b].keys() == ref.keys()
+            for key in ref:
+                x, y = np.asarray(got[b][key]), np.asarray(ref[key])
+                assert x.dtype == y.dtype and x.shape == y.shape and np.array_equal(x, y), (trial, b, key)
