@@ -241,6 +241,16 @@ class AlignmentDecoder:
         return (idx[0, :k].cpu().numpy().astype(np.int64), tint[0, :k].cpu().numpy().astype(np.int64),
                 fc[0].cpu().numpy())
 
+    def plot(self, melspec):
+        """Validation figure of the last decode() (alignment_decoder.py:152-168; hubertfa_amd/plot.py): ``melspec``
+        [1, n_mels, T] (a torch tensor, as MelSpecExtractor returns it); returns the matplotlib figure."""
+        from .plot import phone_index_per_frame, plot_for_valid
+        ph_intervals_int = (self.ph_intervals_pred / self.frame_length).round().astype("int32")
+        ph_idx_frame = phone_index_per_frame(self.ph_idx_seq, self.ph_time_int_pred, self.ph_frame_pred.shape[0])
+        mel = melspec.cpu().numpy() if isinstance(melspec, torch.Tensor) else np.asarray(melspec)
+        return plot_for_valid(mel, self.ph_pred_seq, ph_intervals_int, self.frame_confidence,
+                              self.ph_frame_pred[:, self.ph_seq_id], ph_idx_frame, self.edge_prob)
+
     def ctc(self):
         """Greedy CTC collapse (alignment_decoder.py:145-150); validation-only helper, host numpy."""
         ctc = np.argmax(self.ctc_logits, axis=-1)

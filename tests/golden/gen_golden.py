@@ -13,6 +13,7 @@ Reference call sites exercised:
   * tools/alignment_decoder.py:170-230  AlignmentDecoder.forward_pass   -> dp_cases.npz (dp, bt, curr)
   * tools/alignment_decoder.py:232-294  AlignmentDecoder._decode        -> dp_cases.npz (path, confidence)
   * tools/alignment_decoder.py:26-143   AlignmentDecoder.decode         -> decode_cases.npz
+  * tools/alignment_decoder.py:152-168 + tools/plot.py  AlignmentDecoder.plot -> plot.json / plot.npz
   * networks/g2p/*.py                   G2P plugins                     -> g2p.json
   * networks/g2p/dictionary_g2p.py over dictionary/*.txt (the CLI's default -d)  -> g2p_dicts.json
   * networks/g2p/*.py + alignment_decoder.py:35 on edge inputs (error types)   -> g2p_edges.json
@@ -184,6 +185,73 @@ def gen_decode_cases():
     np.savez_compressed(os.path.join(HERE, "decode_cases.npz"), **arrays)
     with open(os.path.join(HERE, "decode_cases.json"), "w") as f:
         json.dump({"vocab": vocab, "cases": cases}, f, indent=1)
+
+
+def _figure_data(fig) -> dict:
+    """What a validation figure shows, as data: the top axes' vertical lines, phone labels and confidence curve, the
+    bottom axes' image and curves, the figure size and the subplot layout."""
+    ax1, ax2 = fig.axes
+    vl = [float(ln.get_xdata()[0]) for ln in ax1.lines if len(ln.get_xdata()) == 2 and ln.get_xdata()[0] ==
+          ln.get_xdata()[1]]
+    curves1 = [np.asarray(ln.get_ydata(), np.float64) for ln in ax1.lines if len(ln.get_xdata()) != 2]
+    return {"vlines": vl,
+            "texts": [[t.get_text(), float(t.get_position()[0]), float(t.get_position()[1]), str(t.get_color())]
+                      for t in ax1.texts],
+            "conf_curve": curves1[0].tolist() if curves1 else [],
+            "image_shape": list(ax2.images[0].get_array().shape),
+            "bottom_curves": [np.asarray(ln.get_ydata(), np.float64).tolist() for ln in ax2.lines],
+            "size": [float(v) for v in fig.get_size_inches()],
+            "subplotpars": [fig.subplotpars.left, fig.subplotpars.right, fig.subplotpars.top,
+                            fig.subplotpars.bottom, fig.subplotpars.hspace]}
+
+
+def gen_plot():
+    """AlignmentDecoder.plot (tools/alignment_decoder.py:152-168) -> tools/plot.py plot_for_valid on the decode
+    cases, with a seeded synthetic mel spectrogram: the plot's inputs (as the decoder derives them) and the figure's
+    data (plot.json / plot.npz)."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    import torch
+    from tools.alignment_decoder import AlignmentDecoder
+    d = json.load(open(os.path.join(HERE, "decode_cases.json")))
+    z = np.load(os.path.join(HERE, "decode_cases.npz"))
+    dec = AlignmentDecoder(d["vocab"], {"hop_length": 512, "sample_rate": 44100})
+    captured = {}
+    import tools.alignment_decoder as tad
+    real = tad.plot_for_valid
+
+    def capture(*args):
+        captured["args"] = args
+        return real(*args)
+    tad.plot_for_valid = capture
+    arrays, out = {}, []
+    try:
+        for ci, c in enumerate(d["cases"]):
+            lt = torch.from_numpy(z[f"c{ci}_logits"])
+            frame, edge = lt[:, :, 2:], lt[:, :, 0]
+            ctc = torch.cat([lt[:, :, [1]], lt[:, :, 3:]], dim=-1)
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                dec.decode(frame, edge, ctc, c["wav_length"], c["ph_seq"], c["word_seq"], c["ph_idx_to_word_idx"])
+            T = dec.ph_frame_pred.shape[0]
+            mel = synth.rng(500 + ci).standard_normal((1, 64, T)).astype(np.float32)
+            fig = dec.plot(torch.from_numpy(mel))
+            a = captured["args"]
+            arrays[f"c{ci}_mel"] = mel
+            arrays[f"c{ci}_ph_intervals_int"] = np.asarray(a[2], np.int32)
+            arrays[f"c{ci}_frame_confidence"] = np.asarray(a[3])         # each in the dtype the reference passes
+            arrays[f"c{ci}_ph_frame_prob"] = np.asarray(a[4])
+            arrays[f"c{ci}_ph_idx_frame"] = np.asarray(a[5])
+            arrays[f"c{ci}_edge_prob"] = np.asarray(a[6])
+            out.append({"ph_seq": [str(x) for x in a[1]], "figure": _figure_data(fig)})
+            plt.close(fig)
+    finally:
+        tad.plot_for_valid = real
+    np.savez_compressed(os.path.join(HERE, "plot.npz"), **arrays)
+    with open(os.path.join(HERE, "plot.json"), "w") as f:
+        json.dump({"cases": out}, f)
+    print(f"plot: {len(out)} cases")
 
 
 def gen_g2p():
@@ -665,7 +733,7 @@ def main():
          "g2p_edges": gen_g2p_edges,
          "postproc": gen_postproc,
          "gather": gen_gather_index, "hubert": gen_hubert, "unet": gen_unet, "e2e10s": gen_e2e10s,
-         "loaders": gen_loaders}[w]()
+         "loaders": gen_loaders, "plot": gen_plot}[w]()
 
 
 if __name__ == "__main__":
