@@ -79,6 +79,8 @@ def parse():
                          "in the encoder's split GEMMs (f16-class accuracy, not the reference's f32)")
     ap.add_argument("--chunk-seconds", type=float, default=None,
                     help="long-form: encode overlapping windows of this length (config 5 chunked; B=1 only)")
+    ap.add_argument("--two-stage-resample", action="store_true",
+                    help="run the 16 k -> 44.1 k -> 16 k resampling as its two stages (A/B of the one-pass chain)")
     ap.add_argument("--no-config3", action="store_true",
                     help="N > 1: skip the extra BASELINE config-3 measurement (global batch 512) after the timed steps")
     ap.add_argument("--no-extra-configs", action="store_true",
@@ -556,6 +558,8 @@ def main():
     ckpt = synth_checkpoint(encoder=encoder, model_path="synth:0", seed=1)
     task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
     task.on_predict_start()
+    if args.two_stage_resample:
+        task.chain_resample = False
     if args.no_held_dp:
         task.defer_dp_frames = None
     if args.precision == "f16":

@@ -180,7 +180,8 @@ class AlignmentDecoder:
         ep_h = hd.get("edge_prob") if keep_frame_probs else None
         fp_h = hd.get("ph_frame_pred") if keep_frame_probs else None
         if intervals:        # the batch's fractional boundaries in one set of array operations (intervals.py)
-            out = batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, self.frame_length)
+            out = batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, self.frame_length,
+                                tables=dev_out.get("tables"))
         else:
             out = []
             for b in range(len(ph_seqs)):

@@ -129,15 +129,21 @@ class UnitsEncoder:
         return [target_length(int(n), sample_rate, self.encoder_sample_rate) for n in lengths]
 
     @torch.no_grad()
-    def units(self, audio: torch.Tensor, sample_rate: int, lengths=None, gate=None) -> torch.Tensor:
+    def units(self, audio: torch.Tensor, sample_rate: int, lengths=None, gate=None, resampled=None) -> torch.Tensor:
         """[B, N] -> units [B, L, C].  ``lengths``: per-row sample counts of a zero-padded variable-length batch
-        (every row's units then equal what that utterance gives alone)."""
-        audio = audio.to(self.device).float()
-        if audio.dim() == 1:
-            audio = audio[None]
-        audio_res = self._resample(audio, sample_rate)
+        (every row's units then equal what that utterance gives alone).  ``resampled``: the batch already at the
+        encoder rate (task.encode_batch's one-pass chain from the input rate; ``audio`` is then unused)."""
+        if resampled is not None:
+            audio_res = resampled
+        else:
+            audio = audio.to(self.device).float()
+            if audio.dim() == 1:
+                audio = audio[None]
+            audio_res = self._resample(audio, sample_rate)
         if lengths is None:
             if audio_res.size(-1) < 400:   # reference pads the ORIGINAL audio here (encoder.py:51-52)
+                if resampled is not None:
+                    raise ValueError("units: the padding quirk needs the wave at sample_rate (resampled too short)")
                 audio_res = torch.nn.functional.pad(audio, (0, 400 - audio_res.size(-1)))
             return self.model(audio_res, **_g(gate))   # rows with a pitch are fine (conv0 / normalise: row strides)
         lens16 = self.resampled_lengths(lengths, sample_rate)
@@ -187,20 +193,26 @@ class UnitsEncoder:
         return flat.index_select(0, take)[None]
 
     @torch.no_grad()
-    def encode_frames(self, audio: torch.Tensor, sample_rate: int, hop_size: int, pad_to: int = 1, lengths=None,
-                      chunk_frames: int | None = None, overlap_frames: int = 100, gate=None):
+    def encode_frames(self, audio: torch.Tensor | None, sample_rate: int, hop_size: int, pad_to: int = 1,
+                      lengths=None, chunk_frames: int | None = None, overlap_frames: int = 100, gate=None,
+                      resampled: tuple | None = None):
         """[B, N] -> (features [B, T_pad, C] channels-last, n_frames); rows >= n_frames are zero.
 
         With ``lengths`` (per-row sample counts of a zero-padded batch) n_frames is a list (one per row) and
         rows >= n_frames[b] of row b are zero; T_pad covers the longest row.  ``gate``: called before each
-        attention launch (HubertEncoder.attention_block)."""
-        if chunk_frames is not None and lengths is None and audio.shape[0] == 1:
-            audio_res = self._resample(audio.to(self.device).float(), sample_rate)
+        attention launch (HubertEncoder.attention_block).  ``resampled`` = (the batch at the encoder rate, N at
+        ``sample_rate``): the wave at ``sample_rate`` was never formed (task.encode_batch's one-pass chain), only
+        its length, which the frame grid takes (encoder.py:56-57)."""
+        enc = None if resampled is None else resampled[0]
+        n_in = audio.shape[-1] if resampled is None else int(resampled[1])
+        rows = audio.shape[0] if resampled is None else enc.shape[0]
+        if chunk_frames is not None and lengths is None and rows == 1:
+            audio_res = self._resample(audio.to(self.device).float(), sample_rate) if enc is None else enc
             units = self.units_chunked(audio_res.contiguous(), chunk_frames, overlap_frames, gate=gate)
         else:
-            units = self.units(audio, sample_rate, lengths, gate=gate)
+            units = self.units(audio, sample_rate, lengths, gate=gate, resampled=enc)
         if lengths is None:
-            n_frames, ratio = self.grid(audio.shape[-1], sample_rate, hop_size)
+            n_frames, ratio = self.grid(n_in, sample_rate, hop_size)
             T_pad = (n_frames + pad_to - 1) // pad_to * pad_to
             return ops.units_gather(units.contiguous(), n_frames, T_pad, ratio), n_frames
         nfs = [self.grid(int(n), sample_rate, hop_size)[0] for n in lengths]

@@ -74,11 +74,40 @@ def _phones_words(ph_intervals, idx, ph_seq, word_seq, ph_idx_to_word_idx):
             np.array([word_seq[k] for k in w[first].tolist()]), word_iv.clip(min=0, max=None))
 
 
-def batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, frame_length: float) -> list:
+def batch_tables(ph_seqs, word_seqs, p2ws) -> dict:
+    """The transcript side of a batch's host assembly (batch_results): the batch's phone and word tables concatenated
+    (names, lengths, SP mask, word map, offsets).  They depend on the transcripts only, so a pipelined caller builds
+    them while the GPU runs the batch (task.submit) and the assembly after the results land is left with the path
+    arrays alone.  ``src`` keeps the three sequences, so a table is used only for the very objects it was built from."""
+    B = len(ph_seqs)
+    wss = [word_seqs[b] if word_seqs is not None and word_seqs[b] is not None else ph_seqs[b] for b in range(B)]
+    pw0 = [p2ws[b] if p2ws is not None and p2ws[b] is not None else np.arange(len(ph_seqs[b])) for b in range(B)]
+    n_ph = np.fromiter(map(len, ph_seqs), dtype=np.int64, count=B)
+    pws = [np.asarray(p, dtype=np.int64) for p in pw0]
+    odd = np.fromiter((len(p) != k for p, k in zip(pws, n_ph.tolist())), dtype=bool, count=B)
+    pws = [np.zeros(k, np.int64) if o else p for p, k, o in zip(pws, n_ph.tolist(), odd.tolist())]
+    n_w = np.fromiter(map(len, wss), dtype=np.int64, count=B)
+    ph_flat = [p for s in ph_seqs for p in s]
+    w_flat = [x for s in wss for x in s]
+    ph_names = np.array(ph_flat + [""])          # one spare entry: the target of out-of-range paths
+    return dict(src=(ph_seqs, word_seqs, p2ws), wss=wss, pw0=pw0, odd=odd, n_ph=n_ph, n_w=n_w,
+                ph_off=np.concatenate([[0], np.cumsum(n_ph)[:-1]]), w_off=np.concatenate([[0], np.cumsum(n_w)[:-1]]),
+                ph_names=ph_names, w_names=np.array(w_flat + [""]),
+                ph_len=np.fromiter(map(len, ph_flat), dtype=np.int64, count=len(ph_flat)),
+                w_len=np.fromiter(map(len, w_flat), dtype=np.int64, count=len(w_flat)),
+                is_sp=np.append(ph_names[:-1] == "SP", False), pw_flat=np.concatenate(pws + [np.zeros(1, np.int64)]),
+                n_flat=len(ph_flat))
+
+
+def batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, frame_length: float,
+                  tables: dict | None = None) -> list:
     """utterance_result for a whole batch of raw boundary arrays as they leave the GPU (idx / tint [B, >= n], n [B],
-    frame_confidence / edge_diff [B, >= T] f32): the fractional boundaries of every utterance in one set of array
-    operations (elementwise, so each value is the per-utterance form's, bit for bit), the phone / word selection and
-    the confidence per utterance.  Returns the records utterance_result returns."""
+    frame_confidence / edge_diff [B, >= T] f32).  The batch is assembled as one flat phone list: each path position
+    indexes the batch's concatenated phone table (SP mask, word index offset per utterance, name lengths), the kept
+    phones and the word openings are selected once for the batch, and each utterance's record is slices of the
+    result (every value elementwise as the per-utterance form, bit for bit; string dtypes sized per utterance as
+    np.array sizes them).  An utterance whose path leaves its own tables (a kept phone without a word, an index out of
+    range) is assembled alone by _phones_words, whose loop form raises as the reference does."""
     B = len(ph_seqs)
     T = np.asarray(list(Ts[:B]), dtype=np.int64)
     n = np.asarray(n_h[:B], dtype=np.int64)
@@ -89,20 +118,73 @@ def batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, 
     ed = np.where(tint == (T - 1)[:, None], 0.0, ed)          # edge_diff's last frame is 0 (alignment_decoder.py:83)
     body = frame_length * (tint.astype("float32") + (ed / 2).clip(-0.5, 0.5))
     ends = frame_length * T.astype(np.float64)
+    # each phone interval is [its start, the next phone's start or the utterance's end] (:103-108)
+    nxt = np.empty_like(body)
+    nxt[:, :-1] = body[:, 1:]
+    hasn = np.flatnonzero(n > 0)
+    nxt[hasn, n[hasn] - 1] = ends[hasn]
+
+    # the transcript side (batch_tables), built here unless the caller built it for these very sequences
+    src = tables["src"] if tables is not None else None
+    if src is None or src[0] is not ph_seqs or src[1] is not word_seqs or src[2] is not p2ws:
+        tables = batch_tables(ph_seqs, word_seqs, p2ws)
+    wss, pw0, odd, n_ph, n_w = tables["wss"], tables["pw0"], tables["odd"], tables["n_ph"], tables["n_w"]
+    ph_off, w_off, ph_names, w_names = tables["ph_off"], tables["w_off"], tables["ph_names"], tables["w_names"]
+    ph_len, w_len, is_sp, pw_flat = tables["ph_len"], tables["w_len"], tables["is_sp"], tables["pw_flat"]
+    n_flat = tables["n_flat"]
+
+    # the batch's paths as one flat list of (utterance, phone) in path order
+    rows, pos = np.nonzero(valid)
+    loc = idx_h[:B][rows, pos].astype(np.int64)
+    bad_ix = (loc < 0) | (loc >= n_ph[rows])
+    g = np.where(bad_ix, n_flat, loc + ph_off[rows])
+    kept = ~is_sp[g]
+    w_loc = pw_flat[g]
+    bad = bad_ix | (kept & ((w_loc < 0) | (w_loc >= n_w[rows])))
+    alone = odd.copy()                    # a word map not one entry per phone: that utterance alone
+    alone[rows[bad]] = True
+
+    sel = np.flatnonzero(kept & ~alone[rows])
+    ks, kp, kg = rows[sel], pos[sel], g[sel]
+    kw = w_loc[sel] + w_off[ks]
+    ph_iv = np.stack([body[ks, kp], nxt[ks, kp]], axis=1).clip(min=0, max=None)
+    opens = np.concatenate([[True], (kw[1:] != kw[:-1]) | (ks[1:] != ks[:-1])]) if len(sel) else np.zeros(0, bool)
+    first = np.flatnonzero(opens)
+    last = np.concatenate([first[1:] - 1, [len(sel) - 1]]) if len(first) else first
+    word_iv = np.stack([ph_iv[first, 0], ph_iv[last, 1]], axis=1)
+    fw = kw[first]
+    ph_cnt = np.bincount(ks, minlength=B)
+    w_cnt = np.bincount(ks[first], minlength=B)
+    ph_end, w_end = np.cumsum(ph_cnt), np.cumsum(w_cnt)
+    has_p, has_w = np.flatnonzero(ph_cnt), np.flatnonzero(w_cnt)
+    ph_wid, w_wid = np.ones(B, np.int64), np.ones(B, np.int64)     # per utterance: np.array's '<U' width
+    if len(has_p):
+        ph_wid[has_p] = np.maximum(np.maximum.reduceat(ph_len[kg], (ph_end - ph_cnt)[has_p]), 1)
+    if len(has_w):
+        w_wid[has_w] = np.maximum(np.maximum.reduceat(w_len[fw], (w_end - w_cnt)[has_w]), 1)
+    ph_sel, w_sel = ph_names[kg], w_names[fw]
+    log_fc = np.log(fc_h[:B] + 1e-6)                            # total_confidence's elementwise part, the batch at once
+    idx64, tint64 = idx_h[:B].astype(np.int64), tint_h[:B].astype(np.int64)
+    ph_end, w_end, ph_cnt, w_cnt = ph_end.tolist(), w_end.tolist(), ph_cnt.tolist(), w_cnt.tolist()
+    ph_wid, w_wid, alone, n, T = ph_wid.tolist(), w_wid.tolist(), alone.tolist(), n.tolist(), T.tolist()
+
     out = []
     for b in range(B):
-        k, Tb = int(n[b]), int(T[b])
-        ph_seq = ph_seqs[b]
-        ws = word_seqs[b] if word_seqs is not None and word_seqs[b] is not None else ph_seq
-        pw = p2ws[b] if p2ws is not None and p2ws[b] is not None else np.arange(len(ph_seq))
-        tp = np.concatenate([body[b, :k], ends[b:b + 1]])
-        iv = np.stack([tp[:-1], tp[1:]], axis=1)
-        idx = idx_h[b, :k].astype(np.int64)
-        rec = dict(T=Ts[b], ph_idx_seq=idx, ph_time_int=tint_h[b, :k].astype(np.int64),
-                   frame_confidence=fc_h[b, :Tb].copy(), edge_diff=ed_h[b, :Tb].copy())
-        ph_p, ph_iv, w_p, w_iv = _phones_words(iv, idx, ph_seq, ws, pw)
-        out.append(dict(rec, ph_seq=ph_p, ph_intervals=ph_iv, word_seq=w_p, word_intervals=w_iv,
-                        confidence=total_confidence(rec["frame_confidence"])))
+        k, Tb = n[b], T[b]
+        idx = idx64[b, :k].copy()
+        if alone[b]:
+            tp = np.concatenate([body[b, :k], ends[b:b + 1]])
+            res = _phones_words(np.stack([tp[:-1], tp[1:]], axis=1), idx, ph_seqs[b], wss[b], pw0[b])
+        elif ph_cnt[b] == 0:
+            res = np.array([]), np.array([]), np.array([]), np.array([])
+        else:
+            p0, p1, w0, w1 = ph_end[b] - ph_cnt[b], ph_end[b], w_end[b] - w_cnt[b], w_end[b]
+            res = (ph_sel[p0:p1].astype(f"<U{ph_wid[b]}"), ph_iv[p0:p1], w_sel[w0:w1].astype(f"<U{w_wid[b]}"),
+                   word_iv[w0:w1])
+        out.append(dict(T=Ts[b], ph_idx_seq=idx, ph_time_int=tint64[b, :k].copy(),
+                        frame_confidence=fc_h[b, :Tb].copy(), edge_diff=ed_h[b, :Tb].copy(), ph_seq=res[0],
+                        ph_intervals=res[1], word_seq=res[2], word_intervals=res[3],
+                        confidence=np.exp(np.mean(log_fc[b, :Tb]) / 3)))
     return out
 
 

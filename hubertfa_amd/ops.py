@@ -619,9 +619,10 @@ _lib.register("hfa_resample_split_workspace_bytes", [_I_, _I_, _I_, _I_, _I_], c
 _lib.register("hfa_resample_split", [_I_, _I_, _P_, _LL_, _I_, _I_, _P_, _I_, _I_, _I_, _P_, _P_, _LL_, _P_, _P_])
 
 
-def resample_split(x, orig, new, w_planes, G, width, out=None, workspace=None, flag=None):
+def resample_split(x, orig, new, w_planes, G, width, out=None, workspace=None, flag=None, n_out=None):
     """Sinc resample rows of x [B, N] (row stride free, unit element stride) on the split-f16 GEMM; w_planes
-    [2, G, new, Kg] (resample.Resampler builds them).  Returns the [B, ceil(new*N/orig)] view of the output."""
+    [2, G, new, Kg] (resample.Resampler builds them).  Returns the [B, ceil(new*N/orig)] view of the output (``n_out``
+    columns instead: resample.ChainResampler, whose composite filter's length is the two stages')."""
     _need(x, torch.float32, "x", contiguous=False)
     if x.stride(-1) != 1:
         raise ValueError("resample_split: rows must have unit stride")
@@ -638,7 +639,24 @@ def resample_split(x, orig, new, w_planes, G, width, out=None, workspace=None, f
               _ptr(workspace), _ptr(out), out.stride(0), _ptr(split_flag(x.device) if flag is None else flag),
               _stream(x.device))
     from .resample import target_length
-    return out[:, : target_length(N, orig, new)]
+    return out[:, : target_length(N, orig, new) if n_out is None else n_out]
+
+
+_lib.register("hfa_resample_chain_edges", [_I_, _I_, _P_, _P_, _LL_, _I_, _I_, _P_, _I_, _I_, _P_, _I_, _I_, _P_, _LL_,
+                                            _I_, _P_])
+
+
+def resample_chain_edges(x, lens, P, Q, wu_t, wu_width, wd_t, wd_width, y):
+    """Overwrite the edge frames of a composite two-stage resample y [B, >= cols] (hfa_resample_chain_edges): x
+    [B, N] the input rows, ``lens`` an int32 device tensor of per-row input lengths or None (all N)."""
+    _need(x, torch.float32, "x", contiguous=False)
+    _need(y, torch.float32, "y", contiguous=False)
+    if x.stride(-1) != 1 or y.stride(-1) != 1:
+        raise ValueError("resample_chain_edges: rows must have unit stride")
+    B, N = x.shape
+    _lib.call("hfa_resample_chain_edges", B, N, _ptr(lens) if lens is not None else None, _ptr(x), x.stride(0), P, Q,
+              _ptr(wu_t), wu_t.shape[0], wu_width, _ptr(wd_t), wd_t.shape[0], wd_width, _ptr(y), y.stride(0),
+              y.shape[1], _stream(x.device))
 
 
 def resample(x, orig, new, kernel, width, out=None, workspace=None):

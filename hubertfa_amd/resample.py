@@ -90,3 +90,72 @@ class Resampler:
         else:
             y = ops.resample(x2, self.orig, self.new, self.kernel, self.width)
         return y[0] if squeeze else y.reshape(*x.shape[:-1], y.shape[-1])
+
+
+def chain_taps(tu, wu: int, td, wd: int, P: int, Q: int):
+    """Composed taps of two sinc stages rate -> mid -> rate (ChainResampler): tu [Q, kwu] / td [P, kwd] the stages'
+    float32 tap tables (sinc_taps), wu / wd their widths, P / Q the first stage's reduced orig / new.  Returns (C
+    [P, Kg] float64, W): y[P i + q] = sum_m C[q][m] x[P i + m - W] wherever the second stage's window lies inside the
+    intermediate row; Kg a multiple of 32 with Kg >= 2 W + P (hfa_resample_split's bound).  Second-stage tap l of
+    output frame i reads r = Q i - wd + l, i.e. first-stage frame i + fl (fl = floor((l - wd) / Q)) at phase
+    l - wd - Q fl, whose tap k reads input P (i + fl) - wu + k: column P fl - wu + k + W."""
+    kwu, kwd = tu.shape[1], td.shape[1]
+    fl_lo, fl_hi = (-wd) // Q, (kwd - 1 - wd) // Q
+    W = -P * fl_lo + wu                                   # the lowest composed tap lands on column 0
+    K = P * fl_hi + kwu - wu + W
+    Kg = max(-(-K // 32) * 32, -(-(2 * W + P) // 32) * 32)
+    comp = np.zeros((P, Kg), np.float64)
+    tu64, td64 = tu.astype(np.float64), td.astype(np.float64)
+    for fl in range(fl_lo, fl_hi + 1):
+        l0, l1 = max(0, wd + Q * fl), min(kwd, wd + Q * (fl + 1))
+        if l0 < l1:
+            c0 = P * fl - wu + W
+            comp[:, c0:c0 + kwu] += td64[:, l0:l1] @ tu64[np.arange(l0, l1) - wd - Q * fl, :]
+    return comp, W
+
+
+class ChainResampler:
+    """Two sinc stages that return to the input rate as ONE pass: ``rate -> mid`` (width ``up_width``) then ``mid ->
+    rate`` (width ``down_width``) -- HubertFA's 16 kHz input path, load_wav's resample to the melspec rate
+    (tools/load_wav.py:7, width 6) followed by the encoder's resample back to 16 kHz (tools/encoder.py:46-48,
+    width 128), whose 44.1 kHz wave nothing else reads (only its length: the frame grid).
+
+    With P / Q the first stage's gcd-reduced orig / new (160 / 441), output frame i (outputs P i .. P i + P - 1) of
+    the second stage reads the intermediate samples r = Q i - wd_width + l, and each of those reads input samples
+    P (r div Q) - wu_width + k, so the chain is one polyphase filter of stride P over the input: y[P i + q] =
+    sum_m C[q][m] x[P i + m - W], the composed taps C (P x ~494, against the 174 x 441 / 160 + 1155 = 1635 MACs per
+    output of the two stages) summed in float64 from the stages' float32 taps, on the split-f16 GEMM
+    (ops.resample_split, orig = new = P).  That form holds wherever the second stage's window lies inside the
+    intermediate row; at the row's two ends each stage zero-pads its own input, which the composite cannot
+    express, so those few frames (the first ceil(wd_width / Q), the last ~3 of each row) are recomputed exactly as the
+    two stages compute them by ops.resample_chain_edges.  Results agree with the two-stage restatement
+    (oracle/resample.py) within the split path's own tolerance (tests/test_kernels_gpu.py); torchaudio itself is
+    absent, so, like the stages, parity is unpinned."""
+
+    def __init__(self, rate: int, mid: int, up_width: int, down_width: int, device=None):
+        tu, self.wu_width, self.P, self.Q = sinc_taps(rate, mid, up_width)          # [Q, kwu]
+        td, self.wd_width, q2, p2 = sinc_taps(mid, rate, down_width)                # [P, kwd]
+        if (q2, p2) != (self.Q, self.P) or self.P % 8:
+            raise ValueError("ChainResampler: the stages must return to the input rate with P % 8 == 0")
+        comp, self.W = chain_taps(tu, self.wu_width, td, self.wd_width, self.P, self.Q)
+        self.Kg = comp.shape[1]
+        dev = torch.device(device or "cuda")
+        self.taps = comp                                  # float64, for tests
+        self.w_planes = ops.split(torch.from_numpy(comp.astype(np.float32))[None].to(dev))
+        self.wu_t = torch.from_numpy(np.ascontiguousarray(tu.T)).to(dev)            # [kwu, Q]
+        self.wd_t = torch.from_numpy(np.ascontiguousarray(td.T)).to(dev)            # [kwd, P]
+
+    def out_length(self, n: int) -> int:
+        """The two stages' output length for an n-sample row (each stage's float32-quotient ceil)."""
+        return target_length(target_length(int(n), self.P, self.Q), self.Q, self.P)
+
+    def __call__(self, x: torch.Tensor, lens: torch.Tensor | None = None) -> torch.Tensor:
+        """x [B, N] f32 (unit element stride) -> [B, out_length(N)]; ``lens`` (int32 device [B]): per-row input
+        lengths of a zero-padded batch (each row then resamples as it would alone, up to its own output length;
+        the columns past it are not defined: mask them)."""
+        B, N = x.shape
+        P = self.P
+        out = torch.empty((B, (N // P + 1) * P), dtype=torch.float32, device=x.device)
+        y = ops.resample_split(x, P, P, self.w_planes, 1, self.W, out=out, n_out=self.out_length(N))
+        ops.resample_chain_edges(x, lens, P, self.Q, self.wu_t, self.wu_width, self.wd_t, self.wd_width, out)
+        return y

@@ -18,8 +18,9 @@ import yaml
 from . import ops, synth
 from .alignment_decoder import AlignmentDecoder
 from .encoder import UnitsEncoder
-from .resample import Resampler, target_length
+from .resample import ChainResampler, Resampler, target_length
 from .hubert import dev_lengths
+from .intervals import batch_tables
 from .unet import LatticeHead
 from .wav_io import read_wav
 
@@ -66,6 +67,7 @@ class ForcedAlignmentTask:
         self.decoder = AlignmentDecoder(self.vocab, self.melspec_config)
         self.unitsEncoder = None
         self._upsamplers = {}
+        self._chains = {}
 
     # -- checkpoint ---------------------------------------------------------------------------------------------
     @classmethod
@@ -137,19 +139,51 @@ class ForcedAlignmentTask:
         waves = waves.to(self.device).float()
         if lengths is not None and all(int(n) == waves.shape[-1] for n in lengths):
             lengths = None
+        resampled = None
         if wav_sr is not None and wav_sr != sr:
-            up = self.upsampler(wav_sr)
-            waves = up(waves, split=self.unitsEncoder.split_resample)
+            chain = self.chain_resampler(wav_sr, waves.shape[-1], lengths)
+            if chain is not None:        # input rate -> sr -> encoder rate as one pass; the sr wave is never formed
+                if waves.stride(-1) != 1:
+                    waves = waves.contiguous()
+                enc = chain(waves, dev_lengths(lengths, waves.device) if lengths is not None else None)
+                resampled = (enc, target_length(waves.shape[-1], wav_sr, sr))
+            else:
+                up = self.upsampler(wav_sr)
+                waves = up(waves, split=self.unitsEncoder.split_resample)
             if lengths is not None:
                 lengths = [target_length(int(n), wav_sr, sr) for n in lengths]
-                waves = waves.contiguous()
-                ops.mask_rows(waves, dev_lengths(lengths, waves.device))   # sinc tails past each row's end
-        n = waves.shape[-1]
+                if chain is None:
+                    waves = waves.contiguous()
+                    ops.mask_rows(waves, dev_lengths(lengths, waves.device))   # sinc tails past each row's end
+        n = waves.shape[-1] if resampled is None else resampled[1]
         chunk = None if chunk_seconds is None else max(1, int(round(chunk_seconds * 50)))
-        feats, n_frames = self.unitsEncoder.encode_frames(waves, sr, hop, pad_to=self.head.divisible,
-                                                          lengths=lengths, chunk_frames=chunk, gate=gate)
+        feats, n_frames = self.unitsEncoder.encode_frames(waves if resampled is None else None, sr, hop,
+                                                          pad_to=self.head.divisible, lengths=lengths,
+                                                          chunk_frames=chunk, gate=gate, resampled=resampled)
         wl = [n / sr] * waves.shape[0] if lengths is None else [int(m) / sr for m in lengths]
         return feats, n_frames, wl
+
+    # the input rate -> melspec rate -> encoder rate chain as one pass (resample.ChainResampler) when the input is
+    # at the encoder rate (16 kHz files) and the encoder runs split; False: always the two stages
+    chain_resample = True
+
+    def chain_resampler(self, wav_sr: int, n: int, lengths=None):
+        """The one-pass ChainResampler for a batch at ``wav_sr``, or None where the two stages must run: another
+        input rate, the f32 re-run of the range guard, or a row whose encoder-rate length is under the 400 samples
+        where the reference pads the melspec-rate wave (encoder.py:51-52)."""
+        ue = self.unitsEncoder
+        if not self.chain_resample or not ue.split_resample or int(wav_sr) != int(ue.encoder_sample_rate):
+            return None
+        key = int(wav_sr)
+        if key not in self._chains:
+            try:
+                self._chains[key] = ChainResampler(wav_sr, self.melspec_config["sample_rate"], 6, 128, self.device)
+            except ValueError:
+                self._chains[key] = None
+        chain = self._chains[key]
+        if chain is None or chain.out_length(min(int(m) for m in lengths) if lengths is not None else n) < 400:
+            return None
+        return chain
 
     def head_logits(self, feats, n_frames):
         """UNet head (current stream): features -> (logits [B, T, V+2], the head's range-flag snapshot or None)."""
@@ -267,7 +301,13 @@ class ForcedAlignmentTask:
                 self._held = work
             else:
                 work.complete()
-            return work.handle
+        if self.host_tables:         # the host assembly's transcript tables, built while the GPU runs this batch
+            work.handle["tables"] = batch_tables(ph_seqs, word_seqs, p2ws)
+        return work.handle
+
+    # submit builds the batch's transcript tables for decoder.assemble's batch_results (False: a caller that takes
+    # raw records, assemble(intervals=False), as the CLI's export workers do)
+    host_tables = True
 
     # workgroups at most per launch of the side pass's row-streaming kernels (ops.grid_cap; 0: uncapped): beside the
     # next batch's encoder, their one-row workgroups cost the encoder more than their work

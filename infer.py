@@ -88,6 +88,7 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
         raise RuntimeError("fault injected (HFA_FAULT_INJECT_RANK): this rank's shard fails")
     recoverable = _recoverable()
     task.on_predict_start()
+    task.host_tables = False             # raw records leave assemble; their intervals are built at export
     sr = task.melspec_config["sample_rate"]
     items = {}
 

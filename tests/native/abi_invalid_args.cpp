@@ -138,6 +138,12 @@ int main() {
     CHECK(hfa_selftest_erf(-1, fp, fp, fp, st), "erf n<0");
     CHECK(hfa_selftest_gelu(-1, fp, fp, st), "gelu n<0");
     CHECK(hfa_resample_f32(1, 100, fp, 100, 0, 441, fp, 16, 6, ws, fp, 300, st), "resample orig=0");
+    CHECK(hfa_resample_chain_edges(1, 100, nullptr, fp, 100, 160, 441, fp, 174, 7, fp, 1155, 1155, fp, 320, 320, st),
+          "chain edges wd_width >= kwd");
+    CHECK(hfa_resample_chain_edges(1, 100, nullptr, fp, 100, 160, 441, fp, 174, 7, fp, 20000, 357, fp, 320, 320, st),
+          "chain edges window past LDS");
+    CHECK(hfa_resample_chain_edges(1, 100, nullptr, fp, 100, 160, 441, fp, 174, 7, fp, 1155, 357, fp, 100, 320, st),
+          "chain edges y_bs < y_cols");
     // WAV front end (host memory): null arguments, a missing file, a non-RIFF file, a short buffer, a bad channel
     {
         int64_t nf = 0;

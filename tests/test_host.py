@@ -692,8 +692,9 @@ def test_interval_assembly_array_form_matches_loop():
 def test_batch_results_match_per_utterance():
     """intervals.batch_results (decoder.assemble's batched host assembly) gives every utterance exactly what
     utterance_result gives it from its own raw record: ragged n and T, a path ending on the last frame (its edge_diff
-    entry replaced by 0), garbage past n and T in the padded buffers, default word sequences."""
-    from hubertfa_amd.intervals import batch_results, utterance_result
+    entry replaced by 0), garbage past n and T in the padded buffers, default word sequences; with the transcript
+    tables prebuilt (task.submit) for the same sequences, and for a copy of them (rebuilt, not used)."""
+    from hubertfa_amd.intervals import batch_results, batch_tables, utterance_result
     rng = np.random.default_rng(9)
     phones = ["SP", "a", "b", "AP", "cc"]
     for trial in range(20):
@@ -729,7 +730,8 @@ def test_batch_results_match_per_utterance():
             ph_seqs.append(ph)
             word_seqs.append(None if default else words)
             p2ws.append(None if default else p2w)
-        got = batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, 512 / 44100)
+        tabs = batch_tables(ph_seqs, word_seqs, p2ws) if trial % 2 else batch_tables(list(ph_seqs), word_seqs, p2ws)
+        got = batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, 512 / 44100, tables=tabs)
         for b in range(B):
             k, T = int(n_h[b]), Ts[b]
             rec = dict(T=T, ph_idx_seq=idx_h[b, :k].astype(np.int64), ph_time_int=tint_h[b, :k].astype(np.int64),
@@ -741,3 +743,38 @@ def test_batch_results_match_per_utterance():
             for key in ref:
                 x, y = np.asarray(got[b][key]), np.asarray(ref[key])
                 assert x.dtype == y.dtype and x.shape == y.shape and np.array_equal(x, y), (trial, b, key)
+
+
+def test_batch_results_irregular_utterances():
+    """batch_results on utterances the flat batch form cannot take (assembled alone, as the reference's loop would):
+    a kept phone mapped to word -1 after a word (the loop reuses word_seq[-1]) and a word map longer than the phone
+    list, beside regular utterances; and the errors the reference raises (a first kept phone without a word, a word
+    index past the word list, a word map too short) raised the same."""
+    from hubertfa_amd.intervals import batch_results, utterance_result
+    ph = ["SP", "a", "b", "c", "SP", "d"]
+    words = ["w0", "w1", "w2"]
+    good = [[-1, 0, 0, 1, -1, 2], [-1, 0, 1, -1, -1, 2], [-1, 0, 0, 1, -1, 2, 2], [-1, 0, 1, 1, -1, 2]]
+    T, n, B = 40, 6, 4
+    idx_h = np.tile(np.arange(n, dtype=np.int32), (B, 1))
+    tint_h = np.tile(np.array([0, 5, 9, 14, 22, 30], np.int32), (B, 1))
+    rng = np.random.default_rng(3)
+    fc_h = rng.random((B, T)).astype(np.float32)
+    ed_h = rng.standard_normal((B, T)).astype(np.float32)
+    n_h = np.full(B, n, np.int32)
+    Ts, ph_seqs, word_seqs = [T] * B, [ph] * B, [words] * B
+    got = batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, good, 512 / 44100)
+    for b in range(B):
+        rec = dict(T=T, ph_idx_seq=idx_h[b].astype(np.int64), ph_time_int=tint_h[b].astype(np.int64),
+                   frame_confidence=fc_h[b].copy(), edge_diff=ed_h[b].copy())
+        ref = utterance_result(rec, ph, words, good[b], 512 / 44100)
+        for key in ref:
+            x, y = np.asarray(got[b][key]), np.asarray(ref[key])
+            assert x.dtype == y.dtype and x.shape == y.shape and np.array_equal(x, y), (b, key)
+    for bad in ([-1, -1, 0, 1, -1, 2], [-1, 0, 0, 1, -1, 7], [-1, 0, 0, 1, -1]):
+        with pytest.raises(IndexError):
+            utterance_result(dict(T=T, ph_idx_seq=idx_h[0].astype(np.int64), ph_time_int=tint_h[0].astype(np.int64),
+                                  frame_confidence=fc_h[0].copy(), edge_diff=ed_h[0].copy()), ph, words, bad,
+                             512 / 44100)
+        with pytest.raises(IndexError):
+            batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, good[:2] + [bad] + good[3:],
+                          512 / 44100)

@@ -365,6 +365,48 @@ def test_resample_split_vs_f32_and_restatement(o, n, w, N):
     assert float((got.double() - f32.double()).abs().max()) < 2e-6
 
 
+@pytest.mark.parametrize("N", [160000, 4097, 12345, 441 * 3 + 7, 160 * 25 + 159, 4_800_000])
+def test_chain_resampler_vs_two_stages(N):
+    """16 k -> 44.1 k -> 16 k as one composite pass + the exact edge frames (resample.ChainResampler) against the
+    restated two stages (oracle/resample.py, f32 as torchaudio) within the stages' own split-path tolerance, and
+    against the GPU's two-stage split path (which it replaces on the product path) to 2e-6; same length, from
+    row-pitched input; N = 4.8 M is config 5's 300 s row."""
+    from hubertfa_amd.resample import ChainResampler, Resampler
+    from oracle.resample import resample as ref_resample
+    B = 2 if N < 1_000_000 else 1
+    x = _r(B, N + 40, seed=N % 1000, scale=0.2)[:, 5:N + 5]
+    chain = ChainResampler(16000, 44100, 6, 128)
+    xd = x.cuda()
+    got = chain(xd)
+    two = Resampler(44100, 16000, 128)(Resampler(16000, 44100, 6)(xd, split=True).contiguous(), split=True)
+    assert got.shape == two.shape == (B, chain.out_length(N))
+    assert float((got.double() - two.double()).abs().max()) < 2e-6
+    if N <= 200_000:
+        ref = ref_resample(ref_resample(x.contiguous(), 16000, 44100, 6), 44100, 16000, 128)
+        assert got.shape == ref.shape
+        _close(got, ref, 1e-4, 2e-6)
+
+
+def test_chain_resampler_ragged_rows_as_alone():
+    """A zero-padded batch with per-row lengths: every row's first out_length(n) samples are what the row gives
+    alone -- interior frames through the same composite GEMM arithmetic, the last frames recomputed against that
+    row's own end (its intermediate length's float32-quotient ceil)."""
+    from hubertfa_amd.resample import ChainResampler
+    chain = ChainResampler(16000, 44100, 6, 128)
+    lens = [48000, 47999, 30001, 4000, 44100 + 3]
+    N = max(lens)
+    x = torch.zeros(len(lens), N)
+    for b, n in enumerate(lens):
+        x[b, :n] = _r(n, seed=50 + b, scale=0.3)
+    xd = x.cuda()
+    got = chain(xd, torch.tensor(lens, dtype=torch.int32).cuda())
+    for b, n in enumerate(lens):
+        alone = chain(xd[b:b + 1, :n].contiguous())[0]
+        m = chain.out_length(n)
+        assert alone.shape[0] == m
+        assert float((got[b, :m].double() - alone.double()).abs().max()) <= 1e-7, b
+
+
 @pytest.mark.parametrize("N", [16000, 160000, 4097])
 def test_wav_normalize(N):
     from hubertfa_amd import ops
