@@ -25,50 +25,26 @@ __global__ __launch_bounds__(64) void flag_take_kernel(int n, int* __restrict__ 
     }
 }
 
-// ys (optional): the gathered rows also as split-f16 planes (hi, (x - hi) * 2^11; plane stride sps), the UNet's first
-// split GEMMs' operand (task.submit), with *oflow raised for a value past f16 range; out may then be NULL.
 __global__ __launch_bounds__(256) void units_gather_kernel(int U, int C, const float* __restrict__ units,
                                                            long long u_bs, int u_ld, int n_frames, int T_pad,
                                                            float ratio, float* __restrict__ out, long long o_bs,
                                                            int o_ld, const int32_t* __restrict__ nf_b,
-                                                           const int32_t* __restrict__ U_b,
-                                                           _Float16* __restrict__ ys, long long ys_bs, int ys_ld,
-                                                           long long sps, int* __restrict__ oflow) {
+                                                           const int32_t* __restrict__ U_b) {
     const int b = blockIdx.y;
     const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (k >= T_pad) return;
     const int nf = nf_b ? nf_b[b] : n_frames;      // per-utterance lengths of a variable-length batch
     const int Ub = U_b ? U_b[b] : U;
-    float* orow = out ? out + b * o_bs + (long long)k * o_ld : nullptr;
-    _Float16* yrow = ys ? ys + b * ys_bs + (long long)k * ys_ld : nullptr;
+    float* orow = out + b * o_bs + (long long)k * o_ld;
     if (k >= nf) {
-        for (int c = lane * 4; c < C; c += 256) {
-            if (orow) *reinterpret_cast<f32x4*>(orow + c) = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (yrow) {
-                *reinterpret_cast<uint2*>(yrow + c) = uint2{0u, 0u};
-                *reinterpret_cast<uint2*>(yrow + sps + c) = uint2{0u, 0u};
-            }
-        }
+        for (int c = lane * 4; c < C; c += 256) *reinterpret_cast<f32x4*>(orow + c) = f32x4{0.f, 0.f, 0.f, 0.f};
         return;
     }
     int idx = (int)rintf(__fmul_rn(ratio, (float)k));
     idx = idx < Ub - 1 ? idx : Ub - 1;
     const float* irow = units + b * u_bs + (long long)idx * u_ld;
-    hfa::h2v nanacc = {(_Float16)0.0f, (_Float16)0.0f};
-    const float c2048 = 2048.0f;
-    for (int c = lane * 4; c < C; c += 256) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(irow + c);
-        if (orow) *reinterpret_cast<f32x4*>(orow + c) = v;
-        if (yrow) {
-            uint2 h1, h2;
-            hfa::split_pair(v[0], v[1], h1.x, h2.x, nanacc, c2048);
-            hfa::split_pair(v[2], v[3], h1.y, h2.y, nanacc, c2048);
-            *reinterpret_cast<uint2*>(yrow + c) = h1;
-            *reinterpret_cast<uint2*>(yrow + sps + c) = h2;
-        }
-    }
-    if (yrow && hfa::range_bad(nanacc) && oflow) *oflow = 1;
+    for (int c = lane * 4; c < C; c += 256) *reinterpret_cast<f32x4*>(orow + c) = *reinterpret_cast<const f32x4*>(irow + c);
 }
 
 // Zero rows t >= lens[b] of a [B, T, C] tensor (the padding rows of a variable-length batch, which convs with
@@ -221,29 +197,15 @@ extern "C" {
 int hfa_units_gather_f32(int B, int U, int C, const float* units, long long u_bs, int u_ld, int n_frames, int T_pad,
                          float ratio, float* out, long long o_bs, int o_ld, const int32_t* n_frames_b,
                          const int32_t* U_b, hipStream_t stream) {
-    if (!out) {
+    if (B < 0 || U < 1 || C <= 0 || C % 4 || n_frames < 0 || T_pad < n_frames || u_ld % 4 || o_ld % 4 ||
+        u_bs % 4 || o_bs % 4 || (((uintptr_t)units | (uintptr_t)out) & 15)) {
         hfa::set_error("hfa_units_gather_f32: bad arguments");
-        return HFA_EINVAL;
-    }
-    return hfa_units_gather_split(B, U, C, units, u_bs, u_ld, n_frames, T_pad, ratio, out, o_bs, o_ld, n_frames_b,
-                                  U_b, nullptr, 0, 0, 0, nullptr, stream);
-}
-
-int hfa_units_gather_split(int B, int U, int C, const float* units, long long u_bs, int u_ld, int n_frames, int T_pad,
-                           float ratio, float* out, long long o_bs, int o_ld, const int32_t* n_frames_b,
-                           const int32_t* U_b, uint16_t* ys, long long ys_bs, int ys_ld, long long sps, int* oflow,
-                           hipStream_t stream) {
-    if (B < 0 || U < 1 || C <= 0 || C % 4 || n_frames < 0 || T_pad < n_frames || u_ld % 4 || u_bs % 4 ||
-        (!out && !ys) || (out && (o_ld % 4 || o_bs % 4 || ((uintptr_t)out & 15))) || ((uintptr_t)units & 15) ||
-        (ys && (ys_ld % 4 || ys_bs % 4 || sps % 4 || ((uintptr_t)ys & 7)))) {
-        hfa::set_error("hfa_units_gather_split: bad arguments");
         return HFA_EINVAL;
     }
     if (B == 0 || T_pad == 0) return HFA_OK;
     hipLaunchKernelGGL(units_gather_kernel, dim3((T_pad + 3) / 4, B), dim3(256), 0, stream, U, C, units, u_bs, u_ld,
-                       n_frames, T_pad, ratio, out, o_bs, o_ld, n_frames_b, U_b, reinterpret_cast<_Float16*>(ys),
-                       ys_bs, ys_ld, sps, oflow);
-    return hfa::check_launch("hfa_units_gather_split");
+                       n_frames, T_pad, ratio, out, o_bs, o_ld, n_frames_b, U_b);
+    return hfa::check_launch("hfa_units_gather_f32");
 }
 
 int hfa_mask_rows_f32(int B, int T, int C, float* x, long long x_bs, int ldx, const int32_t* lens,

@@ -195,15 +195,14 @@ class UnitsEncoder:
     @torch.no_grad()
     def encode_frames(self, audio: torch.Tensor | None, sample_rate: int, hop_size: int, pad_to: int = 1,
                       lengths=None, chunk_frames: int | None = None, overlap_frames: int = 100, gate=None,
-                      resampled: tuple | None = None, planes: bool = False):
+                      resampled: tuple | None = None):
         """[B, N] -> (features [B, T_pad, C] channels-last, n_frames); rows >= n_frames are zero.
 
         With ``lengths`` (per-row sample counts of a zero-padded batch) n_frames is a list (one per row) and
         rows >= n_frames[b] of row b are zero; T_pad covers the longest row.  ``gate``: called before each
         attention launch (HubertEncoder.attention_block).  ``resampled`` = (the batch at the encoder rate, N at
         ``sample_rate``): the wave at ``sample_rate`` was never formed (task.encode_batch's one-pass chain), only
-        its length, which the frame grid takes (encoder.py:56-57).  ``planes``: the features also as split planes
-        (ops.units_gather), returned third."""
+        its length, which the frame grid takes (encoder.py:56-57)."""
         enc = None if resampled is None else resampled[0]
         n_in = audio.shape[-1] if resampled is None else int(resampled[1])
         rows = audio.shape[0] if resampled is None else enc.shape[0]
@@ -215,16 +214,15 @@ class UnitsEncoder:
         if lengths is None:
             n_frames, ratio = self.grid(n_in, sample_rate, hop_size)
             T_pad = (n_frames + pad_to - 1) // pad_to * pad_to
-            g = ops.units_gather(units.contiguous(), n_frames, T_pad, ratio, planes=planes)
-            return (g[0], n_frames, g[1]) if planes else (g, n_frames)
+            return ops.units_gather(units.contiguous(), n_frames, T_pad, ratio), n_frames
         nfs = [self.grid(int(n), sample_rate, hop_size)[0] for n in lengths]
         _, ratio = self.grid(int(lengths[0]), sample_rate, hop_size)
         Ls = [self.model.frame_lengths(n) for n in self.resampled_lengths(lengths, sample_rate)]
         T_pad = (max(nfs) + pad_to - 1) // pad_to * pad_to
         dev = units.device
-        g = ops.units_gather(units.contiguous(), max(nfs), T_pad, ratio, n_frames_b=dev_lengths(nfs, dev),
-                             U_b=dev_lengths(Ls, dev), planes=planes)
-        return (g[0], nfs, g[1]) if planes else (g, nfs)
+        feats = ops.units_gather(units.contiguous(), max(nfs), T_pad, ratio, n_frames_b=dev_lengths(nfs, dev),
+                                 U_b=dev_lengths(Ls, dev))
+        return feats, nfs
 
     def encode(self, audio, sample_rate, hop_size):
         """[B, N] -> [B, C, T] like the reference; under the split-f16 range guard (a batch whose activations

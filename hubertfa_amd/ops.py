@@ -188,8 +188,6 @@ _lib.register("hfa_conv0_f32", [_I_, _I_, _P_, _LL_, _P_, _P_, _I_, _P_, _P_, _F
 _lib.register("hfa_conv0_split", [_I_, _I_, _P_, _LL_, _P_, _P_, _I_, _P_, _P_, _F_, _P_, _P_, _LL_, _LL_, _P_, _P_,
                                    _P_])
 _lib.register("hfa_units_gather_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _P_, _P_])
-_lib.register("hfa_units_gather_split", [_I_, _I_, _I_, _P_, _LL_, _I_, _I_, _I_, _F_, _P_, _LL_, _I_, _P_, _P_, _P_,
-                                          _LL_, _I_, _LL_, _P_, _P_])
 _lib.register("hfa_mask_rows_f32", [_I_, _I_, _I_, _P_, _LL_, _I_, _P_, _P_])
 _lib.register("hfa_wav_normalize_f32", [_I_, _I_, _P_, _LL_, _F_, _P_, _LL_, _P_, _P_, _P_])
 _lib.register("hfa_wav_normalize_workspace_bytes", [_I_], ctypes.c_longlong)
@@ -541,24 +539,14 @@ def conv0(x, w0, *, bias=None, gamma=None, beta=None, eps=1e-5, out=None, worksp
     return out
 
 
-def units_gather(units, n_frames, T_pad, ratio, out=None, n_frames_b=None, U_b=None, planes=False, flag=None):
-    """units [B, U, C] -> the DP grid's rows [B, T_pad, C] (hfa_units_gather_f32); with ``planes`` also their split
-    planes [2, B, T_pad, C] (hfa_units_gather_split; out-of-range values raise ``flag``, default the device's
-    split_flag) and the pair is returned."""
+def units_gather(units, n_frames, T_pad, ratio, out=None, n_frames_b=None, U_b=None):
     B, U, C = units.shape
     if out is None:
         out = torch.empty((B, T_pad, C), dtype=torch.float32, device=units.device)
     nf, ub = _lens(n_frames_b), _lens(U_b)
-    if not planes:
-        _lib.call("hfa_units_gather_f32", B, U, C, _ptr(units), units.stride(0), units.stride(1), n_frames, T_pad,
-                  float(ratio), _ptr(out), out.stride(0), out.stride(1), _ptr(nf), _ptr(ub), _stream(units.device))
-        return out
-    ys = torch.empty((2, B, T_pad, C), dtype=torch.float16, device=units.device)
-    _lib.call("hfa_units_gather_split", B, U, C, _ptr(units), units.stride(0), units.stride(1), n_frames, T_pad,
-              float(ratio), _ptr(out), out.stride(0), out.stride(1), _ptr(nf), _ptr(ub), _ptr(ys), ys.stride(1),
-              ys.stride(2), ys.stride(0), _ptr(split_flag(units.device) if flag is None else flag),
-              _stream(units.device))
-    return out, ys
+    _lib.call("hfa_units_gather_f32", B, U, C, _ptr(units), units.stride(0), units.stride(1), n_frames, T_pad,
+              float(ratio), _ptr(out), out.stride(0), out.stride(1), _ptr(nf), _ptr(ub), _stream(units.device))
+    return out
 
 
 def mask_rows(x, lens):

@@ -157,20 +157,11 @@ class ForcedAlignmentTask:
                     ops.mask_rows(waves, dev_lengths(lengths, waves.device))   # sinc tails past each row's end
         n = waves.shape[-1] if resampled is None else resampled[1]
         chunk = None if chunk_seconds is None else max(1, int(round(chunk_seconds * 50)))
-        # the features' split planes for the head's first GEMMs, written by the gather on this stream (no conversion
-        # pass on the head's stream); both halves split, so the encoder's range flag (the guard's) covers them
-        enc = getattr(self.unitsEncoder, "model", None)
-        planes = self.gather_planes and self.head.precision == "split" and getattr(enc, "precision", "f32") == "split"
-        got = self.unitsEncoder.encode_frames(waves if resampled is None else None, sr, hop,
-                                              pad_to=self.head.divisible, lengths=lengths, chunk_frames=chunk,
-                                              gate=gate, resampled=resampled, planes=planes)
-        feats, n_frames = got[0], got[1]
-        self._feat_planes = (feats, got[2]) if planes else None
+        feats, n_frames = self.unitsEncoder.encode_frames(waves if resampled is None else None, sr, hop,
+                                                          pad_to=self.head.divisible, lengths=lengths,
+                                                          chunk_frames=chunk, gate=gate, resampled=resampled)
         wl = [n / sr] * waves.shape[0] if lengths is None else [int(m) / sr for m in lengths]
         return feats, n_frames, wl
-
-    # the features' gather writes the head's split operand too (False: the head converts them on its own stream)
-    gather_planes = True
 
     # the input rate -> melspec rate -> encoder rate chain as one pass (resample.ChainResampler) when the input is
     # at the encoder rate (16 kHz files) and the encoder runs split; False: always the two stages
@@ -195,15 +186,12 @@ class ForcedAlignmentTask:
         return chain
 
     def head_logits(self, feats, n_frames):
-        """UNet head (current stream): features -> (logits [B, T, V+2], the head's range-flag snapshot or None).
-        Features that encode_batch just produced come with their split planes (the gather wrote them)."""
-        fp, self._feat_planes = getattr(self, "_feat_planes", None), None
-        xs = fp[1] if fp is not None and fp[0] is feats else None
+        """UNet head (current stream): features -> (logits [B, T, V+2], the head's range-flag snapshot or None)."""
         if isinstance(n_frames, (list, tuple)):          # variable-length batch
             t_pad = [self.head.padded_len(int(t)) for t in n_frames]
-            logits = self.head.logits(feats, t_pad, xs=xs)[:, :max(n_frames)]
+            logits = self.head.logits(feats, t_pad)[:, :max(n_frames)]
         else:
-            logits = self.head.logits(feats, xs=xs)[:, :n_frames]
+            logits = self.head.logits(feats)[:, :n_frames]
         flag = None
         if self.head.precision == "split":      # the head's own range flag, snapshot on the stream that ran it
             flag = ops.flag_take(self.head.flag)
@@ -302,8 +290,6 @@ class ForcedAlignmentTask:
         with torch.cuda.stream(self._side):
             self._side.wait_event(ready)
             feats.record_stream(self._side)      # the caching allocator must not recycle it under the side stream
-            if getattr(self, "_feat_planes", None) is not None:
-                self._feat_planes[1].record_stream(self._side)
             with ops.grid_cap(self.side_grid_cap):
                 dev_out = self.decode_device(feats, n_frames, wl, ph_seqs, word_seqs, p2ws,
                                              dp_ranges=self.dp_ranges if chunk_seconds is None else None)

@@ -211,14 +211,13 @@ class LatticeHead:
         return T if r == 0 else T + self.divisible - r
 
     @torch.no_grad()
-    def backbone(self, x: torch.Tensor, t_pad=None, want_split=False, xs=None):
+    def backbone(self, x: torch.Tensor, t_pad=None, want_split=False):
         """x [B, T_pad, C_in] with T_pad % factor**times == 0 (zero rows beyond the real T).  ``t_pad`` (optional
         host ints [B]): each row's own padded length (a multiple of factor**times) in a variable-length batch; the
         reference runs each utterance alone at that length (unet.py:103-106), so every level masks beyond it.
         Split path: every producer whose consumer is a split GEMM writes that operand's planes (block GroupNorm and
         LayerNorm, down / up convs with the skip add in their epilogue), so no separate conversion runs beyond the
-        input's (``xs``: the input's planes when its producer wrote them -- the features' gather -- zero past each
-        row's length like x).  Returns y, or (y, planes) with ``want_split``."""
+        input's.  Returns y, or (y, planes) with ``want_split``."""
         lv = None
         if t_pad is not None and any(int(t) != x.shape[1] for t in t_pad):
             from .hubert import dev_lengths
@@ -226,7 +225,7 @@ class LatticeHead:
                   for i in range(self.arch.times + 1)]
         L = (lambda i: None) if lv is None else (lambda i: lv[i])
         n_enc = len(self.encoders)
-        h = [(x, xs if self.ctx.precision == "split" else None)]
+        h = [(x, None)]
         for i, enc in enumerate(self.encoders):
             t = h[-1]
             for m in enc:
@@ -245,12 +244,12 @@ class LatticeHead:
         return t if want_split else t[0]
 
     @torch.no_grad()
-    def logits(self, x: torch.Tensor, t_pad=None, xs=None) -> torch.Tensor:
+    def logits(self, x: torch.Tensor, t_pad=None) -> torch.Tensor:
         """x [B, T_pad, C_in] -> logits [B, T_pad, V+2] on the chip-wide launches (every GEMM spreads over the whole
         chip; a row's result depends on its own length only).  The one-kernel and per-op-engine forms of round 3
         were parity-green but slower in the pipeline; they are in git history."""
         if self.ctx.use_split(self.head_ws):
-            y, ys = self.backbone(x, t_pad, want_split=True, xs=xs)
+            y, ys = self.backbone(x, t_pad, want_split=True)
             return self.ctx.linear(y, ys, self.head_wp, self.head_ws, self.head_bp)[0][:, :, :self.head_w.shape[0]]
         y = self.backbone(x, t_pad)
         return self.ctx.linear(y, None, self.head_w, None, self.head_b)[0]

@@ -252,13 +252,6 @@ int hfa_conv0_split(int B, int N, const float* x, long long x_bs, const float* w
 int hfa_units_gather_f32(int B, int U, int C, const float* units, long long u_bs, int u_ld, int n_frames, int T_pad,
                          float ratio, float* out, long long o_bs, int o_ld, const int32_t* n_frames_b,
                          const int32_t* U_b, hipStream_t stream);
-/* The same gather writing the rows also (or only: out NULL) as split-f16 planes ys (hi at ys, lo * 2^11 at ys + sps;
- * [B][T_pad][C] with strides ys_bs / ys_ld halves), the UNet's first split GEMMs' operand, so no conversion pass runs
- * on the head's stream; *oflow (may be NULL) raised for a value past f16 range, as hfa_split_f16. */
-int hfa_units_gather_split(int B, int U, int C, const float* units, long long u_bs, int u_ld, int n_frames, int T_pad,
-                           float ratio, float* out, long long o_bs, int o_ld, const int32_t* n_frames_b,
-                           const int32_t* U_b, uint16_t* ys, long long ys_bs, int ys_ld, long long sps, int* oflow,
-                           hipStream_t stream);
 /* Wav2Vec2FeatureExtractor zero-mean/unit-variance normalisation (tools/encoder.py:94-95), f64 statistics over each
  * row's own lens[b] samples; workspace: hfa_wav_normalize_workspace_bytes(B) bytes of device memory (row partials). */
 long long hfa_wav_normalize_workspace_bytes(int B);

@@ -121,29 +121,3 @@ def test_pipelined_submit_matches_align_batch():
         for u, (g, r) in enumerate(zip(got, a)):
             for k in ("ph_idx_seq", "ph_time_int", "frame_confidence", "edge_diff"):
                 assert np.array_equal(np.asarray(g[k]), np.asarray(r[k])), f"batch {i} utt {u}: {k}"
-
-
-@pytest.mark.parametrize("ragged", [False, True])
-def test_gather_planes_head_bit_identical(ragged):
-    """The head on the features' split planes written by the gather (task.encode_batch -> head_logits: no conversion
-    pass on the side stream) gives the logits the separate conversion gives, bit for bit: uniform and ragged
-    batches (rows past each length zero in both forms)."""
-    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
-    dev = torch.device("cuda")
-    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
-    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
-    task.on_predict_start()
-    B = 3
-    wav, _, _, _ = _inputs(B, 6.0, 20, 99)
-    lens = [wav.shape[1], wav.shape[1] - 16000, wav.shape[1] - 40000] if ragged else None
-    x = torch.from_numpy(wav).to(dev)
-    if ragged:
-        for b, n in enumerate(lens):
-            x[b, n:] = 0
-    feats, n_frames, _ = task.encode_batch(x, 16000, lengths=lens)
-    assert task._feat_planes is not None and task._feat_planes[0] is feats
-    with_planes, _ = task.head_logits(feats, n_frames)                 # takes the gather's planes
-    assert task._feat_planes is None
-    alone, _ = task.head_logits(feats.clone(), n_frames)             # another tensor: converts on its own
-    torch.cuda.synchronize()
-    assert torch.equal(with_planes, alone)
