@@ -163,7 +163,15 @@ def batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, 
     if len(has_w):
         w_wid[has_w] = np.maximum(np.maximum.reduceat(w_len[fw], (w_end - w_cnt)[has_w]), 1)
     ph_sel, w_sel = ph_names[kg], w_names[fw]
-    log_fc = np.log(fc_h[:B] + 1e-6)                            # total_confidence's elementwise part, the batch at once
+    # total_confidence per row, for the rows of each length at once: the mean along each row of a [rows, T] block is
+    # the 1-D mean of that row (numpy's pairwise sum over the contiguous axis), bit for bit
+    log_fc = np.log(fc_h[:B] + 1e-6)
+    conf = [None] * B
+    for Tv in set(T.tolist()):
+        rws = np.flatnonzero(T == Tv)
+        cv = np.exp(np.mean(log_fc[rws, :Tv], axis=1) / 3)
+        for j, r in enumerate(rws.tolist()):
+            conf[r] = cv[j]
     idx64, tint64 = idx_h[:B].astype(np.int64), tint_h[:B].astype(np.int64)
     ph_end, w_end, ph_cnt, w_cnt = ph_end.tolist(), w_end.tolist(), ph_cnt.tolist(), w_cnt.tolist()
     ph_wid, w_wid, alone, n, T = ph_wid.tolist(), w_wid.tolist(), alone.tolist(), n.tolist(), T.tolist()
@@ -184,7 +192,7 @@ def batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, p2ws, 
         out.append(dict(T=Ts[b], ph_idx_seq=idx, ph_time_int=tint64[b, :k].copy(),
                         frame_confidence=fc_h[b, :Tb].copy(), edge_diff=ed_h[b, :Tb].copy(), ph_seq=res[0],
                         ph_intervals=res[1], word_seq=res[2], word_intervals=res[3],
-                        confidence=np.exp(np.mean(log_fc[b, :Tb]) / 3)))
+                        confidence=conf[b]))
     return out
 
 

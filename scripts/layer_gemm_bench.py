@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--H", type=int, default=768)
     ap.add_argument("--F", type=int, default=3072)
     ap.add_argument("--cfgs", default="0", help="split GEMM tile overrides (hfa_gemm_split_tuning), 0 = automatic")
+    ap.add_argument("--dump", default=None, help="write the GEMMs' output digests (sha256) here: A/B bit checks")
     args = ap.parse_args()
     d = torch.device("cuda")
     g = torch.Generator(device=d).manual_seed(0)
@@ -69,6 +70,16 @@ def main():
             ops.attention_split(qs, o, B=B, H=H // 64, L=L, head_dim=64, scale=0.125)
             _lib.lib().hfa_attention_split_tuning(0)
         cases.append(("attention (split, 8 waves)", 4.0 * B * H * L * L, attn8))
+    if args.dump:
+        import hashlib
+        import json
+        dig = {}
+        for (name, _, fn), out in zip(cases[:4], (qkv_out, y, f1_out, y)):
+            fn()
+            torch.cuda.synchronize()
+            dig[name] = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()
+        with open(args.dump, "w") as f:
+            json.dump(dig, f, indent=1)
     for cfg in [int(c) for c in args.cfgs.split(",")]:
         _lib.lib().hfa_gemm_split_tuning(cfg)
         for name, flop, fn in cases:
