@@ -1047,7 +1047,6 @@ __device__ __forceinline__ void gemm_split_tile(const GemmP p, int wgid, int z, 
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, w2[j], acc[i][j], 0, 0, 0);
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, w1[j], acc[i][j], 0, 0, 0);
                     }
-
                 }
             }
             if (more) advance();
