@@ -336,28 +336,10 @@ __device__ __forceinline__ int ceil_f32_quot(long long a, long long n, long long
     return (int)__builtin_ceilf(q);
 }
 
-// One workgroup per (output frame slot, row): slot s < FL is left frame s, slot FL + j the j-th frame of the right
-// edge.  The frame's intermediate window u[Q i - wd_width, Q i - wd_width + kwd) is computed exactly as the first
-// stage computes it (x zero outside [0, Nb); each u a sequential f32 FMA chain over its kwu taps) and zeroed outside
-// [0, len_u) as the second stage's padding has it, in LDS; then the frame's P outputs, each as kChainParts partial
-// f32 FMA chains over consecutive thirds of the window summed in a fixed order (the same bits for a row in any
-// batch).  Taps are k-major (wu_t [kwu][Q], wd_t [kwd][P]) so consecutive phases read consecutive addresses; the
-// tap loops are unrolled so their loads issue ahead of the FMAs.  (A workgroup per edge and phase slice, each
-// first-stage tap column read once for all the edge's frames, measured 3.7x slower: 101 against 27 us for config 2.)
-constexpr int kChainThreads = 512, kChainParts = 3;
-__global__ __launch_bounds__(kChainThreads) void chain_edges_kernel(int N, const int32_t* __restrict__ lens,
-                                                          const float* __restrict__ x, long long x_bs, int P, int Q,
-                                                          const float* __restrict__ wu_t, int kwu, int wu_width,
-                                                          const float* __restrict__ wd_t, int kwd, int wd_width,
-                                                          int FL, float* __restrict__ y, long long y_bs, int y_cols) {
-    extern __shared__ float su[];                          // [kwd] window, then [kChainParts][P] partial sums
-    float* part = su + kwd;
-    const int b = blockIdx.y, slot = blockIdx.x;
-    const int Nb = lens ? lens[b] : N;
-    if (Nb <= 0) return;
-    const int len_u = ceil_f32_quot(Q, Nb, P);
-    const int len_y = ceil_f32_quot(P, len_u, Q);
-    const int tail = kwd - 1 - wd_width;                   // the window's reach past Q i
+// The frame a slot stands for: slot s < FL is left frame s, slot FL + j the j-th frame of the right edge (from the
+// first whose second-stage window reaches len_u); -1 when the row has no such frame.
+__device__ __forceinline__ int chain_slot_frame(int slot, int FL, int len_u, int len_y, int P, int Q, int tail,
+                                                int y_cols) {
     int i;
     if (slot < FL) {
         i = slot;
@@ -365,42 +347,81 @@ __global__ __launch_bounds__(kChainThreads) void chain_edges_kernel(int N, const
         const int num = len_u - tail;
         i = (num <= 0 ? 0 : (num + Q - 1) / Q) + (slot - FL);
     }
-    const int n0 = P * i;
-    if (n0 >= len_y || n0 >= y_cols) return;
-    const int r0 = Q * i - wd_width;
-    const float* xr = x + b * x_bs;
-    for (int t = threadIdx.x; t < kwd; t += kChainThreads) {
-        const int r = r0 + t;
-        float v = 0.0f;
-        if (r >= 0 && r < len_u) {
-            const int f = r / Q, ph = r - f * Q;
-            const int s0 = P * f - wu_width;
-            const int k0 = s0 < 0 ? -s0 : 0, k1 = Nb - s0 < kwu ? Nb - s0 : kwu;
-            const float* w = wu_t + ph;
+    return (P * i >= len_y || P * i >= y_cols) ? -1 : i;
+}
+
+// Edge pass, part 1: one thread per sample of a slot's intermediate window u[Q i - wd_width, + kwd), computed as the
+// first stage computes it (x zero outside [0, Nb); a sequential f32 FMA chain over its kwu taps, k-major taps wu_t
+// [kwu][Q] so consecutive phases read consecutive addresses) and zero outside [0, len_u) as the second stage's
+// padding has it; into the workspace [B][FS][kwd].  Many small workgroups: each CU streams few tap bytes.
+constexpr int kChainUThreads = 128, kChainQW = 32, kChainParts = 16;
+__global__ __launch_bounds__(kChainUThreads) void chain_window_kernel(int N, const int32_t* __restrict__ lens,
+                                                                      const float* __restrict__ x, long long x_bs,
+                                                                      int P, int Q, const float* __restrict__ wu_t,
+                                                                      int kwu, int wu_width, int kwd, int wd_width,
+                                                                      int FL, int FS, int y_cols,
+                                                                      float* __restrict__ uw) {
+    const int b = blockIdx.z, slot = blockIdx.y, t = blockIdx.x * kChainUThreads + threadIdx.x;
+    const int Nb = lens ? lens[b] : N;
+    if (Nb <= 0 || t >= kwd) return;
+    const int len_u = ceil_f32_quot(Q, Nb, P);
+    const int len_y = ceil_f32_quot(P, len_u, Q);
+    const int i = chain_slot_frame(slot, FL, len_u, len_y, P, Q, kwd - 1 - wd_width, y_cols);
+    if (i < 0) return;
+    const int r = Q * i - wd_width + t;
+    float v = 0.0f;
+    if (r >= 0 && r < len_u) {
+        const int f = r / Q, ph = r - f * Q;
+        const int s0 = P * f - wu_width;
+        const int k0 = s0 < 0 ? -s0 : 0, k1 = Nb - s0 < kwu ? Nb - s0 : kwu;
+        const float* w = wu_t + ph;
+        const float* xr = x + b * x_bs + s0;
 #pragma unroll 8
-            for (int k = k0; k < k1; ++k) v = __builtin_fmaf(w[k * Q], xr[s0 + k], v);
-        }
-        su[t] = v;
+        for (int k = k0; k < k1; ++k) v = __builtin_fmaf(w[k * Q], xr[k], v);
     }
+    uw[((long long)b * FS + slot) * kwd + t] = v;
+}
+
+// Edge pass, part 2: one workgroup per (slice of kChainQW output phases, slot, row): the window (LDS) against the
+// slice's columns of the second stage's taps (k-major wd_t [kwd][P]), kChainParts partial FMA chains per output over
+// consecutive l ranges, summed in a fixed order -- the same bits for a row in any batch.
+__global__ __launch_bounds__(kChainQW * kChainParts) void chain_frame_kernel(int N, const int32_t* __restrict__ lens,
+                                                                             int P, int Q, int kwd, int wd_width,
+                                                                             const float* __restrict__ wd_t, int FL,
+                                                                             int FS, const float* __restrict__ uw,
+                                                                             float* __restrict__ y, long long y_bs,
+                                                                             int y_cols) {
+    extern __shared__ float su[];                          // [kwd] window, then [kChainParts][kChainQW] partial sums
+    float* part = su + kwd;
+    const int b = blockIdx.z, slot = blockIdx.y, q0 = blockIdx.x * kChainQW;
+    const int Nb = lens ? lens[b] : N;
+    if (Nb <= 0) return;
+    const int len_u = ceil_f32_quot(Q, Nb, P);
+    const int len_y = ceil_f32_quot(P, len_u, Q);
+    const int i = chain_slot_frame(slot, FL, len_u, len_y, P, Q, kwd - 1 - wd_width, y_cols);
+    if (i < 0) return;
+    const float* u = uw + ((long long)b * FS + slot) * kwd;
+    for (int t = threadIdx.x; t < kwd; t += kChainQW * kChainParts) su[t] = u[t];
     __syncthreads();
+    const int ql = threadIdx.x % kChainQW, pt = threadIdx.x / kChainQW, q = q0 + ql;
     const int span = (kwd + kChainParts - 1) / kChainParts;
-    for (int o = threadIdx.x; o < P * kChainParts; o += kChainThreads) {
-        const int q = o % P, pt = o / P;
-        const int l0 = pt * span, l1 = l0 + span < kwd ? l0 + span : kwd;
-        float acc = 0.0f;
+    const int l0 = pt * span, l1 = l0 + span < kwd ? l0 + span : kwd;
+    float acc = 0.0f;
+    if (q < P) {
         const float* w = wd_t + q;
 #pragma unroll 8
         for (int l = l0; l < l1; ++l) acc = __builtin_fmaf(w[l * P], su[l], acc);
-        part[pt * P + q] = acc;
     }
+    part[pt * kChainQW + ql] = acc;
     __syncthreads();
-    for (int q = threadIdx.x; q < P; q += kChainThreads) {
-        const int n = n0 + q;
-        if (n >= len_y || n >= y_cols) continue;
-        float acc = part[q];
+    if (pt == 0 && q < P) {
+        const int n = P * i + q;
+        if (n < len_y && n < y_cols) {
+            float sum = part[ql];
 #pragma unroll
-        for (int pt = 1; pt < kChainParts; ++pt) acc += part[pt * P + q];
-        y[b * y_bs + n] = acc;
+            for (int k = 1; k < kChainParts; ++k) sum += part[k * kChainQW + ql];
+            y[b * y_bs + n] = sum;
+        }
     }
 }
 
@@ -448,21 +469,35 @@ int hfa_resample_split(int B, int N, const float* x, long long x_bs, int orig, i
                                G == 1 ? 0 : newr, G == 1 ? newr : 8 * newr, 0, oflow, stream);
 }
 
+static inline int chain_slots(int Q, int kwd, int wd_width) {
+    return (wd_width + Q - 1) / Q + (kwd - 1 - wd_width) / Q + 2;   // left frames + right frames (+ slack)
+}
+
+long long hfa_resample_chain_edges_workspace_bytes(int B, int Q, int kwd, int wd_width) {
+    if (B < 0 || Q <= 0 || kwd <= 0 || wd_width < 0 || wd_width >= kwd) return -1;
+    return (long long)B * chain_slots(Q, kwd, wd_width) * kwd * 4 + 64;
+}
+
 int hfa_resample_chain_edges(int B, int N, const int32_t* lens, const float* x, long long x_bs, int P, int Q,
                              const float* wu_t, int kwu, int wu_width, const float* wd_t, int kwd, int wd_width,
-                             float* y, long long y_bs, int y_cols, hipStream_t stream) {
+                             void* workspace, float* y, long long y_bs, int y_cols, hipStream_t stream) {
     if (B < 0 || B > 65535 || N <= 0 || !x || P <= 0 || Q <= 0 || !wu_t || kwu <= 0 || wu_width < 0 || !wd_t ||
-        kwd <= 0 || wd_width < 0 || wd_width >= kwd || !y || y_cols < 0 || y_bs < y_cols ||
-        (long long)(kwd + kChainParts * P) * 4 > 64 * 1024 || (long long)Q * N / P > (1LL << 30)) {
+        kwd <= 0 || wd_width < 0 || wd_width >= kwd || !workspace || ((uintptr_t)workspace & 15) || !y ||
+        y_cols < 0 || y_bs < y_cols || (long long)(kwd + kChainParts * kChainQW) * 4 > 64 * 1024 ||
+        (long long)Q * N / P > (1LL << 30)) {
         hfa::set_error("hfa_resample_chain_edges: bad arguments");
         return HFA_EINVAL;
     }
     if (B == 0 || y_cols == 0) return HFA_OK;
-    const int FL = (wd_width + Q - 1) / Q;                       // left frames: Q i - wd_width < 0
-    const int FR = (kwd - 1 - wd_width) / Q + 2;                 // right frames: Q i + tail >= len_u, to the last
-    hipLaunchKernelGGL(chain_edges_kernel, dim3(FL + FR, B), dim3(kChainThreads),
-                       (kwd + kChainParts * P) * sizeof(float), stream, N, lens, x, x_bs, P, Q, wu_t, kwu, wu_width,
-                       wd_t, kwd, wd_width, FL, y, y_bs, y_cols);
+    const int FL = (wd_width + Q - 1) / Q, FS = chain_slots(Q, kwd, wd_width);
+    float* uw = static_cast<float*>(workspace);
+    hipLaunchKernelGGL(chain_window_kernel, dim3((kwd + kChainUThreads - 1) / kChainUThreads, FS, B),
+                       dim3(kChainUThreads), 0, stream, N, lens, x, x_bs, P, Q, wu_t, kwu, wu_width, kwd, wd_width,
+                       FL, FS, y_cols, uw);
+    if (int rc = hfa::check_launch("hfa_resample_chain_edges")) return rc;
+    hipLaunchKernelGGL(chain_frame_kernel, dim3((P + kChainQW - 1) / kChainQW, FS, B), dim3(kChainQW * kChainParts),
+                       (kwd + kChainParts * kChainQW) * sizeof(float), stream, N, lens, P, Q, kwd, wd_width, wd_t, FL,
+                       FS, uw, y, y_bs, y_cols);
     return hfa::check_launch("hfa_resample_chain_edges");
 }
 

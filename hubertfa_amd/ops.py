@@ -642,8 +642,9 @@ def resample_split(x, orig, new, w_planes, G, width, out=None, workspace=None, f
     return out[:, : target_length(N, orig, new) if n_out is None else n_out]
 
 
-_lib.register("hfa_resample_chain_edges", [_I_, _I_, _P_, _P_, _LL_, _I_, _I_, _P_, _I_, _I_, _P_, _I_, _I_, _P_, _LL_,
-                                            _I_, _P_])
+_lib.register("hfa_resample_chain_edges_workspace_bytes", [_I_, _I_, _I_, _I_], restype=_LL_)
+_lib.register("hfa_resample_chain_edges", [_I_, _I_, _P_, _P_, _LL_, _I_, _I_, _P_, _I_, _I_, _P_, _I_, _I_, _P_, _P_,
+                                            _LL_, _I_, _P_])
 
 
 def resample_chain_edges(x, lens, P, Q, wu_t, wu_width, wd_t, wd_width, y):
@@ -654,8 +655,10 @@ def resample_chain_edges(x, lens, P, Q, wu_t, wu_width, wd_t, wd_width, y):
     if x.stride(-1) != 1 or y.stride(-1) != 1:
         raise ValueError("resample_chain_edges: rows must have unit stride")
     B, N = x.shape
+    nbytes = _lib.lib().hfa_resample_chain_edges_workspace_bytes(B, Q, wd_t.shape[0], wd_width)
+    ws = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=x.device)
     _lib.call("hfa_resample_chain_edges", B, N, _ptr(lens) if lens is not None else None, _ptr(x), x.stride(0), P, Q,
-              _ptr(wu_t), wu_t.shape[0], wu_width, _ptr(wd_t), wd_t.shape[0], wd_width, _ptr(y), y.stride(0),
+              _ptr(wu_t), wu_t.shape[0], wu_width, _ptr(wd_t), wd_t.shape[0], wd_width, _ptr(ws), _ptr(y), y.stride(0),
               y.shape[1], _stream(x.device))
 
 

@@ -294,12 +294,15 @@ int hfa_resample_split(int B, int N, const float* x, long long x_bs, int orig, i
  * overwrites the output frames that pass cannot express -- those whose second-stage window reaches past the
  * intermediate row, where each stage alone zero-pads: the first ceil(wd_width / Q) frames and the frames from
  * ceil((len_u - (kwd - 1 - wd_width)) / Q) to the row's last output, computed as the two stages compute them
- * (f32).  P, Q: the first stage's gcd-reduced orig / new (the second's new / orig); wu_t [kwu][Q] and wd_t
+ * (f32): each frame's intermediate window into the workspace (hfa_resample_chain_edges_workspace_bytes), then the
+ * frame's outputs.  P, Q: the first stage's gcd-reduced orig / new (the second's new / orig); wu_t [kwu][Q] and wd_t
  * [kwd][P] the stages' f32 taps, k-major; lens [B] per-row input lengths (NULL: N); len_u and the row's output
- * length follow torchaudio's float32-quotient ceil.  y: [B][y_bs] (y_cols columns exist); (kwd + 3 P) floats fit 64 KiB. */
+ * length follow torchaudio's float32-quotient ceil.  y: [B][y_bs] (y_cols columns exist); kwd + 512 floats fit
+ * 64 KiB. */
+long long hfa_resample_chain_edges_workspace_bytes(int B, int Q, int kwd, int wd_width);
 int hfa_resample_chain_edges(int B, int N, const int32_t* lens, const float* x, long long x_bs, int P, int Q,
                              const float* wu_t, int kwu, int wu_width, const float* wd_t, int kwd, int wd_width,
-                             float* y, long long y_bs, int y_cols, hipStream_t stream);
+                             void* workspace, float* y, long long y_bs, int y_cols, hipStream_t stream);
 long long hfa_resample_workspace_bytes(int B, int N, int orig, int Kpad);
 int hfa_resample_f32(int B, int N, const float* x, long long x_bs, int orig, int newr, const float* kernel, int Kpad,
                      int width, void* workspace, float* y, long long y_bs, hipStream_t stream);

@@ -138,12 +138,15 @@ int main() {
     CHECK(hfa_selftest_erf(-1, fp, fp, fp, st), "erf n<0");
     CHECK(hfa_selftest_gelu(-1, fp, fp, st), "gelu n<0");
     CHECK(hfa_resample_f32(1, 100, fp, 100, 0, 441, fp, 16, 6, ws, fp, 300, st), "resample orig=0");
-    CHECK(hfa_resample_chain_edges(1, 100, nullptr, fp, 100, 160, 441, fp, 174, 7, fp, 1155, 1155, fp, 320, 320, st),
-          "chain edges wd_width >= kwd");
-    CHECK(hfa_resample_chain_edges(1, 100, nullptr, fp, 100, 160, 441, fp, 174, 7, fp, 20000, 357, fp, 320, 320, st),
-          "chain edges window past LDS");
-    CHECK(hfa_resample_chain_edges(1, 100, nullptr, fp, 100, 160, 441, fp, 174, 7, fp, 1155, 357, fp, 100, 320, st),
-          "chain edges y_bs < y_cols");
+    CHECK(hfa_resample_chain_edges(1, 100, nullptr, fp, 100, 160, 441, fp, 174, 7, fp, 1155, 1155, ws, fp, 320, 320,
+                                   st), "chain edges wd_width >= kwd");
+    CHECK(hfa_resample_chain_edges(1, 100, nullptr, fp, 100, 160, 441, fp, 174, 7, fp, 20000, 357, ws, fp, 320, 320,
+                                   st), "chain edges window past LDS");
+    CHECK(hfa_resample_chain_edges(1, 100, nullptr, fp, 100, 160, 441, fp, 174, 7, fp, 1155, 357, ws, fp, 100, 320,
+                                   st), "chain edges y_bs < y_cols");
+    CHECK(hfa_resample_chain_edges(1, 100, nullptr, fp, 100, 160, 441, fp, 174, 7, fp, 1155, 357, nullptr, fp, 320,
+                                   320, st), "chain edges NULL workspace");
+    if (hfa_resample_chain_edges_workspace_bytes(2, 441, 1155, 357) <= 0) { std::printf("FAIL chain workspace\n"); ++g_fail; }
     // WAV front end (host memory): null arguments, a missing file, a non-RIFF file, a short buffer, a bad channel
     {
         int64_t nf = 0;
