@@ -81,6 +81,9 @@ def parse():
                     help="long-form: encode overlapping windows of this length (config 5 chunked; B=1 only)")
     ap.add_argument("--two-stage-resample", action="store_true",
                     help="run the 16 k -> 44.1 k -> 16 k resampling as its two stages (A/B of the one-pass chain)")
+    ap.add_argument("--defer-dp-frames", type=int, default=None,
+                    help="task.defer_dp_frames (hold lattices of at least this many DP frames for the next encoder's "
+                         "attention launches; A/B of the threshold)")
     ap.add_argument("--no-config3", action="store_true",
                     help="N > 1: skip the extra BASELINE config-3 measurement (global batch 512) after the timed steps")
     ap.add_argument("--no-extra-configs", action="store_true",
@@ -560,6 +563,8 @@ def main():
     task.on_predict_start()
     if args.two_stage_resample:
         task.chain_resample = False
+    if args.defer_dp_frames is not None:
+        task.defer_dp_frames = args.defer_dp_frames
     if args.no_held_dp:
         task.defer_dp_frames = None
     if args.precision == "f16":
