@@ -135,8 +135,9 @@ class ChainResampler:
     def __init__(self, rate: int, mid: int, up_width: int, down_width: int, device=None):
         tu, self.wu_width, self.P, self.Q = sinc_taps(rate, mid, up_width)          # [Q, kwu]
         td, self.wd_width, q2, p2 = sinc_taps(mid, rate, down_width)                # [P, kwd]
-        if (q2, p2) != (self.Q, self.P) or self.P % 8:
-            raise ValueError("ChainResampler: the stages must return to the input rate with P % 8 == 0")
+        if (q2, p2) != (self.Q, self.P) or self.P % 8 or td.shape[1] + 512 > 16384:
+            raise ValueError("ChainResampler: the stages must return to the input rate with P % 8 == 0 and a second "
+                             "stage of at most 15 872 taps (hfa_resample_chain_edges' window)")
         comp, self.W = chain_taps(tu, self.wu_width, td, self.wd_width, self.P, self.Q)
         self.Kg = comp.shape[1]
         dev = torch.device(device or "cuda")
