@@ -149,8 +149,18 @@ def textgrid_text(word_seq, word_intervals, ph_seq, ph_intervals, null=""):
     for i, (name, rows) in enumerate(tiers, 1):
         out += [f"\titem [{i}]:", '\t\tclass = "IntervalTier"', f'\t\tname = "{name}"', "\t\txmin = 0.0",
                 f"\t\txmax = {maxT}", f"\t\tintervals: size = {len(rows)}"]
-        out += [f'\t\t\tintervals [{j}]:\n\t\t\t\txmin = {a}\n\t\t\t\txmax = {b}\n\t\t\t\ttext = "'
-                + str(m).replace('"', '""') + '"' for j, (a, b, m) in enumerate(rows, 1)]
+        # a tier's intervals are contiguous, so each boundary is formatted once: an interval's xmin reuses the
+        # previous xmax's text when it is the same value of the same type (zeros are formatted again: -0.0)
+        prev, sprev = None, None
+        for j, (a, b, m) in enumerate(rows, 1):
+            sa = sprev if (a == prev and type(a) is type(prev) and a != 0) else str(a)
+            sb = str(b)
+            m = str(m)
+            if '"' in m:
+                m = m.replace('"', '""')
+            out.append('\t\t\tintervals [%d]:\n\t\t\t\txmin = %s\n\t\t\t\txmax = %s\n\t\t\t\ttext = "%s"'
+                       % (j, sa, sb, m))
+            prev, sprev = b, sb
     return "\n".join(out) + "\n"
 
 

@@ -56,7 +56,8 @@ class _StreamingExport:
             wav_path, ph_seq, word_seq, p2w = self.rows[i]
             rec = records[i]
             try:
-                r = utterance_result(rec, ph_seq, word_seq, p2w, self.frame_length)
+                # records assembled by the batch (decoder.assemble's batch_results) carry their intervals already
+                r = rec if "ph_seq" in rec else utterance_result(rec, ph_seq, word_seq, p2w, self.frame_length)
                 pred, err = post_process_one((wav_path, rec["n44"] / self.sr, r["confidence"], r["ph_seq"],
                                               r["ph_intervals"], r["word_seq"], r["word_intervals"]))
                 if err is None:
@@ -80,6 +81,8 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
     reference's decode outputs).  A batch that raises a recoverable error is re-run file by file; a file that
     fails alone goes to ``errors`` as [wav_path, exception] (the post-processing log).  ``on_batch(out, keys)``
     is called with each completed batch's dataset indices (the one-GPU streaming export)."""
+    import time
+
     import torch
     from hubertfa_amd.batching import plan_batches, resampled_length
     from hubertfa_amd.wav_io import read_wav_into, wav_info
@@ -88,7 +91,11 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
         raise RuntimeError("fault injected (HFA_FAULT_INJECT_RANK): this rank's shard fails")
     recoverable = _recoverable()
     task.on_predict_start()
-    task.host_tables = False             # raw records leave assemble; their intervals are built at export
+    # one GPU (the streaming export): each batch's intervals assembled as one set of array operations when it lands
+    # (decoder.assemble -> intervals.batch_results, transcript tables built at submit); multi-GPU: raw records,
+    # gathered to rank 0, whose export assembles them (utterance_result: the same values)
+    full = on_batch is not None
+    task.host_tables = full
     sr = task.melspec_config["sample_rate"]
     items = {}
 
@@ -97,10 +104,9 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
             return wav_info(path), None
         except (OSError, ValueError) as e:
             return None, e
-    # Only the RIFF headers are read up front (lengths for the batch plan); each batch's files are decoded when the
-    # batch is submitted, by libhfa's native reader straight into the batch's pinned buffer, so host memory holds
-    # the batches in flight, not the folder.  In the calling thread: ~70 us per 10 s file, less than a thread
-    # pool's hand-offs cost here (measured: scripts/cli_bench.py --profile).
+    # Only the RIFF headers are read up front (lengths for the batch plan); each batch's files are decoded one batch
+    # ahead of its launch, by libhfa's native reader straight into the batch's pinned buffer, so host memory holds
+    # the batches in flight, not the folder (~70 us per 10 s file, on the loader thread below).
     for key, (wav_path, ph_seq, word_seq, p2w), (info, e) in zip(keys, rows, map(_info, [r[0] for r in rows])):
         if e is not None:
             errors.append([wav_path, e])
@@ -115,13 +121,20 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
             raise ValueError(f"{path}: {got} samples read, the header said {n}")
         row[n:] = 0.0                                    # the zero padding past this row's length
 
-    def submit(chunk, file_sr):
-        """-> (fetch handle, per-file sample counts at the melspec rate)."""
+    def load(chunk):
+        """The batch's files decoded straight into one pinned buffer (rows zero-padded past each length)."""
         lens = [c[1] for c in chunk]
         wav_h = torch.empty((len(chunk), max(lens)), dtype=torch.float32, pin_memory=True)
-        wav_np = wav_h.numpy()           # rows decoded straight into pinned memory
+        wav_np = wav_h.numpy()
         for r, c in enumerate(chunk):
             _decode(c[0], wav_np[r], lens[r])
+        return wav_h
+
+    def submit(chunk, file_sr, wav_h=None):
+        """-> (fetch handle, per-file sample counts at the melspec rate)."""
+        lens = [c[1] for c in chunk]
+        if wav_h is None:
+            wav_h = load(chunk)
         wav = task.upload(wav_h)         # pinned non-blocking H2D: no host sync
         handle = task.submit(wav, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
                              wav_sr=file_sr, lengths=lens if len(chunk) > 1 else None)
@@ -132,10 +145,11 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
         handle, ks, n44s = job[:3]
         chunk = [items[k] for k in ks]
         res = task.decoder.assemble(handle, [c[3] for c in chunk], [c[4] for c in chunk], [c[5] for c in chunk],
-                                    intervals=False)      # raw records: intervals are assembled at export
+                                    intervals=full)
         for k, r, n44 in zip(ks, res, n44s):
-            out[k] = dict(n44=n44, T=r["T"], ph_idx_seq=r["ph_idx_seq"], ph_time_int=r["ph_time_int"],
-                          frame_confidence=r["frame_confidence"], edge_diff=r["edge_diff"])
+            out[k] = dict(r, n44=n44) if full else \
+                dict(n44=n44, T=r["T"], ph_idx_seq=r["ph_idx_seq"], ph_time_int=r["ph_time_int"],
+                     frame_confidence=r["frame_confidence"], edge_diff=r["edge_diff"])
         return ks
 
     def emit(ks):
@@ -143,8 +157,23 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
         if on_batch is not None:
             on_batch(out, ks)
 
+    # the next batch's files are decoded on a loader thread while this one is launched and the previous one
+    # assembled and exported (the native reader runs outside the GIL); a decode error surfaces in run(), as inline
+    from concurrent.futures import ThreadPoolExecutor
+    loader, prefetched = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hfa-wav"), {}
+
+    trace = [] if os.environ.get("HFA_CLI_TRACE") else None     # (event, perf_counter) per batch, for profiling
+
     def run(ks, file_sr):
-        handle, n44s = submit([items[k] for k in ks], file_sr)
+        if trace is not None:
+            trace.append(("submit", time.perf_counter()))
+        fut = prefetched.pop(tuple(ks), None)
+        wav_h = fut.result() if fut is not None else None
+        if trace is not None:
+            trace.append(("loaded", time.perf_counter()))
+        handle, n44s = submit([items[k] for k in ks], file_sr, wav_h)
+        if trace is not None:
+            trace.append(("submitted", time.perf_counter()))
         return handle, ks, n44s, file_sr
 
     def alone(k, file_sr):
@@ -157,6 +186,8 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
 
     def settle(job):
         """Complete a batch; a recoverable failure re-runs its files one by one."""
+        if trace is not None:
+            trace.append(("settle", time.perf_counter()))
         try:
             ks = finish(job)
         except recoverable as e:
@@ -166,7 +197,11 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
                 for k in job[1]:
                     alone(k, job[3])
             return
+        if trace is not None:
+            trace.append(("assembled", time.perf_counter()))
         emit(ks)
+        if trace is not None:
+            trace.append(("exported", time.perf_counter()))
 
     # variable-length batches (hubertfa_amd.batching.plan_batches): per sample rate, sorted by length, rows
     # zero-padded and aligned with per-row lengths, which keeps every utterance's result identical to aligning it
@@ -178,24 +213,34 @@ def _predict(task, rows, keys, batch_size: int, errors: list, on_batch=None) -> 
     plan = plan_batches([(k, it[1], it[2]) for k, it in items.items()], batch_size, sr,
                         task.unitsEncoder.encoder_sample_rate)
     pending = []
-    for file_sr, ks in plan:
-        job, err = None, None
-        try:
-            job = run(ks, file_sr)
-        except recoverable as e:
-            err = e
-        depth = 2 if job is not None and "resolve" in job[0] else 1
-        while len(pending) >= depth:
+    try:
+        for bi, (file_sr, ks) in enumerate(plan):
+            if bi + 1 < len(plan):
+                nks = plan[bi + 1][1]
+                prefetched[tuple(nks)] = loader.submit(load, [items[k] for k in nks])
+            job, err = None, None
+            try:
+                job = run(ks, file_sr)
+            except recoverable as e:
+                err = e
+            depth = 2 if job is not None and "resolve" in job[0] else 1
+            while len(pending) >= depth:
+                settle(pending.pop(0))
+            if job is not None:
+                pending.append(job)
+            elif len(ks) == 1:
+                errors.append([items[ks[0]][0], err])
+            else:
+                for k in ks:
+                    alone(k, file_sr)
+        while pending:
             settle(pending.pop(0))
-        if job is not None:
-            pending.append(job)
-        elif len(ks) == 1:
-            errors.append([items[ks[0]][0], err])
-        else:
-            for k in ks:
-                alone(k, file_sr)
-    while pending:
-        settle(pending.pop(0))
+    finally:
+        loader.shutdown(wait=True, cancel_futures=True)
+    if trace is not None:
+        import json
+        with open(os.environ["HFA_CLI_TRACE"], "a", encoding="utf-8") as f:
+            f.write(json.dumps(trace) + "\n")
     return out
 
 

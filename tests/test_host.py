@@ -778,3 +778,46 @@ def test_batch_results_irregular_utterances():
         with pytest.raises(IndexError):
             batch_results(Ts, idx_h, tint_h, n_h, fc_h, ed_h, ph_seqs, word_seqs, good[:2] + [bad] + good[3:],
                           512 / 44100)
+
+
+def test_fill_small_gaps_rows_form_matches_element_form():
+    """post_processing.fill_small_gaps (the reference's loop run on the rows as Python floats, written back in place)
+    against the same loop on numpy elements (tools/post_processing.py:34-67's statement order), 600 random interval
+    sets: AP neighbours on either / both sides, gaps under and over both thresholds, leading and trailing gaps,
+    touching and overlapping intervals; values and the caller's array equal."""
+    from hubertfa_amd.post_processing import MIN_SP_LENGTH, SP_MERGE_LENGTH, fill_small_gaps
+
+    def element_form(seq, iv, wav_length):
+        if iv[0, 0] > 0 and iv[0, 0] < MIN_SP_LENGTH:
+            iv[0, 0] = 0
+        for i in range(len(seq) - 1):
+            if iv[i, 1] < iv[i + 1, 0] and iv[i + 1, 0] - iv[i, 1] < SP_MERGE_LENGTH:
+                if seq[i] == "AP":
+                    if seq[i + 1] == "AP":
+                        iv[i, 1] = (iv[i, 1] + iv[i + 1, 0]) / 2
+                        iv[i + 1, 0] = iv[i, 1]
+                    else:
+                        iv[i, 1] = iv[i + 1, 0]
+                elif seq[i + 1] == "AP":
+                    iv[i + 1, 0] = iv[i, 1]
+                elif iv[i + 1, 0] - iv[i, 1] < MIN_SP_LENGTH:
+                    iv[i, 1] = (iv[i, 1] + iv[i + 1, 0]) / 2
+                    iv[i + 1, 0] = iv[i, 1]
+        if iv[-1, 1] < wav_length and wav_length - iv[-1, 1] < MIN_SP_LENGTH:
+            iv[-1, 1] = wav_length
+        return seq, iv
+
+    rng = np.random.default_rng(11)
+    for case in range(600):
+        n = int(rng.integers(1, 40))
+        seq = [("AP" if rng.random() < 0.3 else f"p{int(rng.integers(0, 5))}") for _ in range(n)]
+        starts = np.cumsum(rng.choice([0.0, 0.05, 0.15, 0.35, rng.uniform(0, 0.5)], n))
+        lens = rng.uniform(0.01, 0.4, n)
+        iv = np.stack([starts + np.arange(n) * 0.2, starts + np.arange(n) * 0.2 + lens], 1)
+        if case % 5 == 0:
+            iv[:, 0] -= rng.uniform(0, 0.1)                  # overlaps and touching ends
+        wav_length = float(iv[-1, 1] + rng.choice([0.0, 0.05, 0.2]))
+        a, b = iv.copy(), iv.copy()
+        _, ra = fill_small_gaps(seq, a, wav_length)
+        _, rb = element_form(seq, b, wav_length)
+        assert ra is a and np.array_equal(a, b), case
