@@ -648,6 +648,17 @@ def main():
     ops.PROBE = probe
     thr0 = thread_cpu()
     step_i = [0]
+    # the cyclic collector's pauses inside the timed region (generation, ms): a full collection over the process's
+    # heap stalls the launching thread (host_cpu.gc_pauses)
+    import gc
+    gc_log, gc_t = [], {}
+
+    def gc_cb(phase, info):
+        if phase == "start":
+            gc_t["t"] = time.perf_counter()
+        elif "t" in gc_t:
+            gc_log.append((info["generation"], 1e3 * (time.perf_counter() - gc_t.pop("t"))))
+    gc.callbacks.append(gc_cb)
 
     step_ev = []                      # one event per timed step at its start (the launching stream)
 
@@ -659,6 +670,7 @@ def main():
         step_ev.append(ev)
     res, el = timed(args.steps, on_step=sample_step)
     thr1 = thread_cpu()
+    gc.callbacks.remove(gc_cb)
     ops.PROBE = None
     probe.active = True
     pipe = probe
@@ -834,6 +846,8 @@ def main():
         "enqueue_cpu_ms_per_step": avg(2), "assemble_cpu_ms_per_step": avg(3), "process_cpu_ms_per_step": avg(4),
         "enqueue_wall_ms_per_step": avg(0), "wait_assemble_wall_ms_per_step": avg(1),
         "threads_cpu_ms_per_step": thread_cpu_diff(thr0, thr1, args.steps),
+        "gc_pauses": {"collections": len(gc_log), "by_generation": [sum(1 for g, _ in gc_log if g == k) for k in range(3)],
+                      "max_ms": max((d for _, d in gc_log), default=0.0), "total_ms": sum(d for _, d in gc_log)},
         "note": "rank 0's host cost per timed step: CPU seconds of the launching thread for the GPU half's enqueue "
                 "(ctypes launches, allocator, events) and for the previous batch's wait + interval assembly, and "
                 "the whole process's CPU (all threads; per thread over the timed region in threads_cpu_ms_per_step, "
