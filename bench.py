@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--defer-dp-frames", type=int, default=None,
                     help="task.defer_dp_frames (hold lattices of at least this many DP frames for the next encoder's "
                          "attention launches; A/B of the threshold)")
+    ap.add_argument("--side-grid-cap", type=int, default=None,
+                    help="task.side_grid_cap (workgroups per launch of the side pass's row kernels; A/B of the cap)")
     ap.add_argument("--no-config3", action="store_true",
                     help="N > 1: skip the extra BASELINE config-3 measurement (global batch 512) after the timed steps")
     ap.add_argument("--no-extra-configs", action="store_true",
@@ -563,6 +565,8 @@ def main():
     task.on_predict_start()
     if args.two_stage_resample:
         task.chain_resample = False
+    if args.side_grid_cap is not None:
+        task.side_grid_cap = args.side_grid_cap
     if args.defer_dp_frames is not None:
         task.defer_dp_frames = args.defer_dp_frames
     if args.no_held_dp:
