@@ -1,6 +1,6 @@
 # Round 6: the PCIe-inclusive path (bench --host-input: each step's waves uploaded from pinned host memory, as the CLI
 # does) with task.upload's H2D on a stream of its own (an --upload-stream knob built for this A/B, since removed)
-# HBM-resident rate beside them; one box, interleaved.
+# against the encoder's stream, with the HBM-resident rate beside them; one box, interleaved.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r06aa
