@@ -337,7 +337,7 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
     model.on_predict_start()                             # the units encoder's weights (reference: predict start)
     # the loaded program's objects (torch, the model, the dataset rows) leave the cyclic collector's scans: a full
     # collection over them inside the batch loop stalled the host for 60-90 ms (the GPU idle meanwhile), once per
-    # 1 024-file run (HFA_CLI_TRACE, scripts/gpu_r06x.sh); objects made from here on are collected as usual
+    # 1 024-file run (HFA_CLI_TRACE, scripts/archive/gpu_r06x.sh); objects made from here on are collected as usual
     import gc
     gc.collect()
     gc.freeze()
