@@ -374,6 +374,7 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
         errors = [e for part in all_errors for e in part]
         if rank != 0:
             dist.destroy_process_group()
+            gc.unfreeze()
             return
 
     if stream is not None:
@@ -400,6 +401,7 @@ def main(ckpt, folder, g2p, save_confidence, hubert_path, batch_size, out_path, 
                        dict(g2p=t_g2p - t_start, load=t_load - t_g2p, align=t_align - t_load, export=t_end - t_align))
     if world > 1:
         dist.destroy_process_group()
+    gc.unfreeze()                                        # (an in-process caller's later runs see a normal collector)
 
 
 if __name__ == "__main__":
