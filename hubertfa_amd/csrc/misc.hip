@@ -362,7 +362,7 @@ __global__ __launch_bounds__(kChainUThreads) void chain_window_kernel(int N, con
                                                                       int FL, int FS, int y_cols,
                                                                       float* __restrict__ uw) {
     const int b = blockIdx.z, slot = blockIdx.y, t = blockIdx.x * kChainUThreads + threadIdx.x;
-    const int Nb = lens ? lens[b] : N;
+    const int Nb = lens ? min(lens[b], N) : N;      // (a row never reads past N)
     if (Nb <= 0 || t >= kwd) return;
     const int len_u = ceil_f32_quot(Q, Nb, P);
     const int len_y = ceil_f32_quot(P, len_u, Q);
@@ -394,7 +394,7 @@ __global__ __launch_bounds__(kChainQW * kChainParts) void chain_frame_kernel(int
     extern __shared__ float su[];                          // [kwd] window, then [kChainParts][kChainQW] partial sums
     float* part = su + kwd;
     const int b = blockIdx.z, slot = blockIdx.y, q0 = blockIdx.x * kChainQW;
-    const int Nb = lens ? lens[b] : N;
+    const int Nb = lens ? min(lens[b], N) : N;      // (a row never reads past N)
     if (Nb <= 0) return;
     const int len_u = ceil_f32_quot(Q, Nb, P);
     const int len_y = ceil_f32_quot(P, len_u, Q);
