@@ -365,7 +365,7 @@ def test_resample_split_vs_f32_and_restatement(o, n, w, N):
     assert float((got.double() - f32.double()).abs().max()) < 2e-6
 
 
-@pytest.mark.parametrize("N", [160000, 4097, 12345, 441 * 3 + 7, 160 * 25 + 159, 4_800_000])
+@pytest.mark.parametrize("N", [160000, 4097, 12345, 441 * 3 + 7, 160 * 25 + 159, 4_800_000, 37, 161])
 def test_chain_resampler_vs_two_stages(N):
     """16 k -> 44.1 k -> 16 k as one composite pass + the exact edge frames (resample.ChainResampler) against the
     restated two stages (oracle/resample.py, f32 as torchaudio) within the stages' own split-path tolerance, and
