@@ -218,7 +218,7 @@ class KernelProbe:
     def dominant(self) -> str:
         return max(self.census, key=self.census.get)
 
-    def __call__(self, name: str, work: float, launch, kind: str = "flops", shape=None, units=None):
+    def __call__(self, name: str, work: float, launch, kind: str = "flops", shape=None, units=None, label=None):
         if self.name is None:
             if kind == "flops":
                 self.census[name] = self.census.get(name, 0.0) + work
@@ -635,9 +635,17 @@ def resample_split(x, orig, new, w_planes, G, width, out=None, workspace=None, f
     if workspace is None:
         nbytes = _lib.lib().hfa_resample_split_workspace_bytes(B, N, orig, Kg, G)
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
-    _lib.call("hfa_resample_split", B, N, _ptr(x), x.stride(0), orig, new, _ptr(w_planes), Kg, G, width,
-              _ptr(workspace), _ptr(out), out.stride(0), _ptr(split_flag(x.device) if flag is None else flag),
-              _stream(x.device))
+    def launch():
+        _lib.call("hfa_resample_split", B, N, _ptr(x), x.stride(0), orig, new, _ptr(w_planes), Kg, G, width,
+                  _ptr(workspace), _ptr(out), out.stride(0), _ptr(split_flag(x.device) if flag is None else flag),
+                  _stream(x.device))
+    if PROBE is None:
+        launch()
+    else:      # (its GEMM shares an instantiation with the encoder's: reported outside the dominant-kernel census)
+        rows = F if G == 1 else -(-F // 8)
+        PROBE(_split_name(rows, new, Kg, B * G, False, 0, Kg), 2.0 * rows * new * Kg * B * G, launch,
+              kind="flops_aux", shape=(rows, new, Kg, B * G),
+              label="resampler chain (one pass)" if orig == new else f"resampler {orig} -> {new} (reduced rates)")
     from .resample import target_length
     return out[:, : target_length(N, orig, new) if n_out is None else n_out]
 

@@ -33,7 +33,7 @@ def main():
     times = {}
 
     class Probe:
-        def __call__(self, name, work, launch, kind="flops", shape=None, units=None):
+        def __call__(self, name, work, launch, kind="flops", shape=None, units=None, label=None):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             launch()

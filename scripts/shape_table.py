@@ -48,6 +48,8 @@ def matches(log_name: str, trace_name: str) -> bool:
 
 def role(entry, enc) -> str:
     name, shape = entry["name"], entry["shape"]
+    if entry.get("label"):
+        return entry["label"]
     if shape is None:
         return name
     if name.startswith("attn_fwd"):

@@ -26,8 +26,9 @@ class LaunchLog:
         self.name = "-"
         self.entries = []
 
-    def __call__(self, name, work, launch, kind="flops", shape=None, units=None):
-        self.entries.append({"name": name, "work": work, "kind": kind, "shape": list(shape) if shape else None})
+    def __call__(self, name, work, launch, kind="flops", shape=None, units=None, label=None):
+        self.entries.append({"name": name, "work": work, "kind": kind, "shape": list(shape) if shape else None,
+                             "label": label})
         return launch()
 
 
