@@ -121,3 +121,35 @@ def test_pipelined_submit_matches_align_batch():
         for u, (g, r) in enumerate(zip(got, a)):
             for k in ("ph_idx_seq", "ph_time_int", "frame_confidence", "edge_diff"):
                 assert np.array_equal(np.asarray(g[k]), np.asarray(r[k])), f"batch {i} utt {u}: {k}"
+
+
+def test_chain_resampler_path_matches_two_stages():
+    """The product path's one-pass resampling chain (task.encode_batch -> resample.ChainResampler) against the two
+    stages it replaces (task.chain_resample = False), end to end at config-2 geometry with a ragged batch: the
+    lattices within the north-star bar of each other (1e-4: the two resamplings differ by f32 rounding, ~2e-5 after
+    twelve layers) and every boundary and phone path identical."""
+    from hubertfa_amd.task import ForcedAlignmentTask, synth_checkpoint
+    dev = torch.device("cuda")
+    ckpt = synth_checkpoint(model_path="synth:0", seed=1)
+    task = ForcedAlignmentTask(**ckpt["hyper_parameters"], state_dict=ckpt["state_dict"], device=dev)
+    task.on_predict_start()
+    B = 4
+    wav, ph_seqs, word_seqs, p2ws = _inputs(B, 10.0, 30, 4242)
+    lens = [wav.shape[1], wav.shape[1] - 16000 * 3 - 7, wav.shape[1] - 12345, wav.shape[1] - 1]
+    x = torch.from_numpy(wav).to(dev)
+    for b, n in enumerate(lens):
+        x[b, n:] = 0
+    got = {}
+    for chain in (True, False):
+        task.chain_resample = chain
+        dev_out = task.align_batch(x, ph_seqs, word_seqs, p2ws, wav_sr=16000, lengths=lens, host=False)
+        got[chain] = (dev_out["lattice"]["prob_log"].cpu().numpy(), task.decoder.assemble(dev_out, ph_seqs, word_seqs,
+                                                                                           p2ws))
+    task.chain_resample = True
+    (pl_c, res_c), (pl_t, res_t) = got[True], got[False]
+    for b in range(B):
+        T, S = res_c[b]["T"], len(ph_seqs[b])
+        assert T == res_t[b]["T"]
+        assert np.abs(pl_c[b, :T, :S] - pl_t[b, :T, :S]).max() < 1e-4, b
+        assert np.array_equal(res_c[b]["ph_idx_seq"], res_t[b]["ph_idx_seq"]), b
+        assert np.array_equal(res_c[b]["ph_time_int"], res_t[b]["ph_time_int"]), b
