@@ -373,3 +373,36 @@ def test_hip_error_fails_the_shard(tmp_path):
     assert len(log) == 1 and str(log[0][0]).endswith("m2.wav")
     assert sorted(p.name for p in (tmp_path / "out").rglob("*.TextGrid")) == \
         sorted(f"m{i}.TextGrid" for i in range(n) if i != 2)
+
+
+def test_predict_decode_error_on_the_loader_thread(tmp_path, monkeypatch):
+    """A file whose decode fails after the header scan (it changed on disk in between) fails on the loader thread,
+    which decodes each batch one batch ahead of its launch: the error surfaces at that batch's launch, the batch is
+    re-run file by file, the file is logged and skipped, and every other file gets exactly its normal result."""
+    import infer
+    import hubertfa_amd.g2p as g2p_mod
+    import torch
+    from hubertfa_amd import wav_io
+    from hubertfa_amd.task import ForcedAlignmentTask
+    seg, dpath, ck, n = _mixed_folder(tmp_path)
+    g = g2p_mod.DictionaryG2P(dictionary=str(dpath))
+    g.set_in_format("lab")
+    rows = list(g.get_dataset(sorted(seg.rglob("*.wav"))))
+    torch.set_grad_enabled(False)
+    task = ForcedAlignmentTask.load_from_checkpoint(str(ck), device=torch.device("cuda"), hubert_model_path="synth:0")
+    keys = list(range(len(rows)))
+    ref = infer._predict(task, rows, keys, 2, [])
+    real = wav_io.read_wav_into
+
+    def flaky(path, row, channel=0):
+        if str(path).endswith("m3.wav"):
+            raise ValueError(f"{path}: changed on disk since the header scan")
+        return real(path, row, channel=channel)
+    monkeypatch.setattr(wav_io, "read_wav_into", flaky)
+    errors = []
+    got = infer._predict(task, rows, keys, 2, errors)
+    assert len(errors) == 1 and str(errors[0][0]).endswith("m3.wav")
+    assert sorted(got) == [k for k in keys if not str(rows[k][0]).endswith("m3.wav")]
+    for k in got:
+        for f in ("ph_time_int", "ph_idx_seq", "frame_confidence", "edge_diff"):
+            assert np.array_equal(got[k][f], ref[k][f]), (k, f)
